@@ -1,0 +1,77 @@
+/*
+ * aero_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * C API of the CPU restatement of airframesio/aero-cli's continuous
+ * 10500-bps OQPSK decode path (decode/oqpskdemodulator.cpp, decode/DSP.cpp,
+ * decode/coarsefreqestimate.cpp, decode/jfft.cpp, decode/hunter.cpp,
+ * decode/aerol.cpp, decode/jconvolutionalcodec.cpp + libcorrect).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library, and only as the checker.  Nothing in the product path
+ * links or calls it.
+ *
+ * Parity status: see oracle/aero_oracle.cpp header.
+ */
+#ifndef AERO_ORACLE_H
+#define AERO_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_chan oracle_chan;
+
+/* flags */
+#define ORACLE_TRACE_PT 1 /* record every rotated pt_qpsk (re,im) */
+
+oracle_chan *oracle_create(int bitrate, int flags);
+void oracle_destroy(oracle_chan *c);
+
+/* One call == one ZMQ message == OqpskDemodulator::dataReceived
+ * (decode/oqpskdemodulator.cpp:624-630). */
+int oracle_push(oracle_chan *c, const int16_t *pcm, size_t n);
+
+/* Soft bits delivered to AeroL (groups of 32, decode/oqpskdemodulator.cpp:534-540). */
+size_t oracle_softbits(const oracle_chan *c, uint8_t *dst, size_t cap);
+
+/* Per coarse-estimate hop, 6 doubles: sample index, freq_offset_est emitted,
+ * mixer2 freq, mixer_center freq (after the slot ran), mse, signal flag. */
+size_t oracle_hops(const oracle_chan *c, double *dst, size_t cap_records);
+
+/* rotated pt_qpsk trace (2 doubles per carrier event), only with ORACLE_TRACE_PT */
+size_t oracle_pt(const oracle_chan *c, double *dst, size_t cap_records);
+
+/* Per decoded P-channel block: 2496 (or 2483 first) decoded bits as bytes 0/1,
+ * prefixed by a uint32 count. */
+size_t oracle_blocks(const oracle_chan *c, uint8_t *dst, size_t cap);
+
+/* Per completed frame: 320 bytes = up to 312 infofield bytes (zero padded),
+ * then uint32 infofield length, then uint32 crc-ok bitmask (26 bits). */
+size_t oracle_frames(const oracle_chan *c, uint8_t *dst, size_t cap);
+
+/* ACARSItems as canonical text lines (see tests/aero_items.py). */
+size_t oracle_items(const oracle_chan *c, char *dst, size_t cap);
+
+/* libcorrect-ABI restatement (r=1/2, K=7, polys {109,79}). */
+size_t oracle_conv_encode(const uint8_t *msg, size_t msg_len, uint8_t *encoded);
+size_t oracle_viterbi_decode_soft(const uint8_t *soft, size_t num_encoded_bits,
+                                  uint8_t *msg);
+
+/* Known-answer helpers */
+uint16_t oracle_crc16_bytes(const uint8_t *bytes, int n);
+void oracle_scrambler_bits(int *dst, int n);
+void oracle_deinterleave_perm(int N, int *src_index_of_dst);
+void oracle_rrc_design(double alpha, int firsize, double fs, double symfreq, double *dst);
+void oracle_cis_table(double *dst); /* 19999 x (cos, sin) */
+void oracle_twiddles(int nfft, int inverse, double *dst);
+
+/* raw JFFT-order transform for the FFT parity test (in place, nfft complex) */
+void oracle_fft(double *x, int nfft, int inverse);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

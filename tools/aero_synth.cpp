@@ -1,0 +1,314 @@
+/*
+ * aero_synth.cpp — synthetic Aero P-channel transmitter (test/bench input).
+ *
+ * Produces what aero-publish would hand aero-decode for one VFO: 48 kHz real
+ * int16 PCM of a 10500-bps OQPSK P-channel (SURVEY.md §8(d) C1/C2 input).
+ * It inverts the receive chain of decode/aerol.cpp so that the reference
+ * decoder recovers every signal unit it carries:
+ *   SUs (12 B, CRC-16/X-25 LE, aerol.h:332-367) -> 26 per 0.5 s frame
+ *   -> LSB-first bits (aerol.cpp:1509-1520) -> scrambler (aerol.h:406-440)
+ *   -> K=7 r=1/2 {109,79} encoder, continuous across frames
+ *      (jconvolutionalcodec.cpp:146-198, libcorrect conventions)
+ *   -> 64x78 interleaver, inverse of deinterleave_ba (aerol.cpp:594-613)
+ *   -> frame = 16 header + 178 dummy + 4992 data + 64 UW (aerol.cpp:1012-1021,
+ *      UW 0xE15AE893 on both arms, aerol.cpp:933-936)
+ *   -> OQPSK: even channel bits on Q, odd on I, Q leading I by T/2
+ *      (oqpskdemodulator.cpp:437-445), RRC alpha=1, real carrier, AWGN.
+ * ACARS payloads follow ParserISU's layout (aerol.cpp:333-489).
+ *
+ * Not part of the product path: tests/ and bench.py use it to make inputs.
+ */
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+extern "C" {
+typedef struct {
+  double fs;          /* 48000 */
+  double carrier_hz;  /* e.g. 12037.5 */
+  double phase0;      /* carrier phase, rad */
+  double amplitude;   /* baseband scale (full scale = 1) */
+  double ebn0_db;     /* >= 99: noiseless */
+  uint64_t seed;
+  double msg_rate;    /* probability of a new ACARS message when the SU queue is empty */
+  int lead_in;        /* samples of noise before the first frame */
+} aero_synth_cfg;
+
+size_t aero_synth_p10500(const aero_synth_cfg *cfg, int16_t *pcm, size_t nsamples,
+                         uint8_t *frames, size_t frames_cap);
+}
+
+namespace {
+
+struct Rng {
+  uint64_t s;
+  explicit Rng(uint64_t seed) : s(seed ? seed : 0x9E3779B97F4A7C15ULL) {}
+  uint64_t next() {  // splitmix64
+    uint64_t z = (s += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+  }
+  double uniform() { return (next() >> 11) * (1.0 / 9007199254740992.0); }
+  int below(int n) { return (int)(uniform() * n); }
+  double gauss() {
+    double u1 = uniform(), u2 = uniform();
+    if (u1 < 1e-300) u1 = 1e-300;
+    return sqrt(-2.0 * log(u1)) * cos(2.0 * M_PI * u2);
+  }
+};
+
+uint16_t crc16(const uint8_t *b, int n) {
+  uint16_t crc = 0xFFFF;
+  for (int i = 0; i < n; i++) {
+    unsigned m = b[i];
+    for (int k = 0; k < 8; k++) {
+      unsigned bit = m & 1;
+      m >>= 1;
+      unsigned cb = crc & 1;
+      crc >>= 1;
+      if (cb ^ bit) crc ^= 0x8408;
+    }
+  }
+  return (uint16_t)~crc;
+}
+
+uint8_t odd(uint8_t c) {
+  c &= 0x7F;
+  return (__builtin_popcount(c) & 1) ? c : (uint8_t)(c | 0x80);
+}
+
+struct SU {
+  uint8_t b[12];
+};
+
+SU make_su(const uint8_t *ten) {
+  SU s;
+  memcpy(s.b, ten, 10);
+  uint16_t c = crc16(ten, 10);
+  s.b[10] = c & 0xFF;
+  s.b[11] = c >> 8;
+  return s;
+}
+
+struct Tx {
+  aero_synth_cfg cfg;
+  Rng rng;
+  std::vector<SU> queue;
+  std::vector<int> scr;
+  int perm[64];
+  unsigned enc_reg = 0;
+  int frame_no = 0;
+  std::vector<int> chan;  // channel bits of the current frame
+  unsigned aes_pool[8];
+  uint8_t refno = 0;
+
+  explicit Tx(const aero_synth_cfg &c) : cfg(c), rng(c.seed) {
+    std::vector<int> st = {1, 1, 0, 1, 0, 0, 1, 0, 1, 0, 1, 1, 0, 0, 1};
+    scr.resize(5000);
+    for (int a = 0; a < 5000; a++) {
+      int v = st[0] ^ st[14];
+      scr[a] = v;
+      for (int i = 14; i > 0; i--) st[i] = st[i - 1];
+      st[0] = v;
+    }
+    for (int i = 0; i < 64; i++) perm[i] = (i * 27) % 64;
+    for (auto &a : aes_pool) a = 0x400000u + (unsigned)rng.below(0x3FFFFF);
+  }
+
+  void push_acars(unsigned aes, uint8_t ges, const std::string &reg, const std::string &label,
+                  uint8_t bi, const std::string &text, bool more) {
+    std::vector<uint8_t> ud;
+    ud.push_back(0xFF);
+    ud.push_back(0xFF);
+    ud.push_back(odd(0x01));
+    ud.push_back(odd('2'));
+    for (int i = 0; i < 7; i++) ud.push_back(odd(i < (int)reg.size() ? reg[i] : '.'));
+    ud.push_back(odd(0x15));
+    ud.push_back(odd(label[0]));
+    ud.push_back(odd(label[1]));
+    ud.push_back(odd(bi));
+    ud.push_back(odd(0x02));
+    for (char ch : text) ud.push_back(odd((uint8_t)ch));
+    ud.push_back(more ? 0x97 : 0x83);
+    ud.push_back((uint8_t)rng.below(256));
+    ud.push_back((uint8_t)rng.below(256));
+    ud.push_back(0x7F);
+    // ISU 0x71 + SSUs (ISUData::update, aerol.cpp:158-227)
+    int rest = (int)ud.size() - 2;
+    int m = (rest + 7) / 8;  // SSUs
+    int r = rest - 8 * (m - 1);
+    uint8_t qno = (uint8_t)rng.below(16), ref = (uint8_t)(refno++ & 0x0F);
+    uint8_t isu[10] = {0x71, (uint8_t)(aes >> 16), (uint8_t)(aes >> 8), (uint8_t)aes, ges,
+                       (uint8_t)((qno << 4) | ref), (uint8_t)(m & 0x3F), (uint8_t)(r << 4), ud[0], ud[1]};
+    queue.push_back(make_su(isu));
+    size_t p = 2;
+    for (int s = m - 1; s >= 0; s--) {
+      uint8_t ssu[10] = {(uint8_t)(0xC0 | s), (uint8_t)((qno << 4) | ref), 0, 0, 0, 0, 0, 0, 0, 0};
+      int nb = s == 0 ? r : 8;
+      for (int i = 0; i < nb; i++) ssu[2 + i] = ud[p++];
+      for (int i = nb; i < 8; i++) ssu[2 + i] = (uint8_t)rng.below(256);
+      queue.push_back(make_su(ssu));
+    }
+  }
+
+  std::string rand_text(int n) {
+    static const char *alpha = "ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789 /.-,:";
+    std::string t;
+    for (int i = 0; i < n; i++) t += alpha[rng.below((int)strlen(alpha))];
+    if (n > 20) t[n / 2] = '\r', t[n / 2 + 1] = '\n';
+    return t;
+  }
+
+  void refill() {
+    double u = rng.uniform();
+    unsigned aes = aes_pool[rng.below(8)];
+    uint8_t ges = (uint8_t)(0x80 + rng.below(8));
+    if (u < cfg.msg_rate) {
+      static const char *labels[] = {"H1", "SA", "_d", "Q0", "B6", "10", "5Z", "AA"};
+      char reg[8];
+      snprintf(reg, sizeof reg, ".N%05u", (unsigned)(aes % 100000));
+      std::string label = labels[rng.below(8)];
+      if (rng.uniform() < 0.15) {  // two-fragment message (ACARSDefragmenter)
+        push_acars(aes, ges, reg, label, 'A', rand_text(40 + rng.below(60)), true);
+        push_acars(aes, ges, reg, label, 'B', rand_text(10 + rng.below(40)), false);
+      } else {
+        push_acars(aes, ges, reg, label, (uint8_t)('A' + rng.below(26)),
+                   rand_text(rng.below(180)), false);
+      }
+    } else if (u < cfg.msg_rate + 0.05) {  // log-on confirm (aerol.cpp:1730-1733)
+      uint8_t su[10] = {0x11, (uint8_t)(aes >> 16), (uint8_t)(aes >> 8), (uint8_t)aes, ges, 0, 0, 0, 0, 0};
+      for (int i = 5; i < 10; i++) su[i] = (uint8_t)rng.below(256);
+      queue.push_back(make_su(su));
+    } else if (u < cfg.msg_rate + 0.10) {  // C channel assignment (aerol.cpp:1804-1812)
+      uint8_t su[10] = {0x34, (uint8_t)(aes >> 16), (uint8_t)(aes >> 8), (uint8_t)aes, ges, 0, 0, 0, 0, 0};
+      for (int i = 5; i < 10; i++) su[i] = (uint8_t)rng.below(256);
+      queue.push_back(make_su(su));
+    } else {  // fill-in signal unit
+      uint8_t su[10] = {0x01};
+      for (int i = 1; i < 10; i++) su[i] = (uint8_t)rng.below(256);
+      queue.push_back(make_su(su));
+    }
+  }
+
+  // builds chan[] (5250 bits) for the next frame; info bytes to *info312
+  void next_frame(uint8_t *info312) {
+    uint8_t info[312];
+    for (int k = 0; k < 26; k++) {
+      while (queue.empty()) refill();
+      memcpy(info + 12 * k, queue.front().b, 12);
+      queue.erase(queue.begin());
+    }
+    if (info312) memcpy(info312, info, 312);
+    // LSB-first bits, scrambled from position 0 (reset each frame)
+    int ibits[2496];
+    for (int h = 0; h < 2496; h++) ibits[h] = ((info[h / 8] >> (h % 8)) & 1) ^ scr[h];
+    // encoder: table[r] bit j = parity(r & poly[j]); symbol j <-> poly[j]
+    int coded[4992];
+    for (int t = 0; t < 2496; t++) {
+      enc_reg = ((enc_reg << 1) | (unsigned)ibits[t]) & 127;
+      coded[2 * t] = __builtin_popcount(enc_reg & 109) & 1;
+      coded[2 * t + 1] = __builtin_popcount(enc_reg & 79) & 1;
+    }
+    int blk[4992];
+    for (int j = 0; j < 78; j++)
+      for (int i = 0; i < 64; i++) blk[perm[i] * 78 + j] = coded[j * 64 + i];
+    chan.assign(5250, 0);
+    unsigned fc = (unsigned)(frame_no & 0xF);
+    unsigned hdr = 0x1000u | ((unsigned)((frame_no >> 4) & 0xF) << 8) | (fc << 4) | fc;
+    for (int b = 0; b < 16; b++) chan[b] = (hdr >> (15 - b)) & 1;
+    for (int b = 16; b < 194; b++) chan[b] = rng.below(2);
+    for (int b = 0; b < 4992; b++) chan[194 + b] = blk[b];
+    const uint32_t uw = 0xE15AE893u;
+    for (int j = 0; j < 32; j++) {
+      int u = (uw >> (31 - j)) & 1;
+      chan[5186 + 2 * j] = u;
+      chan[5186 + 2 * j + 1] = u;
+    }
+    frame_no++;
+  }
+};
+
+// RRC (alpha = 1) continuous pulse at t (in symbol periods)
+double rrc1(double x) {
+  const double a = 1.0;
+  if (fabs(x) < 1e-12) return 1.0 - a + 4.0 * a / M_PI;
+  if (fabs(fabs(x) - 0.25) < 1e-12)
+    return a / sqrt(2.0) * ((1 + 2 / M_PI) * sin(M_PI / 4) + (1 - 2 / M_PI) * cos(M_PI / 4));
+  return (sin(M_PI * x * (1 - a)) + 4 * a * x * cos(M_PI * x * (1 + a))) /
+         (M_PI * x * (1 - 16 * a * a * x * x));
+}
+
+}  // namespace
+
+extern "C" size_t aero_synth_p10500(const aero_synth_cfg *cfg, int16_t *pcm, size_t nsamples,
+                                    uint8_t *frames, size_t frames_cap) {
+  Tx tx(*cfg);
+  const double Fs = cfg->fs, Ts = Fs / 5250.0;  // samples per arm symbol
+  const int SPAN = 8;                           // +- symbols
+  const int OS = 256;                           // table oversampling
+  std::vector<double> tab(2 * SPAN * OS + 2);
+  double energy = 0;
+  for (size_t i = 0; i < tab.size(); i++) {
+    tab[i] = rrc1((double)i / OS - SPAN);
+  }
+  for (int i = 0; i < 2 * SPAN * OS; i++) energy += tab[i] * tab[i];
+  energy /= OS;  // integral of h^2 over symbol periods
+  auto pulse = [&](double x) {
+    double p = (x + SPAN) * OS;
+    if (p <= 0 || p >= 2 * SPAN * OS) return 0.0;
+    int ip = (int)p;
+    double f = p - ip;
+    return tab[ip] * (1 - f) + tab[ip + 1] * f;
+  };
+  // symbols: q[k] from chan bit 2k, i[k] from chan bit 2k+1, generated lazily
+  std::vector<double> qs, is;
+  size_t nframes = 0;
+  auto ensure = [&](size_t k) {
+    while (qs.size() <= k) {
+      uint8_t *dst = (frames && nframes < frames_cap) ? frames + 312 * nframes : nullptr;
+      tx.next_frame(dst);
+      nframes++;
+      for (int b = 0; b < 5250; b += 2) {
+        qs.push_back(tx.chan[b] ? 1.0 : -1.0);
+        is.push_back(tx.chan[b + 1] ? 1.0 : -1.0);
+      }
+    }
+  };
+  // power: A^2 * (E[I^2]+E[Q^2]) / 2 ; E[I^2] = energy (unit symbols, 1 per period)
+  double A = cfg->amplitude;
+  double P = A * A * (2.0 * energy) / 2.0;
+  double sigma = 0;
+  if (cfg->ebn0_db < 99) {
+    double Eb = P / 10500.0;
+    double N0 = Eb / pow(10.0, cfg->ebn0_db / 10.0);
+    sigma = sqrt(N0 / 2.0 * Fs);
+  }
+  Rng nrng(cfg->seed ^ 0xA5A5A5A55A5A5A5AULL);
+  const double w = 2.0 * M_PI * cfg->carrier_hz / Fs;
+  for (size_t n = 0; n < nsamples; n++) {
+    double x = 0;
+    long long nn = (long long)n - cfg->lead_in;
+    if (nn >= 0) {
+      double t = (double)nn / Ts;  // in symbol periods; Q symbol k centred at k, I at k+0.5
+      long long k0 = (long long)floor(t) - SPAN, k1 = (long long)floor(t) + SPAN + 1;
+      if (k0 < 0) k0 = 0;
+      ensure((size_t)k1 + 1);
+      double I = 0, Q = 0;
+      for (long long k = k0; k <= k1; k++) {
+        Q += qs[k] * pulse(t - (double)k);
+        I += is[k] * pulse(t - (double)k - 0.5);
+      }
+      double ph = w * (double)nn + cfg->phase0;
+      x = A * (I * cos(ph) + Q * sin(ph));
+    }
+    if (sigma > 0) x += sigma * nrng.gauss();
+    double v = floor(x * 32768.0 + 0.5);
+    if (v > 32767) v = 32767;
+    if (v < -32768) v = -32768;
+    pcm[n] = (int16_t)v;
+  }
+  return nframes;
+}
