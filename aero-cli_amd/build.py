@@ -1,0 +1,118 @@
+"""Build the in-tree native libraries (no pip, no JIT cache).
+
+  aero-cli_amd/libaero_engine.so   product: HIP kernels for gfx950 + C ABI
+  tools/libaero_synth.so           synthetic Aero P-channel transmitter
+  oracle/liboracle.so              test-only CPU restatement (checker)
+
+Usage: python aero-cli_amd/build.py [--engine] [--synth] [--oracle] [-j N]
+(no flag = everything).  Object files go to aero-cli_amd/build/.
+"""
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, 'csrc')
+BUILD = os.path.join(HERE, 'build')
+ENGINE_SO = os.path.join(HERE, 'libaero_engine.so')
+SYNTH_SO = os.path.join(ROOT, 'tools', 'libaero_synth.so')
+ORACLE_DIR = os.path.join(ROOT, 'oracle')
+
+ARCH = os.environ.get('AERO_OFFLOAD_ARCH', 'gfx950')
+HIPCC = os.environ.get('HIPCC', shutil.which('hipcc') or '/opt/rocm/bin/hipcc')
+# bit-exactness: no FP contraction, no fast math, anywhere on the product path
+FP = ['-ffp-contract=off', '-fno-fast-math']
+HIP_FLAGS = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH, '-munsafe-fp-atomics'] + FP
+CXX_FLAGS = ['-O2', '-std=c++17', '-fPIC', '-Wall'] + FP
+
+HIP_SRCS = ['demod_oqpsk.hip', 'coarse.hip', 'aerol.hip', 'engine.hip']
+CXX_SRCS = ['tables_host.cpp', 'acars_host.cpp']
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError('build failed: %s\n%s%s' % (' '.join(cmd), r.stdout, r.stderr))
+    return r
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_engine(jobs=4):
+    os.makedirs(BUILD, exist_ok=True)
+    headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith('.h')]
+    headers.append(os.path.join(ROOT, 'include', 'aero_engine.h'))
+    tasks, objs = [], []
+    for s in HIP_SRCS + CXX_SRCS:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(BUILD, s + '.o')
+        objs.append(obj)
+        if _stale(obj, [src] + headers):
+            if s.endswith('.hip'):
+                cmd = [HIPCC] + HIP_FLAGS + ['-c', src, '-o', obj]
+            else:
+                cmd = ['g++'] + CXX_FLAGS + ['-c', src, '-o', obj]
+            tasks.append(cmd)
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for f in [ex.submit(_run, t) for t in tasks]:
+            f.result()
+    if tasks or _stale(ENGINE_SO, objs):
+        _run([HIPCC, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', ENGINE_SO] + objs)
+    return ENGINE_SO
+
+
+def build_synth():
+    src = os.path.join(ROOT, 'tools', 'aero_synth.cpp')
+    if _stale(SYNTH_SO, [src]):
+        _run(['g++', '-O2', '-std=c++17', '-fPIC', '-shared', '-o', SYNTH_SO, src, '-lm'])
+    return SYNTH_SO
+
+
+MATHHOST_SO = os.path.join(ROOT, 'tools', 'libaero_mathhost.so')
+
+
+def build_mathhost():
+    src = os.path.join(ROOT, 'tools', 'mathhost.cpp')
+    deps = [src, os.path.join(CSRC, 'aero_math.h'), os.path.join(CSRC, 'aero_math_tables.h')]
+    if _stale(MATHHOST_SO, deps):
+        _run(['g++', '-O2', '-std=c++17', '-fPIC', '-shared', '-ffp-contract=off', '-o', MATHHOST_SO, src, '-lm'])
+    return MATHHOST_SO
+
+
+def build_oracle():
+    _run(['make', '-s', '-C', ORACLE_DIR])
+    return os.path.join(ORACLE_DIR, 'liboracle.so')
+
+
+def build_all(jobs=4):
+    build_oracle()
+    build_synth()
+    build_mathhost()
+    return build_engine(jobs)
+
+
+if __name__ == '__main__':
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--engine', action='store_true')
+    ap.add_argument('--synth', action='store_true')
+    ap.add_argument('--oracle', action='store_true')
+    ap.add_argument('-j', type=int, default=4)
+    a = ap.parse_args()
+    if not (a.engine or a.synth or a.oracle):
+        print(build_all(a.j))
+        sys.exit(0)
+    if a.oracle:
+        print(build_oracle())
+    if a.synth:
+        print(build_synth())
+    if a.engine:
+        print(build_engine(a.j))

@@ -1,0 +1,330 @@
+/*
+ * aerol.hip — AeroL P-channel link layer for 10500 bps on gfx950:
+ *
+ *  frame_kernel   : AeroL::Decode framing state machine, one channel per lane
+ *                   (decode/aerol.cpp:1060-2038): phase-invariant UW search on
+ *                   alternating arms, header, block fill; a full 64x78 block
+ *                   becomes a Viterbi job (double-buffered per channel).
+ *  viterbi_kernel : one wavefront per job.  Deinterleave_ba on load
+ *                   (decode/aerol.cpp:594-613), JConvolutionalCodec::
+ *                   Decode_Continuous framing (decode/jconvolutionalcodec.cpp:
+ *                   146-198) and the libcorrect soft Viterbi (r=1/2, K=7,
+ *                   polys {109,79}; restated in oracle/aero_oracle.cpp): lane s
+ *                   owns trellis state s, predecessors arrive by ds_bpermute,
+ *                   the 64 survivor decisions of a step are one ballot word
+ *                   in LDS.  Then DelayLine dl2, AeroLScrambler, LSB-first byte
+ *                   packing and the per-SU CRC-16 (decode/aerol.cpp:1501-1556).
+ *
+ * Framing never depends on the CRC results: datacd becomes true at the first
+ * UW sync and only the (disabled, wall-clock) DCD timer could clear it, so
+ * the Viterbi/CRC work can run after the framing pass without changing the
+ * framing decisions.
+ */
+#include <hip/hip_runtime.h>
+
+#include "engine_common.h"
+
+namespace aero {
+
+constexpr uint32_t UW = 0xE15AE893u;  // 3780831379 (aerol.cpp:933-936)
+
+__global__ __launch_bounds__(256) void frame_kernel(DevState S, int nch) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nch) return;
+  const int C = S.C;
+  int *is = S.is;
+  long long *ls = S.ls;
+  const long long P = ls[LS_SOFT_P * C + c];
+  long long q = ls[LS_SOFT_C * C + c];
+  const long long E = P & ~31LL;  // delivered in groups of 32 (oqpskdemodulator.cpp:534-540)
+  if (q >= E) return;
+  int realimag = is[IS_RI * C + c], cntr = is[IS_CNTR * C + c], gsl = is[IS_GSL * C + c];
+  uint32_t uwi = (uint32_t)is[IS_UWI * C + c], uwr = (uint32_t)is[IS_UWR * C + c];
+  int inv_i = is[IS_UWI_INV * C + c], inv_r = is[IS_UWR_INV * C + c];
+  int frameinfo = is[IS_FRAMEINFO * C + c], lastframeinfo = is[IS_LASTFRAMEINFO * C + c];
+  int formatid = is[IS_FORMATID * C + c], datacd = is[IS_DATACD * C + c];
+  int scr_pos = is[IS_SCR_POS * C + c], blkbuf = is[IS_BLKBUF * C + c];
+  int has_ov = is[IS_HAS_OVERLAP * C + c];
+  int isu_reset = is[IS_DATACDCD * C + c];  // pending isudata.reset() for the next job
+  const uint8_t *soft = S.soft + (size_t)c * SOFT_RING;
+  const int NumberOfBits = 4992, BitsInHeader = 194, Total = 5250;
+
+  for (; q < E; ++q) {
+    const int sv = soft[q & (SOFT_RING - 1)];
+    int bit = sv >= 128 ? 1 : 0;
+    int soft_bit = sv;
+    int gotsync;
+    realimag++;
+    realimag %= 2;
+    const bool search = (cntr > NumberOfBits - 68 || cntr <= 0 || !datacd);
+    if (search) {
+      // PreambleDetectorPhaseInvariant::Update, tolerance 0 (aerol.cpp:757-777)
+      uint32_t &reg = realimag ? uwi : uwr;
+      int &inv = realimag ? inv_i : inv_r;
+      reg = (reg << 1) | (uint32_t)bit;
+      const int xorsum = __builtin_popcount(reg ^ UW);
+      int g = 0;
+      if (xorsum >= 32) {
+        inv = 1;
+        g = 1;
+      } else if (xorsum <= 0) {
+        inv = 0;
+        g = 1;
+      }
+      gotsync = g;
+      if (!gsl) {
+        gsl = gotsync;
+        gotsync = 0;
+      } else
+        gsl = 0;
+    } else {
+      gotsync = 0;
+      gsl = 0;
+    }
+    if (realimag ? inv_i : inv_r) {
+      bit = 1 - bit;
+      if (soft_bit != 128) soft_bit = 255 - soft_bit;
+    }
+    if (cntr < 1000000000) cntr++;
+    if (cntr < 16) {
+      if (cntr == 0)
+        frameinfo = bit;
+      else
+        frameinfo = ((frameinfo << 1) | bit) & 0xFFFF;
+    }
+    if (cntr == 15) {
+      const int tval = frameinfo;
+      frameinfo = lastframeinfo;
+      lastframeinfo = tval;
+      formatid = (frameinfo >> 12) & 0x000F;
+    }
+    if (cntr >= 16) {
+      int idx = (cntr - BitsInHeader) % BLOCK;
+      if (idx < 0) idx = 0;
+      uint8_t *blk = S.block + ((size_t)c * 2 + blkbuf) * BLOCK;
+      blk[idx] = (uint8_t)soft_bit;
+      if (idx == BLOCK - 1) {
+        const int j = atomicAdd(S.njobs, 1);
+        int4 *jobs = reinterpret_cast<int4 *>(S.jobs);
+        jobs[j] = make_int4(c, blkbuf | ((has_ov ? 0 : 1) << 1) | (isu_reset << 2), scr_pos,
+                            ((cntr - BitsInHeader) == (NumberOfBits - 1) ? 0x100 : 0) | formatid);
+        isu_reset = 0;
+        scr_pos += has_ov ? 2496 : 2483;
+        has_ov = 1;
+        blkbuf ^= 1;
+      }
+    }
+    if (gotsync) {
+      if (cntr + 1 != Total) isu_reset = 1;
+      cntr = -1;
+      datacd = 1;
+      scr_pos = 0;
+    }
+    if (cntr + 1 == Total) {
+      scr_pos = 0;
+      cntr = -1;
+    }
+  }
+  ls[LS_SOFT_C * C + c] = q;
+  is[IS_RI * C + c] = realimag;
+  is[IS_CNTR * C + c] = cntr;
+  is[IS_GSL * C + c] = gsl;
+  is[IS_UWI * C + c] = (int)uwi;
+  is[IS_UWR * C + c] = (int)uwr;
+  is[IS_UWI_INV * C + c] = inv_i;
+  is[IS_UWR_INV * C + c] = inv_r;
+  is[IS_FRAMEINFO * C + c] = frameinfo;
+  is[IS_LASTFRAMEINFO * C + c] = lastframeinfo;
+  is[IS_FORMATID * C + c] = formatid;
+  is[IS_DATACD * C + c] = datacd;
+  is[IS_SCR_POS * C + c] = scr_pos;
+  is[IS_BLKBUF * C + c] = blkbuf;
+  is[IS_HAS_OVERLAP * C + c] = has_ov;
+  is[IS_DATACDCD * C + c] = isu_reset;
+}
+
+// ---------------------------------------------------------------- Viterbi
+__device__ __forceinline__ int conv_table(int r) {  // table[r]: bit j = parity(r & poly[j])
+  return (__builtin_popcount(r & 109) & 1) | ((__builtin_popcount(r & 79) & 1) << 1);
+}
+
+__device__ __forceinline__ int soft_dist(int hard, int a, int b) {  // metric_soft_distance_linear
+  const int x0 = (hard & 1) ? 255 : 0, x1 = (hard & 2) ? 255 : 0;
+  const int d0 = a - x0, d1 = b - x1;
+  return (d0 < 0 ? -d0 : d0) + (d1 < 0 ? -d1 : d1);
+}
+
+__device__ __forceinline__ int shfl_idx(int v, int src) {
+  return __builtin_amdgcn_ds_bpermute(src << 2, v);
+}
+
+constexpr int HCAP = 140, MINTB = 35, RENORM = 128;
+
+__global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, int trace) {
+  __shared__ uint8_t sbuf[VIT_MAX + 2];
+  __shared__ unsigned long long hist[HCAP];
+  __shared__ uint8_t obits[2560];
+  __shared__ uint8_t dl[2496];
+  __shared__ uint8_t info[320];
+  const int job = blockIdx.x;
+  if (job >= *S.njobs) return;
+  const int lane = threadIdx.x;
+  const int4 jd = reinterpret_cast<const int4 *>(S.jobs)[job];
+  const int c = jd.x, buf = jd.y & 1, first = (jd.y >> 1) & 1, reset = (jd.y >> 2) & 1;
+  const int scr_pos = jd.z, formatid = jd.w & 0xFF, frame_done = (jd.w >> 8) & 1;
+  const int C = S.C;
+  const int ov = first ? 0 : 62;
+  const int nsoft = ov + BLOCK + 24;
+  // load: overlap + deinterleaved block + 24 erasures
+  if (!first && lane < 62) sbuf[lane] = S.overlap[(size_t)c * 64 + lane];
+  {
+    const uint8_t *blk = S.block + ((size_t)c * 2 + buf) * BLOCK;
+    const int row = (lane * 27) % 64;  // interleaverowdepermute[lane]
+    for (int j = 0; j < 78; ++j) sbuf[ov + j * 64 + lane] = blk[row * 78 + j];
+  }
+  if (lane < 24) sbuf[ov + BLOCK + lane] = 128;
+  for (int k = lane; k < 2560; k += 64) obits[k] = 0;
+  __syncthreads();
+  // keep the last 62 deinterleaved soft values for the next block
+  if (lane < 62) S.overlap[(size_t)c * 64 + lane] = sbuf[ov + BLOCK - 62 + lane];
+
+  const int sets = nsoft / 2;
+  const int s = lane;
+  const int tab_lo = conv_table(s), tab_hi = conv_table(s | 64);
+  int m = 0;  // uint16 path metric of state s
+  // warmup (decode.c convolutional_decode_warmup): states reachable from 0
+  for (int i = 0; i < 6 && i < sets; ++i) {
+    const int a = sbuf[2 * i], b = sbuf[2 * i + 1];
+    const int prev = shfl_idx(m, s >> 1);
+    if (s < (2 << i)) m = (soft_dist(conv_table(s), a, b) + prev) & 0xFFFF;
+  }
+  int index = 0, len = 0, renorm = 0, outpos = 0;
+  auto search = [&](int skip) -> int {
+    // least metric among states s % skip == 0, lowest index on ties
+    int key = (s % skip == 0) ? ((m << 6) | s) : 0x7FFFFFFF;
+    for (int off = 32; off > 0; off >>= 1) {
+      const int o = __shfl_xor(key, off, 64);
+      key = o < key ? o : key;
+    }
+    return key & 63;
+  };
+  auto traceback = [&](int bestpath, int mintb) {
+    const int nout = len - mintb;
+    if (lane == 0) {
+      int idx = index;
+      for (int j = 0; j < len; ++j) {
+        idx = idx == 0 ? HCAP - 1 : idx - 1;
+        const int hb = (int)((hist[idx] >> bestpath) & 1ULL);
+        bestpath = (bestpath | (hb << 6)) >> 1;
+        if (j >= mintb) obits[outpos + (nout - 1 - (j - mintb))] = (uint8_t)hb;
+      }
+    }
+    outpos += nout;
+    len -= nout;
+    __syncthreads();
+  };
+  auto process = [&](int skip) {
+    index++;
+    if (index == HCAP) index = 0;
+    renorm++;
+    len++;
+    if (renorm == RENORM) {
+      renorm = 0;
+      const int best = search(skip);
+      const int mind = shfl_idx(m, best);
+      m = (m - mind) & 0xFFFF;
+      if (len == HCAP) traceback(best, MINTB);
+    } else if (len == HCAP) {
+      traceback(search(skip), MINTB);
+    }
+  };
+  for (int i = 6; i < sets; ++i) {
+    const int a = sbuf[2 * i], b = sbuf[2 * i + 1];
+    const bool tail = i >= sets - 6;
+    const int skip = tail ? (1 << (7 - (sets - i))) : 1;
+    const int m0 = shfl_idx(m, s >> 1), m1 = shfl_idx(m, (s >> 1) | 32);
+    const int e0 = (m0 + soft_dist(tab_lo, a, b)) & 0xFFFF;
+    const int e1 = (m1 + soft_dist(tab_hi, a, b)) & 0xFFFF;
+    const bool act = (s % skip) == 0;
+    const int h = (e0 <= e1) ? 0 : 1;
+    if (act) m = h ? e1 : e0;
+    const unsigned long long mask = __ballot(act && h);
+    if (lane == 0) hist[index] = mask;
+    __syncthreads();
+    process(skip);
+  }
+  traceback(0, 0);
+  // Decode_Continuous: keep decoded bits [25, 25 + 2496) clipped to size/2
+  const int nbits = (sets - 25) < 2496 ? (sets - 25) : 2496;
+  if (trace) {
+    uint8_t *dbg = S.blocks_dbg + (size_t)c * 2500;
+    if (lane == 0) *reinterpret_cast<int *>(dbg) = nbits;
+    for (int k = lane; k < nbits; k += 64) dbg[4 + k] = obits[25 + k];
+  }
+  // DelayLine dl2 (aerol.h:464-471): out[q] = old[(p+q+1)%L], new[(p+q)%L] = in[q]
+  uint8_t *dlg = S.dl2 + (size_t)c * DL2_LEN;
+  const int p0 = S.is[IS_DL2_PTR * C + c];
+  for (int k = lane; k < nbits; k += 64) {
+    int r = p0 + k + 1;
+    r = r >= DL2_LEN ? r - DL2_LEN : r;
+    dl[k] = dlg[r];
+  }
+  __syncthreads();
+  for (int k = lane; k < nbits; k += 64) {
+    int w = p0 + k;
+    w = w >= DL2_LEN ? w - DL2_LEN : w;
+    dlg[w] = obits[25 + k];
+  }
+  if (lane == 0) S.is[IS_DL2_PTR * C + c] = (p0 + nbits) % DL2_LEN;
+  // scrambler + LSB-first packing (aerol.cpp:1506-1520)
+  const int nbytes = nbits / 8;
+  for (int b = lane; b < nbytes; b += 64) {
+    int v = 0;
+    for (int i = 0; i < 8; ++i) v |= ((dl[8 * b + i] ^ T.scr[scr_pos + 8 * b + i]) & 1) << i;
+    info[b] = (uint8_t)v;
+  }
+  for (int b = nbytes + lane; b < 312; b += 64) info[b] = 0;
+  __syncthreads();
+  // per-SU CRC (aerol.cpp:1531-1543)
+  const int nsu = nbytes / 12;
+  bool ok = false;
+  if (lane < nsu && frame_done) {
+    const uint8_t *su = info + 12 * lane;
+    unsigned crc = 0xFFFF, sum = 0;
+    for (int i = 0; i < 10; ++i) {
+      unsigned mb = su[i];
+      sum += mb;
+      for (int k = 0; k < 8; ++k) {
+        const unsigned bit = mb & 1;
+        mb >>= 1;
+        const unsigned cb = crc & 1;
+        crc >>= 1;
+        if (cb ^ bit) crc ^= 0x8408;
+      }
+    }
+    unsigned calc = (~crc) & 0xFFFF;
+    const unsigned rec = ((unsigned)su[11] << 8) | su[10];
+    if (!rec && calc != rec && sum == 0) calc = 0;
+    ok = calc == rec;
+  }
+  const unsigned long long okm = __ballot(ok);
+  uint8_t *out = S.jobout + (size_t)job * JOB_OUT;
+  for (int b = lane; b < 312; b += 64) out[b] = info[b];
+  if (lane == 0) {
+    int *o = reinterpret_cast<int *>(out + 312);
+    o[0] = frame_done ? nbytes : -1;
+    o[1] = (int)(okm & 0x3FFFFFFULL);
+    o[2] = formatid;
+    o[3] = c | (reset << 30);
+  }
+}
+
+void launch_frame(hipStream_t st, const DevState &S, int nch) {
+  hipLaunchKernelGGL(frame_kernel, dim3((nch + 255) / 256), dim3(256), 0, st, S, nch);
+}
+
+void launch_viterbi(hipStream_t st, const DevState &S, const DevTables &T, int max_jobs, int trace) {
+  if (max_jobs > 0) hipLaunchKernelGGL(viterbi_kernel, dim3(max_jobs), dim3(64), 0, st, S, T, trace);
+}
+
+}  // namespace aero

@@ -1,0 +1,423 @@
+/*
+ * demod_oqpsk.hip — batched continuous 10500-bps OQPSK demodulator for
+ * gfx950.  One VFO channel per lane; a channel's per-sample recurrence
+ * (OqpskDemodulator::writeData, decode/oqpskdemodulator.cpp:284-560) runs
+ * sequentially in its lane, thousands of channels run side by side.
+ *
+ * Bit-exactness rules: built with -ffp-contract=off; every
+ * expression keeps the reference's operation order; std::complex products
+ * are expanded as GCC does ((ac-bd), (ad+bc)); libm calls go to aero_math.h.
+ *
+ * Lane pairs: lanes 2c and 2c+1 both run channel c.  The even lane keeps
+ * the real-part partial sums of the 55-tap RRC, the odd lane the imaginary
+ * part (110 doubles would not fit beside the rest of the state in gfx950's
+ * 256 architected VGPRs); the filter outputs are swapped through DPP and the
+ * remaining recurrence runs identically in both lanes (same values, no
+ * divergence inside a pair).  Only the even lane stores shared state.
+ *
+ * Segment contract: a launch advances every channel from nsamp up to (but
+ * excluding) its next coarse-estimate hop sample, or to the pushed end; it
+ * also writes the coarse-ring entry of the sample after each processed one
+ * (ring fill precedes the hop that uses it, oqpskdemodulator.cpp:351-369).
+ */
+#include <hip/hip_runtime.h>
+
+#include "aero_math.h"
+#include "engine_common.h"
+
+namespace aero {
+
+__constant__ double c_taps[NTAPS];
+__constant__ DelayDesc c_dly[4];  // delays(1), delayt41(T/4), delayt42(T/4), delayt8(T/8)
+__constant__ double c_sr_b[3];    // st resonator (oqpskdemodulator.cpp:218-223)
+__constant__ double c_sr_a[3];
+__constant__ double c_ct_b[3];    // carrier loop filter (oqpskdemodulator.cpp:92-99)
+__constant__ double c_ct_a[3];
+
+__device__ __forceinline__ int cis_index(double WTptr) {  // WaveTable::WTCISValue (DSP.cpp:81-88)
+  int tint = (int)WTptr;
+  if (tint >= WTSIZE) tint = 0;
+  if (tint < 0) tint = WTSIZE - 1;
+  return tint;
+}
+
+__device__ __forceinline__ void nco_next(double &ptr, double &step) {  // WTnextFrame (DSP.cpp:71-79)
+  if (step < 0) step = 0;
+  ptr += step;
+  while (((int)ptr) >= WTSIZE) ptr -= WTSIZE;
+}
+
+__device__ __forceinline__ void set_freq(double &freq, double &step, double f) {  // SetFreq (DSP.cpp:163-168)
+  freq = f;
+  if (freq < 0) freq = 0;
+  step = (freq) * ((double)WTSIZE) / 48000.0;
+}
+
+// Delay<double>::update (DSP.h:365-384) as a shift register; the reference's
+// ring index and fractional weight depend only on the write pointer p.
+template <int N>
+__device__ __forceinline__ double delay_update(double (&h)[N], int &p, const DelayDesc &d, double sig) {
+#pragma unroll
+  for (int i = N - 1; i > 0; --i) h[i] = h[i - 1];
+  h[0] = sig;
+  const double w = d.w[p], omw = d.omw[p];  // per-pointer weights, loaded each call
+  double older = h[0], newer = h[0];
+#pragma unroll
+  for (int a = 0; a < N; ++a) {
+    if (a == d.age_old) older = h[a];
+    if (a == d.age_new) newer = h[a];
+  }
+  p = (p + 1 == N) ? 0 : p + 1;
+  return (w * newer + omw * older);
+}
+
+// IIR::update with 3 b / 3 a coefficients (DSP.cpp:635-685), a[0] == 1
+__device__ __forceinline__ double iir3(double &x1, double &x2, double &y1, double &y2, const double *b,
+                                       const double *a, double sig) {
+  double y = 0;
+  y += x2 * b[2];
+  y += x1 * b[1];
+  y += sig * b[0];
+  y -= y2 * a[2];
+  y -= y1 * a[1];
+  x2 = x1;
+  x1 = sig;
+  y2 = y1;
+  y1 = y;
+  return y;
+}
+
+__device__ __forceinline__ int qround(double d) {  // qRound (Qt 5.9 qglobal.h:525)
+  return d >= 0.0 ? int(d + 0.5) : int(d - double(int(d - 1)) + 0.5) + int(d - 1);
+}
+
+template <bool TRACE>
+__global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables T, int nch, int flush) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = tid >> 1;
+  const int part = tid & 1;
+  const bool lead = part == 0;
+  if (c >= nch) return;  // nch channels -> 2 nch lanes; pairs never straddle the check
+  const int C = S.C;
+  double *ds = S.ds;
+  int *is = S.is;
+  long long *ls = S.ls;
+
+  long long n = ls[LS_NSAMP * C + c];
+  const long long avail = ls[LS_AVAIL * C + c];
+  long long filled = ls[LS_FILLED * C + c];
+  const int hops_done = is[IS_HOPS_DONE * C + c];
+  const long long boundary = (long long)HOP * (hops_done + 1) - 1;
+  long long end = avail < boundary ? avail : boundary;
+  if (!flush && avail <= boundary) end = n;  // wait for a whole segment + the hop's ring entry
+  const long long capm = S.pcm_cap - 1;
+  uint32_t *cring = S.cring + (size_t)c * NFFT;
+
+  double mc_ptr = ds[DS_MC_PTR * C + c], mc_step = ds[DS_MC_STEP * C + c];
+  // coarse-ring catch-up (entry of sample n not yet written)
+  if (filled == n && n < avail) {
+    const int16_t x = S.pcm[(n & capm) * C + c];
+    if (lead) cring[n & (NFFT - 1)] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
+    filled = n + 1;
+  }
+  if (n >= end) {
+    if (lead) ls[LS_FILLED * C + c] = filled;
+    return;
+  }
+
+  double m2_ptr = ds[DS_M2_PTR * C + c], m2_step = ds[DS_M2_STEP * C + c], m2_freq = ds[DS_M2_FREQ * C + c];
+  double so_ptr = ds[DS_SO_PTR * C + c], so_last = ds[DS_SO_LAST * C + c];
+  double so_step = ds[DS_SO_STEP * C + c], so_freq = ds[DS_SO_FREQ * C + c];
+  double agc_sum = ds[DS_AGC_SUM * C + c];
+  double d1[2] = {ds[DS_D1_0 * C + c], ds[DS_D1_1 * C + c]};
+  double d41[4] = {ds[DS_D41_0 * C + c], ds[DS_D41_1 * C + c], ds[DS_D41_2 * C + c], ds[DS_D41_3 * C + c]};
+  double d42[4] = {ds[DS_D42_0 * C + c], ds[DS_D42_1 * C + c], ds[DS_D42_2 * C + c], ds[DS_D42_3 * C + c]};
+  double d8[3] = {ds[DS_D8_0 * C + c], ds[DS_D8_1 * C + c], ds[DS_D8_2 * C + c]};
+  double srx1 = ds[DS_SR_X1 * C + c], srx2 = ds[DS_SR_X2 * C + c];
+  double sry1 = ds[DS_SR_Y1 * C + c], sry2 = ds[DS_SR_Y2 * C + c];
+  double ctx1 = ds[DS_CT_X1 * C + c], ctx2 = ds[DS_CT_X2 * C + c];
+  double cty1 = ds[DS_CT_Y1 * C + c], cty2 = ds[DS_CT_Y2 * C + c];
+  double marg_sum = ds[DS_MARG_SUM * C + c], pm_sum = ds[DS_PM_SUM * C + c], ms_sum = ds[DS_MS_SUM * C + c];
+  double mse = ds[DS_MSE * C + c];
+  double ptd_re = ds[DS_PTD_RE * C + c], ptd_im = ds[DS_PTD_IM * C + c];
+  double s2l_re = ds[DS_S2L_RE * C + c], s2l_im = ds[DS_S2L_IM * C + c];
+  int agc_ptr = is[IS_AGC_PTR * C + c];
+  int p1 = is[IS_D1_P * C + c], p41 = is[IS_D41_P * C + c], p42 = is[IS_D42_P * C + c], p8 = is[IS_D8_P * C + c];
+  int marg_p = is[IS_MARG_P * C + c], dt_p = is[IS_DT_P * C + c];
+  int pm_p = is[IS_PM_P * C + c], ms_p = is[IS_MS_P * C + c];
+  int yui = is[IS_YUI * C + c], s2l_init = is[IS_S2L_INIT * C + c];
+  long long softp = ls[LS_SOFT_P * C + c];
+  long long ptn = TRACE ? ls[LS_PT_N * C + c] : 0;
+
+  // this lane's half of the transposed RRC: R_j(n-1), j = 0..54
+  double q[NTAPS];
+#pragma unroll
+  for (int j = 0; j < NTAPS; ++j) q[j] = S.fir[(size_t)(part * NTAPS + j) * C + c];
+
+  double *marg = S.marg + (size_t)c * MARG_LEN;
+  double2 *dtb = S.dt + (size_t)c * DT_LEN;
+  double *pmb = S.pm + (size_t)c * MSE_LEN;
+  double *msb = S.ms + (size_t)c * MSE_LEN;
+  uint8_t *soft = S.soft + (size_t)c * SOFT_RING;
+  const double PT = 0.4 * WTSIZE;  // IfHavePassedPoint(ee) with ee = 0.4 (oqpskdemodulator.cpp:225)
+
+  for (; n < end; ++n) {
+    const int16_t xs = S.pcm[(n & capm) * C + c];
+    const double dval = ((double)xs) / 32768.0;
+    // mix (oqpskdemodulator.cpp:390): this lane's component of cval
+    const double2 cm = T.cis[cis_index(m2_ptr)];
+    const double cv = (part ? cm.y : cm.x) * dval;
+    // rrc (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
+    const double mine = q[NTAPS - 1];
+    // taps through a laundered scalar pointer: re-read (s_load) every sample
+    // instead of pinning 110 VGPRs of loop invariants
+    const double *tp = T.taps;
+    asm volatile("" : "+s"(tp));
+#pragma unroll
+    for (int j = NTAPS - 1; j >= 1; --j) q[j] = q[j - 1] + tp[j] * cv;
+    q[0] = 0.0 + tp[0] * cv;
+    const double other = __shfl_xor(mine, 1, 64);
+    double s2r = part ? other : mine, s2i = part ? mine : other;
+    // AGC (DSP.cpp:371-380) on |sig2| (oqpskdemodulator.cpp:399-405)
+    const double dab = sqrt(s2r * s2r + s2i * s2i);
+    {
+      double *slot = S.agc + (size_t)agc_ptr * C + c;
+      const double old = *slot;
+      agc_sum = agc_sum - old;
+      agc_sum = agc_sum + fabs(dab);
+      if (lead) *slot = fabs(dab);
+      agc_ptr++;
+      if (agc_ptr == AGC_LEN) agc_ptr = 0;
+      double g = 1.414213562 / fmax(agc_sum / ((double)AGC_LEN), 0.000001);
+      g = fmax(g, 0.000001);
+      s2r *= g;
+      s2i *= g;
+    }
+    // clipping (:408-410)
+    const double ab = aero_hypot(s2r, s2i);
+    if (ab > 2.84) {
+      const double k = 2.84 / ab;
+      s2r = k * s2r;
+      s2i = k * s2i;
+    }
+    // symbol timer (:413-426)
+    const double st_diff = delay_update(d1, p1, c_dly[0], ab * ab) - (ab * ab);
+    const double st_d1out = delay_update(d41, p41, c_dly[1], st_diff);
+    const double st_d2out = delay_update(d42, p42, c_dly[2], st_d1out);
+    double st_eta = (st_d2out - st_diff) * st_d1out;
+    st_eta = iir3(srx1, srx2, sry1, sry2, c_sr_b, c_sr_a, st_eta);
+    const double m1r = st_eta, m1i = -delay_update(d8, p8, c_dly[3], st_eta);
+    const double2 so = T.cis[cis_index(so_ptr)];
+    const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
+    const double st_angle_error = aero_atan2(oim, ore);
+    set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
+    so_ptr += (-st_angle_error * 0.01 / 360.0) * WTSIZE;
+    while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
+    while (so_ptr < 0) so_ptr += WTSIZE;
+    if (so_freq < (10500.0 - 0.1)) set_freq(so_freq, so_step, (10500.0 - 0.1));
+    if (so_freq > (10500.0 + 0.1)) set_freq(so_freq, so_step, (10500.0 + 0.1));
+    if (!s2l_init) {
+      s2l_re = s2r;
+      s2l_im = s2i;
+      s2l_init = 1;
+    }
+    // sample instant (:430) IfHavePassedPoint (DSP.cpp:222-238)
+    double tl = so_last - PT, tw = so_ptr - PT;
+    if (tl < 0.0) tl += WTSIZE;
+    if (tw < 0.0) tw += WTSIZE;
+    if ((tl > 3.0 * WTSIZE / 4.0) && (tw < 1.0 * WTSIZE / 4.0)) {
+      const double pt_last = tw / so_step;
+      const double pt_this = 1.0 - pt_last;
+      const double pr = pt_this * s2r + pt_last * s2l_re;
+      const double pi = pt_this * s2i + pt_last * s2l_im;
+      yui++;
+      yui %= 2;
+      if (!yui) {
+        ptd_re = pr;
+        ptd_im = pi;
+      } else {
+        double qr = pr, qi = ptd_im;  // pt_qpsk
+        // carrier tracking (:456-470); the two tanh split across the pair
+        const double th = aero_tanh(part ? ptd_re : pi);
+        const double tho = __shfl_xor(th, 1, 64);
+        const double ct_xt = (part ? tho : th) * pr;
+        const double ct_xt_d = (part ? th : tho) * ptd_im;
+        double ct_ec = ct_xt_d - ct_xt;
+        if (ct_ec > M_PI) ct_ec = M_PI;
+        if (ct_ec < -M_PI) ct_ec = -M_PI;
+        ct_ec = iir3(ctx1, ctx2, cty1, cty2, c_ct_b, c_ct_a, ct_ec);
+        if (ct_ec > M_PI_2) ct_ec = M_PI_2;
+        if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
+        {  // mixer2.IncresePhaseDeg / SetPhaseDeg (DSP.cpp:177-187)
+          double phase_deg = 1.0 * ct_ec;
+          phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
+          phase_deg = fmod(phase_deg, 360.0);
+          while (phase_deg < 0) phase_deg += 360.0;
+          m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+        }
+        set_freq(m2_freq, m2_step, 0.01 * ct_ec + m2_freq);  // IncreseFreqHz
+        // marg->UpdateSigned (DSP.cpp:419-427)
+        marg_sum = marg_sum - marg[marg_p];
+        marg_sum = marg_sum + (ct_ec);
+        if (lead) marg[marg_p] = ct_ec;
+        marg_p++;
+        marg_p %= MARG_LEN;
+        const double mval = marg_sum / ((double)MARG_LEN);
+        // dt.update (DSP.h:456-461): slot p written, slot p+1 read
+        {
+          const int rp = (dt_p + 1) % DT_LEN;
+          const double2 dv = dtb[rp];
+          if (lead) dtb[dt_p] = make_double2(qr, qi);
+          dt_p = rp;
+          qr = dv.x;
+          qi = dv.y;
+        }
+        double rs, rc;
+        aero_sincos(mval, rs, rc);
+        const double rr = qr * rc - qi * rs, ri = qr * rs + qi * rc;
+        qr = rr;
+        qi = ri;
+        if (TRACE) {
+          if (lead && ptn < S.pt_cap) S.pt[(size_t)c * S.pt_cap + ptn] = make_double2(qr, qi);
+          ptn++;
+        }
+        // MSEcalc::Update (DSP.cpp:449-461)
+        {
+          const double av = aero_hypot(qr, qi);
+          pm_sum = pm_sum - pmb[pm_p];
+          pm_sum = pm_sum + fabs(av);
+          if (lead) pmb[pm_p] = fabs(av);
+          pm_p++;
+          pm_p %= MSE_LEN;
+          double mu = pm_sum / ((double)MSE_LEN);
+          if (mu < 0.000001) mu = 0.000001;
+          const double tr = (1.4142135623730951 * qr) / mu, ti = (1.4142135623730951 * qi) / mu;
+          const double tda = (fabs(tr) - 1.0), tdb = (fabs(ti) - 1.0);
+          const double v = (tda * tda) + (tdb * tdb);
+          ms_sum = ms_sum - msb[ms_p];
+          ms_sum = ms_sum + fabs(v);
+          if (lead) msb[ms_p] = fabs(v);
+          ms_p++;
+          ms_p %= MSE_LEN;
+          mse = ms_sum / ((double)MSE_LEN);
+        }
+        if (mse < 0.65) {  // soft bits, imag first (:516-530)
+          int ibit = qround(0.75 * qi * 127.0 + 128.0);
+          if (ibit > 255) ibit = 255;
+          if (ibit < 0) ibit = 0;
+          int rbit = qround(0.75 * qr * 127.0 + 128.0);
+          if (rbit > 255) rbit = 255;
+          if (rbit < 0) rbit = 0;
+          if (lead) {
+            soft[softp & (SOFT_RING - 1)] = (uint8_t)ibit;
+            soft[(softp + 1) & (SOFT_RING - 1)] = (uint8_t)rbit;
+          }
+          softp += 2;
+        }
+      }
+    }
+    s2l_re = s2r;
+    s2l_im = s2i;
+    nco_next(m2_ptr, m2_step);
+    nco_next(mc_ptr, mc_step);
+    so_last = so_ptr;
+    nco_next(so_ptr, so_step);
+    // coarse-ring fill of the next sample (:351-356)
+    if (n + 1 < avail) {
+      const int16_t xn = S.pcm[((n + 1) & capm) * C + c];
+      if (lead) cring[(n + 1) & (NFFT - 1)] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)xn << 16);
+      filled = n + 2;
+    }
+  }
+
+  // epilogue addresses are recomputed from a laundered channel index so the
+  // compiler cannot keep ~110 prologue addresses live across the sample loop
+  int cl = c;
+  asm volatile("" : "+v"(cl));
+  {
+    double *fir = S.fir + (size_t)part * NTAPS * C + cl;
+#pragma unroll
+    for (int j = 0; j < NTAPS; ++j) fir[(size_t)j * C] = q[j];
+  }
+  if (!lead) return;
+  ds = S.ds + cl;
+  is = S.is + cl;
+  ls = S.ls + cl;
+  const int c0 = 0;
+#define c c0
+  ls[LS_NSAMP * C + c] = n;
+  ls[LS_FILLED * C + c] = filled;
+  ls[LS_SOFT_P * C + c] = softp;
+  if (TRACE) ls[LS_PT_N * C + c] = ptn;
+  ds[DS_M2_PTR * C + c] = m2_ptr;
+  ds[DS_M2_STEP * C + c] = m2_step;
+  ds[DS_M2_FREQ * C + c] = m2_freq;
+  ds[DS_MC_PTR * C + c] = mc_ptr;
+  ds[DS_MC_STEP * C + c] = mc_step;
+  ds[DS_SO_PTR * C + c] = so_ptr;
+  ds[DS_SO_LAST * C + c] = so_last;
+  ds[DS_SO_STEP * C + c] = so_step;
+  ds[DS_SO_FREQ * C + c] = so_freq;
+  ds[DS_AGC_SUM * C + c] = agc_sum;
+  ds[DS_D1_0 * C + c] = d1[0];
+  ds[DS_D1_1 * C + c] = d1[1];
+  ds[DS_D41_0 * C + c] = d41[0];
+  ds[DS_D41_1 * C + c] = d41[1];
+  ds[DS_D41_2 * C + c] = d41[2];
+  ds[DS_D41_3 * C + c] = d41[3];
+  ds[DS_D42_0 * C + c] = d42[0];
+  ds[DS_D42_1 * C + c] = d42[1];
+  ds[DS_D42_2 * C + c] = d42[2];
+  ds[DS_D42_3 * C + c] = d42[3];
+  ds[DS_D8_0 * C + c] = d8[0];
+  ds[DS_D8_1 * C + c] = d8[1];
+  ds[DS_D8_2 * C + c] = d8[2];
+  ds[DS_SR_X1 * C + c] = srx1;
+  ds[DS_SR_X2 * C + c] = srx2;
+  ds[DS_SR_Y1 * C + c] = sry1;
+  ds[DS_SR_Y2 * C + c] = sry2;
+  ds[DS_CT_X1 * C + c] = ctx1;
+  ds[DS_CT_X2 * C + c] = ctx2;
+  ds[DS_CT_Y1 * C + c] = cty1;
+  ds[DS_CT_Y2 * C + c] = cty2;
+  ds[DS_MARG_SUM * C + c] = marg_sum;
+  ds[DS_PM_SUM * C + c] = pm_sum;
+  ds[DS_MS_SUM * C + c] = ms_sum;
+  ds[DS_MSE * C + c] = mse;
+  ds[DS_PTD_RE * C + c] = ptd_re;
+  ds[DS_PTD_IM * C + c] = ptd_im;
+  ds[DS_S2L_RE * C + c] = s2l_re;
+  ds[DS_S2L_IM * C + c] = s2l_im;
+  is[IS_AGC_PTR * C + c] = agc_ptr;
+  is[IS_D1_P * C + c] = p1;
+  is[IS_D41_P * C + c] = p41;
+  is[IS_D42_P * C + c] = p42;
+  is[IS_D8_P * C + c] = p8;
+  is[IS_MARG_P * C + c] = marg_p;
+  is[IS_DT_P * C + c] = dt_p;
+  is[IS_PM_P * C + c] = pm_p;
+  is[IS_MS_P * C + c] = ms_p;
+  is[IS_YUI * C + c] = yui;
+  is[IS_S2L_INIT * C + c] = s2l_init;
+}
+
+#undef c
+void launch_demod(hipStream_t st, const DevState &S, const DevTables &T, int nch, int flush, bool trace) {
+  dim3 grid((2 * nch + 255) / 256), block(256);
+  if (trace)
+    hipLaunchKernelGGL(demod_oqpsk_kernel<true>, grid, block, 0, st, S, T, nch, flush);
+  else
+    hipLaunchKernelGGL(demod_oqpsk_kernel<false>, grid, block, 0, st, S, T, nch, flush);
+}
+
+void upload_demod_constants(const double *taps, const DelayDesc *dly, const double *sr_b, const double *sr_a,
+                            const double *ct_b, const double *ct_a) {
+  hipMemcpyToSymbol(HIP_SYMBOL(c_taps), taps, sizeof(double) * NTAPS);
+  hipMemcpyToSymbol(HIP_SYMBOL(c_dly), dly, sizeof(DelayDesc) * 4);
+  hipMemcpyToSymbol(HIP_SYMBOL(c_sr_b), sr_b, sizeof(double) * 3);
+  hipMemcpyToSymbol(HIP_SYMBOL(c_sr_a), sr_a, sizeof(double) * 3);
+  hipMemcpyToSymbol(HIP_SYMBOL(c_ct_b), ct_b, sizeof(double) * 3);
+  hipMemcpyToSymbol(HIP_SYMBOL(c_ct_a), ct_a, sizeof(double) * 3);
+}
+
+}  // namespace aero

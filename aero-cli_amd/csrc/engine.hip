@@ -1,0 +1,625 @@
+/*
+ * engine.hip — host side of the Aero engine: the C ABI of
+ * include/aero_engine.h, device allocation, host-computed tables (the same
+ * glibc calls the reference makes: decode/DSP.cpp:10-33, decode/DSP.h:325-351,
+ * decode/jfft.cpp:13-67) and the per-run kernel schedule
+ *
+ *   [demod segment] -> [coarse hop + decision] -> [AeroL framing] -> [Viterbi+post]
+ *
+ * repeated until every channel has consumed its pushed samples up to a hop
+ * boundary (aero_run) or to the end (aero_flush).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/aero_engine.h"
+#include "acars_host.h"
+#include "aero_math.h"
+#include "engine_common.h"
+#include "tables_host.h"
+
+namespace aero {
+void launch_demod(hipStream_t, const DevState &, const DevTables &, int, int, bool);
+void upload_demod_constants(const double *, const DelayDesc *, const double *, const double *, const double *,
+                            const double *);
+void launch_coarse(hipStream_t, const DevState &, const DevTables &, int);
+void launch_frame(hipStream_t, const DevState &, int);
+void launch_viterbi(hipStream_t, const DevState &, const DevTables &, int, int);
+}  // namespace aero
+
+using namespace aero;
+
+namespace {
+
+constexpr long long PCM_CAP = 32768;
+constexpr int PT_CAP = 4096;
+constexpr int HOP_CAP = 64;
+
+#define HIPCHK(x)                                   \
+  do {                                              \
+    hipError_t err__ = (x);                         \
+    if (err__ != hipSuccess) {                      \
+      fprintf(stderr, "aero_engine: %s failed: %s\n", #x, hipGetErrorString(err__)); \
+      return AERO_E_HIP;                            \
+    }                                               \
+  } while (0)
+
+__global__ void pcm_scatter_kernel(int16_t *ring, int C, long long capm, const int16_t *src, long long n, long long ld,
+                                   int nch, int c0, long long start) {
+  // src time-major [n][ld]; channel c0 + j, j < nch; ring slot (start + t) & capm
+  const long long total = n * nch;
+  for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < total;
+       k += (long long)gridDim.x * blockDim.x) {
+    const long long t = k / nch;
+    const int j = (int)(k - t * nch);
+    ring[((start + t) & capm) * C + c0 + j] = src[t * ld + j];
+  }
+}
+
+__global__ void math_kernel(int fn, const double *x, const double *y, double *out, size_t n) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double a = x[i], b = y[i];
+  double r = 0;
+  switch (fn) {
+    case 0: r = aero_hypot(a, b); break;
+    case 1: r = aero_atan2(a, b); break;
+    case 2: r = aero_tanh(a); break;
+    case 3: r = aero_sin(a); break;
+    case 4: r = aero_cos(a); break;
+    case 5: r = aero_log10(a); break;
+    case 6: r = sqrt(a); break;
+    case 7: r = fmod(a, 360.0); break;
+    case 8: r = a / b; break;
+    default: break;
+  }
+  out[i] = r;
+}
+
+struct TimingSlot {
+  double ms = 0;
+  long launches = 0;
+};
+
+}  // namespace
+
+struct aero_engine {
+  int device = 0, flags = 0, C = 0, nch = 0;
+  hipStream_t st = nullptr;
+  DevState S{};
+  DevTables T{};
+  void *pool = nullptr;
+  size_t pool_bytes = 0;
+  std::vector<aero_channel_cfg> cfg;
+  // host mirrors of the per-channel counters
+  std::vector<long long> avail, nsamp, hops;
+  std::vector<std::unique_ptr<PChannelHost>> host;
+  std::vector<std::vector<int16_t>> soft_hold;
+  std::vector<std::vector<double>> hop_hold, pt_hold;
+  std::vector<std::vector<uint8_t>> blk_hold, frame_hold;
+  std::vector<long long> soft_seen;
+  // scratch
+  int16_t *d_scratch = nullptr;
+  size_t scratch_cap = 0;
+  std::vector<uint8_t> h_jobout;
+  std::map<std::string, TimingSlot> timing;
+  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending_ev;
+  uint64_t processed = 0;
+};
+
+namespace {
+
+template <class T>
+T *carve(char *&p, size_t count) {
+  T *r = reinterpret_cast<T *>(p);
+  size_t b = (count * sizeof(T) + 255) & ~size_t(255);
+  p += b;
+  return r;
+}
+
+size_t layout(DevState &S, DevTables &T, int C, int flags, char *base) {
+  char *p = base;
+  S.C = C;
+  S.ds = carve<double>(p, (size_t)DS_COUNT * C);
+  S.is = carve<int>(p, (size_t)IS_COUNT * C);
+  S.ls = carve<long long>(p, (size_t)LS_COUNT * C);
+  S.fir = carve<double>(p, (size_t)2 * NTAPS * C);
+  S.agc = carve<double>(p, (size_t)AGC_LEN * C);
+  S.marg = carve<double>(p, (size_t)MARG_LEN * C);
+  S.dt = carve<double2>(p, (size_t)DT_LEN * C);
+  S.pm = carve<double>(p, (size_t)MSE_LEN * C);
+  S.ms = carve<double>(p, (size_t)MSE_LEN * C);
+  S.pcm = carve<int16_t>(p, (size_t)PCM_CAP * C);
+  S.pcm_cap = PCM_CAP;
+  S.cring = carve<uint32_t>(p, (size_t)NFFT * C);
+  S.y = carve<double>(p, (size_t)Y_LEN * C);
+  S.soft = carve<uint8_t>(p, (size_t)SOFT_RING * C);
+  S.pt_cap = (flags & AERO_F_TRACE_PT) ? PT_CAP : 0;
+  S.pt = carve<double2>(p, (size_t)S.pt_cap * C);
+  S.hop_cap = HOP_CAP;
+  S.hops = carve<double>(p, (size_t)HOP_CAP * 6 * C);
+  S.hop_n = carve<int>(p, (size_t)C);
+  S.block = carve<uint8_t>(p, (size_t)2 * BLOCK * C);
+  S.overlap = carve<uint8_t>(p, (size_t)64 * C);
+  S.dl2 = carve<uint8_t>(p, (size_t)DL2_LEN * C);
+  S.jobs = carve<int>(p, (size_t)4 * C);
+  S.njobs = carve<int>(p, 1);
+  S.jobout = carve<uint8_t>(p, (size_t)JOB_OUT * C);
+  S.blocks_dbg = carve<uint8_t>(p, (flags & AERO_F_TRACE_BLOCKS) ? (size_t)2500 * C : 1);
+  T.cis = carve<double2>(p, WTSIZE);
+  T.tw = carve<double2>(p, NFFT);
+  T.twi = carve<double2>(p, NFFT);
+  T.scr = carve<uint8_t>(p, 5000);
+  T.taps = carve<double>(p, 64);
+  return (size_t)(p - base);
+}
+
+void ev_begin(aero_engine *e, const char *name, hipEvent_t &a, hipEvent_t &b) {
+  if (!(e->flags & AERO_F_TIMING)) return;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a, e->st);
+  e->pending_ev.push_back({name, {a, b}});
+}
+void ev_end(aero_engine *e, hipEvent_t b) {
+  if (!(e->flags & AERO_F_TIMING)) return;
+  hipEventRecord(b, e->st);
+}
+void ev_collect(aero_engine *e) {
+  for (auto &pe : e->pending_ev) {
+    float ms = 0;
+    hipEventSynchronize(pe.second.second);
+    hipEventElapsedTime(&ms, pe.second.first, pe.second.second);
+    auto &slot = e->timing[pe.first];
+    slot.ms += ms;
+    slot.launches++;
+    hipEventDestroy(pe.second.first);
+    hipEventDestroy(pe.second.second);
+  }
+  e->pending_ev.clear();
+}
+
+int init_channel_state(aero_engine *e, int c) {
+  // decode/oqpskdemodulator.cpp:9-115 + setSettings(:136-254) as Decoder applies it
+  const int C = e->C;
+  std::vector<double> ds(DS_COUNT, 0.0);
+  std::vector<int> is(IS_COUNT, 0);
+  std::vector<long long> ls(LS_COUNT, 0);
+  ds[DS_SO_FREQ] = 10500;
+  ds[DS_SO_STEP] = (10500.0) * ((double)WTSIZE) / ((float)48000);
+  ds[DS_MSE] = 100;
+  is[IS_COUNTDOWN2] = 5;
+  is[IS_COUNTDOWN] = 4;
+  is[IS_EMPTYCD] = 1;
+  is[IS_CNTR] = 1000000000;
+  for (int f = 0; f < DS_COUNT; f++) HIPCHK(hipMemcpy(e->S.ds + (size_t)f * C + c, &ds[f], 8, hipMemcpyHostToDevice));
+  for (int f = 0; f < IS_COUNT; f++) HIPCHK(hipMemcpy(e->S.is + (size_t)f * C + c, &is[f], 4, hipMemcpyHostToDevice));
+  for (int f = 0; f < LS_COUNT; f++) HIPCHK(hipMemcpy(e->S.ls + (size_t)f * C + c, &ls[f], 8, hipMemcpyHostToDevice));
+  return AERO_OK;
+}
+
+int collect_after_pass(aero_engine *e, int njobs) {
+  const int C = e->C, nch = e->nch;
+  if (njobs > 0) {
+    e->h_jobout.resize((size_t)njobs * JOB_OUT);
+    HIPCHK(hipMemcpyAsync(e->h_jobout.data(), e->S.jobout, (size_t)njobs * JOB_OUT, hipMemcpyDeviceToHost, e->st));
+    std::vector<uint8_t> dbg;
+    if (e->flags & AERO_F_TRACE_BLOCKS) {
+      dbg.resize((size_t)2500 * C);
+      HIPCHK(hipMemcpyAsync(dbg.data(), e->S.blocks_dbg, dbg.size(), hipMemcpyDeviceToHost, e->st));
+    }
+    HIPCHK(hipStreamSynchronize(e->st));
+    for (int j = 0; j < njobs; j++) {
+      const uint8_t *o = e->h_jobout.data() + (size_t)j * JOB_OUT;
+      int meta[4];
+      memcpy(meta, o + 312, 16);
+      const int c = meta[3] & 0x3FFFFFFF;
+      const int reset = (meta[3] >> 30) & 1;
+      if (c < 0 || c >= nch) continue;
+      if (e->flags & AERO_F_TRACE_BLOCKS) {
+        const uint8_t *d = dbg.data() + (size_t)c * 2500;
+        int nb;
+        memcpy(&nb, d, 4);
+        uint32_t L = (uint32_t)nb;
+        auto &h = e->blk_hold[c];
+        h.insert(h.end(), (uint8_t *)&L, (uint8_t *)&L + 4);
+        h.insert(h.end(), d + 4, d + 4 + nb);
+      }
+      if (reset) e->host[c]->isu_reset();
+      if (meta[0] >= 0) {
+        e->host[c]->frame(o, meta[0], (uint32_t)meta[1], meta[2]);
+        uint8_t rec[320] = {0};
+        memcpy(rec, o, 312);
+        const uint32_t L = (uint32_t)meta[0], M = (uint32_t)meta[1];
+        memcpy(rec + 312, &L, 4);
+        memcpy(rec + 316, &M, 4);
+        e->frame_hold[c].insert(e->frame_hold[c].end(), rec, rec + 320);
+      }
+    }
+  }
+  return AERO_OK;
+}
+
+int collect_traces(aero_engine *e) {
+  const int C = e->C, nch = e->nch;
+  std::vector<int> hn(nch);
+  if (e->flags & AERO_F_TRACE_HOPS) HIPCHK(hipMemcpy(hn.data(), e->S.hop_n, sizeof(int) * nch, hipMemcpyDeviceToHost));
+  bool anyhop = false;
+  for (int c = 0; c < nch; c++) anyhop |= hn[c] > 0;
+  if (anyhop) {
+    std::vector<double> h((size_t)HOP_CAP * 6 * nch);
+    HIPCHK(hipMemcpy(h.data(), e->S.hops, h.size() * 8, hipMemcpyDeviceToHost));
+    for (int c = 0; c < nch; c++) {
+      const int n = std::min(hn[c], HOP_CAP);
+      e->hop_hold[c].insert(e->hop_hold[c].end(), h.begin() + (size_t)c * HOP_CAP * 6,
+                            h.begin() + ((size_t)c * HOP_CAP + n) * 6);
+    }
+    HIPCHK(hipMemset(e->S.hop_n, 0, sizeof(int) * nch));
+  }
+  if (e->flags & AERO_F_TRACE_PT) {
+    std::vector<long long> pn(nch);
+    HIPCHK(hipMemcpy(pn.data(), e->S.ls + (size_t)LS_PT_N * C, 8 * nch, hipMemcpyDeviceToHost));
+    std::vector<double2> pts((size_t)PT_CAP * nch);
+    HIPCHK(hipMemcpy(pts.data(), e->S.pt, pts.size() * sizeof(double2), hipMemcpyDeviceToHost));
+    for (int c = 0; c < nch; c++) {
+      if (pn[c] > PT_CAP) return AERO_E_FULL;
+      for (long long k = 0; k < pn[c]; k++) {
+        e->pt_hold[c].push_back(pts[(size_t)c * PT_CAP + k].x);
+        e->pt_hold[c].push_back(pts[(size_t)c * PT_CAP + k].y);
+      }
+    }
+    HIPCHK(hipMemset(e->S.ls + (size_t)LS_PT_N * C, 0, 8 * nch));
+  }
+  // soft bits delivered to AeroL (groups of 32)
+  if (!(e->flags & AERO_F_TRACE_SOFT)) return AERO_OK;
+  std::vector<long long> sp(nch);
+  HIPCHK(hipMemcpy(sp.data(), e->S.ls + (size_t)LS_SOFT_P * C, 8 * nch, hipMemcpyDeviceToHost));
+  std::vector<uint8_t> ring;
+  for (int c = 0; c < nch; c++) {
+    const long long emitted = sp[c] & ~31LL;
+    if (emitted > e->soft_seen[c]) {
+      if (ring.empty()) {
+        ring.resize((size_t)SOFT_RING * nch);
+        HIPCHK(hipMemcpy(ring.data(), e->S.soft, ring.size(), hipMemcpyDeviceToHost));
+      }
+      for (long long k = e->soft_seen[c]; k < emitted; k++)
+        e->soft_hold[c].push_back(ring[(size_t)c * SOFT_RING + (k & (SOFT_RING - 1))]);
+      e->soft_seen[c] = emitted;
+    }
+  }
+  return AERO_OK;
+}
+
+int run_impl(aero_engine *e, int flush) {
+  if (e->nch == 0) return AERO_OK;
+  const int tflags = AERO_F_TRACE_PT | AERO_F_TRACE_BLOCKS | AERO_F_TRACE_SOFT | AERO_F_TRACE_HOPS;
+  const bool trace = (e->flags & tflags) != 0;
+  for (int guard = 0; guard < 1000000; guard++) {
+    // host mirror of the hop and segment rules of coarse.hip / demod_oqpsk.hip
+    bool any_hop = false, progress = false;
+    for (int c = 0; c < e->nch; c++) {
+      const long long boundary = (long long)HOP * (e->hops[c] + 1) - 1;
+      if (e->nsamp[c] == boundary && e->avail[c] > boundary) {
+        e->hops[c]++;
+        any_hop = true;
+      }
+    }
+    for (int c = 0; c < e->nch; c++) {
+      const long long boundary = (long long)HOP * (e->hops[c] + 1) - 1;
+      long long end = std::min(e->avail[c], boundary);
+      if (!flush && e->avail[c] <= boundary) end = e->nsamp[c];
+      if (end > e->nsamp[c]) {
+        e->processed += (uint64_t)(end - e->nsamp[c]);
+        e->nsamp[c] = end;
+        progress = true;
+      }
+    }
+    if (!any_hop && !progress) break;
+    hipEvent_t a, b;
+    if (any_hop) {
+      ev_begin(e, "coarse", a, b);
+      launch_coarse(e->st, e->S, e->T, e->nch);
+      ev_end(e, b);
+    }
+    if (progress) {
+      ev_begin(e, "demod", a, b);
+      launch_demod(e->st, e->S, e->T, e->nch, flush, (e->flags & AERO_F_TRACE_PT) != 0);
+      ev_end(e, b);
+    }
+    HIPCHK(hipMemsetAsync(e->S.njobs, 0, sizeof(int), e->st));
+    ev_begin(e, "frame", a, b);
+    launch_frame(e->st, e->S, e->nch);
+    ev_end(e, b);
+    int njobs = 0;
+    HIPCHK(hipMemcpyAsync(&njobs, e->S.njobs, sizeof(int), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    if (njobs > 0) {
+      ev_begin(e, "viterbi", a, b);
+      launch_viterbi(e->st, e->S, e->T, njobs, (e->flags & AERO_F_TRACE_BLOCKS) ? 1 : 0);
+      ev_end(e, b);
+    }
+    HIPCHK(hipGetLastError());
+    int rc = collect_after_pass(e, njobs);
+    if (rc) return rc;
+    if (trace) {
+      rc = collect_traces(e);
+      if (rc) return rc;
+    }
+  }
+  HIPCHK(hipStreamSynchronize(e->st));
+  ev_collect(e);
+  return AERO_OK;
+}
+
+template <class T>
+int pop_vec(std::vector<T> &v, T *dst, size_t cap, size_t *n) {
+  const size_t k = std::min(cap, v.size());
+  if (dst && k) memcpy(dst, v.data(), k * sizeof(T));
+  if (n) *n = k;
+  v.erase(v.begin(), v.begin() + k);
+  return AERO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *aero_strerror(int rc) {
+  switch (rc) {
+    case AERO_OK: return "ok";
+    case AERO_E_INVALID: return "invalid argument or unsupported configuration";
+    case AERO_E_NOMEM: return "out of memory";
+    case AERO_E_HIP: return "HIP runtime error";
+    case AERO_E_NOGPU: return "no usable gfx950 device";
+    case AERO_E_FULL: return "channel table or ring full";
+    case AERO_E_RATE: return "sample rate mismatch";
+    default: return "unknown error";
+  }
+}
+
+int aero_engine_create(const aero_engine_cfg *cfg, aero_engine **out) {
+  if (!cfg || !out || cfg->max_channels <= 0) return AERO_E_INVALID;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device) return AERO_E_NOGPU;
+  HIPCHK(hipSetDevice(cfg->device));
+  std::unique_ptr<aero_engine> e(new aero_engine());
+  e->device = cfg->device;
+  e->flags = cfg->flags;
+  e->C = (cfg->max_channels + 63) & ~63;
+  DevState S{};
+  DevTables T{};
+  const size_t bytes = layout(S, T, e->C, e->flags, nullptr) + 4096;
+  if (hipMalloc(&e->pool, bytes) != hipSuccess) return AERO_E_NOMEM;
+  e->pool_bytes = bytes;
+  HIPCHK(hipMemset(e->pool, 0, bytes));
+  layout(e->S, e->T, e->C, e->flags, reinterpret_cast<char *>(e->pool));
+  HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
+  // tables (host glibc, g++-compiled: tables_host.cpp)
+  std::vector<double> cis(2 * WTSIZE), tw(2 * NFFT), twi(2 * NFFT), taps(64);
+  std::vector<uint8_t> scr(5000);
+  host_cis(cis.data());
+  host_twiddles(NFFT, tw.data(), twi.data());
+  host_scrambler(scr.data());
+  HIPCHK(hipMemcpy((void *)e->T.cis, cis.data(), sizeof(double) * 2 * WTSIZE, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy((void *)e->T.tw, tw.data(), sizeof(double) * 2 * NFFT, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy((void *)e->T.twi, twi.data(), sizeof(double) * 2 * NFFT, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy((void *)e->T.scr, scr.data(), 5000, hipMemcpyHostToDevice));
+  if (host_rrc(1.0, 55, 48000, 10500 / 2, taps.data()) != NTAPS) return AERO_E_INVALID;
+  HIPCHK(hipMemcpy((void *)e->T.taps, taps.data(), sizeof(double) * NTAPS, hipMemcpyHostToDevice));
+  const double T48 = 48000.0 / (10500.0 / 2);
+  DelayDesc dly[4];
+  if (!host_delay(1, dly[0]) || !host_delay(T48 / 4.0, dly[1]) || !host_delay(T48 / 4.0, dly[2]) ||
+      !host_delay(T48 / 8.0, dly[3]))
+    return AERO_E_INVALID;
+  if (dly[0].size != 2 || dly[1].size != 4 || dly[2].size != 4 || dly[3].size != 3) return AERO_E_INVALID;
+  const double sr_b[3] = {0.00032714218939589035, 0, 0.00032714218939589035};
+  const double sr_a[3] = {1, -0.39005299948210803, 0.99934571562120822};
+  const double ct_b[3] = {0.0010275610653672064, 0.0020551221307344128, 0.0010275610653672064};
+  const double ct_a[3] = {1, -1.9207386815577139, 0.92509247310306331};
+  upload_demod_constants(taps.data(), dly, sr_b, sr_a, ct_b, ct_a);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  *out = e.release();
+  return AERO_OK;
+}
+
+void aero_engine_destroy(aero_engine *e) {
+  if (!e) return;
+  hipSetDevice(e->device);
+  if (e->st) hipStreamSynchronize(e->st);
+  ev_collect(e);
+  if (e->d_scratch) (void)hipFree(e->d_scratch);
+  if (e->pool) (void)hipFree(e->pool);
+  if (e->st) (void)hipStreamDestroy(e->st);
+  delete e;
+}
+
+int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) {
+  if (!e || !cfg || !ch_out) return AERO_E_INVALID;
+  if (cfg->bitrate != 10500 || cfg->burst) return AERO_E_INVALID;  // decode/decode.h:42 subset
+  if (e->nch >= e->C) return AERO_E_FULL;
+  HIPCHK(hipSetDevice(e->device));
+  const int c = e->nch;
+  int rc = init_channel_state(e, c);
+  if (rc) return rc;
+  e->nch++;
+  e->cfg.push_back(*cfg);
+  e->avail.push_back(0);
+  e->nsamp.push_back(0);
+  e->hops.push_back(0);
+  e->host.emplace_back(new PChannelHost(cfg->disable_reassembly != 0));
+  e->soft_hold.emplace_back();
+  e->hop_hold.emplace_back();
+  e->pt_hold.emplace_back();
+  e->blk_hold.emplace_back();
+  e->frame_hold.emplace_back();
+  e->soft_seen.push_back(0);
+  *ch_out = c;
+  return AERO_OK;
+}
+
+static int push_common(aero_engine *e, const int16_t *src, size_t n, size_t ld, int nch, int c0, bool dev) {
+  // keep the ring from overrunning unprocessed samples
+  for (int j = 0; j < nch; j++) {
+    const int c = c0 + j;
+    if (e->avail[c] + (long long)n - e->nsamp[c] > PCM_CAP - 2) {
+      int rc = run_impl(e, 0);
+      if (rc) return rc;
+      if (e->avail[c] + (long long)n - e->nsamp[c] > PCM_CAP - 2) return AERO_E_FULL;
+    }
+  }
+  const int16_t *dsrc = src;
+  if (!dev) {
+    const size_t need = n * ld;
+    if (need > e->scratch_cap) {
+      if (e->d_scratch) (void)hipFree(e->d_scratch);
+      e->d_scratch = nullptr;
+      e->scratch_cap = 0;
+      HIPCHK(hipMalloc(&e->d_scratch, need * sizeof(int16_t)));
+      e->scratch_cap = need;
+    }
+    HIPCHK(hipMemcpyAsync(e->d_scratch, src, need * sizeof(int16_t), hipMemcpyHostToDevice, e->st));
+    dsrc = e->d_scratch;
+  }
+  const long long start = e->avail[c0];
+  for (int j = 1; j < nch; j++)
+    if (e->avail[c0 + j] != start) return AERO_E_INVALID;  // batch pushes are lockstep
+  const long long total = (long long)n * nch;
+  const int grid = (int)std::min<long long>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(pcm_scatter_kernel, dim3(grid), dim3(256), 0, e->st, e->S.pcm, e->C, (long long)PCM_CAP - 1,
+                     dsrc, (long long)n, (long long)ld, nch, c0, start);
+  HIPCHK(hipGetLastError());
+  for (int j = 0; j < nch; j++) e->avail[c0 + j] += (long long)n;
+  // device copy of the counters
+  std::vector<long long> av(e->avail.begin() + c0, e->avail.begin() + c0 + nch);
+  HIPCHK(hipMemcpyAsync(e->S.ls + (size_t)LS_AVAIL * e->C + c0, av.data(), 8 * nch, hipMemcpyHostToDevice, e->st));
+  HIPCHK(hipStreamSynchronize(e->st));
+  return AERO_OK;
+}
+
+int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t fs) {
+  if (!e || ch < 0 || ch >= e->nch || (!pcm && n)) return AERO_E_INVALID;
+  (void)fs;  // the OQPSK demodulator only logs a rate mismatch (oqpskdemodulator.cpp:626-628)
+  if (!n) return AERO_OK;
+  HIPCHK(hipSetDevice(e->device));
+  // split so one piece never exceeds the ring
+  size_t off = 0;
+  while (off < n) {
+    const size_t piece = std::min<size_t>(n - off, PCM_CAP / 2);
+    int rc = push_common(e, pcm + off, piece, 1, 1, ch, false);
+    if (rc) return rc;
+    off += piece;
+  }
+  return AERO_OK;
+}
+
+int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld, int nch, int dev) {
+  if (!e || !pcm || nch <= 0 || nch > e->nch || ld < (size_t)nch) return AERO_E_INVALID;
+  HIPCHK(hipSetDevice(e->device));
+  size_t off = 0;
+  while (off < n) {
+    const size_t piece = std::min<size_t>(n - off, PCM_CAP / 2);
+    int rc = push_common(e, pcm + off * ld, piece, ld, nch, 0, dev != 0);
+    if (rc) return rc;
+    off += piece;
+  }
+  return AERO_OK;
+}
+
+int aero_run(aero_engine *e) {
+  if (!e) return AERO_E_INVALID;
+  HIPCHK(hipSetDevice(e->device));
+  return run_impl(e, 0);
+}
+
+int aero_flush(aero_engine *e) {
+  if (!e) return AERO_E_INVALID;
+  HIPCHK(hipSetDevice(e->device));
+  return run_impl(e, 1);
+}
+
+int aero_pop_softbits(aero_engine *e, int ch, int16_t *dst, size_t cap, size_t *n) {
+  if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  return pop_vec(e->soft_hold[ch], dst, cap, n);
+}
+
+int aero_pop_items(aero_engine *e, int ch, aero_acars_item *dst, size_t cap, size_t *n) {
+  if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  return pop_vec(e->host[ch]->items, dst, cap, n);
+}
+
+int aero_pop_hops(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n) {
+  if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  size_t k = 0;
+  int rc = pop_vec(e->hop_hold[ch], dst, cap_records * 6, &k);
+  if (n) *n = k / 6;
+  return rc;
+}
+
+int aero_pop_pt(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n) {
+  if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  size_t k = 0;
+  int rc = pop_vec(e->pt_hold[ch], dst, cap_records * 2, &k);
+  if (n) *n = k / 2;
+  return rc;
+}
+
+int aero_pop_blocks(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
+  if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  return pop_vec(e->blk_hold[ch], dst, cap, n);
+}
+
+int aero_pop_frames(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
+  if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  return pop_vec(e->frame_hold[ch], dst, cap, n);
+}
+
+int aero_timing(aero_engine *e, const char *name, double *ms, long *launches) {
+  if (!e || !name) return AERO_E_INVALID;
+  ev_collect(e);
+  auto it = e->timing.find(name);
+  if (ms) *ms = it == e->timing.end() ? 0.0 : it->second.ms;
+  if (launches) *launches = it == e->timing.end() ? 0 : it->second.launches;
+  return AERO_OK;
+}
+
+void aero_timing_reset(aero_engine *e) {
+  if (!e) return;
+  ev_collect(e);
+  e->timing.clear();
+}
+
+uint64_t aero_samples_processed(aero_engine *e) { return e ? e->processed : 0; }
+
+int aero_sync(aero_engine *e) {
+  if (!e) return AERO_E_INVALID;
+  HIPCHK(hipStreamSynchronize(e->st));
+  return AERO_OK;
+}
+
+int aero_device_math(aero_engine *e, int fn, const double *x, const double *y, double *out, size_t n) {
+  if (!e || !x || !y || !out) return AERO_E_INVALID;
+  HIPCHK(hipSetDevice(e->device));
+  double *d = nullptr;
+  HIPCHK(hipMalloc(&d, 3 * n * sizeof(double) + 64));
+  HIPCHK(hipMemcpy(d, x, n * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d + n, y, n * 8, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(math_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->st, fn, d, d + n, d + 2 * n, n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(e->st));
+  HIPCHK(hipMemcpy(out, d + 2 * n, n * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipFree(d));
+  return AERO_OK;
+}
+
+}  // extern "C"

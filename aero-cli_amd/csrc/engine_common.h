@@ -1,0 +1,119 @@
+/*
+ * engine_common.h — device-side state layout of the Aero engine (10500-bps
+ * continuous OQPSK, decode/oqpskdemodulator.cpp + decode/aerol.cpp).
+ *
+ * One channel (VFO) per lane.  All per-channel state is struct-of-arrays in
+ * HBM: field f of channel c lives at base[f * C + c], so a wavefront loads
+ * and stores 64 consecutive channels with one coalesced access.  Rings whose
+ * pointer advances in lockstep for every channel (AGC) are time-major; rings
+ * whose pointer depends on each channel's symbol clock (moving averages,
+ * delay lines, the coarse-estimator history) are channel-major so a lane's
+ * successive accesses stay in one cache line.
+ */
+#pragma once
+#include <stdint.h>
+
+#include "tables_host.h"  // DelayDesc
+
+namespace aero {
+
+constexpr int WTSIZE = 19999;         // decode/DSP.h:21
+constexpr int NTAPS = 55;             // RRC taps (decode/oqpskdemodulator.cpp:177)
+constexpr int AGC_LEN = 192000;       // AGC(4, 48000) (decode/DSP.cpp:361)
+constexpr int MARG_LEN = 800;         // MovingAverage(800) (oqpskdemodulator.cpp:41)
+constexpr int DT_LEN = 401;           // DelayThing.setLength(400) (oqpskdemodulator.cpp:42)
+constexpr int MSE_LEN = 400;          // MSEcalc(400) (oqpskdemodulator.cpp:50)
+constexpr int NFFT = 16384;           // coarse estimator 2^14 (decode/decode.cpp:152)
+constexpr int HOP = 4096;             // 75 % overlap (oqpskdemodulator.cpp:357)
+constexpr int SOFT_RING = 4096;       // per-channel soft-bit ring (power of 2)
+constexpr int Y_LO = 2815, Y_HI = 13568;  // y[] bins the fold search reads
+constexpr int Y_LEN = Y_HI - Y_LO + 1;
+constexpr int BLOCK = 4992;           // 78 x 64 interleaver block (aerol.cpp:1012-1016)
+constexpr int DL2_LEN = 4987;         // DelayLine setLength(4992-6) (aerol.cpp:1015)
+constexpr int VIT_MAX = 5078;         // 62 overlap + 4992 + 24 pad
+constexpr int JOB_OUT = 328;          // 312 infofield + len + mask + formatid + channel
+
+// double state fields
+enum DS : int {
+  DS_M2_PTR, DS_M2_STEP, DS_M2_FREQ,
+  DS_MC_PTR, DS_MC_STEP, DS_MC_FREQ,
+  DS_SO_PTR, DS_SO_LAST, DS_SO_STEP, DS_SO_FREQ,
+  DS_AGC_SUM,
+  DS_D1_0, DS_D1_1,
+  DS_D41_0, DS_D41_1, DS_D41_2, DS_D41_3,
+  DS_D42_0, DS_D42_1, DS_D42_2, DS_D42_3,
+  DS_D8_0, DS_D8_1, DS_D8_2,
+  DS_SR_X1, DS_SR_X2, DS_SR_Y1, DS_SR_Y2,
+  DS_CT_X1, DS_CT_X2, DS_CT_Y1, DS_CT_Y2,
+  DS_MARG_SUM, DS_PM_SUM, DS_MS_SUM,
+  DS_MSE,
+  DS_PTD_RE, DS_PTD_IM, DS_S2L_RE, DS_S2L_IM,
+  DS_COUNT
+};
+
+// int state fields
+enum IS : int {
+  IS_AGC_PTR, IS_D1_P, IS_D41_P, IS_D42_P, IS_D8_P,
+  IS_MARG_P, IS_DT_P, IS_PM_P, IS_MS_P,
+  IS_YUI, IS_S2L_INIT,
+  // hop / hunter state (decode/oqpskdemodulator.cpp:572,586; decode/hunter.cpp)
+  IS_COUNTDOWN2, IS_COUNTDOWN, IS_HUNT_ITER, IS_HUNT_SCANS, IS_EMPTYCD, IS_YRESET,
+  IS_HOPS_DONE,
+  // AeroL framing (decode/aerol.cpp:1060-2038)
+  IS_RI, IS_CNTR, IS_GSL, IS_UWI, IS_UWR, IS_UWI_INV, IS_UWR_INV,
+  IS_FRAMEINFO, IS_LASTFRAMEINFO, IS_FORMATID, IS_DATACD, IS_DATACDCD,
+  IS_SCR_POS, IS_BLKBUF, IS_HAS_OVERLAP, IS_DL2_PTR,
+  IS_COUNT
+};
+
+// 64-bit counters
+enum LS : int {
+  LS_NSAMP,       // samples demodulated
+  LS_AVAIL,       // samples pushed
+  LS_FILLED,      // coarse-ring entries written (samples < filled)
+  LS_ZERO_BEFORE, // coarse-ring entries of samples < this are zero
+  LS_SOFT_P,      // soft bits produced
+  LS_SOFT_C,      // soft bits consumed by AeroL
+  LS_PT_N,        // pt trace records
+  LS_COUNT
+};
+
+
+struct DevTables {
+  const double2 *cis;      // [WTSIZE] (CosWT, SinWT)   decode/DSP.cpp:10-33
+  const double2 *tw;       // [NFFT] forward twiddles   decode/jfft.cpp:41-53
+  const double2 *twi;      // [NFFT] inverse twiddles
+  const uint8_t *scr;      // [5000] scrambler bits      decode/aerol.h:408-427
+  const double *taps;      // [NTAPS] RRC taps           decode/DSP.h:325-351
+};
+
+struct DevState {
+  int C;                   // channel stride
+  double *ds;              // [DS_COUNT][C]
+  int *is;                 // [IS_COUNT][C]
+  long long *ls;           // [LS_COUNT][C]
+  double *fir;             // [2*NTAPS][C] transposed-FIR partial sums
+  double *agc;             // [AGC_LEN][C]
+  double *marg;            // [C][MARG_LEN]
+  double2 *dt;             // [C][DT_LEN]
+  double *pm, *ms;         // [C][MSE_LEN] each
+  int16_t *pcm;            // [PCM_CAP][C] input ring (time-major)
+  long long pcm_cap;       // power of 2
+  uint32_t *cring;         // [C][NFFT] coarse ring: cis index | pcm << 16
+  double *y;               // [C][Y_LEN] coarse smoothing state
+  uint8_t *soft;           // [C][SOFT_RING]
+  double2 *pt;             // [C][pt_cap] (trace only)
+  long long pt_cap;
+  double *hops;            // [C][hop_cap][6] per-run hop trace
+  int hop_cap;
+  int *hop_n;              // [C]
+  uint8_t *block;          // [C][2][BLOCK] double-buffered interleaver block
+  uint8_t *overlap;        // [C][64]
+  uint8_t *dl2;            // [C][DL2_LEN]
+  int *jobs;               // [C] job list: channel | (buf << 24)
+  int *njobs;              // [1]
+  uint8_t *jobout;         // [C][JOB_OUT]
+  uint8_t *blocks_dbg;     // [C][2500] decoded bits (trace)
+};
+
+}  // namespace aero

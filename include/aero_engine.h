@@ -1,0 +1,132 @@
+/*
+ * aero_engine.h — C ABI of the MI355X-native Aero demodulation engine.
+ *
+ * Drop-in boundary for aero-decode's per-VFO DSP chain.  In the reference
+ * (airframesio/aero-cli, decode/) the boundary is a set of Qt signal/slot
+ * edges wired in decode/decode.cpp:168-241; each entry point below names the
+ * edge it replaces.  Plain pointers and sizes only; no torch/HIP types.
+ *
+ * Threading: one host thread per engine (the reference runs all DSP on the
+ * Qt main thread); push/run/pop on one engine must be serialised by the
+ * caller.  Ownership: the caller owns every buffer it passes; the engine
+ * copies input before returning and copies output into caller arrays.
+ * Errors: 0 = OK, negative = AERO_E_* (aero_strerror).
+ */
+#ifndef AERO_ENGINE_H
+#define AERO_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AERO_OK 0
+#define AERO_E_INVALID (-1)    /* bad argument / unsupported bit rate      */
+#define AERO_E_NOMEM (-2)      /* device or host allocation failed         */
+#define AERO_E_HIP (-3)        /* HIP runtime error                        */
+#define AERO_E_NOGPU (-4)      /* no gfx950 device / kernels not loadable  */
+#define AERO_E_FULL (-5)       /* channel table or PCM ring full           */
+#define AERO_E_RATE (-6)       /* sample rate differs from the channel's   */
+
+/* engine flags */
+#define AERO_F_TRACE_PT 0x1    /* keep the rotated pt_qpsk trace (parity tests)      */
+#define AERO_F_TRACE_BLOCKS 0x2 /* keep decoded Viterbi blocks (parity tests)         */
+#define AERO_F_TIMING 0x4      /* HIP-event timing of every kernel launch            */
+#define AERO_F_TRACE_SOFT 0x8  /* keep delivered soft bits for aero_pop_softbits      */
+#define AERO_F_TRACE_HOPS 0x10 /* keep per-hop coarse-estimator records              */
+
+typedef struct aero_engine aero_engine;
+
+typedef struct {
+  int device;       /* HIP device ordinal                                   */
+  int max_channels; /* channel table size (memory is sized for this)        */
+  int flags;        /* AERO_F_*                                              */
+} aero_engine_cfg;
+
+typedef struct {
+  int bitrate;            /* 10500 (600/1200 -> AERO_E_INVALID this round)   */
+  int burst;              /* 0 (burst mode -> AERO_E_INVALID this round)     */
+  uint32_t fs;            /* 48000 for 10500 bps (decode/decode.cpp:145)     */
+  int disable_reassembly; /* 1: items are ACARSfragmentsignal (decode.cpp:233) */
+} aero_channel_cfg;
+
+/* ACARSItem (decode/aerol.h:163-197) as a fixed-size POD.  `parsed`
+ * (libacars, absent) and the wall-clock time are not produced. */
+typedef struct {
+  uint32_t aesid;
+  uint8_t gesid, qno, refno, seqno;
+  uint8_t mode, tak, bi, nonacars;
+  uint8_t downlink, valid, hastext, moretocome;
+  uint8_t fragment; /* 1 = ACARSfragmentsignal, 0 = ACARSsignal */
+  uint8_t label_len, reg_len, pad0;
+  char label[4];
+  char reg[16];
+  uint32_t msg_len;  /* bytes used in msg */
+  char msg[3584];    /* Latin-1 text, not NUL-terminated */
+} aero_acars_item;
+
+/* Engine lifetime (replaces Decoder::Decoder / ~Decoder, decode/decode.cpp:72-260). */
+int aero_engine_create(const aero_engine_cfg *cfg, aero_engine **out);
+void aero_engine_destroy(aero_engine *e);
+
+/* Opens one VFO channel: the Decoder ctor's demod + AeroL + hunter wiring
+ * (decode/decode.cpp:117-241) for one -t topic. */
+int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out);
+
+/* One ZMQ message == one call: Decoder::audioReceived ->
+ * OqpskDemodulator::dataReceived (decode/decode.cpp:352,
+ * decode/oqpskdemodulator.cpp:624-630).  pcm: int16 LE real samples. */
+int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t fs);
+
+/* Lockstep batch push for channels [0, nch): pcm is time-major, n samples
+ * per channel, sample t of channel c at pcm[t*ld + c].  dev != 0: pcm is a
+ * HIP device pointer (inputs already resident in HBM). */
+int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld, int nch, int dev);
+
+/* Runs the batched kernels for every channel over all pushed samples that
+ * complete a coarse-estimate hop; aero_flush also processes the tail. */
+int aero_run(aero_engine *e);
+int aero_flush(aero_engine *e);
+
+/* Soft bits delivered to AeroL (groups of 32, 0..255;
+ * decode/oqpskdemodulator.cpp:534-540).  Needs AERO_F_TRACE_SOFT. */
+int aero_pop_softbits(aero_engine *e, int ch, int16_t *dst, size_t cap, size_t *n);
+
+/* ACARSItems emitted on ACARSsignal (or ACARSfragmentsignal with
+ * disable_reassembly), in emission order (decode/aerol.cpp:457,522,2127,2142). */
+int aero_pop_items(aero_engine *e, int ch, aero_acars_item *dst, size_t cap, size_t *n);
+
+/* Diagnostics used by the parity tests and the bench.
+ * hops: 6 doubles per coarse hop (sample index, estimate, mixer2 Hz,
+ * mixer_center Hz, mse, signal). pt: 2 doubles per carrier event.
+ * blocks: uint32 count + decoded bits (bytes 0/1) per Viterbi block.
+ * frames: 320 bytes per completed frame (312 infofield, u32 len, u32 crc mask). */
+int aero_pop_hops(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n);
+int aero_pop_pt(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n);
+int aero_pop_blocks(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
+int aero_pop_frames(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
+
+/* Kernel timing (AERO_F_TIMING): name in {"demod","coarse","frame","viterbi"};
+ * returns summed device milliseconds and launch count since the last reset. */
+int aero_timing(aero_engine *e, const char *name, double *ms, long *launches);
+void aero_timing_reset(aero_engine *e);
+
+/* Total input samples demodulated across channels since creation. */
+uint64_t aero_samples_processed(aero_engine *e);
+
+/* Synchronise the engine's stream. */
+int aero_sync(aero_engine *e);
+
+/* Evaluates the device libm on n inputs (parity test of aero_math.h):
+ * fn 0 hypot, 1 atan2, 2 tanh, 3 sin, 4 cos, 5 log10, 6 sqrt, 7 fmod(x,360),
+ * 8 division x/y.  x, y, out are host arrays. */
+int aero_device_math(aero_engine *e, int fn, const double *x, const double *y, double *out, size_t n);
+
+const char *aero_strerror(int rc);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,147 @@
+"""Test helpers: synthetic VFO input (tools/libaero_synth.so) and the oracle
+(oracle/liboracle.so, the checker).  Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg use the oracle."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, 'aero-cli_amd')
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+
+ORACLE_SO = os.path.join(ROOT, 'oracle', 'liboracle.so')
+SYNTH_SO = os.path.join(ROOT, 'tools', 'libaero_synth.so')
+
+
+class SynthCfg(ctypes.Structure):
+    _fields_ = [('fs', ctypes.c_double), ('carrier_hz', ctypes.c_double), ('phase0', ctypes.c_double),
+                ('amplitude', ctypes.c_double), ('ebn0_db', ctypes.c_double), ('seed', ctypes.c_uint64),
+                ('msg_rate', ctypes.c_double), ('lead_in', ctypes.c_int)]
+
+
+def build_all():
+    import build  # aero-cli_amd/build.py
+    return build.build_all()
+
+
+def build_cpu_only():
+    import build
+    build.build_oracle()
+    build.build_synth()
+
+
+_synth = None
+
+
+def synth(seconds=10.0, seed=0xAE20, carrier=12037.5, ebn0=12.0, amplitude=0.25, phase0=0.3, msg_rate=0.6,
+          lead_in=1000, fs=48000.0, return_frames=False):
+    """int16 PCM of an Aero P-channel (SURVEY.md §8(d) C1/C2 input) + the
+    transmitted 312-byte information fields per frame."""
+    global _synth
+    if _synth is None:
+        _synth = ctypes.CDLL(SYNTH_SO)
+        _synth.aero_synth_p10500.restype = ctypes.c_size_t
+    n = int(fs * seconds)
+    pcm = np.zeros(n, dtype=np.int16)
+    maxf = int(seconds * 2) + 8
+    frames = np.zeros(312 * maxf, dtype=np.uint8)
+    cfg = SynthCfg(fs, carrier, phase0, amplitude, ebn0, seed, msg_rate, lead_in)
+    nf = _synth.aero_synth_p10500(ctypes.byref(cfg), pcm.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n),
+                                  frames.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(maxf))
+    if return_frames:
+        return pcm, frames[:312 * min(nf, maxf)].reshape(-1, 312)
+    return pcm
+
+
+class Oracle:
+    """One reference channel (a whole `aero-decode -b 10500` instance)."""
+    _lib = None
+
+    @classmethod
+    def lib(cls):
+        if cls._lib is None:
+            L = ctypes.CDLL(ORACLE_SO)
+            L.oracle_create.restype = ctypes.c_void_p
+            L.oracle_create.argtypes = [ctypes.c_int, ctypes.c_int]
+            L.oracle_destroy.argtypes = [ctypes.c_void_p]
+            L.oracle_push.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+            for f in ('oracle_softbits', 'oracle_blocks', 'oracle_frames', 'oracle_items'):
+                getattr(L, f).restype = ctypes.c_size_t
+                getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+            for f in ('oracle_hops', 'oracle_pt'):
+                getattr(L, f).restype = ctypes.c_size_t
+                getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+            L.oracle_conv_encode.restype = ctypes.c_size_t
+            L.oracle_conv_encode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+            L.oracle_viterbi_decode_soft.restype = ctypes.c_size_t
+            L.oracle_viterbi_decode_soft.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+            L.oracle_crc16_bytes.restype = ctypes.c_uint16
+            L.oracle_crc16_bytes.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            L.oracle_scrambler_bits.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            L.oracle_deinterleave_perm.argtypes = [ctypes.c_int, ctypes.c_void_p]
+            L.oracle_rrc_design.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                            ctypes.c_void_p]
+            L.oracle_cis_table.argtypes = [ctypes.c_void_p]
+            L.oracle_twiddles.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+            L.oracle_fft.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+            cls._lib = L
+        return cls._lib
+
+    def __init__(self, trace_pt=False):
+        self.L = self.lib()
+        self.h = self.L.oracle_create(10500, 1 if trace_pt else 0)
+
+    def __del__(self):
+        if getattr(self, 'h', None):
+            self.L.oracle_destroy(self.h)
+            self.h = None
+
+    def push(self, pcm):
+        pcm = np.ascontiguousarray(pcm, dtype=np.int16)
+        self.L.oracle_push(self.h, pcm.ctypes.data, pcm.size)
+
+    def push_chunked(self, pcm, chunk=12000):
+        for i in range(0, len(pcm), chunk):
+            self.push(pcm[i:i + chunk])
+
+    def _get(self, fn, dtype, rec=1):
+        n = fn(self.h, None, 0)
+        buf = np.zeros(n * rec, dtype=dtype)
+        fn(self.h, buf.ctypes.data, n)
+        return buf.reshape(-1, rec) if rec > 1 else buf
+
+    def softbits(self):
+        return self._get(self.L.oracle_softbits, np.uint8)
+
+    def hops(self):
+        return self._get(self.L.oracle_hops, np.float64, 6)
+
+    def pt(self):
+        return self._get(self.L.oracle_pt, np.float64, 2)
+
+    def blocks(self):
+        return self._get(self.L.oracle_blocks, np.uint8)
+
+    def frames(self):
+        return self._get(self.L.oracle_frames, np.uint8)
+
+    def item_lines(self, kind='A'):
+        n = self.L.oracle_items(self.h, None, 0)
+        b = ctypes.create_string_buffer(n + 1)
+        self.L.oracle_items(self.h, b, n)
+        lines = b.raw[:n].decode().splitlines()
+        return [l for l in lines if l.startswith(kind + ' ')]
+
+
+def frame_records(raw):
+    """320-byte frame records -> list of (info bytes, crc-ok mask)."""
+    raw = np.asarray(raw, dtype=np.uint8).reshape(-1, 320)
+    out = []
+    for r in raw:
+        L = int(np.frombuffer(r[312:316].tobytes(), np.uint32)[0])
+        m = int(np.frombuffer(r[316:320].tobytes(), np.uint32)[0])
+        out.append((bytes(r[:L]), m))
+    return out

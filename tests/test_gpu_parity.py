@@ -1,0 +1,100 @@
+"""GPU parity: the HIP engine vs the CPU oracle on the same synthetic VFO
+streams.  Integer outputs (soft bits, coarse-hop decisions, Viterbi blocks,
+CRC-checked frames, ACARS items) must be bit-exact; the rotated pt_qpsk
+soft-metric floats within 1e-5 (BASELINE.json north_star)."""
+import numpy as np
+import pytest
+
+import aero_testlib as tl
+
+PT_TOL = 1e-5
+
+CASES = [
+    # seed, carrier Hz, Eb/N0 dB, seconds, message size (samples)
+    (0xAE20, 12037.5, 12.0, 14.0, 12000),
+    (0xAE21, 12038.0, 9.0, 14.0, 12000),
+    (0xAE22, 7020.0, 12.0, 12.0, 3000),
+    (0xAE23, 15500.0, 10.0, 12.0, 48000),
+]
+
+
+def _run_engine(streams, chunks, flags):
+    import aero_engine as ae
+    eng = ae.Engine(max_channels=len(streams), flags=flags)
+    chans = [eng.open_channel(10500, 48000) for _ in streams]
+    pos = [0] * len(streams)
+    while any(p < len(s) for p, s in zip(pos, streams)):
+        for k, (s, ch) in enumerate(zip(streams, chans)):
+            if pos[k] < len(s):
+                eng.push(ch, s[pos[k]:pos[k] + chunks[k]])
+                pos[k] += chunks[k]
+        eng.run()
+    eng.flush()
+    return eng, chans
+
+
+@pytest.mark.gpu
+def test_engine_matches_oracle(engine_lib):
+    import aero_engine as ae
+    streams = [tl.synth(seconds=sec, seed=seed, carrier=f, ebn0=eb) for seed, f, eb, sec, _ in CASES]
+    chunks = [c[4] for c in CASES]
+    eng, chans = _run_engine(streams, chunks, ae.F_TRACE_ALL)
+    for k, (s, ch) in enumerate(zip(streams, chans)):
+        o = tl.Oracle(trace_pt=True)
+        o.push_chunked(s, chunks[k])
+        sb_o, sb_e = o.softbits(), eng.softbits(ch)
+        assert len(sb_o) > 1000, 'oracle did not lock on case %d' % k
+        assert len(sb_e) == len(sb_o), 'case %d soft-bit count %d vs %d' % (k, len(sb_e), len(sb_o))
+        assert np.array_equal(sb_e, sb_o), 'case %d soft bits differ at %s' % (
+            k, np.nonzero(sb_e != sb_o)[0][:10])
+        h_o, h_e = o.hops(), eng.hops(ch)
+        assert h_o.shape == h_e.shape
+        assert np.array_equal(h_e, h_o), 'case %d hop records differ' % k
+        p_o, p_e = o.pt(), eng.pt(ch)
+        assert p_o.shape == p_e.shape
+        assert np.max(np.abs(p_o - p_e)) <= PT_TOL
+        assert np.array_equal(eng.blocks(ch), o.blocks()), 'case %d Viterbi blocks differ' % k
+        assert np.array_equal(eng.frames(ch), o.frames()), 'case %d frames differ' % k
+        items_o = o.item_lines('A')
+        assert len(items_o) > 0
+        assert eng.items(ch) == items_o, 'case %d ACARS items differ' % k
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_fragment_items_disable_reassembly(engine_lib):
+    import aero_engine as ae
+    s = tl.synth(seconds=12.0, seed=0xAE30, carrier=12040.0, ebn0=12.0)
+    eng = ae.Engine(max_channels=1, flags=0)
+    ch = eng.open_channel(10500, 48000, disable_reassembly=True)
+    for i in range(0, len(s), 12000):
+        eng.push(ch, s[i:i + 12000])
+        eng.run()
+    eng.flush()
+    o = tl.Oracle()
+    o.push_chunked(s, 12000)
+    assert eng.items(ch) == o.item_lines('F')
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_batch_push_equals_channel_push(engine_lib):
+    """Lockstep batch ingest (bench path) == per-channel ZMQ-message ingest."""
+    import aero_engine as ae
+    nch = 6
+    streams = [tl.synth(seconds=9.0, seed=0xAE40 + k, carrier=12037.5 + 0.5 * k, ebn0=11.0) for k in range(nch)]
+    pcm = np.stack(streams, axis=1)
+    e1 = ae.Engine(max_channels=nch, flags=ae.F_TRACE_SOFT | ae.F_TRACE_HOPS)
+    for _ in range(nch):
+        e1.open_channel()
+    for i in range(0, pcm.shape[0], 4096):
+        e1.push_batch(pcm[i:i + 4096])
+        e1.run()
+    e1.flush()
+    e2, chans = _run_engine(streams, [12000] * nch, ae.F_TRACE_SOFT | ae.F_TRACE_HOPS)
+    for c in range(nch):
+        assert np.array_equal(e1.softbits(c), e2.softbits(chans[c]))
+        assert np.array_equal(e1.hops(c), e2.hops(chans[c]))
+        assert e1.items(c) == e2.items(chans[c])
+    e1.close()
+    e2.close()
