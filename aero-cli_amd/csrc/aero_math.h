@@ -278,12 +278,13 @@ AERO_HD double aero_atan2(double y, double x) {
   bool swap = ay > ax;
   double a = swap ? ax : ay, b = swap ? ay : ax;
   // scale to keep the residual computation away from under/overflow
-  int eb = (int)((hiw(b) >> 20) & 0x7ff) - 1023;
-  double sc = 1.0;
-  if (eb > 500 || eb < -500) {
-    sc = mkd((uint32_t)((1023 - eb) << 20), 0);
-    a *= sc;
-    b *= sc;
+  const int eb = (int)((hiw(b) >> 20) & 0x7ff) - 1023;
+  if (eb > 500) {  // only the ratio matters: scale by powers of two (exact)
+    a *= 0x1p-600;
+    b *= 0x1p-600;
+  } else if (eb < -500) {
+    a *= 0x1p600;
+    b *= 0x1p600;
   }
   double th = a / b;
   if (th < 0x1p-1000) {
@@ -336,7 +337,9 @@ AERO_HD void dd_sincos_small(double rh, double rl, dd &s, dd &c, bool want_s, bo
   if (want_c) c = dd_add(dd_mul(ck, cd), dd_neg(dd_mul(sk, sd)));
 }
 
-/* x = n*pi/2 + r (Cody-Waite, fdlibm split constants); valid for |x| < 2^20 */
+/* x = n*pi/2 + r (Cody-Waite, fdlibm split constants); valid for |x| < 2^20.
+ * aero_sin/aero_cos/aero_sincos return NaN outside that domain (the demod's
+ * argument is a moving average of clipped loop errors, |x| <= pi/2). */
 AERO_HD int reduce_pio2(double x, double &rh, double &rl) {
   const double pio2_1 = 1.57079632673412561417e+00, pio2_2 = 6.07710050630396597660e-11,
                pio2_3 = 2.02226624871116645580e-21, pio2_3t = 8.47842766036889956997e-32;
@@ -360,6 +363,7 @@ AERO_HD int reduce_pio2(double x, double &rh, double &rl) {
 
 AERO_HD double aero_sin(double x) {
   if (!__builtin_isfinite(x)) return x - x;
+  if (__builtin_fabs(x) >= 0x1p20) return __builtin_nan("");
   if (__builtin_fabs(x) < 0x1p-26) return x;
   double rh, rl;
   int n = reduce_pio2(x, rh, rl);
@@ -380,6 +384,7 @@ AERO_HD double aero_sin(double x) {
 
 AERO_HD double aero_cos(double x) {
   if (!__builtin_isfinite(x)) return x - x;
+  if (__builtin_fabs(x) >= 0x1p20) return __builtin_nan("");
   if (__builtin_fabs(x) < 0x1p-27) return 1.0;
   double rh, rl;
   int n = reduce_pio2(x, rh, rl);
@@ -401,8 +406,8 @@ AERO_HD double aero_cos(double x) {
 /* sin and cos of x together (one reduction, one table lookup); the same
  * correctly-rounded results as aero_sin / aero_cos */
 AERO_HD void aero_sincos(double x, double &so, double &co) {
-  if (!__builtin_isfinite(x)) {
-    so = co = x - x;
+  if (!__builtin_isfinite(x) || __builtin_fabs(x) >= 0x1p20) {
+    so = co = __builtin_nan("");
     return;
   }
   double rh, rl;

@@ -1,0 +1,68 @@
+"""The C ABI library loads on a CPU-only host, exports every symbol that
+include/aero_engine.h declares, and fails cleanly without a GPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import aero_testlib as tl
+
+HEADER = os.path.join(tl.ROOT, 'include', 'aero_engine.h')
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r'\b(aero_[a-z_]+)\s*\(', src)))
+
+
+def test_library_exports_header_symbols(engine_lib):
+    import aero_engine
+    names = _declared()
+    assert 'aero_push_pcm' in names and 'aero_pop_items' in names
+    for n in names:
+        assert hasattr(engine_lib, n), n
+        assert n in aero_engine._SIGS, 'python mirror lacks ' + n
+
+
+def test_create_without_gpu_is_an_error_not_a_crash(engine_lib):
+    import aero_engine
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip('GPU present')
+    except ImportError:
+        pass
+    with pytest.raises(aero_engine.AeroError) as ei:
+        aero_engine.Engine(4)
+    assert ei.value.rc == aero_engine.AERO_E_NOGPU
+
+
+def test_item_struct_layout():
+    import aero_engine
+    assert ctypes.sizeof(aero_engine.AcarsItem) == 4 + 16 + 4 + 16 + 4 + 3584
+
+
+def test_engine_tables_match_oracle(engine_lib, cpu_libs):
+    """Host tables the engine uploads == the oracle's (same glibc calls)."""
+    L = engine_lib
+    cis = np.zeros(2 * 19999)
+    tw = np.zeros(2 * 16384)
+    twi = np.zeros(2 * 16384)
+    taps = np.zeros(64)
+    n = ctypes.c_int()
+    L.aero_host_tables(cis.ctypes.data_as(ctypes.c_void_p), tw.ctypes.data_as(ctypes.c_void_p),
+                       twi.ctypes.data_as(ctypes.c_void_p), taps.ctypes.data_as(ctypes.c_void_p), ctypes.byref(n))
+    O = tl.Oracle.lib()
+    ocis = np.zeros_like(cis)
+    O.oracle_cis_table(ocis.ctypes.data)
+    otw = np.zeros_like(tw)
+    otwi = np.zeros_like(twi)
+    O.oracle_twiddles(16384, 0, otw.ctypes.data)
+    O.oracle_twiddles(16384, 1, otwi.ctypes.data)
+    otaps = np.zeros(64)
+    O.oracle_rrc_design(1.0, 55, 48000.0, 5250.0, otaps.ctypes.data)
+    assert n.value == 55
+    for a, b in ((cis, ocis), (tw, otw), (twi, otwi), (taps, otaps)):
+        assert np.array_equal(a.view(np.int64), b.view(np.int64))

@@ -1,0 +1,46 @@
+"""aero_math.h (the device libm) compiled for the host vs glibc 2.35, the
+library the reference links.  hypot and tanh are glibc's algorithms and must
+be bit-exact; atan2/sin/cos/log10 are correctly rounded and may differ from
+glibc only where glibc itself is not (<= 1 ulp, rare)."""
+import numpy as np
+import pytest
+
+import mathhost
+
+
+def _inputs(n=1000000, seed=11):
+    r = np.random.default_rng(seed)
+    a = r.uniform(-1, 1, n) * np.exp(r.normal(0, 2, n))
+    b = r.uniform(-1, 1, n) * np.exp(r.normal(0, 2, n))
+    return a, b
+
+
+@pytest.mark.parametrize('fn', ['hypot', 'tanh'])
+def test_bit_exact_with_glibc(fn):
+    a, b = _inputs()
+    assert np.array_equal(mathhost.evaluate(fn, a, b).view(np.int64), mathhost.glibc(fn, a, b).view(np.int64))
+
+
+@pytest.mark.parametrize('fn,scale,rate', [('atan2', None, 0.002), ('sin', 2.0, 0.003), ('cos', 2.0, 0.003),
+                                           ('log10', 'pos', 0.001)])
+def test_correctly_rounded_vs_glibc(fn, scale, rate):
+    a, b = _inputs()
+    x = a
+    if scale == 'pos':
+        x = np.abs(a) * 1e3 + 1.0
+    elif scale:
+        x = a * scale
+    d = mathhost.evaluate(fn, x, b).view(np.int64) - mathhost.glibc(fn, x, b).view(np.int64)
+    assert np.abs(d).max() <= 1
+    assert np.count_nonzero(d) / d.size < rate
+
+
+def test_special_values():
+    x = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, 5e-324, 1e308])
+    y = np.array([0.0, 0.0, -0.0, np.inf, 1.0, -np.inf, 1.0, -1e308])
+    for fn in ('atan2', 'hypot'):
+        h, g = mathhost.evaluate(fn, x, y), mathhost.glibc(fn, x, y)
+        assert np.array_equal(np.signbit(h), np.signbit(g)) and np.allclose(h, g, equal_nan=True), fn
+    for fn in ('tanh', 'sin', 'cos'):
+        xs = x[np.isfinite(x) & (np.abs(x) < 2.0 ** 20)]
+        assert np.allclose(mathhost.evaluate(fn, xs), mathhost.glibc(fn, xs), rtol=1e-15, atol=0), fn
