@@ -16,6 +16,7 @@
 #include <complex>
 #include <cstdio>
 #include <cstring>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <string>
@@ -90,6 +91,25 @@ struct TimingSlot {
   long launches = 0;
 };
 
+// wall-clock host section timer (AERO_F_TIMING), reported as "host_<name>"
+struct HostTimer {
+  std::map<std::string, TimingSlot> *t;
+  const char *name;
+  std::chrono::steady_clock::time_point t0;
+  HostTimer(std::map<std::string, TimingSlot> *tm, const char *n) : t(tm), name(n) {
+    if (t) t0 = std::chrono::steady_clock::now();
+  }
+  ~HostTimer() {
+    if (!t) return;
+    auto &slot = (*t)[name];
+    slot.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    slot.launches++;
+  }
+};
+#define HT_CAT2(a, b) a##b
+#define HT_CAT(a, b) HT_CAT2(a, b)
+#define HOST_TIMER(e, n) HostTimer HT_CAT(_ht_, __LINE__)(((e)->flags & AERO_F_TIMING) ? &(e)->timing : nullptr, n)
+
 }  // namespace
 
 struct aero_engine {
@@ -114,6 +134,7 @@ struct aero_engine {
   std::map<std::string, TimingSlot> timing;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending_ev;
   uint64_t processed = 0;
+  int init_lo = 0;  // channels [init_lo, nch) await device state init
 };
 
 namespace {
@@ -188,9 +209,14 @@ void ev_collect(aero_engine *e) {
   e->pending_ev.clear();
 }
 
-int init_channel_state(aero_engine *e, int c) {
-  // decode/oqpskdemodulator.cpp:9-115 + setSettings(:136-254) as Decoder applies it
-  const int C = e->C;
+// Per-channel scalar state as OqpskDemodulator's ctor + setSettings leave it
+// (decode/oqpskdemodulator.cpp:9-115, :136-254, as Decoder applies them).
+// Opened channels are initialised lazily, one strided copy per field for the
+// whole pending range, so opening thousands of channels costs O(fields).
+int flush_pending_init(aero_engine *e) {
+  const int lo = e->init_lo, hi = e->nch;
+  if (lo >= hi) return AERO_OK;
+  const int C = e->C, k = hi - lo;
   std::vector<double> ds(DS_COUNT, 0.0);
   std::vector<int> is(IS_COUNT, 0);
   std::vector<long long> ls(LS_COUNT, 0);
@@ -201,9 +227,22 @@ int init_channel_state(aero_engine *e, int c) {
   is[IS_COUNTDOWN] = 4;
   is[IS_EMPTYCD] = 1;
   is[IS_CNTR] = 1000000000;
-  for (int f = 0; f < DS_COUNT; f++) HIPCHK(hipMemcpy(e->S.ds + (size_t)f * C + c, &ds[f], 8, hipMemcpyHostToDevice));
-  for (int f = 0; f < IS_COUNT; f++) HIPCHK(hipMemcpy(e->S.is + (size_t)f * C + c, &is[f], 4, hipMemcpyHostToDevice));
-  for (int f = 0; f < LS_COUNT; f++) HIPCHK(hipMemcpy(e->S.ls + (size_t)f * C + c, &ls[f], 8, hipMemcpyHostToDevice));
+  std::vector<double> vd(k);
+  std::vector<int> vi(k);
+  std::vector<long long> vl(k);
+  for (int f = 0; f < DS_COUNT; f++) {
+    std::fill(vd.begin(), vd.end(), ds[f]);
+    HIPCHK(hipMemcpy(e->S.ds + (size_t)f * C + lo, vd.data(), 8 * (size_t)k, hipMemcpyHostToDevice));
+  }
+  for (int f = 0; f < IS_COUNT; f++) {
+    std::fill(vi.begin(), vi.end(), is[f]);
+    HIPCHK(hipMemcpy(e->S.is + (size_t)f * C + lo, vi.data(), 4 * (size_t)k, hipMemcpyHostToDevice));
+  }
+  for (int f = 0; f < LS_COUNT; f++) {
+    std::fill(vl.begin(), vl.end(), ls[f]);
+    HIPCHK(hipMemcpy(e->S.ls + (size_t)f * C + lo, vl.data(), 8 * (size_t)k, hipMemcpyHostToDevice));
+  }
+  e->init_lo = hi;
   return AERO_OK;
 }
 
@@ -217,7 +256,11 @@ int collect_after_pass(aero_engine *e, int njobs) {
       dbg.resize((size_t)2500 * C);
       HIPCHK(hipMemcpyAsync(dbg.data(), e->S.blocks_dbg, dbg.size(), hipMemcpyDeviceToHost, e->st));
     }
-    HIPCHK(hipStreamSynchronize(e->st));
+    {
+      HOST_TIMER(e, "host_wait_jobs");
+      HIPCHK(hipStreamSynchronize(e->st));
+    }
+    HOST_TIMER(e, "host_frames");
     for (int j = 0; j < njobs; j++) {
       const uint8_t *o = e->h_jobout.data() + (size_t)j * JOB_OUT;
       int meta[4];
@@ -301,6 +344,8 @@ int collect_traces(aero_engine *e) {
 
 int run_impl(aero_engine *e, int flush) {
   if (e->nch == 0) return AERO_OK;
+  HOST_TIMER(e, "host_run");
+  if (int rc = flush_pending_init(e)) return rc;
   const int tflags = AERO_F_TRACE_PT | AERO_F_TRACE_BLOCKS | AERO_F_TRACE_SOFT | AERO_F_TRACE_HOPS;
   const bool trace = (e->flags & tflags) != 0;
   for (int guard = 0; guard < 1000000; guard++) {
@@ -341,7 +386,10 @@ int run_impl(aero_engine *e, int flush) {
     ev_end(e, b);
     int njobs = 0;
     HIPCHK(hipMemcpyAsync(&njobs, e->S.njobs, sizeof(int), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(hipStreamSynchronize(e->st));
+    {
+      HOST_TIMER(e, "host_wait_njobs");
+      HIPCHK(hipStreamSynchronize(e->st));
+    }
     if (njobs > 0) {
       ev_begin(e, "viterbi", a, b);
       launch_viterbi(e->st, e->S, e->T, njobs, (e->flags & AERO_F_TRACE_BLOCKS) ? 1 : 0);
@@ -450,9 +498,7 @@ int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) 
   if (e->nch >= e->C) return AERO_E_FULL;
   HIPCHK(hipSetDevice(e->device));
   const int c = e->nch;
-  int rc = init_channel_state(e, c);
-  if (rc) return rc;
-  e->nch++;
+  e->nch++;  // device state initialised by flush_pending_init before the next push/run
   e->cfg.push_back(*cfg);
   e->avail.push_back(0);
   e->nsamp.push_back(0);
@@ -469,6 +515,8 @@ int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) 
 }
 
 static int push_common(aero_engine *e, const int16_t *src, size_t n, size_t ld, int nch, int c0, bool dev) {
+  HOST_TIMER(e, "host_push");
+  if (int rc = flush_pending_init(e)) return rc;
   // keep the ring from overrunning unprocessed samples
   for (int j = 0; j < nch; j++) {
     const int c = c0 + j;

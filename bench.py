@@ -115,11 +115,8 @@ def main():
 
     def step_input(s):
         # [HOP, C] time-major; channel c = g*P + p reads stream p at offset off[g]
-        x = torch.empty((HOP, C), dtype=torch.int16, device='cuda')
-        for g in range(C // P):
-            o = int(offsets[g]) + s * HOP
-            x[:, g * P:(g + 1) * P] = pool[:, o:o + HOP].t()
-        return x
+        views = [pool[:, int(o) + s * HOP:int(o) + (s + 1) * HOP] for o in offsets]
+        return torch.stack(views).permute(2, 0, 1).reshape(HOP, C).contiguous()
 
     eng = ae.Engine(max_channels=C, device=local, flags=ae.F_TIMING)
     for _ in range(C):
@@ -155,6 +152,7 @@ def main():
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed, samples = float(tmax[0]), float(t[1])
     kt = {k: eng.timing(k) for k in ('demod', 'coarse', 'frame', 'viterbi')}
+    ht = {k: eng.timing(k) for k in ('host_push', 'host_run', 'host_wait_njobs', 'host_wait_jobs', 'host_frames')}
     if rank == 0:
         value = samples / elapsed / 1e6
         dm_ms, dm_n = kt['demod']
@@ -181,6 +179,7 @@ def main():
                          'traffic': traffic, 'bytes_per_sample': BYTES_PER_SAMPLE,
                          'avg_launch_ms': round(per_launch_s * 1e3, 3)},
             'kernel_ms_per_step': {k: round(v[0] / max(a.steps, 1), 3) for k, v in kt.items()},
+            'host_ms_per_step': {k: round(v[0] / max(a.steps, 1), 3) for k, v in ht.items()},
         }
         if cpu is not None:
             out['cpu_baseline'] = cpu

@@ -108,8 +108,11 @@ int aero_pop_pt(aero_engine *e, int ch, double *dst, size_t cap_records, size_t 
 int aero_pop_blocks(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
 int aero_pop_frames(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
 
-/* Kernel timing (AERO_F_TIMING): name in {"demod","coarse","frame","viterbi"};
- * returns summed device milliseconds and launch count since the last reset. */
+/* Timing (AERO_F_TIMING): kernel names {"demod","coarse","frame","viterbi"}
+ * give summed device milliseconds (HIP events) and launch counts; host
+ * sections {"host_push","host_run","host_wait_njobs","host_wait_jobs",
+ * "host_frames"} give summed wall milliseconds and entry counts.  Both since
+ * the last reset. */
 int aero_timing(aero_engine *e, const char *name, double *ms, long *launches);
 void aero_timing_reset(aero_engine *e);
 
