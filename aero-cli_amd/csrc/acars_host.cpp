@@ -233,55 +233,46 @@ void PChannelHost::send_logon(const uint8_t *info, int k, const char *text) {
   if (!fragments_only_) emit(item, false);
 }
 
+// SU k's line of the reference's per-frame `decline` text (aerol.cpp:1522-1536):
+// only C-channel-assignment items carry it, so it is built on demand.
+static std::string decline_prefix(const uint8_t *su, int k, int formatid) {
+  static const char H[] = "0123456789ABCDEF";
+  std::string d;
+  if (k == 0 && formatid != 1) d += "format ID error\n";
+  d += (char)(k + '0');
+  for (int j = 0; j < 10; j++) {
+    const char b[6] = {' ', '0', 'x', H[su[j] >> 4], H[su[j] & 15], 0};
+    d += b;
+  }
+  d += ' ';
+  return d;
+}
+
 // frame-done SU loop (aerol.cpp:1522-1990): only the branches that emit items
 void PChannelHost::frame(const uint8_t *info, int len, uint32_t okmask, int formatid) {
-  std::string decline;
-  if (formatid != 1) decline += "format ID error\n";
   for (int k = 0; k < len / 12; k++) {
+    if (!(okmask & (1u << k))) continue;
     const uint8_t *su = info + 12 * k;
-    decline += (char)(k + '0');
-    for (int j = 0; j < 10; j++) {
-      char b[8];
-      snprintf(b, sizeof b, " 0x%02X", su[j]);
-      decline += b;
+    const uint8_t m = su[0];
+    bool missing;
+    const char *what = nullptr;
+    switch (m) {
+      case 0x11:
+        send_logon(info, k, "Log on confirm");
+        break;
+      case 0x31: what = "C_channel_assignment_distress"; break;
+      case 0x32: what = "C_channel_assignment_flight_safety"; break;
+      case 0x33: what = "C_channel_assignment_other_safety"; break;
+      case 0x34: what = "C_channel_assignment_non_safety"; break;
+      case 0x21: what = "Call_announcement"; break;
+      case 0x71:
+        isu_update(su, missing);
+        break;
+      default:
+        if ((m & 0xC0) == 0xC0 && isu_update(su, missing)) parse(lastvalid_);
+        break;
     }
-    if (okmask & (1u << k)) {
-      decline += " ";
-      const uint8_t m = su[0];
-      bool missing;
-      switch (m) {
-        case 0x11:
-          send_logon(info, k, "Log on confirm");
-          break;
-        case 0x31:
-          decline += "C_channel_assignment_distress";
-          send_cassign(info, k, decline);
-          break;
-        case 0x32:
-          decline += "C_channel_assignment_flight_safety";
-          send_cassign(info, k, decline);
-          break;
-        case 0x33:
-          decline += "C_channel_assignment_other_safety";
-          send_cassign(info, k, decline);
-          break;
-        case 0x34:
-          decline += "C_channel_assignment_non_safety";
-          send_cassign(info, k, decline);
-          break;
-        case 0x21:
-          decline += "Call_announcement";
-          send_cassign(info, k, decline);
-          break;
-        case 0x71:
-          isu_update(su, missing);
-          break;
-        default:
-          if ((m & 0xC0) == 0xC0 && isu_update(su, missing)) parse(lastvalid_);
-          break;
-      }
-    }
-    decline.clear();
+    if (what) send_cassign(info, k, decline_prefix(su, k, formatid) + what);
   }
 }
 

@@ -257,7 +257,7 @@ AERO_HD dd dd_atan01(double th, double tl) {
   return dd_add(dd{aero_atan_tab[k][0], aero_atan_tab[k][1]}, r);
 }
 
-AERO_HD double aero_atan2(double y, double x) {
+AERO_HD double aero_atan2_dd(double y, double x) {
   if (__builtin_isnan(x) || __builtin_isnan(y)) return x + y;
   bool ny = __builtin_signbit(y) != 0, nx = __builtin_signbit(x) != 0;
   double ay = __builtin_fabs(y), ax = __builtin_fabs(x);
@@ -301,6 +301,63 @@ AERO_HD double aero_atan2(double y, double x) {
   if (nx) r = dd_add(dd{AERO_PI_HI, AERO_PI_LO}, dd_neg(r));
   double out = r.hi + r.lo;
   return ny ? -out : out;
+}
+
+/* reciprocal to ~2^-100 relative after two Newton steps (device: v_rcp_f64) */
+AERO_HD double approx_rcp(double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp(b);
+#else
+  double r = 1.0 / b;
+#endif
+  r = fma(r, fma(-b, r, 1.0), r);
+  r = fma(r, fma(-b, r, 1.0), r);
+  return r;
+}
+
+/* atan2 fast path (Ziv): atan(t) = atan(k/64) + atan(u) evaluated to about
+ * 2^-65 relative without any IEEE division, returned only when that bound
+ * proves the rounding; otherwise (≈2^-10 of arguments, and every special or
+ * extreme-exponent argument) the double-double path decides.  Same results
+ * as aero_atan2_dd by construction (tests/test_math_host.py compares them). */
+AERO_HD double aero_atan2(double y, double x) {
+  const double ay = __builtin_fabs(y), ax = __builtin_fabs(x);
+  if (!(ax >= 0x1p-500 && ax <= 0x1p500 && ay >= 0x1p-500 && ay <= 0x1p500)) return aero_atan2_dd(y, x);
+  const bool swap = ay > ax;
+  const double a = swap ? ax : ay, b = swap ? ay : ax;  // t = a/b in (0, 1]
+  const double rb = approx_rcp(b);
+  const double th = a * rb;
+  const double tl = fma(-th, b, a) * rb;
+  const int k = (int)(th * 64.0 + 0.5);
+  const double c = (double)k * (1.0 / 64.0);
+  // u = (t - c) / (1 + t c), |u| <= 2^-7
+  const dd num = two_sum(th - c, tl);  // th - c exact (Sterbenz)
+  const double ph = th * c, pl = fma(th, c, -ph);
+  const dd den0 = two_sum(1.0, ph);
+  const double dh = den0.hi, dl = den0.lo + (pl + tl * c);
+  const double rd = approx_rcp(dh);
+  const double uh = num.hi * rd;
+  const double ul = ((fma(-uh, dh, num.hi) + num.lo) - uh * dl) * rd;
+  // atan(u) - u = u^3 (-1/3 + u^2/5 - ...) - u^2 ul
+  const double v = uh * uh;
+  double p = -1.0 / 15;
+  p = 1.0 / 13 + v * p;
+  p = -1.0 / 11 + v * p;
+  p = 1.0 / 9 + v * p;
+  p = -1.0 / 7 + v * p;
+  p = 1.0 / 5 + v * p;
+  p = -AERO_INV3_HI + v * p;
+  const double corr = (v * uh) * p - v * ul;
+  // atan(t) = A + u + corr
+  dd r = two_sum(aero_atan_tab[k][0], uh);
+  r.lo += aero_atan_tab[k][1] + (ul + corr);
+  r = quick_two_sum(r.hi, r.lo);
+  if (swap) r = dd_add(dd{AERO_PI_2_HI, AERO_PI_2_LO}, dd_neg(r));
+  if (__builtin_signbit(x)) r = dd_add(dd{AERO_PI_HI, AERO_PI_LO}, dd_neg(r));
+  const double e = 0x1p-63 * __builtin_fabs(r.hi);
+  const double out = r.hi + r.lo;
+  if (out != r.hi + (r.lo + e) || out != r.hi + (r.lo - e)) return aero_atan2_dd(y, x);
+  return __builtin_signbit(y) ? -out : out;
 }
 
 /* sin/cos of r = rh + rl, |r| <= pi/4 + eps, as double-double */

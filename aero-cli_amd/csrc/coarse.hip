@@ -37,8 +37,17 @@ __device__ __forceinline__ int bitrev14(int p) { return (int)(__builtin_bitrever
 
 // one radix-2 DIT stage of half-size n on the thread's 16 values;
 // `lb` is the bit of i that encodes the stage's position bit.
+// `t` is laundered at every stage/exchange so the compiler recomputes the
+// (cheap) per-thread positions instead of keeping hundreds of addresses live
+// across the three transforms (that is what spilled).
+__device__ __forceinline__ int fresh(int t) {
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 template <int PH>
-__device__ __forceinline__ void stage(double2 (&x)[16], int t, int lb, int n, const double2 *__restrict__ TW) {
+__device__ __forceinline__ void stage(double2 (&x)[16], int t0, int lb, int n, const double2 *__restrict__ TW) {
+  const int t = fresh(t0);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     if (i & (1 << lb)) continue;
@@ -57,9 +66,10 @@ __device__ __forceinline__ void stage(double2 (&x)[16], int t, int lb, int n, co
 // move values from layout PH_FROM to PH_TO through LDS (re then im);
 // BR: the destination reads bit-reversed positions (start of a new transform)
 template <int PH_FROM, int PH_TO, bool BR>
-__device__ __forceinline__ void exchange(double2 (&x)[16], int t, double *lds) {
+__device__ __forceinline__ void exchange(double2 (&x)[16], int t0, double *lds) {
 #pragma unroll
   for (int part = 0; part < 2; ++part) {
+    const int t = fresh(t0);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 16; ++i) lds[pad(epos<PH_FROM>(t, i))] = part ? x[i].y : x[i].x;

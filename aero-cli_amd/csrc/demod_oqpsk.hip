@@ -56,11 +56,12 @@ __device__ __forceinline__ void set_freq(double &freq, double &step, double f) {
 // Delay<double>::update (DSP.h:365-384) as a shift register; the reference's
 // ring index and fractional weight depend only on the write pointer p.
 template <int N>
-__device__ __forceinline__ double delay_update(double (&h)[N], int &p, const DelayDesc &d, double sig) {
+__device__ __forceinline__ double delay_update(double (&h)[N], int &p, const DelayDesc &d, const double *wl,
+                                               const double *omwl, double sig) {
 #pragma unroll
   for (int i = N - 1; i > 0; --i) h[i] = h[i - 1];
   h[0] = sig;
-  const double w = d.w[p], omw = d.omw[p];  // per-pointer weights, loaded each call
+  const double w = wl[p], omw = omwl[p];  // per-pointer weights (LDS copy of d.w / d.omw)
   double older = h[0], newer = h[0];
 #pragma unroll
   for (int a = 0; a < N; ++a) {
@@ -93,10 +94,27 @@ __device__ __forceinline__ int qround(double d) {  // qRound (Qt 5.9 qglobal.h:5
 
 template <bool TRACE>
 __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables T, int nch, int flush) {
+  // LDS: RRC taps and delay weights (uniform / tiny per-lane gathers that
+  // would otherwise be global loads every sample), and the coarse-ring
+  // staging area: entries of 16 consecutive samples are collected here and
+  // leave as one 64-byte write per channel instead of sixteen 4-byte ones.
+  __shared__ double s_taps[NTAPS + 1];
+  __shared__ double s_dw[4][4], s_domw[4][4];
+  __shared__ uint32_t s_ring[16][128];
+  {
+    const int l = threadIdx.x;
+    if (l < NTAPS) s_taps[l] = T.taps[l];
+    if (l < 16) {
+      s_dw[l >> 2][l & 3] = c_dly[l >> 2].w[l & 3];
+      s_domw[l >> 2][l & 3] = c_dly[l >> 2].omw[l & 3];
+    }
+    __syncthreads();
+  }
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int c = tid >> 1;
   const int part = tid & 1;
   const bool lead = part == 0;
+  const int pair = threadIdx.x >> 1;
   if (c >= nch) return;  // nch channels -> 2 nch lanes; pairs never straddle the check
   const int C = S.C;
   double *ds = S.ds;
@@ -161,29 +179,41 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
   uint8_t *soft = S.soft + (size_t)c * SOFT_RING;
   const double PT = 0.4 * WTSIZE;  // IfHavePassedPoint(ee) with ee = 0.4 (oqpskdemodulator.cpp:225)
 
+  const long long m_first = n + 1;  // first coarse-ring entry staged by this launch
+  // sample n's PCM word and AGC ring slot are always loaded one sample ahead
+  int16_t pcm_next = S.pcm[(n & capm) * C + c];
+  double agc_next = S.agc[(size_t)agc_ptr * C + c];
   for (; n < end; ++n) {
-    const int16_t xs = S.pcm[(n & capm) * C + c];
+    const int16_t xs = pcm_next;
+    const double agc_old = agc_next;
+    // table lookups of this sample first, then the prefetch for n+1, so the
+    // in-order vmcnt waits below never wait on the prefetch
+    const double2 cm = T.cis[cis_index(m2_ptr)];
+    const double2 so = T.cis[cis_index(so_ptr)];
+    {
+      const int ap = agc_ptr + 1 == AGC_LEN ? 0 : agc_ptr + 1;
+      pcm_next = S.pcm[((n + 1) & capm) * C + c];
+      agc_next = S.agc[(size_t)ap * C + c];
+    }
     const double dval = ((double)xs) / 32768.0;
     // mix (oqpskdemodulator.cpp:390): this lane's component of cval
-    const double2 cm = T.cis[cis_index(m2_ptr)];
     const double cv = (part ? cm.y : cm.x) * dval;
     // rrc (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
     const double mine = q[NTAPS - 1];
-    // taps through a laundered scalar pointer: re-read (s_load) every sample
-    // instead of pinning 110 VGPRs of loop invariants
-    const double *tp = T.taps;
-    asm volatile("" : "+s"(tp));
+    // taps from LDS through an opaque offset: re-read every sample instead of
+    // pinning 110 VGPRs of loop invariants
+    int toff = 0;
+    asm volatile("" : "+v"(toff));
 #pragma unroll
-    for (int j = NTAPS - 1; j >= 1; --j) q[j] = q[j - 1] + tp[j] * cv;
-    q[0] = 0.0 + tp[0] * cv;
+    for (int j = NTAPS - 1; j >= 1; --j) q[j] = q[j - 1] + s_taps[j + toff] * cv;
+    q[0] = 0.0 + s_taps[toff] * cv;
     const double other = __shfl_xor(mine, 1, 64);
     double s2r = part ? other : mine, s2i = part ? mine : other;
     // AGC (DSP.cpp:371-380) on |sig2| (oqpskdemodulator.cpp:399-405)
     const double dab = sqrt(s2r * s2r + s2i * s2i);
     {
       double *slot = S.agc + (size_t)agc_ptr * C + c;
-      const double old = *slot;
-      agc_sum = agc_sum - old;
+      agc_sum = agc_sum - agc_old;
       agc_sum = agc_sum + fabs(dab);
       if (lead) *slot = fabs(dab);
       agc_ptr++;
@@ -201,13 +231,12 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
       s2i = k * s2i;
     }
     // symbol timer (:413-426)
-    const double st_diff = delay_update(d1, p1, c_dly[0], ab * ab) - (ab * ab);
-    const double st_d1out = delay_update(d41, p41, c_dly[1], st_diff);
-    const double st_d2out = delay_update(d42, p42, c_dly[2], st_d1out);
+    const double st_diff = delay_update(d1, p1, c_dly[0], s_dw[0], s_domw[0], ab * ab) - (ab * ab);
+    const double st_d1out = delay_update(d41, p41, c_dly[1], s_dw[1], s_domw[1], st_diff);
+    const double st_d2out = delay_update(d42, p42, c_dly[2], s_dw[2], s_domw[2], st_d1out);
     double st_eta = (st_d2out - st_diff) * st_d1out;
     st_eta = iir3(srx1, srx2, sry1, sry2, c_sr_b, c_sr_a, st_eta);
-    const double m1r = st_eta, m1i = -delay_update(d8, p8, c_dly[3], st_eta);
-    const double2 so = T.cis[cis_index(so_ptr)];
+    const double m1r = st_eta, m1i = -delay_update(d8, p8, c_dly[3], s_dw[3], s_domw[3], st_eta);
     const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
     const double st_angle_error = aero_atan2(oim, ore);
     set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
@@ -236,6 +265,13 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
         ptd_re = pr;
         ptd_im = pi;
       } else {
+        // the four moving-average rings of this symbol, loaded together
+        // before any ring store so their latencies overlap
+        const int dt_rp = (dt_p + 1) % DT_LEN;
+        const double marg_old = marg[marg_p];
+        const double2 dv = dtb[dt_rp];
+        const double pm_old = pmb[pm_p];
+        const double ms_old = msb[ms_p];
         double qr = pr, qi = ptd_im;  // pt_qpsk
         // carrier tracking (:456-470); the two tanh split across the pair
         const double th = aero_tanh(part ? ptd_re : pi);
@@ -257,7 +293,7 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
         }
         set_freq(m2_freq, m2_step, 0.01 * ct_ec + m2_freq);  // IncreseFreqHz
         // marg->UpdateSigned (DSP.cpp:419-427)
-        marg_sum = marg_sum - marg[marg_p];
+        marg_sum = marg_sum - marg_old;
         marg_sum = marg_sum + (ct_ec);
         if (lead) marg[marg_p] = ct_ec;
         marg_p++;
@@ -265,10 +301,8 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
         const double mval = marg_sum / ((double)MARG_LEN);
         // dt.update (DSP.h:456-461): slot p written, slot p+1 read
         {
-          const int rp = (dt_p + 1) % DT_LEN;
-          const double2 dv = dtb[rp];
           if (lead) dtb[dt_p] = make_double2(qr, qi);
-          dt_p = rp;
+          dt_p = dt_rp;
           qr = dv.x;
           qi = dv.y;
         }
@@ -284,7 +318,7 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
         // MSEcalc::Update (DSP.cpp:449-461)
         {
           const double av = aero_hypot(qr, qi);
-          pm_sum = pm_sum - pmb[pm_p];
+          pm_sum = pm_sum - pm_old;
           pm_sum = pm_sum + fabs(av);
           if (lead) pmb[pm_p] = fabs(av);
           pm_p++;
@@ -294,7 +328,7 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
           const double tr = (1.4142135623730951 * qr) / mu, ti = (1.4142135623730951 * qi) / mu;
           const double tda = (fabs(tr) - 1.0), tdb = (fabs(ti) - 1.0);
           const double v = (tda * tda) + (tdb * tdb);
-          ms_sum = ms_sum - msb[ms_p];
+          ms_sum = ms_sum - ms_old;
           ms_sum = ms_sum + fabs(v);
           if (lead) msb[ms_p] = fabs(v);
           ms_p++;
@@ -322,12 +356,32 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
     nco_next(mc_ptr, mc_step);
     so_last = so_ptr;
     nco_next(so_ptr, so_step);
-    // coarse-ring fill of the next sample (:351-356)
+    // coarse-ring fill of the next sample (:351-356), staged in LDS
     if (n + 1 < avail) {
-      const int16_t xn = S.pcm[((n + 1) & capm) * C + c];
-      if (lead) cring[(n + 1) & (NFFT - 1)] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)xn << 16);
+      const long long m = n + 1;
+      const int k = (int)(m & 15);
+      if (lead) {
+        s_ring[k][pair] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)pcm_next << 16);
+        if (k == 15) {
+          uint32_t *dst = cring + ((m - 15) & (NFFT - 1));
+          if (m - 15 >= m_first) {
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4)
+              reinterpret_cast<uint4 *>(dst)[q4] = make_uint4(s_ring[4 * q4][pair], s_ring[4 * q4 + 1][pair],
+                                                              s_ring[4 * q4 + 2][pair], s_ring[4 * q4 + 3][pair]);
+          } else {
+            for (int j = (int)(m_first - (m - 15)); j < 16; ++j) dst[j] = s_ring[j][pair];
+          }
+        }
+      }
       filled = n + 2;
     }
+  }
+  // staged entries of an unfinished 16-sample group
+  if (lead && filled - 1 >= m_first && ((filled - 1) & 15) != 15) {
+    const long long last = filled - 1, g0 = last & ~15LL;
+    uint32_t *dst = cring + (g0 & (NFFT - 1));
+    for (int j = (int)((g0 >= m_first ? g0 : m_first) - g0); j <= (int)(last - g0); ++j) dst[j] = s_ring[j][pair];
   }
 
   // epilogue addresses are recomputed from a laundered channel index so the

@@ -15,11 +15,13 @@
 #include <cmath>
 #include <complex>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <chrono>
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/aero_engine.h"
@@ -135,6 +137,7 @@ struct aero_engine {
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending_ev;
   uint64_t processed = 0;
   int init_lo = 0;  // channels [init_lo, nch) await device state init
+  int host_threads = 1;
 };
 
 namespace {
@@ -261,32 +264,47 @@ int collect_after_pass(aero_engine *e, int njobs) {
       HIPCHK(hipStreamSynchronize(e->st));
     }
     HOST_TIMER(e, "host_frames");
-    for (int j = 0; j < njobs; j++) {
-      const uint8_t *o = e->h_jobout.data() + (size_t)j * JOB_OUT;
-      int meta[4];
-      memcpy(meta, o + 312, 16);
-      const int c = meta[3] & 0x3FFFFFFF;
-      const int reset = (meta[3] >> 30) & 1;
-      if (c < 0 || c >= nch) continue;
-      if (e->flags & AERO_F_TRACE_BLOCKS) {
-        const uint8_t *d = dbg.data() + (size_t)c * 2500;
-        int nb;
-        memcpy(&nb, d, 4);
-        uint32_t L = (uint32_t)nb;
-        auto &h = e->blk_hold[c];
-        h.insert(h.end(), (uint8_t *)&L, (uint8_t *)&L + 4);
-        h.insert(h.end(), d + 4, d + 4 + nb);
+    // host SU/ACARS work, channels partitioned over threads (c % T): a
+    // channel's frames stay in queue order and no two threads share state
+    auto work = [&](int t, int T) {
+      for (int j = 0; j < njobs; j++) {
+        const uint8_t *o = e->h_jobout.data() + (size_t)j * JOB_OUT;
+        int meta[4];
+        memcpy(meta, o + 312, 16);
+        const int c = meta[3] & 0x3FFFFFFF;
+        const int reset = (meta[3] >> 30) & 1;
+        if (c < 0 || c >= nch || c % T != t) continue;
+        if (e->flags & AERO_F_TRACE_BLOCKS) {
+          const uint8_t *d = dbg.data() + (size_t)c * 2500;
+          int nb;
+          memcpy(&nb, d, 4);
+          uint32_t L = (uint32_t)nb;
+          auto &h = e->blk_hold[c];
+          h.insert(h.end(), (uint8_t *)&L, (uint8_t *)&L + 4);
+          h.insert(h.end(), d + 4, d + 4 + nb);
+        }
+        if (reset) e->host[c]->isu_reset();
+        if (meta[0] >= 0) {
+          e->host[c]->frame(o, meta[0], (uint32_t)meta[1], meta[2]);
+          if (e->flags & AERO_F_TRACE_FRAMES) {
+            uint8_t rec[320] = {0};
+            memcpy(rec, o, 312);
+            const uint32_t L = (uint32_t)meta[0], M = (uint32_t)meta[1];
+            memcpy(rec + 312, &L, 4);
+            memcpy(rec + 316, &M, 4);
+            e->frame_hold[c].insert(e->frame_hold[c].end(), rec, rec + 320);
+          }
+        }
       }
-      if (reset) e->host[c]->isu_reset();
-      if (meta[0] >= 0) {
-        e->host[c]->frame(o, meta[0], (uint32_t)meta[1], meta[2]);
-        uint8_t rec[320] = {0};
-        memcpy(rec, o, 312);
-        const uint32_t L = (uint32_t)meta[0], M = (uint32_t)meta[1];
-        memcpy(rec + 312, &L, 4);
-        memcpy(rec + 316, &M, 4);
-        e->frame_hold[c].insert(e->frame_hold[c].end(), rec, rec + 320);
-      }
+    };
+    const int T = std::max(1, std::min<int>({e->host_threads, njobs / 64, nch}));
+    if (T == 1) {
+      work(0, 1);
+    } else {
+      std::vector<std::thread> th;
+      for (int t = 1; t < T; t++) th.emplace_back(work, t, T);
+      work(0, T);
+      for (auto &x : th) x.join();
     }
   }
   return AERO_OK;
@@ -443,6 +461,13 @@ int aero_engine_create(const aero_engine_cfg *cfg, aero_engine **out) {
   std::unique_ptr<aero_engine> e(new aero_engine());
   e->device = cfg->device;
   e->flags = cfg->flags;
+  {
+    // host threads for the per-frame SU/ACARS work (AERO_HOST_THREADS overrides)
+    const char *ev = getenv("AERO_HOST_THREADS");
+    const int hw = (int)std::thread::hardware_concurrency();
+    e->host_threads = ev ? atoi(ev) : std::min(16, std::max(1, hw));
+    if (e->host_threads < 1) e->host_threads = 1;
+  }
   e->C = (cfg->max_channels + 63) & ~63;
   DevState S{};
   DevTables T{};

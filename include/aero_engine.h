@@ -36,6 +36,7 @@ extern "C" {
 #define AERO_F_TIMING 0x4      /* HIP-event timing of every kernel launch            */
 #define AERO_F_TRACE_SOFT 0x8  /* keep delivered soft bits for aero_pop_softbits      */
 #define AERO_F_TRACE_HOPS 0x10 /* keep per-hop coarse-estimator records              */
+#define AERO_F_TRACE_FRAMES 0x20 /* keep per-frame infofield records (aero_pop_frames) */
 
 typedef struct aero_engine aero_engine;
 
@@ -102,7 +103,8 @@ int aero_pop_items(aero_engine *e, int ch, aero_acars_item *dst, size_t cap, siz
  * hops: 6 doubles per coarse hop (sample index, estimate, mixer2 Hz,
  * mixer_center Hz, mse, signal). pt: 2 doubles per carrier event.
  * blocks: uint32 count + decoded bits (bytes 0/1) per Viterbi block.
- * frames: 320 bytes per completed frame (312 infofield, u32 len, u32 crc mask). */
+ * frames: 320 bytes per completed frame (312 infofield, u32 len, u32 crc mask);
+ * needs AERO_F_TRACE_FRAMES. */
 int aero_pop_hops(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n);
 int aero_pop_pt(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n);
 int aero_pop_blocks(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);

@@ -44,3 +44,19 @@ def test_special_values():
     for fn in ('tanh', 'sin', 'cos'):
         xs = x[np.isfinite(x) & (np.abs(x) < 2.0 ** 20)]
         assert np.allclose(mathhost.evaluate(fn, xs), mathhost.glibc(fn, xs), rtol=1e-15, atol=0), fn
+
+
+def test_atan2_fast_path_equals_double_double():
+    """The Ziv fast path of aero_atan2 must return exactly what the
+    double-double path returns (it falls back whenever its bound is unsure)."""
+    rng = np.random.default_rng(7)
+    n = 1_000_000
+    x = rng.standard_normal(n)
+    ys = [rng.standard_normal(n),                                   # generic
+          x * (1 + rng.standard_normal(n) * 1e-9),                  # |t| near 1
+          rng.integers(0, 65, n) / 64 * x * (1 + rng.standard_normal(n) * 1e-13),  # t near k/64
+          rng.standard_normal(n) * np.exp(rng.uniform(-700, 700, n))]            # extreme ratios
+    for y in ys:
+        a = mathhost.evaluate('atan2', y, x).view(np.int64)
+        b = mathhost.evaluate('atan2_dd', y, x).view(np.int64)
+        assert np.array_equal(a, b)

@@ -21,6 +21,7 @@ extern "C" void aero_math_host_eval(int fn, const double *x, const double *y, do
       case 8: r = a / b; break;
       case 9: { double s, c; aero::aero_sincos(a, s, c); r = s; break; }
       case 10: { double s, c; aero::aero_sincos(a, s, c); r = c; break; }
+      case 11: r = aero::aero_atan2_dd(a, b); break;
       default: break;
     }
     out[i] = r;
