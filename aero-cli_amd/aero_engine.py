@@ -73,6 +73,8 @@ _SIGS = {
                                          ctypes.POINTER(ctypes.c_size_t)]),
     'aero_pop_items': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(AcarsItem), ctypes.c_size_t,
                                       ctypes.POINTER(ctypes.c_size_t)]),
+    'aero_pop_items_all': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AcarsItem), ctypes.POINTER(ctypes.c_int),
+                                          ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
     'aero_pop_hops': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                      ctypes.POINTER(ctypes.c_size_t)]),
     'aero_pop_pt': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
@@ -231,6 +233,21 @@ class Engine:
             out.extend(item_line(arr[i]) for i in range(n.value))
             if n.value < 64:
                 return out
+
+    def drain_items(self, lines=False, cap=4096):
+        """Pops the items of every channel (aero_pop_items_all).  Returns the
+        count, or (channel, canonical line) pairs with lines=True."""
+        arr = (AcarsItem * cap)()
+        chs = (ctypes.c_int * cap)()
+        total, out = 0, []
+        while True:
+            n = ctypes.c_size_t()
+            _check(self.lib.aero_pop_items_all(self.h, arr, chs, cap, ctypes.byref(n)), 'aero_pop_items_all')
+            total += n.value
+            if lines:
+                out.extend((chs[i], item_line(arr[i])) for i in range(n.value))
+            if n.value < cap:
+                return out if lines else total
 
     def timing(self, name):
         ms = ctypes.c_double()

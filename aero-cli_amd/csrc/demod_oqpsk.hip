@@ -88,6 +88,14 @@ __device__ __forceinline__ double iir3(double &x1, double &x2, double &y1, doubl
   return y;
 }
 
+// value of the other lane of this lane's pair (DPP quad_perm [1,0,3,2])
+__device__ __forceinline__ double pair_swap(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), 0xB1, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
 __device__ __forceinline__ int qround(double d) {  // qRound (Qt 5.9 qglobal.h:525)
   return d >= 0.0 ? int(d + 0.5) : int(d - double(int(d - 1)) + 0.5) + int(d - 1);
 }
@@ -183,198 +191,221 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
   // sample n's PCM word and AGC ring slot are always loaded one sample ahead
   int16_t pcm_next = S.pcm[(n & capm) * C + c];
   double agc_next = S.agc[(size_t)agc_ptr * C + c];
-  for (; n < end; ++n) {
-    const int16_t xs = pcm_next;
-    const double agc_old = agc_next;
-    // table lookups of this sample first, then the prefetch for n+1, so the
-    // in-order vmcnt waits below never wait on the prefetch
-    const double2 cm = T.cis[cis_index(m2_ptr)];
-    const double2 so = T.cis[cis_index(so_ptr)];
-    {
-      const int ap = agc_ptr + 1 == AGC_LEN ? 0 : agc_ptr + 1;
-      pcm_next = S.pcm[((n + 1) & capm) * C + c];
-      agc_next = S.agc[(size_t)ap * C + c];
-    }
-    const double dval = ((double)xs) / 32768.0;
-    // mix (oqpskdemodulator.cpp:390): this lane's component of cval
-    const double cv = (part ? cm.y : cm.x) * dval;
-    // rrc (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
-    const double mine = q[NTAPS - 1];
-    // taps from LDS through an opaque offset: re-read every sample instead of
-    // pinning 110 VGPRs of loop invariants
-    int toff = 0;
-    asm volatile("" : "+v"(toff));
+  // Event-aligned iteration.  The carrier/MSE/soft-bit step runs at every
+  // second sample instant (one channel in ~9 samples), but in lockstep
+  // sample order some lane of a wave has one at almost every sample, so the
+  // whole wave would pay for it every sample.  Instead each lane runs its
+  // own samples until its next carrier event (inner loop), and the carrier
+  // step then runs once for all lanes together.  Per lane the operations and
+  // their order are exactly the reference's; only the interleaving of
+  // different channels changes.
+  double ev_pr = 0.0, ev_pi = 0.0;
+  while (n < end) {
+    bool pend = false;
+    do {
+      const int16_t xs = pcm_next;
+      const double agc_old = agc_next;
+      // table lookups of this sample first, then the prefetch for n+1, so the
+      // in-order vmcnt waits below never wait on the prefetch
+      const double2 cm = T.cis[cis_index(m2_ptr)];
+      const double2 so = T.cis[cis_index(so_ptr)];
+      {
+        const int ap = agc_ptr + 1 == AGC_LEN ? 0 : agc_ptr + 1;
+        pcm_next = S.pcm[((n + 1) & capm) * C + c];
+        agc_next = S.agc[(size_t)ap * C + c];
+      }
+      const double dval = ((double)xs) / 32768.0;
+      // mix (oqpskdemodulator.cpp:390): this lane's component of cval
+      const double cv = (part ? cm.y : cm.x) * dval;
+      // rrc (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
+      const double mine = q[NTAPS - 1];
+      // taps from LDS through an opaque offset: re-read every sample instead of
+      // pinning 110 VGPRs of loop invariants
+      int toff = 0;
+      asm volatile("" : "+v"(toff));
 #pragma unroll
-    for (int j = NTAPS - 1; j >= 1; --j) q[j] = q[j - 1] + s_taps[j + toff] * cv;
-    q[0] = 0.0 + s_taps[toff] * cv;
-    const double other = __shfl_xor(mine, 1, 64);
-    double s2r = part ? other : mine, s2i = part ? mine : other;
-    // AGC (DSP.cpp:371-380) on |sig2| (oqpskdemodulator.cpp:399-405)
-    const double dab = sqrt(s2r * s2r + s2i * s2i);
-    {
-      double *slot = S.agc + (size_t)agc_ptr * C + c;
-      agc_sum = agc_sum - agc_old;
-      agc_sum = agc_sum + fabs(dab);
-      if (lead) *slot = fabs(dab);
-      agc_ptr++;
-      if (agc_ptr == AGC_LEN) agc_ptr = 0;
-      double g = 1.414213562 / fmax(agc_sum / ((double)AGC_LEN), 0.000001);
-      g = fmax(g, 0.000001);
-      s2r *= g;
-      s2i *= g;
-    }
-    // clipping (:408-410)
-    const double ab = aero_hypot(s2r, s2i);
-    if (ab > 2.84) {
-      const double k = 2.84 / ab;
-      s2r = k * s2r;
-      s2i = k * s2i;
-    }
-    // symbol timer (:413-426)
-    const double st_diff = delay_update(d1, p1, c_dly[0], s_dw[0], s_domw[0], ab * ab) - (ab * ab);
-    const double st_d1out = delay_update(d41, p41, c_dly[1], s_dw[1], s_domw[1], st_diff);
-    const double st_d2out = delay_update(d42, p42, c_dly[2], s_dw[2], s_domw[2], st_d1out);
-    double st_eta = (st_d2out - st_diff) * st_d1out;
-    st_eta = iir3(srx1, srx2, sry1, sry2, c_sr_b, c_sr_a, st_eta);
-    const double m1r = st_eta, m1i = -delay_update(d8, p8, c_dly[3], s_dw[3], s_domw[3], st_eta);
-    const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
-    const double st_angle_error = aero_atan2(oim, ore);
-    set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
-    so_ptr += (-st_angle_error * 0.01 / 360.0) * WTSIZE;
-    while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
-    while (so_ptr < 0) so_ptr += WTSIZE;
-    if (so_freq < (10500.0 - 0.1)) set_freq(so_freq, so_step, (10500.0 - 0.1));
-    if (so_freq > (10500.0 + 0.1)) set_freq(so_freq, so_step, (10500.0 + 0.1));
-    if (!s2l_init) {
+      for (int j = NTAPS - 1; j >= 1; --j) q[j] = q[j - 1] + s_taps[j + toff] * cv;
+      q[0] = 0.0 + s_taps[toff] * cv;
+      const double other = pair_swap(mine);
+      double s2r = part ? other : mine, s2i = part ? mine : other;
+      // AGC (DSP.cpp:371-380) on |sig2| (oqpskdemodulator.cpp:399-405)
+      const double dab = sqrt(s2r * s2r + s2i * s2i);
+      {
+        double *slot = S.agc + (size_t)agc_ptr * C + c;
+        agc_sum = agc_sum - agc_old;
+        agc_sum = agc_sum + fabs(dab);
+        if (lead) *slot = fabs(dab);
+        agc_ptr++;
+        if (agc_ptr == AGC_LEN) agc_ptr = 0;
+        double g = 1.414213562 / fmax(agc_sum / ((double)AGC_LEN), 0.000001);
+        g = fmax(g, 0.000001);
+        s2r *= g;
+        s2i *= g;
+      }
+      // clipping (:408-410)
+      const double ab = aero_hypot(s2r, s2i);
+      if (ab > 2.84) {
+        const double k = 2.84 / ab;
+        s2r = k * s2r;
+        s2i = k * s2i;
+      }
+      // symbol timer (:413-426)
+      const double st_diff = delay_update(d1, p1, c_dly[0], s_dw[0], s_domw[0], ab * ab) - (ab * ab);
+      const double st_d1out = delay_update(d41, p41, c_dly[1], s_dw[1], s_domw[1], st_diff);
+      const double st_d2out = delay_update(d42, p42, c_dly[2], s_dw[2], s_domw[2], st_d1out);
+      double st_eta = (st_d2out - st_diff) * st_d1out;
+      st_eta = iir3(srx1, srx2, sry1, sry2, c_sr_b, c_sr_a, st_eta);
+      const double m1r = st_eta, m1i = -delay_update(d8, p8, c_dly[3], s_dw[3], s_domw[3], st_eta);
+      const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
+      const double st_angle_error = aero_atan2(oim, ore);
+      set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
+      so_ptr += (-st_angle_error * 0.01 / 360.0) * WTSIZE;
+      while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
+      while (so_ptr < 0) so_ptr += WTSIZE;
+      if (so_freq < (10500.0 - 0.1)) set_freq(so_freq, so_step, (10500.0 - 0.1));
+      if (so_freq > (10500.0 + 0.1)) set_freq(so_freq, so_step, (10500.0 + 0.1));
+      if (!s2l_init) {
+        s2l_re = s2r;
+        s2l_im = s2i;
+        s2l_init = 1;
+      }
+      // sample instant (:430) IfHavePassedPoint (DSP.cpp:222-238)
+      double tl = so_last - PT, tw = so_ptr - PT;
+      if (tl < 0.0) tl += WTSIZE;
+      if (tw < 0.0) tw += WTSIZE;
+      if ((tl > 3.0 * WTSIZE / 4.0) && (tw < 1.0 * WTSIZE / 4.0)) {
+        const double pt_last = tw / so_step;
+        const double pt_this = 1.0 - pt_last;
+        const double pr = pt_this * s2r + pt_last * s2l_re;
+        const double pi = pt_this * s2i + pt_last * s2l_im;
+        yui++;
+        yui %= 2;
+        if (!yui) {
+          ptd_re = pr;
+          ptd_im = pi;
+        } else {
+          ev_pr = pr;
+          ev_pi = pi;
+          pend = true;  // carrier step below, before mixer2 advances
+        }
+      }
       s2l_re = s2r;
       s2l_im = s2i;
-      s2l_init = 1;
-    }
-    // sample instant (:430) IfHavePassedPoint (DSP.cpp:222-238)
-    double tl = so_last - PT, tw = so_ptr - PT;
-    if (tl < 0.0) tl += WTSIZE;
-    if (tw < 0.0) tw += WTSIZE;
-    if ((tl > 3.0 * WTSIZE / 4.0) && (tw < 1.0 * WTSIZE / 4.0)) {
-      const double pt_last = tw / so_step;
-      const double pt_this = 1.0 - pt_last;
-      const double pr = pt_this * s2r + pt_last * s2l_re;
-      const double pi = pt_this * s2i + pt_last * s2l_im;
-      yui++;
-      yui %= 2;
-      if (!yui) {
-        ptd_re = pr;
-        ptd_im = pi;
-      } else {
-        // the four moving-average rings of this symbol, loaded together
-        // before any ring store so their latencies overlap
-        const int dt_rp = (dt_p + 1) % DT_LEN;
-        const double marg_old = marg[marg_p];
-        const double2 dv = dtb[dt_rp];
-        const double pm_old = pmb[pm_p];
-        const double ms_old = msb[ms_p];
-        double qr = pr, qi = ptd_im;  // pt_qpsk
-        // carrier tracking (:456-470); the two tanh split across the pair
-        const double th = aero_tanh(part ? ptd_re : pi);
-        const double tho = __shfl_xor(th, 1, 64);
-        const double ct_xt = (part ? tho : th) * pr;
-        const double ct_xt_d = (part ? th : tho) * ptd_im;
-        double ct_ec = ct_xt_d - ct_xt;
-        if (ct_ec > M_PI) ct_ec = M_PI;
-        if (ct_ec < -M_PI) ct_ec = -M_PI;
-        ct_ec = iir3(ctx1, ctx2, cty1, cty2, c_ct_b, c_ct_a, ct_ec);
-        if (ct_ec > M_PI_2) ct_ec = M_PI_2;
-        if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
-        {  // mixer2.IncresePhaseDeg / SetPhaseDeg (DSP.cpp:177-187)
-          double phase_deg = 1.0 * ct_ec;
-          phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
-          phase_deg = fmod(phase_deg, 360.0);
-          while (phase_deg < 0) phase_deg += 360.0;
-          m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
-        }
-        set_freq(m2_freq, m2_step, 0.01 * ct_ec + m2_freq);  // IncreseFreqHz
-        // marg->UpdateSigned (DSP.cpp:419-427)
-        marg_sum = marg_sum - marg_old;
-        marg_sum = marg_sum + (ct_ec);
-        if (lead) marg[marg_p] = ct_ec;
-        marg_p++;
-        marg_p %= MARG_LEN;
-        const double mval = marg_sum / ((double)MARG_LEN);
-        // dt.update (DSP.h:456-461): slot p written, slot p+1 read
-        {
-          if (lead) dtb[dt_p] = make_double2(qr, qi);
-          dt_p = dt_rp;
-          qr = dv.x;
-          qi = dv.y;
-        }
-        double rs, rc;
-        aero_sincos(mval, rs, rc);
-        const double rr = qr * rc - qi * rs, ri = qr * rs + qi * rc;
-        qr = rr;
-        qi = ri;
-        if (TRACE) {
-          if (lead && ptn < S.pt_cap) S.pt[(size_t)c * S.pt_cap + ptn] = make_double2(qr, qi);
-          ptn++;
-        }
-        // MSEcalc::Update (DSP.cpp:449-461)
-        {
-          const double av = aero_hypot(qr, qi);
-          pm_sum = pm_sum - pm_old;
-          pm_sum = pm_sum + fabs(av);
-          if (lead) pmb[pm_p] = fabs(av);
-          pm_p++;
-          pm_p %= MSE_LEN;
-          double mu = pm_sum / ((double)MSE_LEN);
-          if (mu < 0.000001) mu = 0.000001;
-          const double tr = (1.4142135623730951 * qr) / mu, ti = (1.4142135623730951 * qi) / mu;
-          const double tda = (fabs(tr) - 1.0), tdb = (fabs(ti) - 1.0);
-          const double v = (tda * tda) + (tdb * tdb);
-          ms_sum = ms_sum - ms_old;
-          ms_sum = ms_sum + fabs(v);
-          if (lead) msb[ms_p] = fabs(v);
-          ms_p++;
-          ms_p %= MSE_LEN;
-          mse = ms_sum / ((double)MSE_LEN);
-        }
-        if (mse < 0.65) {  // soft bits, imag first (:516-530)
-          int ibit = qround(0.75 * qi * 127.0 + 128.0);
-          if (ibit > 255) ibit = 255;
-          if (ibit < 0) ibit = 0;
-          int rbit = qround(0.75 * qr * 127.0 + 128.0);
-          if (rbit > 255) rbit = 255;
-          if (rbit < 0) rbit = 0;
-          if (lead) {
-            soft[softp & (SOFT_RING - 1)] = (uint8_t)ibit;
-            soft[(softp + 1) & (SOFT_RING - 1)] = (uint8_t)rbit;
-          }
-          softp += 2;
-        }
-      }
-    }
-    s2l_re = s2r;
-    s2l_im = s2i;
-    nco_next(m2_ptr, m2_step);
-    nco_next(mc_ptr, mc_step);
-    so_last = so_ptr;
-    nco_next(so_ptr, so_step);
-    // coarse-ring fill of the next sample (:351-356), staged in LDS
-    if (n + 1 < avail) {
-      const long long m = n + 1;
-      const int k = (int)(m & 15);
-      if (lead) {
-        s_ring[k][pair] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)pcm_next << 16);
-        if (k == 15) {
-          uint32_t *dst = cring + ((m - 15) & (NFFT - 1));
-          if (m - 15 >= m_first) {
+      nco_next(mc_ptr, mc_step);
+      so_last = so_ptr;
+      nco_next(so_ptr, so_step);
+      // coarse-ring fill of the next sample (:351-356), staged in LDS
+      if (n + 1 < avail) {
+        const long long m = n + 1;
+        const int k = (int)(m & 15);
+        if (lead) {
+          s_ring[k][pair] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)pcm_next << 16);
+          if (k == 15) {
+            uint32_t *dst = cring + ((m - 15) & (NFFT - 1));
+            if (m - 15 >= m_first) {
 #pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4)
-              reinterpret_cast<uint4 *>(dst)[q4] = make_uint4(s_ring[4 * q4][pair], s_ring[4 * q4 + 1][pair],
-                                                              s_ring[4 * q4 + 2][pair], s_ring[4 * q4 + 3][pair]);
-          } else {
-            for (int j = (int)(m_first - (m - 15)); j < 16; ++j) dst[j] = s_ring[j][pair];
+              for (int q4 = 0; q4 < 4; ++q4)
+                reinterpret_cast<uint4 *>(dst)[q4] = make_uint4(s_ring[4 * q4][pair], s_ring[4 * q4 + 1][pair],
+                                                                s_ring[4 * q4 + 2][pair], s_ring[4 * q4 + 3][pair]);
+            } else {
+              for (int j = (int)(m_first - (m - 15)); j < 16; ++j) dst[j] = s_ring[j][pair];
+            }
           }
         }
+        filled = n + 2;
       }
-      filled = n + 2;
+      if (!pend) {
+        nco_next(m2_ptr, m2_step);
+        ++n;
+      }
+    } while (!pend && n < end);
+    if (pend) {
+      const double pr = ev_pr, pi = ev_pi;
+      // the four moving-average rings of this symbol, loaded together
+      // before any ring store so their latencies overlap
+      const int dt_rp = (dt_p + 1) % DT_LEN;
+      const double marg_old = marg[marg_p];
+      const double2 dv = dtb[dt_rp];
+      const double pm_old = pmb[pm_p];
+      const double ms_old = msb[ms_p];
+      double qr = pr, qi = ptd_im;  // pt_qpsk
+      // carrier tracking (:456-470); the two tanh split across the pair
+      const double th = aero_tanh(part ? ptd_re : pi);
+      const double tho = pair_swap(th);
+      const double ct_xt = (part ? tho : th) * pr;
+      const double ct_xt_d = (part ? th : tho) * ptd_im;
+      double ct_ec = ct_xt_d - ct_xt;
+      if (ct_ec > M_PI) ct_ec = M_PI;
+      if (ct_ec < -M_PI) ct_ec = -M_PI;
+      ct_ec = iir3(ctx1, ctx2, cty1, cty2, c_ct_b, c_ct_a, ct_ec);
+      if (ct_ec > M_PI_2) ct_ec = M_PI_2;
+      if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
+      {  // mixer2.IncresePhaseDeg / SetPhaseDeg (DSP.cpp:177-187)
+        double phase_deg = 1.0 * ct_ec;
+        phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
+        phase_deg = fmod(phase_deg, 360.0);
+        while (phase_deg < 0) phase_deg += 360.0;
+        m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+      }
+      set_freq(m2_freq, m2_step, 0.01 * ct_ec + m2_freq);  // IncreseFreqHz
+      // marg->UpdateSigned (DSP.cpp:419-427)
+      marg_sum = marg_sum - marg_old;
+      marg_sum = marg_sum + (ct_ec);
+      if (lead) marg[marg_p] = ct_ec;
+      marg_p++;
+      marg_p %= MARG_LEN;
+      const double mval = marg_sum / ((double)MARG_LEN);
+      // dt.update (DSP.h:456-461): slot p written, slot p+1 read
+      {
+        if (lead) dtb[dt_p] = make_double2(qr, qi);
+        dt_p = dt_rp;
+        qr = dv.x;
+        qi = dv.y;
+      }
+      double rs, rc;
+      aero_sincos(mval, rs, rc);
+      const double rr = qr * rc - qi * rs, ri = qr * rs + qi * rc;
+      qr = rr;
+      qi = ri;
+      if (TRACE) {
+        if (lead && ptn < S.pt_cap) S.pt[(size_t)c * S.pt_cap + ptn] = make_double2(qr, qi);
+        ptn++;
+      }
+      // MSEcalc::Update (DSP.cpp:449-461)
+      {
+        const double av = aero_hypot(qr, qi);
+        pm_sum = pm_sum - pm_old;
+        pm_sum = pm_sum + fabs(av);
+        if (lead) pmb[pm_p] = fabs(av);
+        pm_p++;
+        pm_p %= MSE_LEN;
+        double mu = pm_sum / ((double)MSE_LEN);
+        if (mu < 0.000001) mu = 0.000001;
+        const double tr = (1.4142135623730951 * qr) / mu, ti = (1.4142135623730951 * qi) / mu;
+        const double tda = (fabs(tr) - 1.0), tdb = (fabs(ti) - 1.0);
+        const double v = (tda * tda) + (tdb * tdb);
+        ms_sum = ms_sum - ms_old;
+        ms_sum = ms_sum + fabs(v);
+        if (lead) msb[ms_p] = fabs(v);
+        ms_p++;
+        ms_p %= MSE_LEN;
+        mse = ms_sum / ((double)MSE_LEN);
+      }
+      if (mse < 0.65) {  // soft bits, imag first (:516-530)
+        int ibit = qround(0.75 * qi * 127.0 + 128.0);
+        if (ibit > 255) ibit = 255;
+        if (ibit < 0) ibit = 0;
+        int rbit = qround(0.75 * qr * 127.0 + 128.0);
+        if (rbit > 255) rbit = 255;
+        if (rbit < 0) rbit = 0;
+        if (lead) {
+          soft[softp & (SOFT_RING - 1)] = (uint8_t)ibit;
+          soft[(softp + 1) & (SOFT_RING - 1)] = (uint8_t)rbit;
+        }
+        softp += 2;
+      }
+      nco_next(m2_ptr, m2_step);
+      ++n;
     }
   }
   // staged entries of an unfinished 16-sample group

@@ -18,6 +18,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <map>
 #include <memory>
 #include <string>
@@ -114,6 +117,71 @@ struct HostTimer {
 
 }  // namespace
 
+// Persistent host workers for the per-frame SU/ACARS work.  One task at a
+// time: the previous pass's frames are finished before the next pass's are
+// started, so a channel's frames keep their order.  submit() returns at
+// once, so while a task runs the caller goes on launching GPU work (frames
+// of step k are parsed while step k+1 demodulates).
+class HostPool {
+ public:
+  explicit HostPool(int n) : n_(std::max(1, n)) {
+    for (int t = 0; t < n_; t++) th_.emplace_back([this, t] { loop(t); });
+  }
+  ~HostPool() {
+    wait();
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &x : th_) x.join();
+  }
+  int size() const { return n_; }
+  // runs fn(t, T) for t in [0, T) on the pool's threads
+  void submit(std::function<void(int, int)> fn, int T) {
+    wait();
+    {
+      std::lock_guard<std::mutex> g(m_);
+      fn_ = std::move(fn);
+      tn_ = std::max(1, std::min(T, n_));
+      left_ = tn_;
+      gen_++;
+    }
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> g(m_);
+    done_cv_.wait(g, [this] { return left_ == 0; });
+  }
+
+ private:
+  void loop(int t) {
+    uint64_t seen = 0;
+    for (;;) {
+      int T;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        T = tn_;
+      }
+      if (t >= T) continue;
+      fn_(t, T);  // fn_ is only replaced after every worker of this task is done
+      std::lock_guard<std::mutex> g(m_);
+      if (--left_ == 0) done_cv_.notify_all();
+    }
+  }
+  int n_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  std::function<void(int, int)> fn_;
+  int tn_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 struct aero_engine {
   int device = 0, flags = 0, C = 0, nch = 0;
   hipStream_t st = nullptr;
@@ -132,12 +200,14 @@ struct aero_engine {
   // scratch
   int16_t *d_scratch = nullptr;
   size_t scratch_cap = 0;
-  std::vector<uint8_t> h_jobout;
+  std::vector<uint8_t> h_jobout, h_dbg;
   std::map<std::string, TimingSlot> timing;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending_ev;
   uint64_t processed = 0;
   int init_lo = 0;  // channels [init_lo, nch) await device state init
   int host_threads = 1;
+  std::unique_ptr<HostPool> hpool;
+  std::vector<uint8_t> h_jobs_task, h_dbg_task;  // buffers owned by the running host task
 };
 
 namespace {
@@ -249,65 +319,67 @@ int flush_pending_init(aero_engine *e) {
   return AERO_OK;
 }
 
+// Frame records of a pass -> host SU/ACARS work on the worker pool
+// (asynchronous; host_wait() joins it).
 int collect_after_pass(aero_engine *e, int njobs) {
   const int C = e->C, nch = e->nch;
-  if (njobs > 0) {
-    e->h_jobout.resize((size_t)njobs * JOB_OUT);
-    HIPCHK(hipMemcpyAsync(e->h_jobout.data(), e->S.jobout, (size_t)njobs * JOB_OUT, hipMemcpyDeviceToHost, e->st));
-    std::vector<uint8_t> dbg;
-    if (e->flags & AERO_F_TRACE_BLOCKS) {
-      dbg.resize((size_t)2500 * C);
-      HIPCHK(hipMemcpyAsync(dbg.data(), e->S.blocks_dbg, dbg.size(), hipMemcpyDeviceToHost, e->st));
-    }
-    {
-      HOST_TIMER(e, "host_wait_jobs");
-      HIPCHK(hipStreamSynchronize(e->st));
-    }
-    HOST_TIMER(e, "host_frames");
-    // host SU/ACARS work, channels partitioned over threads (c % T): a
-    // channel's frames stay in queue order and no two threads share state
-    auto work = [&](int t, int T) {
-      for (int j = 0; j < njobs; j++) {
-        const uint8_t *o = e->h_jobout.data() + (size_t)j * JOB_OUT;
-        int meta[4];
-        memcpy(meta, o + 312, 16);
-        const int c = meta[3] & 0x3FFFFFFF;
-        const int reset = (meta[3] >> 30) & 1;
-        if (c < 0 || c >= nch || c % T != t) continue;
-        if (e->flags & AERO_F_TRACE_BLOCKS) {
-          const uint8_t *d = dbg.data() + (size_t)c * 2500;
-          int nb;
-          memcpy(&nb, d, 4);
-          uint32_t L = (uint32_t)nb;
-          auto &h = e->blk_hold[c];
-          h.insert(h.end(), (uint8_t *)&L, (uint8_t *)&L + 4);
-          h.insert(h.end(), d + 4, d + 4 + nb);
-        }
-        if (reset) e->host[c]->isu_reset();
-        if (meta[0] >= 0) {
-          e->host[c]->frame(o, meta[0], (uint32_t)meta[1], meta[2]);
-          if (e->flags & AERO_F_TRACE_FRAMES) {
-            uint8_t rec[320] = {0};
-            memcpy(rec, o, 312);
-            const uint32_t L = (uint32_t)meta[0], M = (uint32_t)meta[1];
-            memcpy(rec + 312, &L, 4);
-            memcpy(rec + 316, &M, 4);
-            e->frame_hold[c].insert(e->frame_hold[c].end(), rec, rec + 320);
-          }
+  if (njobs <= 0) return AERO_OK;
+  e->h_jobout.resize((size_t)njobs * JOB_OUT);
+  HIPCHK(hipMemcpyAsync(e->h_jobout.data(), e->S.jobout, (size_t)njobs * JOB_OUT, hipMemcpyDeviceToHost, e->st));
+  const bool blocks = (e->flags & AERO_F_TRACE_BLOCKS) != 0;
+  if (blocks) {
+    e->h_dbg.resize((size_t)2500 * C);
+    HIPCHK(hipMemcpyAsync(e->h_dbg.data(), e->S.blocks_dbg, e->h_dbg.size(), hipMemcpyDeviceToHost, e->st));
+  }
+  {
+    HOST_TIMER(e, "host_wait_jobs");
+    HIPCHK(hipStreamSynchronize(e->st));
+  }
+  HOST_TIMER(e, "host_frames");
+  e->hpool->wait();  // previous pass's frames first (per-channel order)
+  std::swap(e->h_jobs_task, e->h_jobout);
+  std::swap(e->h_dbg_task, e->h_dbg);
+  // channels partitioned over workers (c % T): a channel's frames stay in
+  // queue order and no two workers share state
+  auto work = [e, njobs, nch, blocks](int t, int T) {
+    const uint8_t *jobs = e->h_jobs_task.data();
+    for (int j = 0; j < njobs; j++) {
+      const uint8_t *o = jobs + (size_t)j * JOB_OUT;
+      int meta[4];
+      memcpy(meta, o + 312, 16);
+      const int c = meta[3] & 0x3FFFFFFF;
+      const int reset = (meta[3] >> 30) & 1;
+      if (c < 0 || c >= nch || c % T != t) continue;
+      if (blocks) {
+        const uint8_t *d = e->h_dbg_task.data() + (size_t)c * 2500;
+        int nb;
+        memcpy(&nb, d, 4);
+        uint32_t L = (uint32_t)nb;
+        auto &h = e->blk_hold[c];
+        h.insert(h.end(), (uint8_t *)&L, (uint8_t *)&L + 4);
+        h.insert(h.end(), d + 4, d + 4 + nb);
+      }
+      if (reset) e->host[c]->isu_reset();
+      if (meta[0] >= 0) {
+        e->host[c]->frame(o, meta[0], (uint32_t)meta[1], meta[2]);
+        if (e->flags & AERO_F_TRACE_FRAMES) {
+          uint8_t rec[320] = {0};
+          memcpy(rec, o, 312);
+          const uint32_t L = (uint32_t)meta[0], M = (uint32_t)meta[1];
+          memcpy(rec + 312, &L, 4);
+          memcpy(rec + 316, &M, 4);
+          e->frame_hold[c].insert(e->frame_hold[c].end(), rec, rec + 320);
         }
       }
-    };
-    const int T = std::max(1, std::min<int>({e->host_threads, njobs / 64, nch}));
-    if (T == 1) {
-      work(0, 1);
-    } else {
-      std::vector<std::thread> th;
-      for (int t = 1; t < T; t++) th.emplace_back(work, t, T);
-      work(0, T);
-      for (auto &x : th) x.join();
     }
-  }
+  };
+  e->hpool->submit(work, std::max(1, std::min(njobs / 64, nch)));
   return AERO_OK;
+}
+
+// joins the asynchronous host frame work (before any host-side output is read)
+void host_wait(aero_engine *e) {
+  if (e->hpool) e->hpool->wait();
 }
 
 int collect_traces(aero_engine *e) {
@@ -467,6 +539,7 @@ int aero_engine_create(const aero_engine_cfg *cfg, aero_engine **out) {
     const int hw = (int)std::thread::hardware_concurrency();
     e->host_threads = ev ? atoi(ev) : std::min(16, std::max(1, hw));
     if (e->host_threads < 1) e->host_threads = 1;
+    e->hpool.reset(new HostPool(e->host_threads));
   }
   e->C = (cfg->max_channels + 63) & ~63;
   DevState S{};
@@ -510,6 +583,7 @@ void aero_engine_destroy(aero_engine *e) {
   if (!e) return;
   hipSetDevice(e->device);
   if (e->st) hipStreamSynchronize(e->st);
+  host_wait(e);
   ev_collect(e);
   if (e->d_scratch) (void)hipFree(e->d_scratch);
   if (e->pool) (void)hipFree(e->pool);
@@ -522,6 +596,7 @@ int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) 
   if (cfg->bitrate != 10500 || cfg->burst) return AERO_E_INVALID;  // decode/decode.h:42 subset
   if (e->nch >= e->C) return AERO_E_FULL;
   HIPCHK(hipSetDevice(e->device));
+  host_wait(e);  // the host task indexes the per-channel tables
   const int c = e->nch;
   e->nch++;  // device state initialised by flush_pending_init before the next push/run
   e->cfg.push_back(*cfg);
@@ -628,7 +703,26 @@ int aero_pop_softbits(aero_engine *e, int ch, int16_t *dst, size_t cap, size_t *
 
 int aero_pop_items(aero_engine *e, int ch, aero_acars_item *dst, size_t cap, size_t *n) {
   if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  host_wait(e);
   return pop_vec(e->host[ch]->items, dst, cap, n);
+}
+
+int aero_pop_items_all(aero_engine *e, aero_acars_item *dst, int *ch, size_t cap, size_t *n) {
+  if (!e || (cap && (!dst || !ch))) return AERO_E_INVALID;
+  host_wait(e);
+  size_t k = 0;
+  for (int c = 0; c < e->nch && k < cap; c++) {
+    auto &v = e->host[c]->items;
+    const size_t m = std::min(cap - k, v.size());
+    for (size_t i = 0; i < m; i++) {
+      dst[k + i] = v[i];
+      ch[k + i] = c;
+    }
+    v.erase(v.begin(), v.begin() + m);
+    k += m;
+  }
+  if (n) *n = k;
+  return AERO_OK;
 }
 
 int aero_pop_hops(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n) {
@@ -649,11 +743,13 @@ int aero_pop_pt(aero_engine *e, int ch, double *dst, size_t cap_records, size_t 
 
 int aero_pop_blocks(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
   if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  host_wait(e);
   return pop_vec(e->blk_hold[ch], dst, cap, n);
 }
 
 int aero_pop_frames(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
   if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  host_wait(e);
   return pop_vec(e->frame_hold[ch], dst, cap, n);
 }
 
@@ -677,6 +773,7 @@ uint64_t aero_samples_processed(aero_engine *e) { return e ? e->processed : 0; }
 int aero_sync(aero_engine *e) {
   if (!e) return AERO_E_INVALID;
   HIPCHK(hipStreamSynchronize(e->st));
+  host_wait(e);
   return AERO_OK;
 }
 

@@ -127,6 +127,7 @@ def main():
         torch.cuda.synchronize()
         eng.push_batch_device(x.data_ptr(), HOP, C, C)
         eng.run()
+        eng.drain_items()
     timed_inputs = [step_input(a.warmup + s) for s in range(a.steps)]
     eng.sync()
     torch.cuda.synchronize()
@@ -136,10 +137,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    items = 0
     for x in timed_inputs:
         eng.push_batch_device(x.data_ptr(), HOP, C, C)
         eng.run()
+        items += eng.drain_items()  # ACARS items leave every step, as a serving host would take them
     eng.sync()
+    items += eng.drain_items()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -179,6 +183,7 @@ def main():
                          'traffic': traffic, 'bytes_per_sample': BYTES_PER_SAMPLE,
                          'avg_launch_ms': round(per_launch_s * 1e3, 3)},
             'kernel_ms_per_step': {k: round(v[0] / max(a.steps, 1), 3) for k, v in kt.items()},
+            'acars_items': items,
             'host_ms_per_step': {k: round(v[0] / max(a.steps, 1), 3) for k, v in ht.items()},
         }
         if cpu is not None:

@@ -99,6 +99,11 @@ int aero_pop_softbits(aero_engine *e, int ch, int16_t *dst, size_t cap, size_t *
  * disable_reassembly), in emission order (decode/aerol.cpp:457,522,2127,2142). */
 int aero_pop_items(aero_engine *e, int ch, aero_acars_item *dst, size_t cap, size_t *n);
 
+/* Items of every channel in one call (channel order, then emission order);
+ * ch[i] receives item i's channel.  For hosts that serve many VFOs from one
+ * engine: one call per aero_run instead of one per channel. */
+int aero_pop_items_all(aero_engine *e, aero_acars_item *dst, int *ch, size_t cap, size_t *n);
+
 /* Diagnostics used by the parity tests and the bench.
  * hops: 6 doubles per coarse hop (sample index, estimate, mixer2 Hz,
  * mixer_center Hz, mse, signal). pt: 2 doubles per carrier event.
