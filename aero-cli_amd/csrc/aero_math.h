@@ -502,8 +502,8 @@ AERO_HD dd dd_log12(double m) {
   return dd_add(dd{aero_log_tab[k][0], aero_log_tab[k][1]}, r);
 }
 
-/* glibc e_log10.c composition around a correctly rounded __ieee754_log */
-AERO_HD double aero_log(double x) {
+/* correctly rounded natural log, double-double evaluation */
+AERO_HD double aero_log_dd(double x) {
   if (!(x > 0.0) || !__builtin_isfinite(x)) {
     if (x == 0.0) return -__builtin_inf();
     if (x < 0.0 || __builtin_isnan(x)) return (x - x) / (x - x);
@@ -523,6 +523,40 @@ AERO_HD double aero_log(double x) {
   dd lm = dd_log12(m);
   dd r = dd_add(dd_mul_d(dd{AERO_LN2_HI, AERO_LN2_LO}, (double)k), lm);
   return r.hi + r.lo;
+}
+
+/* log fast path (Ziv): log(x) = k ln2 + log(c) + 2 atanh(u), u = (m-c)/(m+c),
+ * evaluated to about 2^-66 without IEEE division; returned only when that
+ * bound proves the rounding, otherwise aero_log_dd decides (same results). */
+AERO_HD double aero_log(double x) {
+  if (!(x >= 0x1p-1000 && x <= 0x1p1000)) return aero_log_dd(x);
+  const uint64_t ux = d2u(x);
+  const int k = (int)((ux >> 52) & 0x7ff) - 1023;
+  const double m = u2d((ux & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL);
+  const int j = (int)((m - 1.0) * 64.0 + 0.5);
+  const double c = 1.0 + (double)j * (1.0 / 64.0);
+  const double nh = m - c;                 // exact (Sterbenz)
+  const dd den = two_sum(m, c);
+  const double rd = approx_rcp(den.hi);
+  const double uh = nh * rd;               // |u| <= 2^-8
+  const double ul = (fma(-uh, den.hi, nh) - uh * den.lo) * rd;
+  const double v = uh * uh;
+  double p = 1.0 / 13;
+  p = 1.0 / 11 + v * p;
+  p = 1.0 / 9 + v * p;
+  p = 1.0 / 7 + v * p;
+  p = 1.0 / 5 + v * p;
+  p = AERO_INV3_HI + v * p;
+  const double corr = 2.0 * ((v * uh) * p + v * ul);  // 2 atanh(u) - 2u
+  // log(c) + 2u + corr + k ln2
+  dd r = two_sum(aero_log_tab[j][0], 2.0 * uh);
+  r.lo += aero_log_tab[j][1] + (2.0 * ul + corr);
+  r = quick_two_sum(r.hi, r.lo);
+  if (k) r = dd_add(dd_mul_d(dd{AERO_LN2_HI, AERO_LN2_LO}, (double)k), r);
+  const double e = 0x1p-63 * __builtin_fabs(r.hi);
+  const double out = r.hi + r.lo;
+  if (out != r.hi + (r.lo + e) || out != r.hi + (r.lo - e)) return aero_log_dd(x);
+  return out;
 }
 
 AERO_HD double aero_log10(double x) {

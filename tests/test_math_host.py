@@ -60,3 +60,14 @@ def test_atan2_fast_path_equals_double_double():
         a = mathhost.evaluate('atan2', y, x).view(np.int64)
         b = mathhost.evaluate('atan2_dd', y, x).view(np.int64)
         assert np.array_equal(a, b)
+
+
+def test_log_fast_path_equals_double_double():
+    rng = np.random.default_rng(11)
+    for x in (np.exp(rng.uniform(0, 28, 1_000_000)),                      # coarse-estimator |X| range
+              1 + rng.uniform(0, 1e-6, 200_000),                            # near 1
+              np.exp(rng.uniform(-700, 700, 500_000)),                      # wide exponents
+              (1 + rng.integers(0, 65, 500_000) / 64) * (1 + rng.standard_normal(500_000) * 1e-13)):
+        a = mathhost.evaluate('log', x).view(np.int64)
+        b = mathhost.evaluate('log_dd', x).view(np.int64)
+        assert np.array_equal(a, b)
