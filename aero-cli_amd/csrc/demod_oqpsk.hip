@@ -53,23 +53,20 @@ __device__ __forceinline__ void set_freq(double &freq, double &step, double f) {
   step = (freq) * ((double)WTSIZE) / 48000.0;
 }
 
-// Delay<double>::update (DSP.h:365-384) as a shift register; the reference's
-// ring index and fractional weight depend only on the write pointer p.
-template <int N>
-__device__ __forceinline__ double delay_update(double (&h)[N], int &p, const DelayDesc &d, const double *wl,
-                                               const double *omwl, double sig) {
+// Delay<double>::update (DSP.h:365-384) as a shift register: h[0] is the
+// newest sample.  The reference reads the ring at fixed ages behind its
+// write pointer and weights them with per-pointer weights; at 48 kHz /
+// 10500 bps the ages are compile-time constants and the weights do not
+// depend on the pointer (engine.hip checks both at engine creation), so
+// only the cells up to the oldest age read are kept.
+template <int N, int AGE_OLD, int AGE_NEW>
+__device__ __forceinline__ double delay_tap(double (&h)[N], const DelayDesc &d, double sig) {
+  static_assert(AGE_OLD < N + 1 && AGE_NEW < N + 1, "ring ages");
 #pragma unroll
   for (int i = N - 1; i > 0; --i) h[i] = h[i - 1];
   h[0] = sig;
-  const double w = wl[p], omw = omwl[p];  // per-pointer weights (LDS copy of d.w / d.omw)
-  double older = h[0], newer = h[0];
-#pragma unroll
-  for (int a = 0; a < N; ++a) {
-    if (a == d.age_old) older = h[a];
-    if (a == d.age_new) newer = h[a];
-  }
-  p = (p + 1 == N) ? 0 : p + 1;
-  return (w * newer + omw * older);
+  const double w = d.w[0], omw = d.omw[0];  // uniform: scalar loads
+  return (w * h[AGE_NEW] + omw * h[AGE_OLD]);
 }
 
 // IIR::update with 3 b / 3 a coefficients (DSP.cpp:635-685), a[0] == 1
@@ -100,22 +97,28 @@ __device__ __forceinline__ int qround(double d) {  // qRound (Qt 5.9 qglobal.h:5
   return d >= 0.0 ? int(d + 0.5) : int(d - double(int(d - 1)) + 0.5) + int(d - 1);
 }
 
+// carrier-step state kept in LDS (read and written once per carrier event,
+// i.e. once per ~9 samples): keeping it out of VGPRs leaves the per-sample
+// path room for the 55 FIR partial sums without spilling
+enum { PD_CTX1, PD_CTX2, PD_CTY1, PD_CTY2, PD_MARG_SUM, PD_PM_SUM, PD_MS_SUM, PD_MSE, PD_PTD_RE, PD_PTD_IM,
+       PD_M2_FREQ, PD_N };
+enum { PI_MARG_P, PI_DT_P, PI_PM_P, PI_MS_P, PI_N };
+enum { PL_SOFTP, PL_PTN, PL_N };
+
 template <bool TRACE>
 __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables T, int nch, int flush) {
-  // LDS: RRC taps and delay weights (uniform / tiny per-lane gathers that
-  // would otherwise be global loads every sample), and the coarse-ring
-  // staging area: entries of 16 consecutive samples are collected here and
-  // leave as one 64-byte write per channel instead of sixteen 4-byte ones.
-  __shared__ double s_taps[NTAPS + 1];
-  __shared__ double s_dw[4][4], s_domw[4][4];
+  // LDS: RRC taps (symmetric, 28 distinct values), the
+  // coarse-ring staging area (entries of 16 consecutive samples leave as one
+  // 64-byte write per channel instead of sixteen 4-byte ones) and the
+  // carrier-step state of the block's 128 channels.
+  __shared__ double s_taps[32];
   __shared__ uint32_t s_ring[16][128];
+  __shared__ double s_pd[PD_N][128];
+  __shared__ long long s_pl[PL_N][128];
+  __shared__ int s_pi[PI_N][128];
   {
     const int l = threadIdx.x;
-    if (l < NTAPS) s_taps[l] = T.taps[l];
-    if (l < 16) {
-      s_dw[l >> 2][l & 3] = c_dly[l >> 2].w[l & 3];
-      s_domw[l >> 2][l & 3] = c_dly[l >> 2].omw[l & 3];
-    }
+    if (l < (NTAPS + 1) / 2) s_taps[l] = T.taps[l];  // h[j] == h[54 - j] bit for bit (host-checked)
     __syncthreads();
   }
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -125,71 +128,73 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
   const int pair = threadIdx.x >> 1;
   if (c >= nch) return;  // nch channels -> 2 nch lanes; pairs never straddle the check
   const int C = S.C;
-  double *ds = S.ds;
-  int *is = S.is;
-  long long *ls = S.ls;
 
-  long long n = ls[LS_NSAMP * C + c];
-  const long long avail = ls[LS_AVAIL * C + c];
-  long long filled = ls[LS_FILLED * C + c];
-  const int hops_done = is[IS_HOPS_DONE * C + c];
+  // sample counters relative to n0 (a launch covers at most one hop)
+  const long long n0 = S.ls[LS_NSAMP * C + c];
+  const long long avail = S.ls[LS_AVAIL * C + c];
+  const long long filled0 = S.ls[LS_FILLED * C + c];
+  const int hops_done = S.is[IS_HOPS_DONE * C + c];
   const long long boundary = (long long)HOP * (hops_done + 1) - 1;
   long long end = avail < boundary ? avail : boundary;
-  if (!flush && avail <= boundary) end = n;  // wait for a whole segment + the hop's ring entry
-  const long long capm = S.pcm_cap - 1;
-  uint32_t *cring = S.cring + (size_t)c * NFFT;
+  if (!flush && avail <= boundary) end = n0;  // wait for a whole segment + the hop's ring entry
+  const int capm = S.pcm_cap - 1;
+  const int pb = (int)(n0 & capm);          // PCM ring row of sample n0
+  const int rb = (int)(n0 & (NFFT - 1));    // coarse-ring slot of sample n0
+  const int ia = (int)(avail - n0);         // pushed samples beyond n0 (<= ring size)
+  const int ie = (int)(end - n0);
+  int ifl = (int)(filled0 - n0);            // coarse-ring entries written: samples < n0 + ifl
 
-  double mc_ptr = ds[DS_MC_PTR * C + c], mc_step = ds[DS_MC_STEP * C + c];
-  // coarse-ring catch-up (entry of sample n not yet written)
-  if (filled == n && n < avail) {
-    const int16_t x = S.pcm[(n & capm) * C + c];
-    if (lead) cring[n & (NFFT - 1)] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
-    filled = n + 1;
+  double mc_ptr = S.ds[DS_MC_PTR * C + c], mc_step = S.ds[DS_MC_STEP * C + c];
+  // coarse-ring catch-up (entry of sample n0 not yet written)
+  if (ifl == 0 && ia > 0) {
+    const int16_t x = S.pcm[(size_t)pb * C + c];
+    if (lead) S.cring[(size_t)c * NFFT + rb] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
+    ifl = 1;
   }
-  if (n >= end) {
-    if (lead) ls[LS_FILLED * C + c] = filled;
+  if (ie <= 0) {
+    if (lead) S.ls[LS_FILLED * C + c] = n0 + ifl;
     return;
   }
 
-  double m2_ptr = ds[DS_M2_PTR * C + c], m2_step = ds[DS_M2_STEP * C + c], m2_freq = ds[DS_M2_FREQ * C + c];
-  double so_ptr = ds[DS_SO_PTR * C + c], so_last = ds[DS_SO_LAST * C + c];
-  double so_step = ds[DS_SO_STEP * C + c], so_freq = ds[DS_SO_FREQ * C + c];
-  double agc_sum = ds[DS_AGC_SUM * C + c];
-  double d1[2] = {ds[DS_D1_0 * C + c], ds[DS_D1_1 * C + c]};
-  double d41[4] = {ds[DS_D41_0 * C + c], ds[DS_D41_1 * C + c], ds[DS_D41_2 * C + c], ds[DS_D41_3 * C + c]};
-  double d42[4] = {ds[DS_D42_0 * C + c], ds[DS_D42_1 * C + c], ds[DS_D42_2 * C + c], ds[DS_D42_3 * C + c]};
-  double d8[3] = {ds[DS_D8_0 * C + c], ds[DS_D8_1 * C + c], ds[DS_D8_2 * C + c]};
-  double srx1 = ds[DS_SR_X1 * C + c], srx2 = ds[DS_SR_X2 * C + c];
-  double sry1 = ds[DS_SR_Y1 * C + c], sry2 = ds[DS_SR_Y2 * C + c];
-  double ctx1 = ds[DS_CT_X1 * C + c], ctx2 = ds[DS_CT_X2 * C + c];
-  double cty1 = ds[DS_CT_Y1 * C + c], cty2 = ds[DS_CT_Y2 * C + c];
-  double marg_sum = ds[DS_MARG_SUM * C + c], pm_sum = ds[DS_PM_SUM * C + c], ms_sum = ds[DS_MS_SUM * C + c];
-  double mse = ds[DS_MSE * C + c];
-  double ptd_re = ds[DS_PTD_RE * C + c], ptd_im = ds[DS_PTD_IM * C + c];
-  double s2l_re = ds[DS_S2L_RE * C + c], s2l_im = ds[DS_S2L_IM * C + c];
-  int agc_ptr = is[IS_AGC_PTR * C + c];
-  int p1 = is[IS_D1_P * C + c], p41 = is[IS_D41_P * C + c], p42 = is[IS_D42_P * C + c], p8 = is[IS_D8_P * C + c];
-  int marg_p = is[IS_MARG_P * C + c], dt_p = is[IS_DT_P * C + c];
-  int pm_p = is[IS_PM_P * C + c], ms_p = is[IS_MS_P * C + c];
-  int yui = is[IS_YUI * C + c], s2l_init = is[IS_S2L_INIT * C + c];
-  long long softp = ls[LS_SOFT_P * C + c];
-  long long ptn = TRACE ? ls[LS_PT_N * C + c] : 0;
+  double m2_ptr = S.ds[DS_M2_PTR * C + c], m2_step = S.ds[DS_M2_STEP * C + c];
+  double so_ptr = S.ds[DS_SO_PTR * C + c], so_last = S.ds[DS_SO_LAST * C + c];
+  double so_step = S.ds[DS_SO_STEP * C + c], so_freq = S.ds[DS_SO_FREQ * C + c];
+  double agc_sum = S.ds[DS_AGC_SUM * C + c];
+  double d1[2], d41[4], d42[4], d8[3];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) d1[k] = S.ds[(DS_D1_0 + k) * C + c];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d41[k] = S.ds[(DS_D41_0 + k) * C + c];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d42[k] = S.ds[(DS_D42_0 + k) * C + c];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) d8[k] = S.ds[(DS_D8_0 + k) * C + c];
+  double srx1 = S.ds[DS_SR_X1 * C + c], srx2 = S.ds[DS_SR_X2 * C + c];
+  double sry1 = S.ds[DS_SR_Y1 * C + c], sry2 = S.ds[DS_SR_Y2 * C + c];
+  double s2l_re = S.ds[DS_S2L_RE * C + c], s2l_im = S.ds[DS_S2L_IM * C + c];
+  int agc_ptr = S.is[IS_AGC_PTR * C + c];
+  int yui = S.is[IS_YUI * C + c], s2l_init = S.is[IS_S2L_INIT * C + c];
+  {  // carrier-step state -> LDS (both lanes of a pair write the same values)
+    static constexpr int pd_src[PD_N] = {DS_CT_X1, DS_CT_X2, DS_CT_Y1, DS_CT_Y2, DS_MARG_SUM, DS_PM_SUM,
+                                         DS_MS_SUM, DS_MSE, DS_PTD_RE, DS_PTD_IM, DS_M2_FREQ};
+    static constexpr int pi_src[PI_N] = {IS_MARG_P, IS_DT_P, IS_PM_P, IS_MS_P};
+#pragma unroll
+    for (int k = 0; k < PD_N; ++k) s_pd[k][pair] = S.ds[pd_src[k] * C + c];
+#pragma unroll
+    for (int k = 0; k < PI_N; ++k) s_pi[k][pair] = S.is[pi_src[k] * C + c];
+    s_pl[PL_SOFTP][pair] = S.ls[LS_SOFT_P * C + c];
+    s_pl[PL_PTN][pair] = TRACE ? S.ls[LS_PT_N * C + c] : 0;
+  }
 
   // this lane's half of the transposed RRC: R_j(n-1), j = 0..54
   double q[NTAPS];
 #pragma unroll
   for (int j = 0; j < NTAPS; ++j) q[j] = S.fir[(size_t)(part * NTAPS + j) * C + c];
 
-  double *marg = S.marg + (size_t)c * MARG_LEN;
-  double2 *dtb = S.dt + (size_t)c * DT_LEN;
-  double *pmb = S.pm + (size_t)c * MSE_LEN;
-  double *msb = S.ms + (size_t)c * MSE_LEN;
-  uint8_t *soft = S.soft + (size_t)c * SOFT_RING;
   const double PT = 0.4 * WTSIZE;  // IfHavePassedPoint(ee) with ee = 0.4 (oqpskdemodulator.cpp:225)
 
-  const long long m_first = n + 1;  // first coarse-ring entry staged by this launch
-  // sample n's PCM word and AGC ring slot are always loaded one sample ahead
-  int16_t pcm_next = S.pcm[(n & capm) * C + c];
+  // sample n0+i's PCM word and AGC ring slot are always loaded one sample ahead
+  int16_t pcm_next = S.pcm[(size_t)pb * C + c];
   double agc_next = S.agc[(size_t)agc_ptr * C + c];
   // Event-aligned iteration.  The carrier/MSE/soft-bit step runs at every
   // second sample instant (one channel in ~9 samples), but in lockstep
@@ -199,19 +204,19 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
   // step then runs once for all lanes together.  Per lane the operations and
   // their order are exactly the reference's; only the interleaving of
   // different channels changes.
+  int i = 0;
   double ev_pr = 0.0, ev_pi = 0.0;
-  while (n < end) {
+  while (i < ie) {
     bool pend = false;
     do {
       const int16_t xs = pcm_next;
       const double agc_old = agc_next;
-      // table lookups of this sample first, then the prefetch for n+1, so the
-      // in-order vmcnt waits below never wait on the prefetch
+      // table lookups of this sample first, then the prefetch for the next
       const double2 cm = T.cis[cis_index(m2_ptr)];
       const double2 so = T.cis[cis_index(so_ptr)];
       {
         const int ap = agc_ptr + 1 == AGC_LEN ? 0 : agc_ptr + 1;
-        pcm_next = S.pcm[((n + 1) & capm) * C + c];
+        pcm_next = S.pcm[(size_t)((pb + i + 1) & capm) * C + c];
         agc_next = S.agc[(size_t)ap * C + c];
       }
       const double dval = ((double)xs) / 32768.0;
@@ -219,22 +224,31 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
       const double cv = (part ? cm.y : cm.x) * dval;
       // rrc (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
       const double mine = q[NTAPS - 1];
-      // taps from LDS through an opaque offset: re-read every sample instead of
-      // pinning 110 VGPRs of loop invariants
-      int toff = 0;
-      asm volatile("" : "+v"(toff));
+      {
+        // taps from LDS through an opaque offset, in groups, so they are
+        // re-read every sample instead of pinning registers
+        int toff = 0;
+        asm volatile("" : "+v"(toff));
 #pragma unroll
-      for (int j = NTAPS - 1; j >= 1; --j) q[j] = q[j - 1] + s_taps[j + toff] * cv;
-      q[0] = 0.0 + s_taps[toff] * cv;
+        for (int j = NTAPS - 1; j >= 1; --j) {
+          const int tj = j < NTAPS - 1 - j ? j : NTAPS - 1 - j;
+          q[j] = q[j - 1] + s_taps[tj + toff] * cv;
+          if ((j & 7) == 0) asm volatile("" : "+v"(toff));
+        }
+        q[0] = 0.0 + s_taps[toff] * cv;
+        // pin the update here: left alone the compiler sinks it to the loop
+        // latch and keeps cv and all 28 taps live across the whole sample
+#pragma unroll
+        for (int j = 0; j < NTAPS; ++j) asm volatile("" : "+v"(q[j]));
+      }
       const double other = pair_swap(mine);
       double s2r = part ? other : mine, s2i = part ? mine : other;
       // AGC (DSP.cpp:371-380) on |sig2| (oqpskdemodulator.cpp:399-405)
       const double dab = sqrt(s2r * s2r + s2i * s2i);
       {
-        double *slot = S.agc + (size_t)agc_ptr * C + c;
         agc_sum = agc_sum - agc_old;
         agc_sum = agc_sum + fabs(dab);
-        if (lead) *slot = fabs(dab);
+        if (lead) S.agc[(size_t)agc_ptr * C + c] = fabs(dab);
         agc_ptr++;
         if (agc_ptr == AGC_LEN) agc_ptr = 0;
         double g = 1.414213562 / fmax(agc_sum / ((double)AGC_LEN), 0.000001);
@@ -250,12 +264,12 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
         s2i = k * s2i;
       }
       // symbol timer (:413-426)
-      const double st_diff = delay_update(d1, p1, c_dly[0], s_dw[0], s_domw[0], ab * ab) - (ab * ab);
-      const double st_d1out = delay_update(d41, p41, c_dly[1], s_dw[1], s_domw[1], st_diff);
-      const double st_d2out = delay_update(d42, p42, c_dly[2], s_dw[2], s_domw[2], st_d1out);
+      const double st_diff = delay_tap<2, 1, 0>(d1, c_dly[0], ab * ab) - (ab * ab);
+      const double st_d1out = delay_tap<4, 3, 2>(d41, c_dly[1], st_diff);
+      const double st_d2out = delay_tap<4, 3, 2>(d42, c_dly[2], st_d1out);
       double st_eta = (st_d2out - st_diff) * st_d1out;
       st_eta = iir3(srx1, srx2, sry1, sry2, c_sr_b, c_sr_a, st_eta);
-      const double m1r = st_eta, m1i = -delay_update(d8, p8, c_dly[3], s_dw[3], s_domw[3], st_eta);
+      const double m1r = st_eta, m1i = -delay_tap<3, 2, 1>(d8, c_dly[3], st_eta);
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
       const double st_angle_error = aero_atan2(oim, ore);
       set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
@@ -281,8 +295,8 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
         yui++;
         yui %= 2;
         if (!yui) {
-          ptd_re = pr;
-          ptd_im = pi;
+          s_pd[PD_PTD_RE][pair] = pr;
+          s_pd[PD_PTD_IM][pair] = pi;
         } else {
           ev_pr = pr;
           ev_pi = pi;
@@ -295,31 +309,41 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
       so_last = so_ptr;
       nco_next(so_ptr, so_step);
       // coarse-ring fill of the next sample (:351-356), staged in LDS
-      if (n + 1 < avail) {
-        const long long m = n + 1;
-        const int k = (int)(m & 15);
+      if (i + 1 < ia) {
+        const int m = rb + i + 1;  // ring slot before masking
+        const int k = m & 15;
         if (lead) {
           s_ring[k][pair] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)pcm_next << 16);
           if (k == 15) {
-            uint32_t *dst = cring + ((m - 15) & (NFFT - 1));
-            if (m - 15 >= m_first) {
+            uint32_t *dst = S.cring + (size_t)c * NFFT + ((m - 15) & (NFFT - 1));
+            if (i + 1 - 15 >= 1) {  // the whole group was staged by this launch
 #pragma unroll
               for (int q4 = 0; q4 < 4; ++q4)
                 reinterpret_cast<uint4 *>(dst)[q4] = make_uint4(s_ring[4 * q4][pair], s_ring[4 * q4 + 1][pair],
                                                                 s_ring[4 * q4 + 2][pair], s_ring[4 * q4 + 3][pair]);
             } else {
-              for (int j = (int)(m_first - (m - 15)); j < 16; ++j) dst[j] = s_ring[j][pair];
+              for (int j = 15 - i; j < 16; ++j) dst[j] = s_ring[j][pair];
             }
           }
         }
-        filled = n + 2;
+        ifl = i + 2;
       }
       if (!pend) {
         nco_next(m2_ptr, m2_step);
-        ++n;
+        ++i;
       }
-    } while (!pend && n < end);
+    } while (!pend && i < ie);
     if (pend) {
+      // channel-row pointers from a laundered index: recomputed here, not
+      // kept live across the sample loop
+      int cl = c;
+      asm volatile("" : "+v"(cl));
+      double *marg = S.marg + (size_t)cl * MARG_LEN;
+      double2 *dtb = S.dt + (size_t)cl * DT_LEN;
+      double *pmb = S.pm + (size_t)cl * MSE_LEN;
+      double *msb = S.ms + (size_t)cl * MSE_LEN;
+      int marg_p = s_pi[PI_MARG_P][pair], dt_p = s_pi[PI_DT_P][pair];
+      int pm_p = s_pi[PI_PM_P][pair], ms_p = s_pi[PI_MS_P][pair];
       const double pr = ev_pr, pi = ev_pi;
       // the four moving-average rings of this symbol, loaded together
       // before any ring store so their latencies overlap
@@ -328,6 +352,12 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
       const double2 dv = dtb[dt_rp];
       const double pm_old = pmb[pm_p];
       const double ms_old = msb[ms_p];
+      double ctx1 = s_pd[PD_CTX1][pair], ctx2 = s_pd[PD_CTX2][pair];
+      double cty1 = s_pd[PD_CTY1][pair], cty2 = s_pd[PD_CTY2][pair];
+      double marg_sum = s_pd[PD_MARG_SUM][pair], pm_sum = s_pd[PD_PM_SUM][pair];
+      double ms_sum = s_pd[PD_MS_SUM][pair], mse;
+      const double ptd_re = s_pd[PD_PTD_RE][pair], ptd_im = s_pd[PD_PTD_IM][pair];
+      double m2_freq = s_pd[PD_M2_FREQ][pair];
       double qr = pr, qi = ptd_im;  // pt_qpsk
       // carrier tracking (:456-470); the two tanh split across the pair
       const double th = aero_tanh(part ? ptd_re : pi);
@@ -356,20 +386,19 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
       marg_p %= MARG_LEN;
       const double mval = marg_sum / ((double)MARG_LEN);
       // dt.update (DSP.h:456-461): slot p written, slot p+1 read
-      {
-        if (lead) dtb[dt_p] = make_double2(qr, qi);
-        dt_p = dt_rp;
-        qr = dv.x;
-        qi = dv.y;
-      }
+      if (lead) dtb[dt_p] = make_double2(qr, qi);
+      dt_p = dt_rp;
+      qr = dv.x;
+      qi = dv.y;
       double rs, rc;
       aero_sincos(mval, rs, rc);
       const double rr = qr * rc - qi * rs, ri = qr * rs + qi * rc;
       qr = rr;
       qi = ri;
       if (TRACE) {
-        if (lead && ptn < S.pt_cap) S.pt[(size_t)c * S.pt_cap + ptn] = make_double2(qr, qi);
-        ptn++;
+        const long long ptn = s_pl[PL_PTN][pair];
+        if (lead && ptn < S.pt_cap) S.pt[(size_t)cl * S.pt_cap + ptn] = make_double2(qr, qi);
+        s_pl[PL_PTN][pair] = ptn + 1;
       }
       // MSEcalc::Update (DSP.cpp:449-461)
       {
@@ -398,21 +427,37 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
         int rbit = qround(0.75 * qr * 127.0 + 128.0);
         if (rbit > 255) rbit = 255;
         if (rbit < 0) rbit = 0;
+        const long long softp = s_pl[PL_SOFTP][pair];
         if (lead) {
+          uint8_t *soft = S.soft + (size_t)cl * SOFT_RING;
           soft[softp & (SOFT_RING - 1)] = (uint8_t)ibit;
           soft[(softp + 1) & (SOFT_RING - 1)] = (uint8_t)rbit;
         }
-        softp += 2;
+        s_pl[PL_SOFTP][pair] = softp + 2;
       }
+      s_pd[PD_CTX1][pair] = ctx1;
+      s_pd[PD_CTX2][pair] = ctx2;
+      s_pd[PD_CTY1][pair] = cty1;
+      s_pd[PD_CTY2][pair] = cty2;
+      s_pd[PD_MARG_SUM][pair] = marg_sum;
+      s_pd[PD_PM_SUM][pair] = pm_sum;
+      s_pd[PD_MS_SUM][pair] = ms_sum;
+      s_pd[PD_MSE][pair] = mse;
+      s_pd[PD_M2_FREQ][pair] = m2_freq;
+      s_pi[PI_MARG_P][pair] = marg_p;
+      s_pi[PI_DT_P][pair] = dt_p;
+      s_pi[PI_PM_P][pair] = pm_p;
+      s_pi[PI_MS_P][pair] = ms_p;
       nco_next(m2_ptr, m2_step);
-      ++n;
+      ++i;
     }
   }
   // staged entries of an unfinished 16-sample group
-  if (lead && filled - 1 >= m_first && ((filled - 1) & 15) != 15) {
-    const long long last = filled - 1, g0 = last & ~15LL;
-    uint32_t *dst = cring + (g0 & (NFFT - 1));
-    for (int j = (int)((g0 >= m_first ? g0 : m_first) - g0); j <= (int)(last - g0); ++j) dst[j] = s_ring[j][pair];
+  if (lead && ifl - 1 >= 1 && ((rb + ifl - 1) & 15) != 15) {
+    const int last = ifl - 1;                  // relative sample of the last staged entry
+    const int g0 = last - ((rb + last) & 15);  // relative sample of its group's slot 0
+    uint32_t *dst = S.cring + (size_t)c * NFFT + ((rb + g0) & (NFFT - 1));
+    for (int j = (g0 >= 1 ? 0 : 1 - g0); j <= last - g0; ++j) dst[j] = s_ring[j][pair];
   }
 
   // epilogue addresses are recomputed from a laundered channel index so the
@@ -425,68 +470,50 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
     for (int j = 0; j < NTAPS; ++j) fir[(size_t)j * C] = q[j];
   }
   if (!lead) return;
-  ds = S.ds + cl;
-  is = S.is + cl;
-  ls = S.ls + cl;
-  const int c0 = 0;
-#define c c0
-  ls[LS_NSAMP * C + c] = n;
-  ls[LS_FILLED * C + c] = filled;
-  ls[LS_SOFT_P * C + c] = softp;
-  if (TRACE) ls[LS_PT_N * C + c] = ptn;
-  ds[DS_M2_PTR * C + c] = m2_ptr;
-  ds[DS_M2_STEP * C + c] = m2_step;
-  ds[DS_M2_FREQ * C + c] = m2_freq;
-  ds[DS_MC_PTR * C + c] = mc_ptr;
-  ds[DS_MC_STEP * C + c] = mc_step;
-  ds[DS_SO_PTR * C + c] = so_ptr;
-  ds[DS_SO_LAST * C + c] = so_last;
-  ds[DS_SO_STEP * C + c] = so_step;
-  ds[DS_SO_FREQ * C + c] = so_freq;
-  ds[DS_AGC_SUM * C + c] = agc_sum;
-  ds[DS_D1_0 * C + c] = d1[0];
-  ds[DS_D1_1 * C + c] = d1[1];
-  ds[DS_D41_0 * C + c] = d41[0];
-  ds[DS_D41_1 * C + c] = d41[1];
-  ds[DS_D41_2 * C + c] = d41[2];
-  ds[DS_D41_3 * C + c] = d41[3];
-  ds[DS_D42_0 * C + c] = d42[0];
-  ds[DS_D42_1 * C + c] = d42[1];
-  ds[DS_D42_2 * C + c] = d42[2];
-  ds[DS_D42_3 * C + c] = d42[3];
-  ds[DS_D8_0 * C + c] = d8[0];
-  ds[DS_D8_1 * C + c] = d8[1];
-  ds[DS_D8_2 * C + c] = d8[2];
-  ds[DS_SR_X1 * C + c] = srx1;
-  ds[DS_SR_X2 * C + c] = srx2;
-  ds[DS_SR_Y1 * C + c] = sry1;
-  ds[DS_SR_Y2 * C + c] = sry2;
-  ds[DS_CT_X1 * C + c] = ctx1;
-  ds[DS_CT_X2 * C + c] = ctx2;
-  ds[DS_CT_Y1 * C + c] = cty1;
-  ds[DS_CT_Y2 * C + c] = cty2;
-  ds[DS_MARG_SUM * C + c] = marg_sum;
-  ds[DS_PM_SUM * C + c] = pm_sum;
-  ds[DS_MS_SUM * C + c] = ms_sum;
-  ds[DS_MSE * C + c] = mse;
-  ds[DS_PTD_RE * C + c] = ptd_re;
-  ds[DS_PTD_IM * C + c] = ptd_im;
-  ds[DS_S2L_RE * C + c] = s2l_re;
-  ds[DS_S2L_IM * C + c] = s2l_im;
-  is[IS_AGC_PTR * C + c] = agc_ptr;
-  is[IS_D1_P * C + c] = p1;
-  is[IS_D41_P * C + c] = p41;
-  is[IS_D42_P * C + c] = p42;
-  is[IS_D8_P * C + c] = p8;
-  is[IS_MARG_P * C + c] = marg_p;
-  is[IS_DT_P * C + c] = dt_p;
-  is[IS_PM_P * C + c] = pm_p;
-  is[IS_MS_P * C + c] = ms_p;
-  is[IS_YUI * C + c] = yui;
-  is[IS_S2L_INIT * C + c] = s2l_init;
+  double *ds = S.ds + cl;
+  int *is = S.is + cl;
+  long long *ls = S.ls + cl;
+  ls[LS_NSAMP * C] = n0 + i;
+  ls[LS_FILLED * C] = n0 + ifl;
+  ls[LS_SOFT_P * C] = s_pl[PL_SOFTP][pair];
+  if (TRACE) ls[LS_PT_N * C] = s_pl[PL_PTN][pair];
+  {
+    static constexpr int pd_dst[PD_N] = {DS_CT_X1, DS_CT_X2, DS_CT_Y1, DS_CT_Y2, DS_MARG_SUM, DS_PM_SUM,
+                                         DS_MS_SUM, DS_MSE, DS_PTD_RE, DS_PTD_IM, DS_M2_FREQ};
+    static constexpr int pi_dst[PI_N] = {IS_MARG_P, IS_DT_P, IS_PM_P, IS_MS_P};
+#pragma unroll
+    for (int k = 0; k < PD_N; ++k) ds[pd_dst[k] * C] = s_pd[k][pair];
+#pragma unroll
+    for (int k = 0; k < PI_N; ++k) is[pi_dst[k] * C] = s_pi[k][pair];
+  }
+  ds[DS_M2_PTR * C] = m2_ptr;
+  ds[DS_M2_STEP * C] = m2_step;
+  ds[DS_MC_PTR * C] = mc_ptr;
+  ds[DS_MC_STEP * C] = mc_step;
+  ds[DS_SO_PTR * C] = so_ptr;
+  ds[DS_SO_LAST * C] = so_last;
+  ds[DS_SO_STEP * C] = so_step;
+  ds[DS_SO_FREQ * C] = so_freq;
+  ds[DS_AGC_SUM * C] = agc_sum;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) ds[(DS_D1_0 + k) * C] = d1[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ds[(DS_D41_0 + k) * C] = d41[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ds[(DS_D42_0 + k) * C] = d42[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) ds[(DS_D8_0 + k) * C] = d8[k];
+  ds[DS_SR_X1 * C] = srx1;
+  ds[DS_SR_X2 * C] = srx2;
+  ds[DS_SR_Y1 * C] = sry1;
+  ds[DS_SR_Y2 * C] = sry2;
+  ds[DS_S2L_RE * C] = s2l_re;
+  ds[DS_S2L_IM * C] = s2l_im;
+  is[IS_AGC_PTR * C] = agc_ptr;
+  is[IS_YUI * C] = yui;
+  is[IS_S2L_INIT * C] = s2l_init;
 }
 
-#undef c
 void launch_demod(hipStream_t st, const DevState &S, const DevTables &T, int nch, int flush, bool trace) {
   dim3 grid((2 * nch + 255) / 256), block(256);
   if (trace)

@@ -568,6 +568,17 @@ int aero_engine_create(const aero_engine_cfg *cfg, aero_engine **out) {
       !host_delay(T48 / 8.0, dly[3]))
     return AERO_E_INVALID;
   if (dly[0].size != 2 || dly[1].size != 4 || dly[2].size != 4 || dly[3].size != 3) return AERO_E_INVALID;
+  // the demod kernel bakes in what these designs give at 48 kHz / 10500 bps:
+  // the ring ages it reads (template arguments of delay_tap) and weights that
+  // do not depend on the write pointer; refuse to run if that ever changes
+  static const int ages[4][2] = {{1, 0}, {3, 2}, {3, 2}, {2, 1}};  // {age_old, age_new}
+  for (int k = 0; k < 4; k++) {
+    if (dly[k].age_old != ages[k][0] || dly[k].age_new != ages[k][1]) return AERO_E_INVALID;
+    for (int p = 1; p < dly[k].size; p++)
+      if (memcmp(&dly[k].w[p], &dly[k].w[0], 8) || memcmp(&dly[k].omw[p], &dly[k].omw[0], 8)) return AERO_E_INVALID;
+  }
+  for (int j = 0; j < NTAPS; j++)  // the kernel stores the 28 distinct taps of the symmetric RRC
+    if (memcmp(&taps[j], &taps[NTAPS - 1 - j], 8)) return AERO_E_INVALID;
   const double sr_b[3] = {0.00032714218939589035, 0, 0.00032714218939589035};
   const double sr_a[3] = {1, -0.39005299948210803, 0.99934571562120822};
   const double ct_b[3] = {0.0010275610653672064, 0.0020551221307344128, 0.0010275610653672064};
