@@ -96,11 +96,13 @@ _SIGS = {
 _lib = None
 
 
-def load_library(path=LIB_PATH):
-    """Loads libaero_engine.so; raises when the HIP build is missing."""
+def load_library(path=None):
+    """Loads libaero_engine.so (or $AERO_ENGINE_SO, an experimental build of
+    the same sources); raises when the HIP build is missing."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get('AERO_ENGINE_SO') or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError('libaero_engine.so not built (%s); run aero-cli_amd/build.py' % path)
     lib = ctypes.CDLL(path)

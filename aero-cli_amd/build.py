@@ -47,27 +47,33 @@ def _stale(out, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_engine(jobs=4):
-    os.makedirs(BUILD, exist_ok=True)
+def build_engine(jobs=4, variant=None, defines=()):
+    """Builds aero-cli_amd/libaero_engine.so.  `variant`/`defines` build an
+    experimental copy (libaero_engine_<variant>.so, objects in build/<variant>)
+    for A/B kernel measurements; select it with AERO_ENGINE_SO=<path>."""
+    bdir = BUILD if variant is None else os.path.join(BUILD, variant)
+    out = ENGINE_SO if variant is None else os.path.join(HERE, 'libaero_engine_%s.so' % variant)
+    os.makedirs(bdir, exist_ok=True)
     headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith('.h')]
     headers.append(os.path.join(ROOT, 'include', 'aero_engine.h'))
+    dflags = ['-D' + d for d in defines]
     tasks, objs = [], []
     for s in HIP_SRCS + CXX_SRCS:
         src = os.path.join(CSRC, s)
-        obj = os.path.join(BUILD, s + '.o')
+        obj = os.path.join(bdir, s + '.o')
         objs.append(obj)
         if _stale(obj, [src] + headers):
             if s.endswith('.hip'):
-                cmd = [HIPCC] + HIP_FLAGS + ['-c', src, '-o', obj]
+                cmd = [HIPCC] + HIP_FLAGS + dflags + ['-c', src, '-o', obj]
             else:
-                cmd = ['g++'] + CXX_FLAGS + ['-c', src, '-o', obj]
+                cmd = ['g++'] + CXX_FLAGS + dflags + ['-c', src, '-o', obj]
             tasks.append(cmd)
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         for f in [ex.submit(_run, t) for t in tasks]:
             f.result()
-    if tasks or _stale(ENGINE_SO, objs):
-        _run([HIPCC, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', ENGINE_SO] + objs)
-    return ENGINE_SO
+    if tasks or _stale(out, objs):
+        _run([HIPCC, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', out] + objs)
+    return out
 
 
 def build_synth():

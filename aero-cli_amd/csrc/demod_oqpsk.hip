@@ -8,12 +8,11 @@
  * expression keeps the reference's operation order; std::complex products
  * are expanded as GCC does ((ac-bd), (ad+bc)); libm calls go to aero_math.h.
  *
- * Lane pairs: lanes 2c and 2c+1 both run channel c.  The even lane keeps
- * the real-part partial sums of the 55-tap RRC, the odd lane the imaginary
- * part (110 doubles would not fit beside the rest of the state in gfx950's
- * 256 architected VGPRs); the filter outputs are swapped through DPP and the
- * remaining recurrence runs identically in both lanes (same values, no
- * divergence inside a pair).  Only the even lane stores shared state.
+ * One lane per channel.  The 55-tap RRC runs in transposed form: the real
+ * partial sums live in VGPRs, the imaginary ones in LDS ([tap][lane], read
+ * and rewritten in descending tap order so the slots never move); together
+ * they would not fit beside the rest of the state in gfx950's 256
+ * architected VGPRs.
  *
  * Segment contract: a launch advances every channel from nsamp up to (but
  * excluding) its next coarse-estimate hop sample, or to the pushed end; it
@@ -85,14 +84,6 @@ __device__ __forceinline__ double iir3(double &x1, double &x2, double &y1, doubl
   return y;
 }
 
-// value of the other lane of this lane's pair (DPP quad_perm [1,0,3,2])
-__device__ __forceinline__ double pair_swap(double v) {
-  const uint64_t u = __builtin_bit_cast(uint64_t, v);
-  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, 0xB1, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), 0xB1, 0xF, 0xF, false);
-  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-
 __device__ __forceinline__ int qround(double d) {  // qRound (Qt 5.9 qglobal.h:525)
   return d >= 0.0 ? int(d + 0.5) : int(d - double(int(d - 1)) + 0.5) + int(d - 1);
 }
@@ -105,28 +96,28 @@ enum { PD_CTX1, PD_CTX2, PD_CTY1, PD_CTY2, PD_MARG_SUM, PD_PM_SUM, PD_MS_SUM, PD
 enum { PI_MARG_P, PI_DT_P, PI_PM_P, PI_MS_P, PI_N };
 enum { PL_SOFTP, PL_PTN, PL_N };
 
+constexpr int DEMOD_BLOCK = 256;  // channels (= lanes) per workgroup
+
 template <bool TRACE>
-__global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables T, int nch, int flush) {
-  // LDS: RRC taps (symmetric, 28 distinct values), the
-  // coarse-ring staging area (entries of 16 consecutive samples leave as one
-  // 64-byte write per channel instead of sixteen 4-byte ones) and the
-  // carrier-step state of the block's 128 channels.
+__global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, DevTables T, int nch, int flush) {
+  // LDS (≈156 KB, one 256-channel block per CU): the imaginary RRC partial
+  // sums, RRC taps (symmetric, 28 distinct values), the coarse-ring staging
+  // area (entries of 16 consecutive samples leave as one 64-byte write per
+  // channel instead of sixteen 4-byte ones) and the carrier-step state.
+  __shared__ double s_qim[NTAPS][DEMOD_BLOCK];
   __shared__ double s_taps[32];
-  __shared__ uint32_t s_ring[16][128];
-  __shared__ double s_pd[PD_N][128];
-  __shared__ long long s_pl[PL_N][128];
-  __shared__ int s_pi[PI_N][128];
+  __shared__ uint32_t s_ring[16][DEMOD_BLOCK];
+  __shared__ double s_pd[PD_N][DEMOD_BLOCK];
+  __shared__ long long s_pl[PL_N][DEMOD_BLOCK];
+  __shared__ int s_pi[PI_N][DEMOD_BLOCK];
   {
     const int l = threadIdx.x;
     if (l < (NTAPS + 1) / 2) s_taps[l] = T.taps[l];  // h[j] == h[54 - j] bit for bit (host-checked)
     __syncthreads();
   }
-  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int c = tid >> 1;
-  const int part = tid & 1;
-  const bool lead = part == 0;
-  const int pair = threadIdx.x >> 1;
-  if (c >= nch) return;  // nch channels -> 2 nch lanes; pairs never straddle the check
+  const int c = blockIdx.x * DEMOD_BLOCK + threadIdx.x;
+  const int pair = threadIdx.x;  // this channel's LDS column
+  if (c >= nch) return;
   const int C = S.C;
 
   // sample counters relative to n0 (a launch covers at most one hop)
@@ -148,11 +139,11 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
   // coarse-ring catch-up (entry of sample n0 not yet written)
   if (ifl == 0 && ia > 0) {
     const int16_t x = S.pcm[(size_t)pb * C + c];
-    if (lead) S.cring[(size_t)c * NFFT + rb] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
+    S.cring[(size_t)c * NFFT + rb] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
     ifl = 1;
   }
   if (ie <= 0) {
-    if (lead) S.ls[LS_FILLED * C + c] = n0 + ifl;
+    S.ls[LS_FILLED * C + c] = n0 + ifl;
     return;
   }
 
@@ -174,7 +165,7 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
   double s2l_re = S.ds[DS_S2L_RE * C + c], s2l_im = S.ds[DS_S2L_IM * C + c];
   int agc_ptr = S.is[IS_AGC_PTR * C + c];
   int yui = S.is[IS_YUI * C + c], s2l_init = S.is[IS_S2L_INIT * C + c];
-  {  // carrier-step state -> LDS (both lanes of a pair write the same values)
+  {  // carrier-step state -> LDS
     static constexpr int pd_src[PD_N] = {DS_CT_X1, DS_CT_X2, DS_CT_Y1, DS_CT_Y2, DS_MARG_SUM, DS_PM_SUM,
                                          DS_MS_SUM, DS_MSE, DS_PTD_RE, DS_PTD_IM, DS_M2_FREQ};
     static constexpr int pi_src[PI_N] = {IS_MARG_P, IS_DT_P, IS_PM_P, IS_MS_P};
@@ -186,10 +177,13 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
     s_pl[PL_PTN][pair] = TRACE ? S.ls[LS_PT_N * C + c] : 0;
   }
 
-  // this lane's half of the transposed RRC: R_j(n-1), j = 0..54
+  // transposed RRC partial sums R_j(n-1), j = 0..54: real part in VGPRs,
+  // imaginary part in LDS
   double q[NTAPS];
 #pragma unroll
-  for (int j = 0; j < NTAPS; ++j) q[j] = S.fir[(size_t)(part * NTAPS + j) * C + c];
+  for (int j = 0; j < NTAPS; ++j) q[j] = S.fir[(size_t)j * C + c];
+#pragma unroll
+  for (int j = 0; j < NTAPS; ++j) s_qim[j][pair] = S.fir[(size_t)(NTAPS + j) * C + c];
 
   const double PT = 0.4 * WTSIZE;  // IfHavePassedPoint(ee) with ee = 0.4 (oqpskdemodulator.cpp:225)
 
@@ -220,10 +214,10 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
         agc_next = S.agc[(size_t)ap * C + c];
       }
       const double dval = ((double)xs) / 32768.0;
-      // mix (oqpskdemodulator.cpp:390): this lane's component of cval
-      const double cv = (part ? cm.y : cm.x) * dval;
+      // mix (oqpskdemodulator.cpp:390): cval = CIS * dval, componentwise
+      const double cv = cm.x * dval, cvi = cm.y * dval;
       // rrc (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
-      const double mine = q[NTAPS - 1];
+      double s2r = q[NTAPS - 1], s2i = s_qim[NTAPS - 1][pair];
       {
         // taps from LDS through an opaque offset, in groups, so they are
         // re-read every sample instead of pinning registers
@@ -236,19 +230,31 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
           if ((j & 7) == 0) asm volatile("" : "+v"(toff));
         }
         q[0] = 0.0 + s_taps[toff] * cv;
-        // pin the update here: left alone the compiler sinks it to the loop
-        // latch and keeps cv and all 28 taps live across the whole sample
+#ifdef AERO_PIN_FIR
+        // (experiment) pin the update here instead of letting the compiler
+        // sink it to the loop latch: fewer live registers, but measured
+        // slower, the sunk FIR fills the latency gaps of the serial chain
 #pragma unroll
         for (int j = 0; j < NTAPS; ++j) asm volatile("" : "+v"(q[j]));
+#endif
       }
-      const double other = pair_swap(mine);
-      double s2r = part ? other : mine, s2i = part ? mine : other;
+      {
+        // imaginary partial sums: descending taps, so slot j-1 is read
+        // before it is rewritten; groups of 8 keep few reads in flight
+#pragma unroll
+        for (int j = NTAPS - 1; j >= 1; --j) {
+          const int tj = j < NTAPS - 1 - j ? j : NTAPS - 1 - j;
+          s_qim[j][pair] = s_qim[j - 1][pair] + s_taps[tj] * cvi;
+          if ((j & 7) == 0) asm volatile("" : : : "memory");
+        }
+        s_qim[0][pair] = 0.0 + s_taps[0] * cvi;
+      }
       // AGC (DSP.cpp:371-380) on |sig2| (oqpskdemodulator.cpp:399-405)
       const double dab = sqrt(s2r * s2r + s2i * s2i);
       {
         agc_sum = agc_sum - agc_old;
         agc_sum = agc_sum + fabs(dab);
-        if (lead) S.agc[(size_t)agc_ptr * C + c] = fabs(dab);
+        S.agc[(size_t)agc_ptr * C + c] = fabs(dab);
         agc_ptr++;
         if (agc_ptr == AGC_LEN) agc_ptr = 0;
         double g = 1.414213562 / fmax(agc_sum / ((double)AGC_LEN), 0.000001);
@@ -312,7 +318,7 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
       if (i + 1 < ia) {
         const int m = rb + i + 1;  // ring slot before masking
         const int k = m & 15;
-        if (lead) {
+        {
           s_ring[k][pair] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)pcm_next << 16);
           if (k == 15) {
             uint32_t *dst = S.cring + (size_t)c * NFFT + ((m - 15) & (NFFT - 1));
@@ -359,11 +365,9 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
       const double ptd_re = s_pd[PD_PTD_RE][pair], ptd_im = s_pd[PD_PTD_IM][pair];
       double m2_freq = s_pd[PD_M2_FREQ][pair];
       double qr = pr, qi = ptd_im;  // pt_qpsk
-      // carrier tracking (:456-470); the two tanh split across the pair
-      const double th = aero_tanh(part ? ptd_re : pi);
-      const double tho = pair_swap(th);
-      const double ct_xt = (part ? tho : th) * pr;
-      const double ct_xt_d = (part ? th : tho) * ptd_im;
+      // carrier tracking (:456-470)
+      const double ct_xt = aero_tanh(pi) * pr;
+      const double ct_xt_d = aero_tanh(ptd_re) * ptd_im;
       double ct_ec = ct_xt_d - ct_xt;
       if (ct_ec > M_PI) ct_ec = M_PI;
       if (ct_ec < -M_PI) ct_ec = -M_PI;
@@ -381,12 +385,12 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
       // marg->UpdateSigned (DSP.cpp:419-427)
       marg_sum = marg_sum - marg_old;
       marg_sum = marg_sum + (ct_ec);
-      if (lead) marg[marg_p] = ct_ec;
+      marg[marg_p] = ct_ec;
       marg_p++;
       marg_p %= MARG_LEN;
       const double mval = marg_sum / ((double)MARG_LEN);
       // dt.update (DSP.h:456-461): slot p written, slot p+1 read
-      if (lead) dtb[dt_p] = make_double2(qr, qi);
+      dtb[dt_p] = make_double2(qr, qi);
       dt_p = dt_rp;
       qr = dv.x;
       qi = dv.y;
@@ -397,7 +401,7 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
       qi = ri;
       if (TRACE) {
         const long long ptn = s_pl[PL_PTN][pair];
-        if (lead && ptn < S.pt_cap) S.pt[(size_t)cl * S.pt_cap + ptn] = make_double2(qr, qi);
+        if (ptn < S.pt_cap) S.pt[(size_t)cl * S.pt_cap + ptn] = make_double2(qr, qi);
         s_pl[PL_PTN][pair] = ptn + 1;
       }
       // MSEcalc::Update (DSP.cpp:449-461)
@@ -405,7 +409,7 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
         const double av = aero_hypot(qr, qi);
         pm_sum = pm_sum - pm_old;
         pm_sum = pm_sum + fabs(av);
-        if (lead) pmb[pm_p] = fabs(av);
+        pmb[pm_p] = fabs(av);
         pm_p++;
         pm_p %= MSE_LEN;
         double mu = pm_sum / ((double)MSE_LEN);
@@ -415,7 +419,7 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
         const double v = (tda * tda) + (tdb * tdb);
         ms_sum = ms_sum - ms_old;
         ms_sum = ms_sum + fabs(v);
-        if (lead) msb[ms_p] = fabs(v);
+        msb[ms_p] = fabs(v);
         ms_p++;
         ms_p %= MSE_LEN;
         mse = ms_sum / ((double)MSE_LEN);
@@ -428,7 +432,7 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
         if (rbit > 255) rbit = 255;
         if (rbit < 0) rbit = 0;
         const long long softp = s_pl[PL_SOFTP][pair];
-        if (lead) {
+        {
           uint8_t *soft = S.soft + (size_t)cl * SOFT_RING;
           soft[softp & (SOFT_RING - 1)] = (uint8_t)ibit;
           soft[(softp + 1) & (SOFT_RING - 1)] = (uint8_t)rbit;
@@ -453,7 +457,7 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
     }
   }
   // staged entries of an unfinished 16-sample group
-  if (lead && ifl - 1 >= 1 && ((rb + ifl - 1) & 15) != 15) {
+  if (ifl - 1 >= 1 && ((rb + ifl - 1) & 15) != 15) {
     const int last = ifl - 1;                  // relative sample of the last staged entry
     const int g0 = last - ((rb + last) & 15);  // relative sample of its group's slot 0
     uint32_t *dst = S.cring + (size_t)c * NFFT + ((rb + g0) & (NFFT - 1));
@@ -465,11 +469,12 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
   int cl = c;
   asm volatile("" : "+v"(cl));
   {
-    double *fir = S.fir + (size_t)part * NTAPS * C + cl;
+    double *fir = S.fir + cl;
 #pragma unroll
     for (int j = 0; j < NTAPS; ++j) fir[(size_t)j * C] = q[j];
+#pragma unroll
+    for (int j = 0; j < NTAPS; ++j) fir[(size_t)(NTAPS + j) * C] = s_qim[j][pair];
   }
-  if (!lead) return;
   double *ds = S.ds + cl;
   int *is = S.is + cl;
   long long *ls = S.ls + cl;
@@ -515,7 +520,7 @@ __global__ __launch_bounds__(256) void demod_oqpsk_kernel(DevState S, DevTables 
 }
 
 void launch_demod(hipStream_t st, const DevState &S, const DevTables &T, int nch, int flush, bool trace) {
-  dim3 grid((2 * nch + 255) / 256), block(256);
+  dim3 grid((nch + DEMOD_BLOCK - 1) / DEMOD_BLOCK), block(DEMOD_BLOCK);
   if (trace)
     hipLaunchKernelGGL(demod_oqpsk_kernel<true>, grid, block, 0, st, S, T, nch, flush);
   else

@@ -39,7 +39,7 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=48, help='hops before timing (hunter scan + lock)')
-    ap.add_argument('--channels', type=int, default=32768, help='VFO channels per GPU')
+    ap.add_argument('--channels', type=int, default=65536, help='VFO channels per GPU (one lane each: 65536 fill the 1024 SIMDs at one wave each)')
     ap.add_argument('--pool', type=int, default=64, help='distinct synthetic streams per GPU')
     ap.add_argument('--cpu-seconds', type=float, default=240.0, help='signal seconds per CPU-baseline process (~10 s CPU each)')
     ap.add_argument('--cpu-procs', type=int, default=8)
