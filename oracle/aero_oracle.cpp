@@ -47,6 +47,7 @@
 #include <algorithm>
 #include <cmath>
 #include <complex>
+#include <memory>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -487,6 +488,11 @@ struct Hunter {
   bool enabled = true;
   uint32_t maxTries = 15, fullScans = 0, minFreq = 0, maxFreq = 25000,
            bandwidth = 10500, iterationsSinceSignal = 0;
+  void setParams(uint32_t mn, uint32_t mx, uint32_t bw) {  // hunter.cpp:14-19
+    minFreq = mn;
+    maxFreq = mx;
+    bandwidth = bw;
+  }
   // returns true and sets fc when newFreqCenter is emitted
   bool updatedSignalStatus(bool gotasignal, double &fc) {
     if (!enabled) return false;
@@ -1033,9 +1039,13 @@ struct Parser {
 
 /* ------------------------------------------------------- AeroL P-channel */
 struct AeroL {
-  // settings for 10500 (decode/aerol.cpp:1012-1021)
-  const int NumberOfBits = 4992, BitsInHeader = 16 + 178, TotalNumberOfBits = 16 + 178 + 4992 + 64;
+  // AeroL::setSettings(fb, burstmode=false) (decode/aerol.cpp:960-1039):
+  // 10500: N=78, 4992 + 16 + 178 + 64; 600/1200: N=6/9, 1152 + 16 + 32
+  int NumberOfBits = 4992, BitsInHeader = 16 + 178, TotalNumberOfBits = 16 + 178 + 4992 + 64;
+  int leaverN = 78;
+  bool useingOQPSK = true;
   UWDetector uw_imag, uw_real;
+  uint32_t pd_reg = 0;  // PreambleDetector (aerol.cpp:686-725): 32-bit shift register
   int realimag = 0, muw = 0, cntr = 1000000000, gotsync_last = 0, blockcnt = -1;
   int formatid = 0, supfrmaker = 0, framecounter1 = 0, framecounter2 = 0;
   uint16_t frameinfo = 0, lastframeinfo = 0;
@@ -1057,13 +1067,23 @@ struct AeroL {
   // outputs
   std::vector<uint8_t> *blocks_out = nullptr, *frames_out = nullptr;
 
-  AeroL() {
+  explicit AeroL(int bitrate = 10500) {
     uw_imag.setPreamble(3780831379ULL, 32);
     uw_real.setPreamble(3780831379ULL, 32);
-    block.assign(4992, 0);
     perm.resize(64);
     for (int i = 0; i < 64; i++) perm[i] = (i * 27) % 64;
-    dl2.assign(4986 + 1, 0);
+    if (bitrate == 10500) {
+      leaverN = 78;
+      dl2.assign(4986 + 1, 0);
+    } else {  // 600 / 1200 (aerol.cpp:975-993)
+      leaverN = bitrate == 600 ? 6 : 9;
+      dl2.assign(570 + 1, 0);
+      NumberOfBits = 1152;
+      BitsInHeader = 16;
+      TotalNumberOfBits = 16 + 1152 + 32;
+      useingOQPSK = false;
+    }
+    block.assign(leaverN * 64, 0);
     pre_state = scrambler_table();
   }
 
@@ -1225,39 +1245,47 @@ struct AeroL {
       }
       if (muw < 100000) muw++;
       int gotsync;
-      realimag++;
-      realimag %= 2;
-      if (realimag) {
-        if (cntr > NumberOfBits - 68 || cntr <= 0 || !datacd) {
-          gotsync = uw_imag.Update(bit);
-          if (!gotsync_last) {
-            gotsync_last = gotsync;
-            gotsync = 0;
-          } else
-            gotsync_last = 0;
-        } else {
-          gotsync = false;
-          gotsync_last = false;
-        }
+      if (!useingOQPSK) {
+        // continuous MSK: PreambleDetector::Update, exact match, buffer
+        // cleared on a hit (aerol.cpp:716-725, :1178-1180); no inversion
+        pd_reg = (pd_reg << 1) | bit;
+        gotsync = pd_reg == 3780831379u;
+        if (gotsync) pd_reg = 0;
       } else {
-        if (cntr > NumberOfBits - 68 || cntr <= 0 || !datacd) {
-          gotsync = uw_real.Update(bit);
-          if (!gotsync_last) {
-            gotsync_last = gotsync;
-            gotsync = 0;
-          } else
-            gotsync_last = 0;
+        realimag++;
+        realimag %= 2;
+        if (realimag) {
+          if (cntr > NumberOfBits - 68 || cntr <= 0 || !datacd) {
+            gotsync = uw_imag.Update(bit);
+            if (!gotsync_last) {
+              gotsync_last = gotsync;
+              gotsync = 0;
+            } else
+              gotsync_last = 0;
+          } else {
+            gotsync = false;
+            gotsync_last = false;
+          }
         } else {
-          gotsync = false;
-          gotsync_last = false;
+          if (cntr > NumberOfBits - 68 || cntr <= 0 || !datacd) {
+            gotsync = uw_real.Update(bit);
+            if (!gotsync_last) {
+              gotsync_last = gotsync;
+              gotsync = 0;
+            } else
+              gotsync_last = 0;
+          } else {
+            gotsync = false;
+            gotsync_last = false;
+          }
         }
-      }
-      if ((realimag && uw_imag.inverted) || (!realimag && uw_real.inverted)) {
-        bit = 1 - bit;
-        if (soft_bit > 128)
-          soft_bit = 255 - soft_bit;
-        else if (soft_bit < 128)
-          soft_bit = 255 - soft_bit;
+        if ((realimag && uw_imag.inverted) || (!realimag && uw_real.inverted)) {
+          bit = 1 - bit;
+          if (soft_bit > 128)
+            soft_bit = 255 - soft_bit;
+          else if (soft_bit < 128)
+            soft_bit = 255 - soft_bit;
+        }
       }
       if (cntr < 1000000000) cntr++;
       if (cntr < 16) {
@@ -1285,11 +1313,11 @@ struct AeroL {
         block[idx] = soft_bit;
         if (idx == (int)block.size() - 1) {
           blockcnt++;
-          // deinterleave_ba(block, 0) with N=78 (aerol.cpp:594-613)
-          std::vector<uint8_t> del(4992);
+          // deinterleave_ba(block, 0) (aerol.cpp:594-613)
+          std::vector<uint8_t> del(block.size());
           int kk = 0;
-          for (int j = 0; j < 78; j++)
-            for (int ii = 0; ii < 64; ii++) del[kk++] = (uint8_t)block[perm[ii] * 78 + j];
+          for (int j = 0; j < leaverN; j++)
+            for (int ii = 0; ii < 64; ii++) del[kk++] = (uint8_t)block[perm[ii] * leaverN + j];
           std::vector<int> deconvol = decode_continuous(del);
           if (blocks_out) {
             uint32_t L = (uint32_t)deconvol.size();
@@ -1564,6 +1592,225 @@ struct Oqpsk {
   }
 };
 
+/* -------------------------------------------------------- MSK demodulator */
+// DiffDecode::UpdateSoft (decode/DSP.cpp:523-548)
+struct DiffDecode {
+  double lastsoftstate = -1;
+  double UpdateSoft(double soft) {
+    double retval = 0;
+    if (soft < 0 && lastsoftstate < 0) {
+      retval = lastsoftstate;
+      lastsoftstate = soft;
+    } else if (soft > 0 && lastsoftstate > 0) {
+      retval = -lastsoftstate;
+      lastsoftstate = soft;
+    } else {
+      retval = std::fabs(lastsoftstate);
+      lastsoftstate = soft;
+    }
+    return retval;
+  }
+};
+
+// MskDemodulator (decode/mskdemodulator.cpp:7-250 ctor + setSettings, as
+// Decoder applies them, decode/decode.cpp:142-150): Fs 12000 (600 bps) or
+// 24000 (1200 bps), fb stays 600 for both, freq_center 0, lockingbw 900,
+// signalthreshold 0.5, coarse fft power 13, AFC on, CPUReduce off.
+// MSKEbNoMeasure is output-dead (EbNoMeasurmentSignal is unconnected) and the
+// spectrum/constellation buffers are GUI-only; neither is run.
+struct Msk {
+  double Fs, lockingbw = 900, fb = 600, signalthreshold = 0.5, ee, correctionfactor = 1.0;
+  int SamplesPerSymbol;
+  bool afc = true, dcd = false;
+  double mse = 10.0;
+  std::vector<cpx> bbcycbuff;
+  int bbcycbuff_ptr = 0, bbnfft = 8192;
+  FIR fir_re, fir_im;
+  AGC agc;
+  MovingAverage msema{600}, marg{80};
+  DelayThingC dt, delayedsmpl;
+  Delay delayt8;
+  IIR st_iir_resonator;
+  WaveTable st_osc, mixer_center, mixer2;
+  Coarse coarse;
+  DiffDecode diffdecode;
+  std::vector<short> RxDataBits;
+  int countdown = 4;  // function static (mskdemodulator.cpp:434)
+  Hunter hunter;
+  AeroL aerol;
+  long long nsamples = 0;
+  std::vector<uint8_t> soft_out;
+  std::vector<double> hops, pts;
+  bool trace_pt = false;
+
+  explicit Msk(int bitrate) : aerol(bitrate) {
+    trig();
+    // ctor at Fs 48000 (mskdemodulator.cpp:7-80): only state that survives setSettings matters
+    mixer_center.SetFreq(1000, 48000);
+    mixer2.SetFreq(1000, 48000);
+    st_osc.SetFreq(600 / 2, 48000);
+    dt.setLength(40);
+    coarse.setSettings(13, 500, 125, 8000);   // CoarseFreqEstimate ctor defaults
+    coarse.setSettings(14, 900, 600, 48000);  // mskdemodulator.cpp:70
+    // setSettings (mskdemodulator.cpp:94-218)
+    Fs = bitrate == 600 ? 12000 : 24000;
+    double freq_center = 0;
+    if (freq_center > ((Fs / 2.0) - (lockingbw / 2.0))) freq_center = ((Fs / 2.0) - (lockingbw / 2.0));
+    SamplesPerSymbol = int(Fs / fb);
+    bbnfft = 8192;
+    bbcycbuff.assign(bbnfft, cpx(0, 0));
+    bbcycbuff_ptr = 0;
+    coarse.setSettings(13, lockingbw, fb, Fs);
+    mixer_center.SetFreq(freq_center, (int)Fs);
+    mixer2.SetFreq(freq_center, (int)Fs);
+    st_osc.SetFreq(fb / 2, (int)Fs);
+    std::vector<double> mf(2 * SamplesPerSymbol);
+    for (int i = 0; i < 2 * SamplesPerSymbol; i++)
+      mf[i] = sin(M_PI * i / (2.0 * SamplesPerSymbol)) / (2.0 * SamplesPerSymbol);
+    fir_re.init(mf);
+    fir_im.init(mf);
+    agc.init(1, Fs);
+    mse = 10.0;
+    // fb < 1200 and Fs != 48000 for both bit rates: the 12 kHz design (:191-203)
+    st_iir_resonator.a[0] = 1;
+    st_iir_resonator.a[1] = -1.974342917561558;
+    st_iir_resonator.a[2] = 0.998953350377616;
+    st_iir_resonator.b[0] = 5.233248111921052e-04;
+    st_iir_resonator.b[1] = 0;
+    st_iir_resonator.b[2] = -5.233248111921052e-04;
+    ee = 0.0125;
+    correctionfactor = 1.0;
+    st_iir_resonator.init();
+    marg = MovingAverage(SamplesPerSymbol);
+    dt.setLength(SamplesPerSymbol / 2);
+    delayedsmpl.setLength(SamplesPerSymbol);
+    delayt8.setdelay((SamplesPerSymbol) / 2.0);
+    hunter.setParams(0, 6000, 900);  // decode/decode.cpp:193
+  }
+
+  void CenterFreqChangedSlot(double freq_center) {  // mskdemodulator.cpp:220-240
+    if (freq_center < (0.75 * fb)) freq_center = 0.75 * fb;
+    if (freq_center > (Fs / 2.0 - 0.75 * fb)) freq_center = Fs / 2.0 - 0.75 * fb;
+    mixer_center.SetFreq(freq_center, (int)Fs);
+    if (afc) mixer2.SetFreq(mixer_center.GetFreqHz());
+    if ((mixer2.GetFreqHz() - mixer_center.GetFreqHz()) > (lockingbw / 2.0))
+      mixer2.SetFreq(mixer_center.GetFreqHz() + (lockingbw / 2.0));
+    if ((mixer2.GetFreqHz() - mixer_center.GetFreqHz()) < (-lockingbw / 2.0))
+      mixer2.SetFreq(mixer_center.GetFreqHz() - (lockingbw / 2.0));
+    for (auto &v : bbcycbuff) v = 0;
+  }
+
+  void FreqOffsetEstimateSlot(double est) {  // mskdemodulator.cpp:430-469
+    if ((mse > signalthreshold) && (fabs(mixer2.GetFreqHz() - (mixer_center.GetFreqHz() + est)) > 0.0))
+      mixer2.SetFreq(mixer_center.GetFreqHz() + est);
+    // the AFC branch needs dcd, which stays false (DCDstatSlot is unconnected)
+    if ((afc) && (dcd) && (fabs(mixer2.GetFreqHz() - mixer_center.GetFreqHz()) > 2.0)) {
+      if (countdown > 0)
+        countdown--;
+      else {
+        mixer_center.SetFreq(mixer2.GetFreqHz());
+        if (mixer_center.GetFreqHz() < lockingbw / 2.0) mixer_center.SetFreq(lockingbw / 2.0);
+        if (mixer_center.GetFreqHz() > (Fs / 2.0 - lockingbw / 2.0)) mixer_center.SetFreq(Fs / 2.0 - lockingbw / 2.0);
+        coarse.bigchange();
+        for (auto &v : bbcycbuff) v = 0;
+      }
+    } else
+      countdown = 4;
+    bool sig = !(mse > signalthreshold);
+    double fc;
+    if (hunter.updatedSignalStatus(sig, fc)) CenterFreqChangedSlot(fc);
+  }
+
+  void writeData(const short *ptr, int n) {  // mskdemodulator.cpp:252-428
+    std::vector<cpx> bbtmp(bbnfft);
+    for (int i = 0; i < n; i++, ptr++, nsamples++) {
+      double dval = ((double)(*ptr)) / 32768.0;
+      bbcycbuff[bbcycbuff_ptr] = mixer_center.WTCISValue() * dval;
+      bbcycbuff_ptr++;
+      bbcycbuff_ptr %= bbnfft;
+      if (bbcycbuff_ptr % (bbnfft / 4) == 0) {
+        for (int j = 0; j < bbnfft; j++) {
+          bbtmp[j] = bbcycbuff[bbcycbuff_ptr];
+          bbcycbuff_ptr++;
+          bbcycbuff_ptr %= bbnfft;
+        }
+        double est = coarse.process(bbtmp);
+        FreqOffsetEstimateSlot(est);
+        hops.push_back((double)nsamples);
+        hops.push_back(est);
+        hops.push_back(mixer2.GetFreqHz());
+        hops.push_back(mixer_center.GetFreqHz());
+        hops.push_back(mse);
+        hops.push_back(mse > signalthreshold ? 0.0 : 1.0);
+      }
+      cpx cval = mixer2.WTCISValue() * (dval);
+      cpx sig2 = cpx(fir_re.FIRUpdateAndProcess(cval.real()), fir_im.FIRUpdateAndProcess(cval.imag()));
+      double dabval = std::sqrt(sig2.real() * sig2.real() + sig2.imag() * sig2.imag());
+      sig2 *= agc.Update(dabval);
+      double abval = std::sqrt(sig2.real() * sig2.real() + sig2.imag() * sig2.imag());
+      if (abval > 2.84) sig2 = (2.84 / abval) * sig2;
+      cpx pt_d = sig2;
+      {  // DelayThing::update_dont_touch (DSP.h:468-473)
+        cpx tmp = sig2;
+        delayedsmpl.update(tmp);
+        pt_d = tmp;
+      }
+      cpx pt_msk = cpx(sig2.real(), pt_d.imag());
+      double st_eta = st_iir_resonator.update(std::abs(pt_msk));
+      cpx st_m1 = cpx(st_eta, -delayt8.update(st_eta));
+      cpx st_out = st_osc.WTCISValue() * st_m1;
+      double st_angle_error = std::arg(st_out);
+      double weighting = fabs(tanh(st_angle_error));
+      if (!dcd)
+        st_osc.AdvanceFractionOfWave(-(1.0 - weighting) * st_angle_error * (0.05 / 360.0));
+      else
+        st_osc.AdvanceFractionOfWave(-(1.0 - weighting) * st_angle_error * (0.003 / 360.0));
+      if (st_osc.IfHavePassedPoint(ee)) {
+        double ct_xt = tanh(sig2.imag()) * sig2.real();
+        double ct_xt_d = tanh(pt_d.real()) * pt_d.imag();
+        double ct_ec = ct_xt_d - ct_xt;
+        if (ct_ec > M_PI) ct_ec = M_PI;
+        if (ct_ec < -M_PI) ct_ec = -M_PI;
+        if (ct_ec > M_PI_2) ct_ec = M_PI_2;
+        if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
+        double carrier_aggression = 12.0 * correctionfactor;
+        if (dcd) carrier_aggression = 8.0 * correctionfactor;
+        mixer2.IncresePhaseDeg(carrier_aggression * 1.0 * ct_ec);
+        mixer2.IncreseFreqHz(carrier_aggression * 0.01 * ct_ec);
+        marg.UpdateSigned(ct_ec / 2.0);
+        dt.update(pt_msk);
+        pt_msk *= cpx(cos(marg.Val), sin(marg.Val));
+        if (trace_pt) {
+          pts.push_back(pt_msk.real());
+          pts.push_back(pt_msk.imag());
+        }
+        double tda = (fabs((pt_msk).real() * 0.75) - 1.0);
+        double tdb = (fabs((pt_msk).imag() * 0.75) - 1.0);
+        mse = msema.Update((tda * tda) + (tdb * tdb));
+        double imagin = diffdecode.UpdateSoft(pt_msk.imag());
+        int ibit = qRound((imagin) * 127.0 + 128.0);
+        if (ibit > 255) ibit = 255;
+        if (ibit < 0) ibit = 0;
+        RxDataBits.push_back((short)(uint8_t)ibit);
+        double real = diffdecode.UpdateSoft(pt_msk.real());
+        real = -real;
+        ibit = qRound((real) * 127.0 + 128.0);
+        if (ibit > 255) ibit = 255;
+        if (ibit < 0) ibit = 0;
+        RxDataBits.push_back((short)(uint8_t)ibit);
+        if (RxDataBits.size() >= 12) {
+          for (short s : RxDataBits) soft_out.push_back((uint8_t)s);
+          aerol.decode(RxDataBits.data(), (int)RxDataBits.size());
+          RxDataBits.clear();
+        }
+      }
+      mixer2.WTnextFrame();
+      mixer_center.WTnextFrame();
+      st_osc.WTnextFrame();
+    }
+  }
+};
+
 template <class T>
 size_t copy_out(const std::vector<T> &v, T *dst, size_t cap) {
   size_t n = std::min(cap, v.size());
@@ -1574,36 +1821,51 @@ size_t copy_out(const std::vector<T> &v, T *dst, size_t cap) {
 }  // namespace
 
 struct oracle_chan {
-  Oqpsk d;
+  std::unique_ptr<Oqpsk> oq;
+  std::unique_ptr<Msk> msk;
   std::vector<uint8_t> blocks, frames;
   std::string items;
+  AeroL &aerol() { return oq ? oq->aerol : msk->aerol; }
+  const std::vector<uint8_t> &soft() const { return oq ? oq->soft_out : msk->soft_out; }
+  const std::vector<double> &hops() const { return oq ? oq->hops : msk->hops; }
+  const std::vector<double> &pts() const { return oq ? oq->pts : msk->pts; }
 };
 
 extern "C" {
 
 oracle_chan *oracle_create(int bitrate, int flags) {
-  if (bitrate != 10500) return nullptr;
+  if (bitrate != 10500 && bitrate != 600 && bitrate != 1200) return nullptr;
   oracle_chan *c = new oracle_chan();
-  c->d.trace_pt = (flags & ORACLE_TRACE_PT) != 0;
-  c->d.aerol.blocks_out = &c->blocks;
-  c->d.aerol.frames_out = &c->frames;
-  c->d.aerol.parser.items = &c->items;
+  const bool tp = (flags & ORACLE_TRACE_PT) != 0;
+  if (bitrate == 10500) {
+    c->oq.reset(new Oqpsk());
+    c->oq->trace_pt = tp;
+  } else {
+    c->msk.reset(new Msk(bitrate));
+    c->msk->trace_pt = tp;
+  }
+  c->aerol().blocks_out = &c->blocks;
+  c->aerol().frames_out = &c->frames;
+  c->aerol().parser.items = &c->items;
   return c;
 }
 void oracle_destroy(oracle_chan *c) { delete c; }
 int oracle_push(oracle_chan *c, const int16_t *pcm, size_t n) {
   if (!n) return 0;
-  c->d.writeData(pcm, (int)n);
+  if (c->oq)
+    c->oq->writeData(pcm, (int)n);
+  else
+    c->msk->writeData(pcm, (int)n);
   return 0;
 }
 size_t oracle_softbits(const oracle_chan *c, uint8_t *dst, size_t cap) {
-  return copy_out(c->d.soft_out, dst, cap);
+  return copy_out(c->soft(), dst, cap);
 }
 size_t oracle_hops(const oracle_chan *c, double *dst, size_t cap_records) {
-  return copy_out(c->d.hops, dst, cap_records * 6) / 6;
+  return copy_out(c->hops(), dst, cap_records * 6) / 6;
 }
 size_t oracle_pt(const oracle_chan *c, double *dst, size_t cap_records) {
-  return copy_out(c->d.pts, dst, cap_records * 2) / 2;
+  return copy_out(c->pts(), dst, cap_records * 2) / 2;
 }
 size_t oracle_blocks(const oracle_chan *c, uint8_t *dst, size_t cap) {
   return copy_out(c->blocks, dst, cap);

@@ -56,8 +56,32 @@ def synth(seconds=10.0, seed=0xAE20, carrier=12037.5, ebn0=12.0, amplitude=0.25,
     return pcm
 
 
+def synth_msk(seconds=10.0, bitrate=600, seed=0xAE40, carrier=1800.0, ebn0=12.0, amplitude=0.25, phase0=0.3,
+              msg_rate=0.6, lead_in=500, baud=None, return_frames=False):
+    """int16 PCM of a 600/1200-bps MSK P-channel at 12/24 kHz (SURVEY.md §8(d)
+    C3 input) + the transmitted 72-byte information fields per frame.  `baud`
+    (default = bitrate) is the modulation rate; the frame layout follows
+    `bitrate`."""
+    global _synth
+    if _synth is None:
+        _synth = ctypes.CDLL(SYNTH_SO)
+    _synth.aero_synth_msk.restype = ctypes.c_size_t
+    fs = 12000.0 if bitrate == 600 else 24000.0
+    n = int(fs * seconds)
+    pcm = np.zeros(n, dtype=np.int16)
+    maxf = int(seconds * (baud or bitrate) / 1200) + 8
+    frames = np.zeros(72 * maxf, dtype=np.uint8)
+    cfg = SynthCfg(fs, carrier, phase0, amplitude, ebn0, seed, msg_rate, lead_in)
+    nf = _synth.aero_synth_msk(ctypes.byref(cfg), ctypes.c_int(bitrate), ctypes.c_int(baud or bitrate),
+                               pcm.ctypes.data_as(ctypes.c_void_p),
+                               ctypes.c_size_t(n), frames.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(maxf))
+    if return_frames:
+        return pcm, frames[:72 * min(nf, maxf)].reshape(-1, 72)
+    return pcm
+
+
 class Oracle:
-    """One reference channel (a whole `aero-decode -b 10500` instance)."""
+    """One reference channel (a whole `aero-decode -b <bitrate>` instance)."""
     _lib = None
 
     @classmethod
@@ -90,9 +114,11 @@ class Oracle:
             cls._lib = L
         return cls._lib
 
-    def __init__(self, trace_pt=False):
+    def __init__(self, trace_pt=False, bitrate=10500):
         self.L = self.lib()
-        self.h = self.L.oracle_create(10500, 1 if trace_pt else 0)
+        self.bitrate = bitrate
+        self.h = self.L.oracle_create(bitrate, 1 if trace_pt else 0)
+        assert self.h, 'oracle_create(%d) failed' % bitrate
 
     def __del__(self):
         if getattr(self, 'h', None):

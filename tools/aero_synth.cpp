@@ -38,6 +38,9 @@ typedef struct {
 
 size_t aero_synth_p10500(const aero_synth_cfg *cfg, int16_t *pcm, size_t nsamples,
                          uint8_t *frames, size_t frames_cap);
+/* 600/1200-bps MSK P-channel (cfg->fs = 12000 / 24000); frames: 72 info bytes each */
+size_t aero_synth_msk(const aero_synth_cfg *cfg, int bitrate, int baud, int16_t *pcm, size_t nsamples,
+                      uint8_t *frames, size_t frames_cap);
 }
 
 namespace {
@@ -193,6 +196,37 @@ struct Tx {
     }
   }
 
+  // 600/1200-bps frame (aerol.cpp:975-993): 16 header + 1152 data (blocks of
+  // N x 64, N = 6 / 9) + 32-bit UW at the end; 6 SUs = 72 info bytes
+  void next_frame_msk(int N, uint8_t *info72) {
+    uint8_t info[72];
+    for (int k = 0; k < 6; k++) {
+      while (queue.empty()) refill();
+      memcpy(info + 12 * k, queue.front().b, 12);
+      queue.erase(queue.begin());
+    }
+    if (info72) memcpy(info72, info, 72);
+    int ibits[576];
+    for (int h = 0; h < 576; h++) ibits[h] = ((info[h / 8] >> (h % 8)) & 1) ^ scr[h];
+    int coded[1152];
+    for (int t = 0; t < 576; t++) {
+      enc_reg = ((enc_reg << 1) | (unsigned)ibits[t]) & 127;
+      coded[2 * t] = __builtin_popcount(enc_reg & 109) & 1;
+      coded[2 * t + 1] = __builtin_popcount(enc_reg & 79) & 1;
+    }
+    chan.assign(1200, 0);
+    unsigned fc = (unsigned)(frame_no & 0xF);
+    unsigned hdr = 0x1000u | ((unsigned)((frame_no >> 4) & 0xF) << 8) | (fc << 4) | fc;
+    for (int b = 0; b < 16; b++) chan[b] = (hdr >> (15 - b)) & 1;
+    const int B = N * 64;
+    for (int b0 = 0; b0 < 1152; b0 += B)
+      for (int j = 0; j < N; j++)
+        for (int i = 0; i < 64; i++) chan[16 + b0 + perm[i] * N + j] = coded[b0 + j * 64 + i];
+    const uint32_t uw = 0xE15AE893u;
+    for (int j = 0; j < 32; j++) chan[1168 + j] = (uw >> (31 - j)) & 1;
+    frame_no++;
+  }
+
   // builds chan[] (5250 bits) for the next frame; info bytes to *info312
   void next_frame(uint8_t *info312) {
     uint8_t info[312];
@@ -302,6 +336,74 @@ extern "C" size_t aero_synth_p10500(const aero_synth_cfg *cfg, int16_t *pcm, siz
         I += is[k] * pulse(t - (double)k - 0.5);
       }
       double ph = w * (double)nn + cfg->phase0;
+      x = A * (I * cos(ph) + Q * sin(ph));
+    }
+    if (sigma > 0) x += sigma * nrng.gauss();
+    double v = floor(x * 32768.0 + 0.5);
+    if (v > 32767) v = 32767;
+    if (v < -32768) v = -32768;
+    pcm[n] = (int16_t)v;
+  }
+  return nframes;
+}
+
+/* MSK: channel bits b_n are differentially encoded onto alternating arms so
+ * that MskDemodulator's DiffDecode (decode/DSP.cpp:523-548) and its negated
+ * real arm (decode/mskdemodulator.cpp:387-401) give them back: on the arm the
+ * receiver reads first (imag) a 1 is a sign change, on the other a 1 is no
+ * change.  Half-sine pulses over two bit periods (the receiver's matched
+ * filter, mskdemodulator.cpp:126-133), arms offset by one bit period. */
+extern "C" size_t aero_synth_msk(const aero_synth_cfg *cfg, int bitrate, int baud, int16_t *pcm, size_t nsamples,
+                                 uint8_t *frames, size_t frames_cap) {
+  // bitrate selects the frame layout (N = 6 / 9), baud the modulation rate.
+  // aero-decode -b 1200 demodulates at fb = 600 (decode/decode.cpp:142-150
+  // never sets fb), so only 600-baud input exercises its 1200 framing.
+  Tx tx(*cfg);
+  const int N = bitrate == 600 ? 6 : 9;
+  const double Fs = cfg->fs, Tb = Fs / (double)baud;
+  std::vector<double> arm;  // +-1 per channel bit
+  size_t nframes = 0;
+  double last = 1.0;
+  auto ensure = [&](size_t k) {
+    while (arm.size() <= k) {
+      uint8_t *dst = (frames && nframes < frames_cap) ? frames + 72 * nframes : nullptr;
+      tx.next_frame_msk(N, dst);
+      nframes++;
+      for (int b = 0; b < 1200; b++) {
+        const size_t n = arm.size();
+        const bool flip = (n % 2 == 0) ? !tx.chan[b] : tx.chan[b];
+        last = flip ? -last : last;
+        arm.push_back(last);
+      }
+    }
+  };
+  const double A = cfg->amplitude;
+  const double P = A * A / 2.0;  // half-sine arms: E[I^2] = E[Q^2] = 1/2
+  double sigma = 0;
+  if (cfg->ebn0_db < 99) {
+    double Eb = P / (double)baud;
+    double N0 = Eb / pow(10.0, cfg->ebn0_db / 10.0);
+    sigma = sqrt(N0 / 2.0 * Fs);
+  }
+  Rng nrng(cfg->seed ^ 0xA5A5A5A55A5A5A5AULL);
+  const double w = 2.0 * M_PI * cfg->carrier_hz / Fs;
+  for (size_t n = 0; n < nsamples; n++) {
+    double x = 0;
+    long long nn = (long long)n - cfg->lead_in;
+    if (nn >= 0) {
+      const double t = (double)nn / Tb;  // in bit periods
+      const long long k1 = (long long)floor(t), k0 = k1 - 1;
+      ensure((size_t)k1 + 1);
+      double I = 0, Q = 0;
+      for (long long k = k0; k <= k1; k++) {
+        if (k < 0) continue;
+        const double p = sin(M_PI * (t - (double)k) / 2.0);  // pulse over [k, k+2)
+        if (k % 2 == 0)
+          I += arm[k] * p;
+        else
+          Q += arm[k] * p;
+      }
+      const double ph = w * (double)nn + cfg->phase0;
       x = A * (I * cos(ph) + Q * sin(ph));
     }
     if (sigma > 0) x += sigma * nrng.gauss();
