@@ -151,6 +151,7 @@ class Engine:
         _check(self.lib.aero_engine_create(ctypes.byref(cfg), ctypes.byref(h)), 'aero_engine_create')
         self.h = h
         self.flags = flags
+        self._fs = {}
 
     def close(self):
         if self.h:
@@ -169,14 +170,20 @@ class Engine:
     def __exit__(self, *a):
         self.close()
 
-    def open_channel(self, bitrate=10500, fs=48000, disable_reassembly=False, burst=False):
+    # sample rate aero-decode feeds each bit rate (decode/decode.cpp:142-159)
+    RATE = {10500: 48000, 600: 12000, 1200: 24000}
+
+    def open_channel(self, bitrate=10500, fs=None, disable_reassembly=False, burst=False):
+        fs = fs or self.RATE.get(bitrate, 48000)
         cfg = ChannelCfg(bitrate, int(burst), fs, int(disable_reassembly))
         ch = ctypes.c_int()
         _check(self.lib.aero_channel_open(self.h, ctypes.byref(cfg), ctypes.byref(ch)), 'aero_channel_open')
+        self._fs[ch.value] = fs
         return ch.value
 
-    def push(self, ch, pcm, fs=48000):
+    def push(self, ch, pcm, fs=None):
         pcm = np.ascontiguousarray(pcm, dtype=np.int16)
+        fs = fs or self._fs.get(ch, 48000)
         _check(self.lib.aero_push_pcm(self.h, ch, pcm.ctypes.data, pcm.size, fs), 'aero_push_pcm')
 
     def push_batch(self, pcm, nch=None):

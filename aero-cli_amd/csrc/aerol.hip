@@ -143,6 +143,96 @@ __global__ __launch_bounds__(256) void frame_kernel(DevState S, int nch) {
   is[IS_DATACDCD * C + c] = isu_reset;
 }
 
+// AeroL::Decode for continuous 600/1200 bps (decode/aerol.cpp:1060-2038 with
+// useingOQPSK false, burstmode false): PreambleDetector::Update, an exact
+// 32-bit UW match that clears its buffer on a hit (aerol.cpp:716-725), no
+// phase inversion; 16 header bits + 1152 data bits in blocks of N x 64 +
+// 32 UW bits per frame.  A job also carries whether the infofield was
+// cleared (cntr == 0) since the previous block, so the host can assemble a
+// frame's SUs from its blocks exactly as infofield is built (aerol.cpp:1509-1520).
+template <int M>
+__global__ __launch_bounds__(256) void frame_msk_kernel(DevState S, int nch) {
+  constexpr int N = MskK<M>::LEAVER, B = N * 64;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nch) return;
+  const int C = S.C;
+  int *is = S.is;
+  long long *ls = S.ls;
+  const long long P = ls[LS_SOFT_P * C + c];
+  long long q = ls[LS_SOFT_C * C + c];
+  const long long E = P - P % 12;  // delivered in groups of 12 (mskdemodulator.cpp:404-407)
+  if (q >= E) return;
+  int cntr = is[IS_CNTR * C + c];
+  uint32_t reg = (uint32_t)is[IS_MSK_PD * C + c];
+  int frameinfo = is[IS_FRAMEINFO * C + c], lastframeinfo = is[IS_LASTFRAMEINFO * C + c];
+  int formatid = is[IS_FORMATID * C + c];
+  int scr_pos = is[IS_SCR_POS * C + c], blkbuf = is[IS_BLKBUF * C + c];
+  int has_ov = is[IS_HAS_OVERLAP * C + c];
+  int isu_reset = is[IS_DATACDCD * C + c];
+  int since_clear = is[IS_BLK_SINCE_CLEAR * C + c];
+  const uint8_t *soft = S.soft + (size_t)c * SOFT_RING;
+  const int NumberOfBits = 1152, BitsInHeader = 16, Total = 16 + 1152 + 32;
+
+  for (; q < E; ++q) {
+    const int sv = soft[q & (SOFT_RING - 1)];
+    const int bit = sv >= 128 ? 1 : 0;
+    reg = (reg << 1) | (uint32_t)bit;
+    const int gotsync = reg == UW;
+    if (gotsync) reg = 0;
+    if (cntr < 1000000000) cntr++;
+    if (cntr < 16) {
+      if (cntr == 0) {
+        frameinfo = bit;
+        since_clear = 0;  // infofield.clear()
+      } else
+        frameinfo = ((frameinfo << 1) | bit) & 0xFFFF;
+    }
+    if (cntr == 15) {
+      const int tval = frameinfo;
+      frameinfo = lastframeinfo;
+      lastframeinfo = tval;
+      formatid = (frameinfo >> 12) & 0x000F;
+    }
+    if (cntr >= 16) {
+      int idx = (cntr - BitsInHeader) % B;
+      if (idx < 0) idx = 0;
+      uint8_t *blk = S.block + ((size_t)c * 2 + blkbuf) * B;
+      blk[idx] = (uint8_t)sv;
+      if (idx == B - 1) {
+        const int j = atomicAdd(S.njobs, 1);
+        int4 *jobs = reinterpret_cast<int4 *>(S.jobs);
+        jobs[j] = make_int4(c, blkbuf | ((has_ov ? 0 : 1) << 1) | (isu_reset << 2) | ((since_clear == 0) << 3),
+                            scr_pos, ((cntr - BitsInHeader) == (NumberOfBits - 1) ? 0x100 : 0) | formatid);
+        isu_reset = 0;
+        since_clear++;
+        scr_pos += has_ov ? B / 2 : (B + 24) / 2 - 25;
+        has_ov = 1;
+        blkbuf ^= 1;
+      }
+    }
+    if (gotsync) {
+      if (cntr + 1 != Total) isu_reset = 1;
+      cntr = -1;
+      scr_pos = 0;
+    }
+    if (cntr + 1 == Total) {
+      scr_pos = 0;
+      cntr = -1;
+    }
+  }
+  ls[LS_SOFT_C * C + c] = q;
+  is[IS_CNTR * C + c] = cntr;
+  is[IS_MSK_PD * C + c] = (int)reg;
+  is[IS_FRAMEINFO * C + c] = frameinfo;
+  is[IS_LASTFRAMEINFO * C + c] = lastframeinfo;
+  is[IS_FORMATID * C + c] = formatid;
+  is[IS_SCR_POS * C + c] = scr_pos;
+  is[IS_BLKBUF * C + c] = blkbuf;
+  is[IS_HAS_OVERLAP * C + c] = has_ov;
+  is[IS_DATACDCD * C + c] = isu_reset;
+  is[IS_BLK_SINCE_CLEAR * C + c] = since_clear;
+}
+
 // ---------------------------------------------------------------- Viterbi
 __device__ __forceinline__ int conv_table(int r) {  // table[r]: bit j = parity(r & poly[j])
   return (__builtin_popcount(r & 109) & 1) | ((__builtin_popcount(r & 79) & 1) << 1);
@@ -160,33 +250,36 @@ __device__ __forceinline__ int shfl_idx(int v, int src) {
 
 constexpr int HCAP = 140, MINTB = 35, RENORM = 128;
 
+// BLK = interleaver block (N x 64 soft bits), N = BLK / 64; DL2 = dl2 length + 1
+template <int BLK, int DL2>
 __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, int trace) {
-  __shared__ uint8_t sbuf[VIT_MAX + 2];
+  constexpr int NL = BLK / 64, HALF = BLK / 2;
+  __shared__ uint8_t sbuf[62 + BLK + 24 + 2];
   __shared__ unsigned long long hist[HCAP];
-  __shared__ uint8_t obits[2560];
-  __shared__ uint8_t dl[2496];
+  __shared__ uint8_t obits[HALF + 64];
+  __shared__ uint8_t dl[HALF];
   __shared__ uint8_t info[320];
   const int job = blockIdx.x;
   if (job >= *S.njobs) return;
   const int lane = threadIdx.x;
   const int4 jd = reinterpret_cast<const int4 *>(S.jobs)[job];
-  const int c = jd.x, buf = jd.y & 1, first = (jd.y >> 1) & 1, reset = (jd.y >> 2) & 1;
+  const int c = jd.x, buf = jd.y & 1, first = (jd.y >> 1) & 1, reset = (jd.y >> 2) & 1, clear = (jd.y >> 3) & 1;
   const int scr_pos = jd.z, formatid = jd.w & 0xFF, frame_done = (jd.w >> 8) & 1;
   const int C = S.C;
   const int ov = first ? 0 : 62;
-  const int nsoft = ov + BLOCK + 24;
+  const int nsoft = ov + BLK + 24;
   // load: overlap + deinterleaved block + 24 erasures
   if (!first && lane < 62) sbuf[lane] = S.overlap[(size_t)c * 64 + lane];
   {
-    const uint8_t *blk = S.block + ((size_t)c * 2 + buf) * BLOCK;
+    const uint8_t *blk = S.block + ((size_t)c * 2 + buf) * BLK;
     const int row = (lane * 27) % 64;  // interleaverowdepermute[lane]
-    for (int j = 0; j < 78; ++j) sbuf[ov + j * 64 + lane] = blk[row * 78 + j];
+    for (int j = 0; j < NL; ++j) sbuf[ov + j * 64 + lane] = blk[row * NL + j];
   }
-  if (lane < 24) sbuf[ov + BLOCK + lane] = 128;
-  for (int k = lane; k < 2560; k += 64) obits[k] = 0;
+  if (lane < 24) sbuf[ov + BLK + lane] = 128;
+  for (int k = lane; k < HALF + 64; k += 64) obits[k] = 0;
   __syncthreads();
   // keep the last 62 deinterleaved soft values for the next block
-  if (lane < 62) S.overlap[(size_t)c * 64 + lane] = sbuf[ov + BLOCK - 62 + lane];
+  if (lane < 62) S.overlap[(size_t)c * 64 + lane] = sbuf[ov + BLK - 62 + lane];
 
   const int sets = nsoft / 2;
   const int s = lane;
@@ -254,28 +347,31 @@ __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, in
     process(skip);
   }
   traceback(0, 0);
-  // Decode_Continuous: keep decoded bits [25, 25 + 2496) clipped to size/2
-  const int nbits = (sets - 25) < 2496 ? (sets - 25) : 2496;
+  // Decode_Continuous: keep decoded bits [25, 25 + BLK/2) clipped to size/2
+  const int nbits = (sets - 25) < HALF ? (sets - 25) : HALF;
   if (trace) {
     uint8_t *dbg = S.blocks_dbg + (size_t)c * 2500;
     if (lane == 0) *reinterpret_cast<int *>(dbg) = nbits;
     for (int k = lane; k < nbits; k += 64) dbg[4 + k] = obits[25 + k];
   }
   // DelayLine dl2 (aerol.h:464-471): out[q] = old[(p+q+1)%L], new[(p+q)%L] = in[q]
-  uint8_t *dlg = S.dl2 + (size_t)c * DL2_LEN;
+  // (nbits < DL2: one wrap at most)
+  static_assert(HALF < DL2, "delay line longer than a block");
+  uint8_t *dlg = S.dl2 + (size_t)c * DL2;
   const int p0 = S.is[IS_DL2_PTR * C + c];
   for (int k = lane; k < nbits; k += 64) {
     int r = p0 + k + 1;
-    r = r >= DL2_LEN ? r - DL2_LEN : r;
+    r = r >= DL2 ? r - DL2 : r;
+    r = r >= DL2 ? r - DL2 : r;
     dl[k] = dlg[r];
   }
   __syncthreads();
   for (int k = lane; k < nbits; k += 64) {
     int w = p0 + k;
-    w = w >= DL2_LEN ? w - DL2_LEN : w;
+    w = w >= DL2 ? w - DL2 : w;
     dlg[w] = obits[25 + k];
   }
-  if (lane == 0) S.is[IS_DL2_PTR * C + c] = (p0 + nbits) % DL2_LEN;
+  if (lane == 0) S.is[IS_DL2_PTR * C + c] = (p0 + nbits) % DL2;
   // scrambler + LSB-first packing (aerol.cpp:1506-1520)
   const int nbytes = nbits / 8;
   for (int b = lane; b < nbytes; b += 64) {
@@ -285,10 +381,11 @@ __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, in
   }
   for (int b = nbytes + lane; b < 312; b += 64) info[b] = 0;
   __syncthreads();
-  // per-SU CRC (aerol.cpp:1531-1543)
+  // per-SU CRC (aerol.cpp:1531-1543); a 600/1200 frame spans 2-3 blocks and
+  // its SUs are checked on the host once the frame's infofield is complete
   const int nsu = nbytes / 12;
   bool ok = false;
-  if (lane < nsu && frame_done) {
+  if (lane < nsu && frame_done && BLK == BLOCK) {
     const uint8_t *su = info + 12 * lane;
     unsigned crc = 0xFFFF, sum = 0;
     for (int i = 0; i < 10; ++i) {
@@ -312,19 +409,36 @@ __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, in
   for (int b = lane; b < 312; b += 64) out[b] = info[b];
   if (lane == 0) {
     int *o = reinterpret_cast<int *>(out + 312);
-    o[0] = frame_done ? nbytes : -1;
-    o[1] = (int)(okm & 0x3FFFFFFULL);
+    if (BLK == BLOCK) {
+      o[0] = frame_done ? nbytes : -1;
+      o[1] = (int)(okm & 0x3FFFFFFULL);
+    } else {  // block bytes; bit 8: frame done, bit 9: infofield cleared before this block
+      o[0] = nbytes | (frame_done << 8) | (clear << 9);
+      o[1] = 0;
+    }
     o[2] = formatid;
     o[3] = c | (reset << 30);
   }
 }
 
-void launch_frame(hipStream_t st, const DevState &S, int nch) {
-  hipLaunchKernelGGL(frame_kernel, dim3((nch + 255) / 256), dim3(256), 0, st, S, nch);
+void launch_frame(hipStream_t st, int mode, const DevState &S, int nch) {
+  const dim3 g((nch + 255) / 256), b(256);
+  if (mode == MODE_OQPSK)
+    hipLaunchKernelGGL(frame_kernel, g, b, 0, st, S, nch);
+  else if (mode == MODE_MSK600)
+    hipLaunchKernelGGL(frame_msk_kernel<MODE_MSK600>, g, b, 0, st, S, nch);
+  else
+    hipLaunchKernelGGL(frame_msk_kernel<MODE_MSK1200>, g, b, 0, st, S, nch);
 }
 
-void launch_viterbi(hipStream_t st, const DevState &S, const DevTables &T, int max_jobs, int trace) {
-  if (max_jobs > 0) hipLaunchKernelGGL(viterbi_kernel, dim3(max_jobs), dim3(64), 0, st, S, T, trace);
+void launch_viterbi(hipStream_t st, int mode, const DevState &S, const DevTables &T, int max_jobs, int trace) {
+  if (max_jobs <= 0) return;
+  if (mode == MODE_OQPSK)
+    hipLaunchKernelGGL((viterbi_kernel<BLOCK, DL2_LEN>), dim3(max_jobs), dim3(64), 0, st, S, T, trace);
+  else if (mode == MODE_MSK600)
+    hipLaunchKernelGGL((viterbi_kernel<6 * 64, MSK_DL2_LEN>), dim3(max_jobs), dim3(64), 0, st, S, T, trace);
+  else
+    hipLaunchKernelGGL((viterbi_kernel<9 * 64, MSK_DL2_LEN>), dim3(max_jobs), dim3(64), 0, st, S, T, trace);
 }
 
 }  // namespace aero

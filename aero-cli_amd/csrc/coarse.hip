@@ -15,25 +15,52 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "aero_math.h"
 #include "engine_common.h"
 
 namespace aero {
 
-constexpr int FT = 1024;  // threads per channel FFT
-constexpr int PADDED = NFFT + NFFT / 16;
+// Geometry of one channel's coarse estimate (decode/coarsefreqestimate.cpp:39-76
+// with the settings each demodulator applies).  OQPSK: setSettings(14, 10500,
+// 10500, 48000); MSK: setSettings(13, 900, 600, Fs).
+template <int M>
+struct CoarseK;
+template <>
+struct CoarseK<MODE_OQPSK> {
+  static constexpr int LOG2N = 14, HOPN = 4096, START = 3584, STOP = 12800, ILO = 4608, IHI = 11776, EPB = 1792;
+  static constexpr int YLO = 2815, YHI = 13568;
+  static constexpr double FS = 48000.0;
+};
+template <>
+struct CoarseK<MODE_MSK600> {
+  static constexpr int LOG2N = 13, HOPN = 2048, START = 614, STOP = 7578, ILO = 3482, IHI = 4710, EPB = 205;
+  static constexpr int YLO = 3276, YHI = 4915;
+  static constexpr double FS = 12000.0;
+};
+template <>
+struct CoarseK<MODE_MSK1200> {
+  static constexpr int LOG2N = 13, HOPN = 2048, START = 307, STOP = 7885, ILO = 3789, IHI = 4403, EPB = 102;
+  static constexpr int YLO = 3686, YHI = 4505;
+  static constexpr double FS = 24000.0;
+};
 
 __device__ __forceinline__ int pad(int p) { return p + (p >> 4); }
 
-template <int PH>
+// position of value i of thread t in register phase PH (4 FFT stages per
+// phase; the last phase holds the LOG2N - 12 remaining stage bits in i's low bits)
+template <int LOG2N, int PH>
 __device__ __forceinline__ int epos(int t, int i) {
+  constexpr int LFT = LOG2N - 4, R = LOG2N - 12;
   if (PH == 0) return (t << 4) | i;
   if (PH == 1) return (t & 15) | (i << 4) | ((t >> 4) << 8);
   if (PH == 2) return (t & 255) | (i << 8) | ((t >> 8) << 12);
-  return (t & 1023) | ((i >> 2) << 10) | ((i & 3) << 12);
+  return (t & ((1 << LFT) - 1)) | ((i >> R) << LFT) | ((i & ((1 << R) - 1)) << (LOG2N - R));
 }
 
-__device__ __forceinline__ int bitrev14(int p) { return (int)(__builtin_bitreverse32((uint32_t)p) >> 18); }
+template <int LOG2N>
+__device__ __forceinline__ int bitrev(int p) { return (int)(__builtin_bitreverse32((uint32_t)p) >> (32 - LOG2N)); }
 
 // one radix-2 DIT stage of half-size n on the thread's 16 values;
 // `lb` is the bit of i that encodes the stage's position bit.
@@ -45,14 +72,14 @@ __device__ __forceinline__ int fresh(int t) {
   return t;
 }
 
-template <int PH>
+template <int LOG2N, int PH>
 __device__ __forceinline__ void stage(double2 (&x)[16], int t0, int lb, int n, const double2 *__restrict__ TW) {
   const int t = fresh(t0);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     if (i & (1 << lb)) continue;
     const int il = i | (1 << lb);
-    const int pk = epos<PH>(t, i);
+    const int pk = epos<LOG2N, PH>(t, i);
     const double2 w = TW[n - 1 + (pk & (n - 1))];
     const double yr = w.x * x[il].x - w.y * x[il].y;
     const double yi = w.x * x[il].y + w.y * x[il].x;
@@ -65,19 +92,19 @@ __device__ __forceinline__ void stage(double2 (&x)[16], int t0, int lb, int n, c
 
 // move values from layout PH_FROM to PH_TO through LDS (re then im);
 // BR: the destination reads bit-reversed positions (start of a new transform)
-template <int PH_FROM, int PH_TO, bool BR>
+template <int LOG2N, int PH_FROM, int PH_TO, bool BR>
 __device__ __forceinline__ void exchange(double2 (&x)[16], int t0, double *lds) {
 #pragma unroll
   for (int part = 0; part < 2; ++part) {
     const int t = fresh(t0);
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 16; ++i) lds[pad(epos<PH_FROM>(t, i))] = part ? x[i].y : x[i].x;
+    for (int i = 0; i < 16; ++i) lds[pad(epos<LOG2N, PH_FROM>(t, i))] = part ? x[i].y : x[i].x;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      int p = epos<PH_TO>(t, i);
-      if (BR) p = bitrev14(p);
+      int p = epos<LOG2N, PH_TO>(t, i);
+      if (BR) p = bitrev<LOG2N>(p);
       const double v = lds[pad(p)];
       if (part)
         x[i].y = v;
@@ -89,33 +116,131 @@ __device__ __forceinline__ void exchange(double2 (&x)[16], int t0, double *lds) 
 
 // full JFFT::fft on values already loaded in bit-reversed order in layout 0;
 // leaves the natural-order result in layout 3
-__device__ __forceinline__ void fft16k(double2 (&x)[16], int t, double *lds, const double2 *__restrict__ TW) {
-  stage<0>(x, t, 0, 1, TW);
-  stage<0>(x, t, 1, 2, TW);
-  stage<0>(x, t, 2, 4, TW);
-  stage<0>(x, t, 3, 8, TW);
-  exchange<0, 1, false>(x, t, lds);
-  stage<1>(x, t, 0, 16, TW);
-  stage<1>(x, t, 1, 32, TW);
-  stage<1>(x, t, 2, 64, TW);
-  stage<1>(x, t, 3, 128, TW);
-  exchange<1, 2, false>(x, t, lds);
-  stage<2>(x, t, 0, 256, TW);
-  stage<2>(x, t, 1, 512, TW);
-  stage<2>(x, t, 2, 1024, TW);
-  stage<2>(x, t, 3, 2048, TW);
-  exchange<2, 3, false>(x, t, lds);
-  stage<3>(x, t, 0, 4096, TW);
-  stage<3>(x, t, 1, 8192, TW);
+template <int L>
+__device__ __forceinline__ void fft_dit(double2 (&x)[16], int t, double *lds, const double2 *__restrict__ TW) {
+  static_assert(L == 13 || L == 14, "register phases cover 13 or 14 stages");
+  stage<L, 0>(x, t, 0, 1, TW);
+  stage<L, 0>(x, t, 1, 2, TW);
+  stage<L, 0>(x, t, 2, 4, TW);
+  stage<L, 0>(x, t, 3, 8, TW);
+  exchange<L, 0, 1, false>(x, t, lds);
+  stage<L, 1>(x, t, 0, 16, TW);
+  stage<L, 1>(x, t, 1, 32, TW);
+  stage<L, 1>(x, t, 2, 64, TW);
+  stage<L, 1>(x, t, 3, 128, TW);
+  exchange<L, 1, 2, false>(x, t, lds);
+  stage<L, 2>(x, t, 0, 256, TW);
+  stage<L, 2>(x, t, 1, 512, TW);
+  stage<L, 2>(x, t, 2, 1024, TW);
+  stage<L, 2>(x, t, 3, 2048, TW);
+  exchange<L, 2, 3, false>(x, t, lds);
+  stage<L, 3>(x, t, 0, 4096, TW);
+  if (L == 14) stage<L, 3>(x, t, 1, 8192, TW);
 }
 
-__device__ __forceinline__ void set_freq1(double &freq, double &step, double f) {  // SetFreq (DSP.cpp:163-168)
+__device__ __forceinline__ void set_freq1(double &freq, double &step, double f, double fs) {  // SetFreq (DSP.cpp:163-168)
   freq = f;
   if (freq < 0) freq = 0;
-  step = (freq) * ((double)WTSIZE) / 48000.0;
+  step = (freq) * ((double)WTSIZE) / fs;
 }
 
-__global__ __launch_bounds__(FT) void coarse_kernel(DevState S, DevTables T, int nch) {
+struct HopCtl {
+  double m2f, m2s, mcf, mcs;
+  int countdown2, countdown, ecd, yres_next;
+  long long zb;
+};
+
+// OqpskDemodulator::FreqOffsetEstimateSlot (decode/oqpskdemodulator.cpp:562-620),
+// SignalHunter (decode/hunter.cpp:21-42; maxTries 15, params 0/25000/10500,
+// decode/decode.cpp:161,169) and CenterFreqChangedSlot (:256-280).  dcd is
+// never set (DCDstatSlot unconnected, decode/decode.cpp:168-241).
+__device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<int, MODE_OQPSK>, double est,
+                                            double mse, unsigned &iter, int &scans, long long nk) {
+  const double thr = 0.65, lockingbw = 10500.0, Fs = 48000.0;
+  if (mse < thr) {
+    if (h.countdown2 > 0)
+      h.countdown2--;
+    else
+      set_freq1(h.m2f, h.m2s, h.mcf + est, Fs);
+  } else
+    h.countdown2 = 5;
+  if ((mse > thr) && (fabs(h.m2f - (h.mcf + est)) > 3.0)) set_freq1(h.m2f, h.m2s, h.mcf + est, Fs);
+  if ((mse < thr) && (fabs(h.m2f - h.mcf) > 3.0)) {
+    if (h.countdown > 0)
+      h.countdown--;
+    else {
+      set_freq1(h.mcf, h.mcs, h.m2f, Fs);
+      if (h.mcf < lockingbw / 2.0) set_freq1(h.mcf, h.mcs, lockingbw / 2.0, Fs);
+      if (h.mcf > (Fs / 2.0 - lockingbw / 2.0)) set_freq1(h.mcf, h.mcs, Fs / 2.0 - lockingbw / 2.0, Fs);
+      h.ecd = 4;  // bigchange (coarsefreqestimate.cpp:128-132)
+      h.yres_next = 1;
+      h.zb = nk + 1;  // bbcycbuff zeroed
+    }
+  } else
+    h.countdown = 4;
+  const bool gotasignal = !(mse > thr);
+  if (gotasignal) {
+    iter = 0;
+  } else {
+    iter++;
+    if (iter > 0 && iter % 15u == 0) {
+      double fc = 0u + (10500u >> 1) * (int)(iter / 15u);
+      if (fc > 25000u - (10500u >> 1)) {
+        fc = 0.0;
+        iter = 0;
+        scans++;
+      }
+      // CenterFreqChangedSlot, fb != 8400, afc on
+      if (fc < (0.5 * 10500.0)) fc = 0.5 * 10500.0;
+      if (fc > (Fs / 2.0 - 0.5 * 10500.0)) fc = Fs / 2.0 - 0.5 * 10500.0;
+      set_freq1(h.mcf, h.mcs, fc, Fs);
+      set_freq1(h.m2f, h.m2s, h.mcf, Fs);
+      if ((h.m2f - h.mcf) > (lockingbw / 2.0)) set_freq1(h.m2f, h.m2s, h.mcf + (lockingbw / 2.0), Fs);
+      if ((h.m2f - h.mcf) < (-lockingbw / 2.0)) set_freq1(h.m2f, h.m2s, h.mcf - (lockingbw / 2.0), Fs);
+      h.zb = nk + 1;
+    }
+  }
+  return gotasignal;
+}
+
+// MskDemodulator::FreqOffsetEstimateSlot (decode/mskdemodulator.cpp:430-469;
+// its AFC branch needs dcd, never set), SignalHunter with params 0/6000/900
+// (decode/decode.cpp:193) and MskDemodulator::CenterFreqChangedSlot (:220-240).
+template <int M>
+__device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<int, M>, double est, double mse,
+                                            unsigned &iter, int &scans, long long nk) {
+  const double thr = 0.5, lockingbw = 900.0, fb = 600.0, Fs = CoarseK<M>::FS;
+  if ((mse > thr) && (fabs(h.m2f - (h.mcf + est)) > 0.0)) set_freq1(h.m2f, h.m2s, h.mcf + est, Fs);
+  h.countdown = 4;
+  const bool gotasignal = !(mse > thr);
+  if (gotasignal) {
+    iter = 0;
+  } else {
+    iter++;
+    if (iter > 0 && iter % 15u == 0) {
+      double fc = 0u + (900u >> 1) * (int)(iter / 15u);
+      if (fc > 6000u - (900u >> 1)) {
+        fc = 0.0;
+        iter = 0;
+        scans++;
+      }
+      if (fc < (0.75 * fb)) fc = 0.75 * fb;
+      if (fc > (Fs / 2.0 - 0.75 * fb)) fc = Fs / 2.0 - 0.75 * fb;
+      set_freq1(h.mcf, h.mcs, fc, Fs);
+      set_freq1(h.m2f, h.m2s, h.mcf, Fs);
+      if ((h.m2f - h.mcf) > (lockingbw / 2.0)) set_freq1(h.m2f, h.m2s, h.mcf + (lockingbw / 2.0), Fs);
+      if ((h.m2f - h.mcf) < (-lockingbw / 2.0)) set_freq1(h.m2f, h.m2s, h.mcf - (lockingbw / 2.0), Fs);
+      h.zb = nk + 1;
+    }
+  }
+  return gotasignal;
+}
+
+template <int M>
+__global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4)) void coarse_kernel(DevState S, DevTables T, int nch) {
+  using K = CoarseK<M>;
+  constexpr int L = K::LOG2N, N = 1 << L, FT = N / 16, PADDED = N + N / 16;
+  constexpr int YLEN = K::YHI - K::YLO + 1;
   __shared__ double lds[PADDED];
   __shared__ double red_v[FT / 64];
   __shared__ int red_i[FT / 64];
@@ -123,11 +248,11 @@ __global__ __launch_bounds__(FT) void coarse_kernel(DevState S, DevTables T, int
   const int t = threadIdx.x;
   if (c >= nch) return;
   const int C = S.C;
-  // hop due? sample n_k = 4096 k - 1, demod stopped there and the ring holds it
+  // hop due? sample n_k = HOP k - 1, demod stopped there and the ring holds it
   const long long nsamp = S.ls[LS_NSAMP * C + c];
   const long long filled = S.ls[LS_FILLED * C + c];
   const int hops_done = S.is[IS_HOPS_DONE * C + c];
-  const long long nk = (long long)HOP * (hops_done + 1) - 1;
+  const long long nk = (long long)K::HOPN * (hops_done + 1) - 1;
   const long long avail = S.ls[LS_AVAIL * C + c];
   if (nsamp != nk || avail <= nk) return;
   const long long zero_before = S.ls[LS_ZERO_BEFORE * C + c];
@@ -139,70 +264,70 @@ __global__ __launch_bounds__(FT) void coarse_kernel(DevState S, DevTables T, int
     if (tint >= WTSIZE) tint = 0;
     if (tint < 0) tint = WTSIZE - 1;
     const int16_t xs = S.pcm[(nk & (S.pcm_cap - 1)) * C + c];
-    S.cring[(size_t)c * NFFT + (nk & (NFFT - 1))] = (uint32_t)tint | ((uint32_t)(uint16_t)xs << 16);
+    S.cring[(size_t)c * N + (nk & (N - 1))] = (uint32_t)tint | ((uint32_t)(uint16_t)xs << 16);
     S.ls[LS_FILLED * C + c] = nk + 1;
   }
   __syncthreads();
 
-  // ring words -> LDS (as uint32 in the first 64 KB)
+  // ring words -> LDS (as uint32 in the first N*4 bytes)
   uint32_t *ring_lds = reinterpret_cast<uint32_t *>(lds);
-  const uint32_t *ring = S.cring + (size_t)c * NFFT;
-  for (int j = t; j < NFFT; j += FT) ring_lds[j] = ring[j];
+  const uint32_t *ring = S.cring + (size_t)c * N;
+  for (int j = t; j < N; j += FT) ring_lds[j] = ring[j];
   __syncthreads();
   double2 x[16];
-  const long long s0 = nk - (NFFT - 1);  // sample of snapshot element 0 (oqpskdemodulator.cpp:359-365)
+  const long long s0 = nk - (N - 1);  // sample of snapshot element 0 (oqpskdemodulator.cpp:359-365)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int j = bitrev14(epos<0>(t, i));
+    const int j = bitrev<L>(epos<L, 0>(t, i));
     const long long s = s0 + j;
     if (s < 0 || s < zero_before) {
       x[i] = make_double2(0.0, 0.0);
     } else {
-      const uint32_t w = ring_lds[s & (NFFT - 1)];
+      const uint32_t w = ring_lds[s & (N - 1)];
       const double dval = ((double)(int16_t)(w >> 16)) / 32768.0;
       const double2 cs = T.cis[w & 0xFFFF];
       x[i] = make_double2(cs.x * dval, cs.y * dval);
     }
   }
   // forward FFT
-  fft16k(x, t, lds, T.tw);
+  fft_dit<L>(x, t, lds, T.tw);
   // boxcar: zero bins startbin..stopbin (coarsefreqestimate.cpp:143-146)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int p = epos<3>(t, i);
-    if (p >= 3584 && p <= 12800) x[i] = make_double2(0.0, 0.0);
+    const int p = epos<L, 3>(t, i);
+    if (p >= K::START && p <= K::STOP) x[i] = make_double2(0.0, 0.0);
   }
   // inverse FFT (JFFT scales by 1/N, FFTWrapper multiplies by N)
-  exchange<3, 0, true>(x, t, lds);
-  fft16k(x, t, lds, T.twi);
+  exchange<L, 3, 0, true>(x, t, lds);
+  fft_dit<L>(x, t, lds, T.twi);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    x[i].x *= (1.0 / ((double)NFFT));
-    x[i].y *= (1.0 / ((double)NFFT));
-    x[i].x *= (double)NFFT;
-    x[i].y *= (double)NFFT;
+    x[i].x *= (1.0 / ((double)N));
+    x[i].y *= (1.0 / ((double)N));
+    x[i].x *= (double)N;
+    x[i].y *= (double)N;
     // square
     const double r = x[i].x * x[i].x - x[i].y * x[i].y;
     const double im = x[i].x * x[i].y + x[i].y * x[i].x;
     x[i] = make_double2(r, im);
   }
-  exchange<3, 0, true>(x, t, lds);
-  fft16k(x, t, lds, T.tw);
+  exchange<L, 3, 0, true>(x, t, lds);
+  fft_dit<L>(x, t, lds, T.tw);
   // fftshift + smoothing y = 0.9 y + 10 log10(max(|X|,1)) over the bins the fold reads:
   // |X| per bin to LDS first (keeps the log10 out of the register-heavy FFT scope)
   __syncthreads();
-  double *ylds = lds;  // [Y_LEN]
+  double *ylds = lds;  // [YLEN]
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int yi = epos<3>(t, i) ^ (NFFT / 2);
-    if (yi >= Y_LO && yi <= Y_HI) ylds[yi - Y_LO] = aero_hypot(x[i].x, x[i].y);
+    const int yi = epos<L, 3>(t, i) ^ (N / 2);
+    if (yi >= K::YLO && yi <= K::YHI) ylds[yi - K::YLO] = aero_hypot(x[i].x, x[i].y);
   }
   __syncthreads();
   {
-    double *yg = S.y + (size_t)c * Y_LEN;
+    double *yg = S.y + (size_t)c * YLEN;
     const int yreset = S.is[IS_YRESET * C + c];
 #pragma unroll 1
-    for (int k = t; k < Y_LEN; k += FT) {
+    for (int k = t; k < YLEN; k += FT) {
       const double yold = yreset ? 20.0 : yg[k];
       const double ynew = yold * 0.9 + 0.1 * 10 * aero_log10(fmax(ylds[k], 1.0));
       yg[k] = ynew;
@@ -213,11 +338,11 @@ __global__ __launch_bounds__(FT) void coarse_kernel(DevState S, DevTables T, int
   // fold search (coarsefreqestimate.cpp:166-185): first strict maximum above 0
   double bv = 0.0;
   int bi = 0x7fffffff;
-  for (int r = 0; r < 7; ++r) {
-    const int i = 4608 + t + FT * r;
-    if (i >= 11776) break;
+  for (int r = 0;; ++r) {
+    const int i = K::ILO + t + FT * r;
+    if (i >= K::IHI) break;
     double val = 0;
-    for (int j = -1; j <= 1; j++) val += (ylds[i - 1792 - j - Y_LO] + ylds[i + 1792 + j - Y_LO]);
+    for (int j = -1; j <= 1; j++) val += (ylds[i - K::EPB - j - K::YLO] + ylds[i + K::EPB + j - K::YLO]);
     if (val > bv) {
       bv = val;
       bi = i;
@@ -244,9 +369,9 @@ __global__ __launch_bounds__(FT) void coarse_kernel(DevState S, DevTables T, int
       bi = red_i[w];
     }
   }
-  const int zmaxloc = (bv > 0.0) ? bi : NFFT / 2;
-  const double nfft = (double)NFFT;
-  const double freq_offset_est = -((double)(zmaxloc - nfft / 2)) * (48000.0 / nfft) * 0.5;
+  const int zmaxloc = (bv > 0.0) ? bi : N / 2;
+  const double nfft = (double)N;
+  const double freq_offset_est = -((double)(zmaxloc - nfft / 2)) * (K::FS / nfft) * 0.5;
   double est;
   int ecd = S.is[IS_EMPTYCD * C + c];
   if (ecd <= 0) {
@@ -255,88 +380,55 @@ __global__ __launch_bounds__(FT) void coarse_kernel(DevState S, DevTables T, int
     ecd--;
     est = 0;
   }
-  int yres_next = 0;
 
-  // ---- FreqOffsetEstimateSlot (dcd never set: DCDstatSlot unconnected, decode.cpp:168-241)
   double *ds = S.ds;
   int *is = S.is;
-  const double thr = 0.65, lockingbw = 10500.0, Fs = 48000.0;
   const double mse = ds[DS_MSE * C + c];
-  double m2f = ds[DS_M2_FREQ * C + c], m2s = ds[DS_M2_STEP * C + c];
-  double mcf = ds[DS_MC_FREQ * C + c], mcs = ds[DS_MC_STEP * C + c];
-  int countdown2 = is[IS_COUNTDOWN2 * C + c], countdown = is[IS_COUNTDOWN * C + c];
-  long long zb = zero_before;
-  if (mse < thr) {
-    if (countdown2 > 0)
-      countdown2--;
-    else
-      set_freq1(m2f, m2s, mcf + est);
-  } else
-    countdown2 = 5;
-  if ((mse > thr) && (fabs(m2f - (mcf + est)) > 3.0)) set_freq1(m2f, m2s, mcf + est);
-  if ((mse < thr) && (fabs(m2f - mcf) > 3.0)) {
-    if (countdown > 0)
-      countdown--;
-    else {
-      set_freq1(mcf, mcs, m2f);
-      if (mcf < lockingbw / 2.0) set_freq1(mcf, mcs, lockingbw / 2.0);
-      if (mcf > (Fs / 2.0 - lockingbw / 2.0)) set_freq1(mcf, mcs, Fs / 2.0 - lockingbw / 2.0);
-      ecd = 4;  // bigchange (coarsefreqestimate.cpp:128-132)
-      yres_next = 1;
-      zb = nk + 1;  // bbcycbuff zeroed
-    }
-  } else
-    countdown = 4;
-  // ---- SignalStatus -> SignalHunter (hunter.cpp:21-42, maxTries 15, params 0/25000/10500)
-  const bool gotasignal = !(mse > thr);
+  HopCtl h;
+  h.m2f = ds[DS_M2_FREQ * C + c];
+  h.m2s = ds[DS_M2_STEP * C + c];
+  h.mcf = ds[DS_MC_FREQ * C + c];
+  h.mcs = ds[DS_MC_STEP * C + c];
+  h.countdown2 = is[IS_COUNTDOWN2 * C + c];
+  h.countdown = is[IS_COUNTDOWN * C + c];
+  h.ecd = ecd;
+  h.yres_next = 0;
+  h.zb = zero_before;
   unsigned iter = (unsigned)is[IS_HUNT_ITER * C + c];
-  if (gotasignal) {
-    iter = 0;
-  } else {
-    iter++;
-    if (iter > 0 && iter % 15u == 0) {
-      double fc = 0u + (10500u >> 1) * (int)(iter / 15u);
-      if (fc > 25000u - (10500u >> 1)) {
-        fc = 0.0;
-        iter = 0;
-        is[IS_HUNT_SCANS * C + c]++;
-      }
-      // CenterFreqChangedSlot (oqpskdemodulator.cpp:256-280), fb != 8400, afc on
-      if (fc < (0.5 * 10500.0)) fc = 0.5 * 10500.0;
-      if (fc > (Fs / 2.0 - 0.5 * 10500.0)) fc = Fs / 2.0 - 0.5 * 10500.0;
-      set_freq1(mcf, mcs, fc);
-      set_freq1(m2f, m2s, mcf);
-      if ((m2f - mcf) > (lockingbw / 2.0)) set_freq1(m2f, m2s, mcf + (lockingbw / 2.0));
-      if ((m2f - mcf) < (-lockingbw / 2.0)) set_freq1(m2f, m2s, mcf - (lockingbw / 2.0));
-      zb = nk + 1;
-    }
-  }
+  int scans = is[IS_HUNT_SCANS * C + c];
+  const bool gotasignal = hop_control(h, std::integral_constant<int, M>(), est, mse, iter, scans, nk);
   is[IS_HUNT_ITER * C + c] = (int)iter;
-  ds[DS_M2_FREQ * C + c] = m2f;
-  ds[DS_M2_STEP * C + c] = m2s;
-  ds[DS_MC_FREQ * C + c] = mcf;
-  ds[DS_MC_STEP * C + c] = mcs;
-  is[IS_COUNTDOWN2 * C + c] = countdown2;
-  is[IS_COUNTDOWN * C + c] = countdown;
-  is[IS_EMPTYCD * C + c] = ecd;
-  is[IS_YRESET * C + c] = yres_next;
+  is[IS_HUNT_SCANS * C + c] = scans;
+  ds[DS_M2_FREQ * C + c] = h.m2f;
+  ds[DS_M2_STEP * C + c] = h.m2s;
+  ds[DS_MC_FREQ * C + c] = h.mcf;
+  ds[DS_MC_STEP * C + c] = h.mcs;
+  is[IS_COUNTDOWN2 * C + c] = h.countdown2;
+  is[IS_COUNTDOWN * C + c] = h.countdown;
+  is[IS_EMPTYCD * C + c] = h.ecd;
+  is[IS_YRESET * C + c] = h.yres_next;
   is[IS_HOPS_DONE * C + c] = hops_done + 1;
-  S.ls[LS_ZERO_BEFORE * C + c] = zb;
+  S.ls[LS_ZERO_BEFORE * C + c] = h.zb;
   const int hn = S.hop_n[c];
   if (hn < S.hop_cap) {
-    double *h = S.hops + ((size_t)c * S.hop_cap + hn) * 6;
-    h[0] = (double)nk;
-    h[1] = est;
-    h[2] = m2f;
-    h[3] = mcf;
-    h[4] = mse;
-    h[5] = gotasignal ? 1.0 : 0.0;
+    double *hr = S.hops + ((size_t)c * S.hop_cap + hn) * 6;
+    hr[0] = (double)nk;
+    hr[1] = est;
+    hr[2] = h.m2f;
+    hr[3] = h.mcf;
+    hr[4] = mse;
+    hr[5] = gotasignal ? 1.0 : 0.0;
   }
   S.hop_n[c] = hn + 1;
 }
 
-void launch_coarse(hipStream_t st, const DevState &S, const DevTables &T, int nch) {
-  hipLaunchKernelGGL(coarse_kernel, dim3(nch), dim3(FT), 0, st, S, T, nch);
+void launch_coarse(hipStream_t st, int mode, const DevState &S, const DevTables &T, int nch) {
+  if (mode == MODE_OQPSK)
+    hipLaunchKernelGGL(coarse_kernel<MODE_OQPSK>, dim3(nch), dim3(1024), 0, st, S, T, nch);
+  else if (mode == MODE_MSK600)
+    hipLaunchKernelGGL(coarse_kernel<MODE_MSK600>, dim3(nch), dim3(512), 0, st, S, T, nch);
+  else
+    hipLaunchKernelGGL(coarse_kernel<MODE_MSK1200>, dim3(nch), dim3(512), 0, st, S, T, nch);
 }
 
 }  // namespace aero

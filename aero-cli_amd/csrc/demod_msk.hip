@@ -1,0 +1,390 @@
+/*
+ * demod_msk.hip — batched continuous MSK demodulator (600 / 1200 bps) for
+ * gfx950: MskDemodulator::writeData (decode/mskdemodulator.cpp:252-428) as
+ * aero-decode configures it (decode/decode.cpp:142-150: Fs 12000 / 24000,
+ * fb stays 600, freq_center 0, AFC on, dcd never set).
+ *
+ * One VFO channel per lane, thousands side by side, the same structure as
+ * demod_oqpsk.hip:
+ *   - the 2*SPS-tap half-sine matched filter runs in transposed form, real
+ *     partial sums in VGPRs, imaginary ones in LDS [tap][lane];
+ *   - the per-sample delay lines (delayedsmpl, delayt8) and the AGC ring are
+ *     time-major HBM rings indexed by sample number, so channels that move in
+ *     step read and write one coalesced row;
+ *   - the symbol event (carrier loop, rotation, MSE, differential soft bits)
+ *     runs once per st_osc cycle, 1 sample in 2*SPS; lanes run their samples
+ *     up to their next event (inner loop) and the event step then runs for
+ *     all lanes together, so a wave does not pay for one lane's event every
+ *     sample.  Per lane, operations and their order are the reference's.
+ *
+ * Bit-exactness rules as demod_oqpsk.hip (-ffp-contract=off, reference
+ * operation order, std::complex products expanded as GCC does, libm from
+ * aero_math.h).  std::sqrt is IEEE (correctly rounded) on both sides.
+ */
+#include <hip/hip_runtime.h>
+
+#include "aero_math.h"
+#include "engine_common.h"
+
+namespace aero {
+
+__constant__ double c_msk_sr_b[3];  // st resonator, 12 kHz design (mskdemodulator.cpp:191-203)
+__constant__ double c_msk_sr_a[3];
+__constant__ double c_msk_d8w[2];   // delayt8 weights {weighting, 1 - weighting} (pointer-independent, host-checked)
+
+namespace {
+
+__device__ __forceinline__ int cis_index(double WTptr) {  // WaveTable::WTCISValue (DSP.cpp:81-88)
+  int tint = (int)WTptr;
+  if (tint >= WTSIZE) tint = 0;
+  if (tint < 0) tint = WTSIZE - 1;
+  return tint;
+}
+
+__device__ __forceinline__ void nco_next(double &ptr, double &step) {  // WTnextFrame (DSP.cpp:71-79)
+  if (step < 0) step = 0;
+  ptr += step;
+  while (((int)ptr) >= WTSIZE) ptr -= WTSIZE;
+}
+
+__device__ __forceinline__ int qround(double d) {  // qRound (Qt 5.9 qglobal.h:525)
+  return d >= 0.0 ? int(d + 0.5) : int(d - double(int(d - 1)) + 0.5) + int(d - 1);
+}
+
+__device__ __forceinline__ double diff_soft(double &last, double soft) {  // DiffDecode::UpdateSoft (DSP.cpp:523-548)
+  double retval;
+  if (soft < 0 && last < 0) {
+    retval = last;
+  } else if (soft > 0 && last > 0) {
+    retval = -last;
+  } else {
+    retval = fabs(last);
+  }
+  last = soft;
+  return retval;
+}
+
+}  // namespace
+
+template <int M>
+__global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevTables T, int nch, int flush) {
+  using K = MskK<M>;
+  constexpr int WG = K::WG;
+  constexpr int SPS = K::SPS;
+  constexpr int NT = 2 * SPS;            // matched filter taps (mskdemodulator.cpp:126-133)
+  constexpr int AGC = K::FS;             // AGC(1, Fs) (mskdemodulator.cpp:135)
+  constexpr int DSM = SPS + 1;           // delayedsmpl.setLength(SPS)
+  constexpr int D8 = SPS / 2 + 1;        // delayt8.setdelay(SPS / 2.0): ceil + 1 slots
+  constexpr int DTL = SPS / 2 + 1;       // dt.setLength(SPS / 2)
+  constexpr int MARG = SPS;              // marg = MovingAverage(SPS)
+  constexpr double FS = (double)K::FS;
+  __shared__ double s_qim[NT][WG];
+  __shared__ double s_taps[NT];
+  {
+    const int l = threadIdx.x;
+    if (l < NT) s_taps[l] = T.taps[l];
+    __syncthreads();
+  }
+  const int c = blockIdx.x * WG + threadIdx.x;
+  const int lane = threadIdx.x;
+  if (c >= nch) return;
+  const int C = S.C;
+  const int HOPN = MSK_HOP, NF = MSK_NFFT;
+
+  const long long n0 = S.ls[LS_NSAMP * C + c];
+  const long long avail = S.ls[LS_AVAIL * C + c];
+  const long long filled0 = S.ls[LS_FILLED * C + c];
+  const int hops_done = S.is[IS_HOPS_DONE * C + c];
+  const long long boundary = (long long)HOPN * (hops_done + 1) - 1;
+  long long end = avail < boundary ? avail : boundary;
+  if (!flush && avail <= boundary) end = n0;
+  const int capm = (int)S.pcm_cap - 1;
+  const int ia = (int)(avail - n0);
+  const int ie = (int)(end - n0);
+  int ifl = (int)(filled0 - n0);
+
+  double mc_ptr = S.ds[DS_MC_PTR * C + c], mc_step = S.ds[DS_MC_STEP * C + c];
+  if (ifl == 0 && ia > 0) {  // coarse-ring entry of sample n0
+    const int16_t x = S.pcm[(size_t)(n0 & capm) * C + c];
+    S.cring[(size_t)c * NF + (n0 & (NF - 1))] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
+    ifl = 1;
+  }
+  if (ie <= 0) {
+    S.ls[LS_FILLED * C + c] = n0 + ifl;
+    return;
+  }
+
+  double m2_ptr = S.ds[DS_M2_PTR * C + c], m2_step = S.ds[DS_M2_STEP * C + c];
+  double m2_freq = S.ds[DS_M2_FREQ * C + c];
+  double so_ptr = S.ds[DS_SO_PTR * C + c], so_last = S.ds[DS_SO_LAST * C + c];
+  const double so_step = S.ds[DS_SO_STEP * C + c];
+  double agc_sum = S.ds[DS_AGC_SUM * C + c];
+  double srx1 = S.ds[DS_SR_X1 * C + c], srx2 = S.ds[DS_SR_X2 * C + c];
+  double sry1 = S.ds[DS_SR_Y1 * C + c], sry2 = S.ds[DS_SR_Y2 * C + c];
+  double marg_sum = S.ds[DS_MARG_SUM * C + c], ms_sum = S.ds[DS_MS_SUM * C + c];
+  double mse = S.ds[DS_MSE * C + c], diff_last = S.ds[DS_DIFF_LAST * C + c];
+  long long ev = S.ls[LS_EVENTS * C + c];
+  long long softp = S.ls[LS_SOFT_P * C + c];
+  long long ptn = S.ls[LS_PT_N * C + c];
+
+  double q[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) q[j] = S.fir[(size_t)j * C + c];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) s_qim[j][lane] = S.fir[(size_t)(NT + j) * C + c];
+
+  const double PT = 0.0125 * WTSIZE;  // IfHavePassedPoint(ee), ee = 0.0125 (mskdemodulator.cpp:203)
+  const double d8w = c_msk_d8w[0], d8omw = c_msk_d8w[1];
+
+  int i = 0;
+  // event operands carried out of the sample loop
+  double e_s2r = 0, e_s2i = 0, e_pdr = 0, e_pdi = 0;
+  while (i < ie) {
+    bool pend = false;
+    do {
+      const long long n = n0 + i;
+      const int16_t xs = S.pcm[(size_t)(n & capm) * C + c];
+      const double dval = ((double)xs) / 32768.0;
+      const double2 cm = T.cis[cis_index(m2_ptr)];
+      const double cv = cm.x * dval, cvi = cm.y * dval;  // mixer2.WTCISValue() * dval
+      // matched filter: FIRUpdateAndProcess reads the 2*SPS samples before the newest
+      double s2r = q[NT - 1], s2i = s_qim[NT - 1][lane];
+#pragma unroll
+      for (int j = NT - 1; j >= 1; --j) q[j] = q[j - 1] + s_taps[j] * cv;
+      q[0] = 0.0 + s_taps[0] * cv;
+#pragma unroll
+      for (int j = NT - 1; j >= 1; --j) {
+        s_qim[j][lane] = s_qim[j - 1][lane] + s_taps[j] * cvi;
+        if ((j & 7) == 0) asm volatile("" : : : "memory");
+      }
+      s_qim[0][lane] = 0.0 + s_taps[0] * cvi;
+      const double dab = sqrt(s2r * s2r + s2i * s2i);
+      {  // AGC::Update (DSP.cpp:371-380)
+        const int ap = (int)(n % AGC);
+        double *slot = S.agc + (size_t)ap * C + c;
+        agc_sum = agc_sum - *slot;
+        agc_sum = agc_sum + fabs(dab);
+        *slot = fabs(dab);
+        double g = 1.414213562 / fmax(agc_sum / ((double)AGC), 0.000001);
+        g = fmax(g, 0.000001);
+        s2r *= g;
+        s2i *= g;
+      }
+      const double ab = sqrt(s2r * s2r + s2i * s2i);
+      if (ab > 2.84) {
+        const double k = 2.84 / ab;
+        s2r = k * s2r;
+        s2i = k * s2i;
+      }
+      // pt_d = delayedsmpl.update_dont_touch(sig2) (DSP.h:468-473)
+      double pdr, pdi;
+      {
+        S.dsm[(size_t)(n % DSM) * C + c] = make_double2(s2r, s2i);
+        const double2 o = S.dsm[(size_t)((n + 1) % DSM) * C + c];
+        pdr = o.x;
+        pdi = o.y;
+      }
+      // st_eta = resonator(|pt_msk|), pt_msk = (sig2.re, pt_d.im)
+      double st_eta;
+      {
+        const double sig = aero_hypot(s2r, pdi);
+        double y = 0;
+        y += srx2 * c_msk_sr_b[2];
+        y += srx1 * c_msk_sr_b[1];
+        y += sig * c_msk_sr_b[0];
+        y -= sry2 * c_msk_sr_a[2];
+        y -= sry1 * c_msk_sr_a[1];
+        srx2 = srx1;
+        srx1 = sig;
+        sry2 = sry1;
+        sry1 = y;
+        st_eta = y;
+      }
+      // delayt8.update(st_eta) (DSP.h:365-384): ages SPS/2 and SPS/2 - 1
+      double d8v;
+      {
+        S.d8[(size_t)(n % D8) * C + c] = st_eta;
+        const double older = S.d8[(size_t)((n + 1) % D8) * C + c];
+        const double newer = S.d8[(size_t)((n + 2) % D8) * C + c];
+        d8v = (d8w * newer + d8omw * older);
+      }
+      const double m1r = st_eta, m1i = -d8v;
+      const double2 so = T.cis[cis_index(so_ptr)];
+      const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
+      const double ang = aero_atan2(oim, ore);
+      const double weighting = fabs(aero_tanh(ang));
+      {  // st_osc.AdvanceFractionOfWave (DSP.h:59-65), dcd false
+        so_ptr += (-(1.0 - weighting) * ang * (0.05 / 360.0)) * WTSIZE;
+        while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
+        while (so_ptr < 0) so_ptr += WTSIZE;
+      }
+      {  // IfHavePassedPoint (DSP.cpp:222-238)
+        double tl = so_last - PT, tw = so_ptr - PT;
+        if (tl < 0.0) tl += WTSIZE;
+        if (tw < 0.0) tw += WTSIZE;
+        if ((tl > 3.0 * WTSIZE / 4.0) && (tw < 1.0 * WTSIZE / 4.0)) {
+          pend = true;
+          e_s2r = s2r;
+          e_s2i = s2i;
+          e_pdr = pdr;
+          e_pdi = pdi;
+        }
+      }
+      // the coarse-ring entry of the next sample (mskdemodulator.cpp:284-287)
+      nco_next(mc_ptr, mc_step);
+      so_last = so_ptr;
+      {
+        double st = so_step;
+        nco_next(so_ptr, st);
+      }
+      if (i + 1 < ia) {
+        const long long n1 = n + 1;
+        const int16_t x1 = S.pcm[(size_t)(n1 & capm) * C + c];
+        S.cring[(size_t)c * NF + (n1 & (NF - 1))] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)x1 << 16);
+        ifl = i + 2;
+      }
+      if (!pend) {
+        nco_next(m2_ptr, m2_step);
+        ++i;
+      }
+    } while (!pend && i < ie);
+    if (pend) {
+      // carrier tracking (mskdemodulator.cpp:333-357)
+      const double ct_xt = aero_tanh(e_s2i) * e_s2r;
+      const double ct_xt_d = aero_tanh(e_pdr) * e_pdi;
+      double ct_ec = ct_xt_d - ct_xt;
+      if (ct_ec > M_PI) ct_ec = M_PI;
+      if (ct_ec < -M_PI) ct_ec = -M_PI;
+      if (ct_ec > M_PI_2) ct_ec = M_PI_2;
+      if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
+      const double carrier_aggression = 12.0 * 1.0;  // correctionfactor 1.0 (fb < 1200)
+      {  // mixer2.IncresePhaseDeg (DSP.cpp:177-187)
+        double phase_deg = carrier_aggression * 1.0 * ct_ec;
+        phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
+        phase_deg = fmod(phase_deg, 360.0);
+        while (phase_deg < 0) phase_deg += 360.0;
+        m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+      }
+      {  // mixer2.IncreseFreqHz -> SetFreq(double) (DSP.cpp:163-175)
+        double f = carrier_aggression * 0.01 * ct_ec;
+        f += m2_freq;
+        m2_freq = f;
+        if (m2_freq < 0) m2_freq = 0;
+        m2_step = (m2_freq) * ((double)WTSIZE) / FS;
+      }
+      int cl = c;
+      asm volatile("" : "+v"(cl));
+      // marg->UpdateSigned(ct_ec / 2.0) (DSP.cpp:419-427)
+      double mval;
+      {
+        double *mb = S.marg + (size_t)cl * MARG;
+        const int p = (int)(ev % MARG);
+        const double nv = ct_ec / 2.0;
+        marg_sum = marg_sum - mb[p];
+        marg_sum = marg_sum + (nv);
+        mb[p] = nv;
+        mval = marg_sum / ((double)MARG);
+      }
+      // dt.update(pt_msk) (DSP.h:463-467)
+      double pr, pi;
+      {
+        double2 *db = S.dt + (size_t)cl * DTL;
+        db[ev % DTL] = make_double2(e_s2r, e_pdi);
+        const double2 o = db[(ev + 1) % DTL];
+        pr = o.x;
+        pi = o.y;
+      }
+      {  // pt_msk *= cpx(cos(marg->Val), sin(marg->Val))
+        double rs, rc;
+        aero_sincos(mval, rs, rc);
+        const double rr = pr * rc - pi * rs, ri = pr * rs + pi * rc;
+        pr = rr;
+        pi = ri;
+      }
+      if (S.pt_cap) {
+        if (ptn < S.pt_cap) S.pt[(size_t)cl * S.pt_cap + ptn] = make_double2(pr, pi);
+        ptn++;
+      }
+      {  // mse = msema->Update(tda^2 + tdb^2) (DSP.cpp:405-413)
+        const double tda = (fabs((pr) * 0.75) - 1.0);
+        const double tdb = (fabs((pi) * 0.75) - 1.0);
+        const double v = (tda * tda) + (tdb * tdb);
+        double *mb = S.ms + (size_t)cl * MSK_MSEMA;
+        const int p = (int)(ev % MSK_MSEMA);
+        ms_sum = ms_sum - mb[p];
+        ms_sum = ms_sum + fabs(v);
+        mb[p] = fabs(v);
+        mse = ms_sum / ((double)MSK_MSEMA);
+      }
+      {  // differential soft bits, imag first, real negated (mskdemodulator.cpp:381-401)
+        const double imagin = diff_soft(diff_last, pi);
+        int ibit = qround((imagin) * 127.0 + 128.0);
+        if (ibit > 255) ibit = 255;
+        if (ibit < 0) ibit = 0;
+        double real = diff_soft(diff_last, pr);
+        real = -real;
+        int rbit = qround((real) * 127.0 + 128.0);
+        if (rbit > 255) rbit = 255;
+        if (rbit < 0) rbit = 0;
+        uint8_t *soft = S.soft + (size_t)cl * SOFT_RING;
+        soft[softp & (SOFT_RING - 1)] = (uint8_t)ibit;
+        soft[(softp + 1) & (SOFT_RING - 1)] = (uint8_t)rbit;
+        softp += 2;
+      }
+      ev++;
+      nco_next(m2_ptr, m2_step);
+      ++i;
+    }
+  }
+
+  int cl = c;
+  asm volatile("" : "+v"(cl));
+  {
+    double *fir = S.fir + cl;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) fir[(size_t)j * C] = q[j];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) fir[(size_t)(NT + j) * C] = s_qim[j][lane];
+  }
+  double *ds = S.ds + cl;
+  long long *ls = S.ls + cl;
+  ls[LS_NSAMP * C] = n0 + i;
+  ls[LS_FILLED * C] = n0 + ifl;
+  ls[LS_SOFT_P * C] = softp;
+  ls[LS_EVENTS * C] = ev;
+  if (S.pt_cap) ls[LS_PT_N * C] = ptn;
+  ds[DS_M2_PTR * C] = m2_ptr;
+  ds[DS_M2_STEP * C] = m2_step;
+  ds[DS_M2_FREQ * C] = m2_freq;
+  ds[DS_MC_PTR * C] = mc_ptr;
+  ds[DS_MC_STEP * C] = mc_step;
+  ds[DS_SO_PTR * C] = so_ptr;
+  ds[DS_SO_LAST * C] = so_last;
+  ds[DS_AGC_SUM * C] = agc_sum;
+  ds[DS_SR_X1 * C] = srx1;
+  ds[DS_SR_X2 * C] = srx2;
+  ds[DS_SR_Y1 * C] = sry1;
+  ds[DS_SR_Y2 * C] = sry2;
+  ds[DS_MARG_SUM * C] = marg_sum;
+  ds[DS_MS_SUM * C] = ms_sum;
+  ds[DS_MSE * C] = mse;
+  ds[DS_DIFF_LAST * C] = diff_last;
+}
+
+void launch_demod_msk(hipStream_t st, int mode, const DevState &S, const DevTables &T, int nch, int flush) {
+  if (mode == MODE_MSK600) {
+    constexpr int WG = MskK<MODE_MSK600>::WG;
+    hipLaunchKernelGGL(demod_msk_kernel<MODE_MSK600>, dim3((nch + WG - 1) / WG), dim3(WG), 0, st, S, T, nch, flush);
+  } else {
+    constexpr int WG = MskK<MODE_MSK1200>::WG;
+    hipLaunchKernelGGL(demod_msk_kernel<MODE_MSK1200>, dim3((nch + WG - 1) / WG), dim3(WG), 0, st, S, T, nch, flush);
+  }
+}
+
+void upload_msk_constants(const double *sr_b, const double *sr_a, const double *d8w) {
+  hipMemcpyToSymbol(HIP_SYMBOL(c_msk_sr_b), sr_b, sizeof(double) * 3);
+  hipMemcpyToSymbol(HIP_SYMBOL(c_msk_sr_a), sr_a, sizeof(double) * 3);
+  hipMemcpyToSymbol(HIP_SYMBOL(c_msk_d8w), d8w, sizeof(double) * 2);
+}
+
+}  // namespace aero

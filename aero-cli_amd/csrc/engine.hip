@@ -2,7 +2,8 @@
  * engine.hip — host side of the Aero engine: the C ABI of
  * include/aero_engine.h, device allocation, host-computed tables (the same
  * glibc calls the reference makes: decode/DSP.cpp:10-33, decode/DSP.h:325-351,
- * decode/jfft.cpp:13-67) and the per-run kernel schedule
+ * decode/jfft.cpp:13-67, decode/mskdemodulator.cpp:126-133) and the per-run
+ * kernel schedule of each channel kind (10500 OQPSK, 600 / 1200 MSK)
  *
  *   [demod segment] -> [coarse hop + decision] -> [AeroL framing] -> [Viterbi+post]
  *
@@ -37,9 +38,11 @@ namespace aero {
 void launch_demod(hipStream_t, const DevState &, const DevTables &, int, int, bool);
 void upload_demod_constants(const double *, const DelayDesc *, const double *, const double *, const double *,
                             const double *);
-void launch_coarse(hipStream_t, const DevState &, const DevTables &, int);
-void launch_frame(hipStream_t, const DevState &, int);
-void launch_viterbi(hipStream_t, const DevState &, const DevTables &, int, int);
+void launch_demod_msk(hipStream_t, int, const DevState &, const DevTables &, int, int);
+void upload_msk_constants(const double *, const double *, const double *);
+void launch_coarse(hipStream_t, int, const DevState &, const DevTables &, int);
+void launch_frame(hipStream_t, int, const DevState &, int);
+void launch_viterbi(hipStream_t, int, const DevState &, const DevTables &, int, int);
 }  // namespace aero
 
 using namespace aero;
@@ -181,18 +184,25 @@ class HostPool {
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
-
-struct aero_engine {
+// One group per channel kind (Mode): its own device pool, stream, tables and
+// kernels.  aero_engine routes every channel to its kind's group.
+struct Group {
+  int mode = MODE_OQPSK;
+  ModeGeom g{};
   int device = 0, flags = 0, C = 0, nch = 0;
+  const char *tag = "";  // timing-name prefix ("" for OQPSK, "msk600_", "msk1200_")
   hipStream_t st = nullptr;
   DevState S{};
   DevTables T{};
   void *pool = nullptr;
   size_t pool_bytes = 0;
+  HostPool *hpool = nullptr;  // the engine's
   std::vector<aero_channel_cfg> cfg;
+  std::vector<int> gch;  // local -> engine channel id
   // host mirrors of the per-channel counters
   std::vector<long long> avail, nsamp, hops;
   std::vector<std::unique_ptr<PChannelHost>> host;
+  std::vector<std::vector<uint8_t>> infofield;  // 600/1200: the frame being assembled from its blocks
   std::vector<std::vector<int16_t>> soft_hold;
   std::vector<std::vector<double>> hop_hold, pt_hold;
   std::vector<std::vector<uint8_t>> blk_hold, frame_hold;
@@ -205,9 +215,15 @@ struct aero_engine {
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending_ev;
   uint64_t processed = 0;
   int init_lo = 0;  // channels [init_lo, nch) await device state init
-  int host_threads = 1;
-  std::unique_ptr<HostPool> hpool;
   std::vector<uint8_t> h_jobs_task, h_dbg_task;  // buffers owned by the running host task
+};
+
+struct aero_engine {
+  int device = 0, flags = 0, max_channels = 0;
+  std::unique_ptr<Group> groups[MODE_COUNT];
+  std::vector<std::pair<int, int>> chmap;  // engine channel -> (mode, local index)
+  std::unique_ptr<HostPool> hpool;
+  std::map<std::string, TimingSlot> timing;  // engine-level host sections
 };
 
 namespace {
@@ -220,55 +236,63 @@ T *carve(char *&p, size_t count) {
   return r;
 }
 
-size_t layout(DevState &S, DevTables &T, int C, int flags, char *base) {
+size_t layout(DevState &S, DevTables &T, int mode, int C, int flags, char *base) {
+  const ModeGeom g = mode_geom(mode);
+  const bool msk = mode != MODE_OQPSK;
   char *p = base;
   S.C = C;
+  S.mode = mode;
+  S.g = g;
   S.ds = carve<double>(p, (size_t)DS_COUNT * C);
   S.is = carve<int>(p, (size_t)IS_COUNT * C);
   S.ls = carve<long long>(p, (size_t)LS_COUNT * C);
-  S.fir = carve<double>(p, (size_t)2 * NTAPS * C);
-  S.agc = carve<double>(p, (size_t)AGC_LEN * C);
-  S.marg = carve<double>(p, (size_t)MARG_LEN * C);
-  S.dt = carve<double2>(p, (size_t)DT_LEN * C);
-  S.pm = carve<double>(p, (size_t)MSE_LEN * C);
-  S.ms = carve<double>(p, (size_t)MSE_LEN * C);
+  S.fir = carve<double>(p, (size_t)2 * g.ntaps * C);
+  S.agc = carve<double>(p, (size_t)g.agc_len * C);
+  S.dsm = carve<double2>(p, msk ? (size_t)g.dsm_len * C : 1);
+  S.d8 = carve<double>(p, msk ? (size_t)g.d8_len * C : 1);
+  S.marg = carve<double>(p, (size_t)g.marg_len * C);
+  S.dt = carve<double2>(p, (size_t)g.dt_len * C);
+  S.pm = carve<double>(p, msk ? 1 : (size_t)g.ms_len * C);
+  S.ms = carve<double>(p, (size_t)g.ms_len * C);
   S.pcm = carve<int16_t>(p, (size_t)PCM_CAP * C);
   S.pcm_cap = PCM_CAP;
-  S.cring = carve<uint32_t>(p, (size_t)NFFT * C);
-  S.y = carve<double>(p, (size_t)Y_LEN * C);
+  S.cring = carve<uint32_t>(p, (size_t)g.nfft * C);
+  S.y = carve<double>(p, (size_t)(g.y_hi - g.y_lo + 1) * C);
   S.soft = carve<uint8_t>(p, (size_t)SOFT_RING * C);
   S.pt_cap = (flags & AERO_F_TRACE_PT) ? PT_CAP : 0;
   S.pt = carve<double2>(p, (size_t)S.pt_cap * C);
   S.hop_cap = HOP_CAP;
   S.hops = carve<double>(p, (size_t)HOP_CAP * 6 * C);
   S.hop_n = carve<int>(p, (size_t)C);
-  S.block = carve<uint8_t>(p, (size_t)2 * BLOCK * C);
+  S.block = carve<uint8_t>(p, (size_t)2 * g.block * C);
   S.overlap = carve<uint8_t>(p, (size_t)64 * C);
-  S.dl2 = carve<uint8_t>(p, (size_t)DL2_LEN * C);
+  S.dl2 = carve<uint8_t>(p, (size_t)g.dl2_len * C);
   S.jobs = carve<int>(p, (size_t)4 * C);
   S.njobs = carve<int>(p, 1);
   S.jobout = carve<uint8_t>(p, (size_t)JOB_OUT * C);
   S.blocks_dbg = carve<uint8_t>(p, (flags & AERO_F_TRACE_BLOCKS) ? (size_t)2500 * C : 1);
   T.cis = carve<double2>(p, WTSIZE);
-  T.tw = carve<double2>(p, NFFT);
-  T.twi = carve<double2>(p, NFFT);
+  T.tw = carve<double2>(p, g.nfft);
+  T.twi = carve<double2>(p, g.nfft);
   T.scr = carve<uint8_t>(p, 5000);
-  T.taps = carve<double>(p, 64);
+  T.taps = carve<double>(p, 128);
   return (size_t)(p - base);
 }
 
-void ev_begin(aero_engine *e, const char *name, hipEvent_t &a, hipEvent_t &b) {
+std::string tname(const Group *e, const char *name) { return std::string(e->tag) + name; }
+
+void ev_begin(Group *e, const char *name, hipEvent_t &a, hipEvent_t &b) {
   if (!(e->flags & AERO_F_TIMING)) return;
   hipEventCreate(&a);
   hipEventCreate(&b);
   hipEventRecord(a, e->st);
-  e->pending_ev.push_back({name, {a, b}});
+  e->pending_ev.push_back({tname(e, name), {a, b}});
 }
-void ev_end(aero_engine *e, hipEvent_t b) {
+void ev_end(Group *e, hipEvent_t b) {
   if (!(e->flags & AERO_F_TIMING)) return;
   hipEventRecord(b, e->st);
 }
-void ev_collect(aero_engine *e) {
+void ev_collect(Group *e) {
   for (auto &pe : e->pending_ev) {
     float ms = 0;
     hipEventSynchronize(pe.second.second);
@@ -282,20 +306,30 @@ void ev_collect(aero_engine *e) {
   e->pending_ev.clear();
 }
 
-// Per-channel scalar state as OqpskDemodulator's ctor + setSettings leave it
-// (decode/oqpskdemodulator.cpp:9-115, :136-254, as Decoder applies them).
-// Opened channels are initialised lazily, one strided copy per field for the
-// whole pending range, so opening thousands of channels costs O(fields).
-int flush_pending_init(aero_engine *e) {
+// Per-channel scalar state as the demodulator ctor + setSettings leave it.
+// OQPSK: decode/oqpskdemodulator.cpp:9-115, :136-254; MSK:
+// decode/mskdemodulator.cpp:7-218 (both as Decoder applies them); AeroL ctor
+// (decode/aerol.cpp:875-954).  Opened channels are initialised lazily, one
+// strided copy per field for the whole pending range.
+int flush_pending_init(Group *e) {
   const int lo = e->init_lo, hi = e->nch;
   if (lo >= hi) return AERO_OK;
   const int C = e->C, k = hi - lo;
   std::vector<double> ds(DS_COUNT, 0.0);
   std::vector<int> is(IS_COUNT, 0);
   std::vector<long long> ls(LS_COUNT, 0);
-  ds[DS_SO_FREQ] = 10500;
-  ds[DS_SO_STEP] = (10500.0) * ((double)WTSIZE) / ((float)48000);
-  ds[DS_MSE] = 100;
+  if (e->mode == MODE_OQPSK) {
+    ds[DS_SO_FREQ] = 10500;
+    ds[DS_SO_STEP] = (10500.0) * ((double)WTSIZE) / ((float)48000);
+    ds[DS_MSE] = 100;
+  } else {
+    // st_osc.SetFreq(fb / 2, Fs) (mskdemodulator.cpp:117); mse = 10.0 (:146);
+    // DiffDecode::lastsoftstate = -1 (DSP.cpp:517-520)
+    ds[DS_SO_FREQ] = 300;
+    ds[DS_SO_STEP] = (300.0) * ((double)WTSIZE) / ((float)e->g.fs);
+    ds[DS_MSE] = 10.0;
+    ds[DS_DIFF_LAST] = -1;
+  }
   is[IS_COUNTDOWN2] = 5;
   is[IS_COUNTDOWN] = 4;
   is[IS_EMPTYCD] = 1;
@@ -319,9 +353,30 @@ int flush_pending_init(aero_engine *e) {
   return AERO_OK;
 }
 
+// CRC-16 of one SU (AeroLcrc16::calcusingbytes, decode/aerol.h:332-367) and the
+// all-zero special case (decode/aerol.cpp:1531-1543)
+bool su_crc_ok(const uint8_t *su) {
+  unsigned crc = 0xFFFF, sum = 0;
+  for (int i = 0; i < 10; ++i) {
+    unsigned mb = su[i];
+    sum += mb;
+    for (int k = 0; k < 8; ++k) {
+      const unsigned bit = mb & 1;
+      mb >>= 1;
+      const unsigned cb = crc & 1;
+      crc >>= 1;
+      if (cb ^ bit) crc ^= 0x8408;
+    }
+  }
+  unsigned calc = (~crc) & 0xFFFF;
+  const unsigned rec = ((unsigned)su[11] << 8) | su[10];
+  if (!rec && calc != rec && sum == 0) calc = 0;
+  return calc == rec;
+}
+
 // Frame records of a pass -> host SU/ACARS work on the worker pool
 // (asynchronous; host_wait() joins it).
-int collect_after_pass(aero_engine *e, int njobs) {
+int collect_after_pass(Group *e, int njobs) {
   const int C = e->C, nch = e->nch;
   if (njobs <= 0) return AERO_OK;
   e->h_jobout.resize((size_t)njobs * JOB_OUT);
@@ -339,9 +394,10 @@ int collect_after_pass(aero_engine *e, int njobs) {
   e->hpool->wait();  // previous pass's frames first (per-channel order)
   std::swap(e->h_jobs_task, e->h_jobout);
   std::swap(e->h_dbg_task, e->h_dbg);
+  const bool msk = e->mode != MODE_OQPSK;
   // channels partitioned over workers (c % T): a channel's frames stay in
   // queue order and no two workers share state
-  auto work = [e, njobs, nch, blocks](int t, int T) {
+  auto work = [e, njobs, nch, blocks, msk](int t, int T) {
     const uint8_t *jobs = e->h_jobs_task.data();
     for (int j = 0; j < njobs; j++) {
       const uint8_t *o = jobs + (size_t)j * JOB_OUT;
@@ -360,12 +416,31 @@ int collect_after_pass(aero_engine *e, int njobs) {
         h.insert(h.end(), d + 4, d + 4 + nb);
       }
       if (reset) e->host[c]->isu_reset();
-      if (meta[0] >= 0) {
-        e->host[c]->frame(o, meta[0], (uint32_t)meta[1], meta[2]);
+      int flen = -1;
+      uint32_t mask = (uint32_t)meta[1];
+      const uint8_t *info = o;
+      if (msk) {
+        // 600/1200: a frame's infofield is the bytes of its blocks since the
+        // last cntr == 0 (aerol.cpp:1247-1250, 1509-1520); SUs checked when done
+        auto &inf = e->infofield[c];
+        if (meta[0] & (1 << 9)) inf.clear();
+        inf.insert(inf.end(), o, o + (meta[0] & 0xFF));
+        if (meta[0] & (1 << 8)) {
+          flen = (int)std::min<size_t>(inf.size(), 312);
+          mask = 0;
+          for (int k = 0; k < flen / 12; k++)
+            if (su_crc_ok(inf.data() + 12 * k)) mask |= 1u << k;
+          info = inf.data();
+        }
+      } else {
+        flen = meta[0];
+      }
+      if (flen >= 0) {
+        e->host[c]->frame(info, flen, mask, meta[2]);
         if (e->flags & AERO_F_TRACE_FRAMES) {
           uint8_t rec[320] = {0};
-          memcpy(rec, o, 312);
-          const uint32_t L = (uint32_t)meta[0], M = (uint32_t)meta[1];
+          memcpy(rec, info, flen);
+          const uint32_t L = (uint32_t)flen, M = mask;
           memcpy(rec + 312, &L, 4);
           memcpy(rec + 316, &M, 4);
           e->frame_hold[c].insert(e->frame_hold[c].end(), rec, rec + 320);
@@ -382,7 +457,7 @@ void host_wait(aero_engine *e) {
   if (e->hpool) e->hpool->wait();
 }
 
-int collect_traces(aero_engine *e) {
+int collect_traces(Group *e) {
   const int C = e->C, nch = e->nch;
   std::vector<int> hn(nch);
   if (e->flags & AERO_F_TRACE_HOPS) HIPCHK(hipMemcpy(hn.data(), e->S.hop_n, sizeof(int) * nch, hipMemcpyDeviceToHost));
@@ -412,13 +487,13 @@ int collect_traces(aero_engine *e) {
     }
     HIPCHK(hipMemset(e->S.ls + (size_t)LS_PT_N * C, 0, 8 * nch));
   }
-  // soft bits delivered to AeroL (groups of 32)
+  // soft bits delivered to AeroL (groups of 32 / 12)
   if (!(e->flags & AERO_F_TRACE_SOFT)) return AERO_OK;
   std::vector<long long> sp(nch);
   HIPCHK(hipMemcpy(sp.data(), e->S.ls + (size_t)LS_SOFT_P * C, 8 * nch, hipMemcpyDeviceToHost));
   std::vector<uint8_t> ring;
   for (int c = 0; c < nch; c++) {
-    const long long emitted = sp[c] & ~31LL;
+    const long long emitted = sp[c] - sp[c] % e->g.soft_group;
     if (emitted > e->soft_seen[c]) {
       if (ring.empty()) {
         ring.resize((size_t)SOFT_RING * nch);
@@ -432,24 +507,26 @@ int collect_traces(aero_engine *e) {
   return AERO_OK;
 }
 
-int run_impl(aero_engine *e, int flush) {
+int run_group(Group *e, int flush) {
   if (e->nch == 0) return AERO_OK;
+  HIPCHK(hipSetDevice(e->device));
   HOST_TIMER(e, "host_run");
   if (int rc = flush_pending_init(e)) return rc;
   const int tflags = AERO_F_TRACE_PT | AERO_F_TRACE_BLOCKS | AERO_F_TRACE_SOFT | AERO_F_TRACE_HOPS;
   const bool trace = (e->flags & tflags) != 0;
+  const long long HOPN = e->g.hop;
   for (int guard = 0; guard < 1000000; guard++) {
-    // host mirror of the hop and segment rules of coarse.hip / demod_oqpsk.hip
+    // host mirror of the hop and segment rules of coarse.hip / demod_*.hip
     bool any_hop = false, progress = false;
     for (int c = 0; c < e->nch; c++) {
-      const long long boundary = (long long)HOP * (e->hops[c] + 1) - 1;
+      const long long boundary = HOPN * (e->hops[c] + 1) - 1;
       if (e->nsamp[c] == boundary && e->avail[c] > boundary) {
         e->hops[c]++;
         any_hop = true;
       }
     }
     for (int c = 0; c < e->nch; c++) {
-      const long long boundary = (long long)HOP * (e->hops[c] + 1) - 1;
+      const long long boundary = HOPN * (e->hops[c] + 1) - 1;
       long long end = std::min(e->avail[c], boundary);
       if (!flush && e->avail[c] <= boundary) end = e->nsamp[c];
       if (end > e->nsamp[c]) {
@@ -462,17 +539,20 @@ int run_impl(aero_engine *e, int flush) {
     hipEvent_t a, b;
     if (any_hop) {
       ev_begin(e, "coarse", a, b);
-      launch_coarse(e->st, e->S, e->T, e->nch);
+      launch_coarse(e->st, e->mode, e->S, e->T, e->nch);
       ev_end(e, b);
     }
     if (progress) {
       ev_begin(e, "demod", a, b);
-      launch_demod(e->st, e->S, e->T, e->nch, flush, (e->flags & AERO_F_TRACE_PT) != 0);
+      if (e->mode == MODE_OQPSK)
+        launch_demod(e->st, e->S, e->T, e->nch, flush, (e->flags & AERO_F_TRACE_PT) != 0);
+      else
+        launch_demod_msk(e->st, e->mode, e->S, e->T, e->nch, flush);
       ev_end(e, b);
     }
     HIPCHK(hipMemsetAsync(e->S.njobs, 0, sizeof(int), e->st));
     ev_begin(e, "frame", a, b);
-    launch_frame(e->st, e->S, e->nch);
+    launch_frame(e->st, e->mode, e->S, e->nch);
     ev_end(e, b);
     int njobs = 0;
     HIPCHK(hipMemcpyAsync(&njobs, e->S.njobs, sizeof(int), hipMemcpyDeviceToHost, e->st));
@@ -482,7 +562,7 @@ int run_impl(aero_engine *e, int flush) {
     }
     if (njobs > 0) {
       ev_begin(e, "viterbi", a, b);
-      launch_viterbi(e->st, e->S, e->T, njobs, (e->flags & AERO_F_TRACE_BLOCKS) ? 1 : 0);
+      launch_viterbi(e->st, e->mode, e->S, e->T, njobs, (e->flags & AERO_F_TRACE_BLOCKS) ? 1 : 0);
       ev_end(e, b);
     }
     HIPCHK(hipGetLastError());
@@ -498,6 +578,15 @@ int run_impl(aero_engine *e, int flush) {
   return AERO_OK;
 }
 
+int run_impl(aero_engine *e, int flush) {
+  for (auto &g : e->groups)
+    if (g) {
+      int rc = run_group(g.get(), flush);
+      if (rc) return rc;
+    }
+  return AERO_OK;
+}
+
 template <class T>
 int pop_vec(std::vector<T> &v, T *dst, size_t cap, size_t *n) {
   const size_t k = std::min(cap, v.size());
@@ -507,132 +596,105 @@ int pop_vec(std::vector<T> &v, T *dst, size_t cap, size_t *n) {
   return AERO_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-const char *aero_strerror(int rc) {
-  switch (rc) {
-    case AERO_OK: return "ok";
-    case AERO_E_INVALID: return "invalid argument or unsupported configuration";
-    case AERO_E_NOMEM: return "out of memory";
-    case AERO_E_HIP: return "HIP runtime error";
-    case AERO_E_NOGPU: return "no usable gfx950 device";
-    case AERO_E_FULL: return "channel table or ring full";
-    case AERO_E_RATE: return "sample rate mismatch";
-    default: return "unknown error";
-  }
-}
-
-int aero_engine_create(const aero_engine_cfg *cfg, aero_engine **out) {
-  if (!cfg || !out || cfg->max_channels <= 0) return AERO_E_INVALID;
-  *out = nullptr;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device) return AERO_E_NOGPU;
-  HIPCHK(hipSetDevice(cfg->device));
-  std::unique_ptr<aero_engine> e(new aero_engine());
-  e->device = cfg->device;
-  e->flags = cfg->flags;
-  {
-    // host threads for the per-frame SU/ACARS work (AERO_HOST_THREADS overrides)
-    const char *ev = getenv("AERO_HOST_THREADS");
-    const int hw = (int)std::thread::hardware_concurrency();
-    e->host_threads = ev ? atoi(ev) : std::min(16, std::max(1, hw));
-    if (e->host_threads < 1) e->host_threads = 1;
-    e->hpool.reset(new HostPool(e->host_threads));
-  }
-  e->C = (cfg->max_channels + 63) & ~63;
+// group tables and kernel constants (host glibc, g++-compiled: tables_host.cpp)
+int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
+  std::unique_ptr<Group> e(new Group());
+  e->mode = mode;
+  e->g = mode_geom(mode);
+  e->device = E->device;
+  e->flags = E->flags;
+  e->hpool = E->hpool.get();
+  e->tag = mode == MODE_OQPSK ? "" : (mode == MODE_MSK600 ? "msk600_" : "msk1200_");
+  e->C = (E->max_channels + 63) & ~63;
   DevState S{};
   DevTables T{};
-  const size_t bytes = layout(S, T, e->C, e->flags, nullptr) + 4096;
+  const size_t bytes = layout(S, T, mode, e->C, e->flags, nullptr) + 4096;
   if (hipMalloc(&e->pool, bytes) != hipSuccess) return AERO_E_NOMEM;
   e->pool_bytes = bytes;
   HIPCHK(hipMemset(e->pool, 0, bytes));
-  layout(e->S, e->T, e->C, e->flags, reinterpret_cast<char *>(e->pool));
+  layout(e->S, e->T, mode, e->C, e->flags, reinterpret_cast<char *>(e->pool));
   HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
-  // tables (host glibc, g++-compiled: tables_host.cpp)
-  std::vector<double> cis(2 * WTSIZE), tw(2 * NFFT), twi(2 * NFFT), taps(64);
+  const int nfft = e->g.nfft;
+  std::vector<double> cis(2 * WTSIZE), tw(2 * nfft), twi(2 * nfft), taps(128, 0.0);
   std::vector<uint8_t> scr(5000);
   host_cis(cis.data());
-  host_twiddles(NFFT, tw.data(), twi.data());
+  host_twiddles(nfft, tw.data(), twi.data());
   host_scrambler(scr.data());
   HIPCHK(hipMemcpy((void *)e->T.cis, cis.data(), sizeof(double) * 2 * WTSIZE, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy((void *)e->T.tw, tw.data(), sizeof(double) * 2 * NFFT, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy((void *)e->T.twi, twi.data(), sizeof(double) * 2 * NFFT, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy((void *)e->T.tw, tw.data(), sizeof(double) * 2 * nfft, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy((void *)e->T.twi, twi.data(), sizeof(double) * 2 * nfft, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy((void *)e->T.scr, scr.data(), 5000, hipMemcpyHostToDevice));
-  if (host_rrc(1.0, 55, 48000, 10500 / 2, taps.data()) != NTAPS) return AERO_E_INVALID;
-  HIPCHK(hipMemcpy((void *)e->T.taps, taps.data(), sizeof(double) * NTAPS, hipMemcpyHostToDevice));
-  const double T48 = 48000.0 / (10500.0 / 2);
-  DelayDesc dly[4];
-  if (!host_delay(1, dly[0]) || !host_delay(T48 / 4.0, dly[1]) || !host_delay(T48 / 4.0, dly[2]) ||
-      !host_delay(T48 / 8.0, dly[3]))
-    return AERO_E_INVALID;
-  if (dly[0].size != 2 || dly[1].size != 4 || dly[2].size != 4 || dly[3].size != 3) return AERO_E_INVALID;
-  // the demod kernel bakes in what these designs give at 48 kHz / 10500 bps:
-  // the ring ages it reads (template arguments of delay_tap) and weights that
-  // do not depend on the write pointer; refuse to run if that ever changes
-  static const int ages[4][2] = {{1, 0}, {3, 2}, {3, 2}, {2, 1}};  // {age_old, age_new}
-  for (int k = 0; k < 4; k++) {
-    if (dly[k].age_old != ages[k][0] || dly[k].age_new != ages[k][1]) return AERO_E_INVALID;
-    for (int p = 1; p < dly[k].size; p++)
-      if (memcmp(&dly[k].w[p], &dly[k].w[0], 8) || memcmp(&dly[k].omw[p], &dly[k].omw[0], 8)) return AERO_E_INVALID;
+  if (mode == MODE_OQPSK) {
+    if (host_rrc(1.0, 55, 48000, 10500 / 2, taps.data()) != NTAPS) return AERO_E_INVALID;
+    const double T48 = 48000.0 / (10500.0 / 2);
+    DelayDesc dly[4];
+    if (!host_delay(1, dly[0]) || !host_delay(T48 / 4.0, dly[1]) || !host_delay(T48 / 4.0, dly[2]) ||
+        !host_delay(T48 / 8.0, dly[3]))
+      return AERO_E_INVALID;
+    if (dly[0].size != 2 || dly[1].size != 4 || dly[2].size != 4 || dly[3].size != 3) return AERO_E_INVALID;
+    // the demod kernel bakes in what these designs give at 48 kHz / 10500 bps:
+    // the ring ages it reads (template arguments of delay_tap) and weights that
+    // do not depend on the write pointer; refuse to run if that ever changes
+    static const int ages[4][2] = {{1, 0}, {3, 2}, {3, 2}, {2, 1}};  // {age_old, age_new}
+    for (int k = 0; k < 4; k++) {
+      if (dly[k].age_old != ages[k][0] || dly[k].age_new != ages[k][1]) return AERO_E_INVALID;
+      for (int p = 1; p < dly[k].size; p++)
+        if (memcmp(&dly[k].w[p], &dly[k].w[0], 8) || memcmp(&dly[k].omw[p], &dly[k].omw[0], 8))
+          return AERO_E_INVALID;
+    }
+    for (int j = 0; j < NTAPS; j++)  // the kernel stores the 28 distinct taps of the symmetric RRC
+      if (memcmp(&taps[j], &taps[NTAPS - 1 - j], 8)) return AERO_E_INVALID;
+    const double sr_b[3] = {0.00032714218939589035, 0, 0.00032714218939589035};
+    const double sr_a[3] = {1, -0.39005299948210803, 0.99934571562120822};
+    const double ct_b[3] = {0.0010275610653672064, 0.0020551221307344128, 0.0010275610653672064};
+    const double ct_a[3] = {1, -1.9207386815577139, 0.92509247310306331};
+    upload_demod_constants(taps.data(), dly, sr_b, sr_a, ct_b, ct_a);
+  } else {
+    // matched filter sin(pi i / 2SPS) / 2SPS (mskdemodulator.cpp:126-133)
+    const int sps = e->g.fs / 600;
+    host_msk_taps(sps, taps.data());
+    // delayt8.setdelay(SPS / 2.0) (mskdemodulator.cpp:215): the kernel reads
+    // ages SPS/2 and SPS/2 - 1 with pointer-independent weights
+    int size, age_old, age_new;
+    double w, omw;
+    if (!host_delay_uniform(sps / 2.0, size, age_old, age_new, w, omw)) return AERO_E_INVALID;
+    if (size != e->g.d8_len || age_old != sps / 2 || age_new != sps / 2 - 1) return AERO_E_INVALID;
+    const double d8w[2] = {w, omw};
+    const double sr_b[3] = {5.233248111921052e-04, 0, -5.233248111921052e-04};
+    const double sr_a[3] = {1, -1.974342917561558, 0.998953350377616};
+    upload_msk_constants(sr_b, sr_a, d8w);
   }
-  for (int j = 0; j < NTAPS; j++)  // the kernel stores the 28 distinct taps of the symmetric RRC
-    if (memcmp(&taps[j], &taps[NTAPS - 1 - j], 8)) return AERO_E_INVALID;
-  const double sr_b[3] = {0.00032714218939589035, 0, 0.00032714218939589035};
-  const double sr_a[3] = {1, -0.39005299948210803, 0.99934571562120822};
-  const double ct_b[3] = {0.0010275610653672064, 0.0020551221307344128, 0.0010275610653672064};
-  const double ct_a[3] = {1, -1.9207386815577139, 0.92509247310306331};
-  upload_demod_constants(taps.data(), dly, sr_b, sr_a, ct_b, ct_a);
+  HIPCHK(hipMemcpy((void *)e->T.taps, taps.data(), sizeof(double) * 128, hipMemcpyHostToDevice));
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
-  *out = e.release();
+  out = std::move(e);
   return AERO_OK;
 }
 
-void aero_engine_destroy(aero_engine *e) {
+void group_destroy(Group *e) {
   if (!e) return;
-  hipSetDevice(e->device);
   if (e->st) hipStreamSynchronize(e->st);
-  host_wait(e);
   ev_collect(e);
   if (e->d_scratch) (void)hipFree(e->d_scratch);
   if (e->pool) (void)hipFree(e->pool);
   if (e->st) (void)hipStreamDestroy(e->st);
-  delete e;
 }
 
-int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) {
-  if (!e || !cfg || !ch_out) return AERO_E_INVALID;
-  if (cfg->bitrate != 10500 || cfg->burst) return AERO_E_INVALID;  // decode/decode.h:42 subset
-  if (e->nch >= e->C) return AERO_E_FULL;
-  HIPCHK(hipSetDevice(e->device));
-  host_wait(e);  // the host task indexes the per-channel tables
-  const int c = e->nch;
-  e->nch++;  // device state initialised by flush_pending_init before the next push/run
-  e->cfg.push_back(*cfg);
-  e->avail.push_back(0);
-  e->nsamp.push_back(0);
-  e->hops.push_back(0);
-  e->host.emplace_back(new PChannelHost(cfg->disable_reassembly != 0));
-  e->soft_hold.emplace_back();
-  e->hop_hold.emplace_back();
-  e->pt_hold.emplace_back();
-  e->blk_hold.emplace_back();
-  e->frame_hold.emplace_back();
-  e->soft_seen.push_back(0);
-  *ch_out = c;
-  return AERO_OK;
+// engine channel -> (group, local index); nullptr if out of range
+Group *route(aero_engine *e, int ch, int &local) {
+  if (!e || ch < 0 || ch >= (int)e->chmap.size()) return nullptr;
+  local = e->chmap[ch].second;
+  return e->groups[e->chmap[ch].first].get();
 }
 
-static int push_common(aero_engine *e, const int16_t *src, size_t n, size_t ld, int nch, int c0, bool dev) {
+int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int c0, bool dev) {
   HOST_TIMER(e, "host_push");
   if (int rc = flush_pending_init(e)) return rc;
   // keep the ring from overrunning unprocessed samples
   for (int j = 0; j < nch; j++) {
     const int c = c0 + j;
     if (e->avail[c] + (long long)n - e->nsamp[c] > PCM_CAP - 2) {
-      int rc = run_impl(e, 0);
+      int rc = run_group(e, 0);
       if (rc) return rc;
       if (e->avail[c] + (long long)n - e->nsamp[c] > PCM_CAP - 2) return AERO_E_FULL;
     }
@@ -666,16 +728,109 @@ static int push_common(aero_engine *e, const int16_t *src, size_t n, size_t ld, 
   return AERO_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+const char *aero_strerror(int rc) {
+  switch (rc) {
+    case AERO_OK: return "ok";
+    case AERO_E_INVALID: return "invalid argument or unsupported configuration";
+    case AERO_E_NOMEM: return "out of memory";
+    case AERO_E_HIP: return "HIP runtime error";
+    case AERO_E_NOGPU: return "no usable gfx950 device";
+    case AERO_E_FULL: return "channel table or ring full";
+    case AERO_E_RATE: return "sample rate mismatch";
+    default: return "unknown error";
+  }
+}
+
+int aero_engine_create(const aero_engine_cfg *cfg, aero_engine **out) {
+  if (!cfg || !out || cfg->max_channels <= 0) return AERO_E_INVALID;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device) return AERO_E_NOGPU;
+  HIPCHK(hipSetDevice(cfg->device));
+  std::unique_ptr<aero_engine> e(new aero_engine());
+  e->device = cfg->device;
+  e->flags = cfg->flags;
+  e->max_channels = cfg->max_channels;
+  {
+    // host threads for the per-frame SU/ACARS work (AERO_HOST_THREADS overrides)
+    const char *ev = getenv("AERO_HOST_THREADS");
+    const int hw = (int)std::thread::hardware_concurrency();
+    int n = ev ? atoi(ev) : std::min(16, std::max(1, hw));
+    if (n < 1) n = 1;
+    e->hpool.reset(new HostPool(n));
+  }
+  // the 10500 group is created up front (the hot path), MSK groups on first use
+  if (int rc = group_create(e.get(), MODE_OQPSK, e->groups[MODE_OQPSK])) return rc;
+  *out = e.release();
+  return AERO_OK;
+}
+
+void aero_engine_destroy(aero_engine *e) {
+  if (!e) return;
+  hipSetDevice(e->device);
+  host_wait(e);
+  for (auto &g : e->groups) group_destroy(g.get());
+  delete e;
+}
+
+int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) {
+  if (!e || !cfg || !ch_out) return AERO_E_INVALID;
+  if (cfg->burst) return AERO_E_INVALID;  // burst modes: not built this round
+  int mode;
+  if (cfg->bitrate == 10500 && cfg->fs == 48000)
+    mode = MODE_OQPSK;
+  else if (cfg->bitrate == 600 && cfg->fs == 12000)  // decode/decode.cpp:145
+    mode = MODE_MSK600;
+  else if (cfg->bitrate == 1200 && cfg->fs == 24000)
+    mode = MODE_MSK1200;
+  else
+    return AERO_E_INVALID;  // decode/decode.h:42 validBitRates, with their rates
+  HIPCHK(hipSetDevice(e->device));
+  if (!e->groups[mode]) {
+    if (int rc = group_create(e, mode, e->groups[mode])) return rc;
+  }
+  Group *g = e->groups[mode].get();
+  if (g->nch >= g->C) return AERO_E_FULL;
+  host_wait(e);  // the host task indexes the per-channel tables
+  const int c = g->nch;
+  g->nch++;  // device state initialised by flush_pending_init before the next push/run
+  g->cfg.push_back(*cfg);
+  g->gch.push_back((int)e->chmap.size());
+  g->avail.push_back(0);
+  g->nsamp.push_back(0);
+  g->hops.push_back(0);
+  g->host.emplace_back(new PChannelHost(cfg->disable_reassembly != 0));
+  g->infofield.emplace_back();
+  g->soft_hold.emplace_back();
+  g->hop_hold.emplace_back();
+  g->pt_hold.emplace_back();
+  g->blk_hold.emplace_back();
+  g->frame_hold.emplace_back();
+  g->soft_seen.push_back(0);
+  *ch_out = (int)e->chmap.size();
+  e->chmap.push_back({mode, c});
+  return AERO_OK;
+}
+
 int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t fs) {
-  if (!e || ch < 0 || ch >= e->nch || (!pcm && n)) return AERO_E_INVALID;
-  (void)fs;  // the OQPSK demodulator only logs a rate mismatch (oqpskdemodulator.cpp:626-628)
+  int c;
+  Group *g = route(e, ch, c);
+  if (!g || (!pcm && n)) return AERO_E_INVALID;
+  // OQPSK only logs a rate mismatch (oqpskdemodulator.cpp:626-628); the MSK
+  // demodulator would re-apply its settings at the new rate
+  // (mskdemodulator.cpp:472-480), which this engine does not support
+  if (g->mode != MODE_OQPSK && fs != (uint32_t)g->g.fs) return AERO_E_RATE;
   if (!n) return AERO_OK;
   HIPCHK(hipSetDevice(e->device));
   // split so one piece never exceeds the ring
   size_t off = 0;
   while (off < n) {
     const size_t piece = std::min<size_t>(n - off, PCM_CAP / 2);
-    int rc = push_common(e, pcm + off, piece, 1, 1, ch, false);
+    int rc = push_common(g, pcm + off, piece, 1, 1, c, false);
     if (rc) return rc;
     off += piece;
   }
@@ -683,12 +838,17 @@ int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t
 }
 
 int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld, int nch, int dev) {
-  if (!e || !pcm || nch <= 0 || nch > e->nch || ld < (size_t)nch) return AERO_E_INVALID;
+  if (!e || !pcm || nch <= 0 || nch > (int)e->chmap.size() || ld < (size_t)nch) return AERO_E_INVALID;
+  // channels [0, nch) must be one kind, opened in order (local == engine index)
+  const int mode = e->chmap[0].first;
+  for (int j = 0; j < nch; j++)
+    if (e->chmap[j].first != mode || e->chmap[j].second != j) return AERO_E_INVALID;
+  Group *g = e->groups[mode].get();
   HIPCHK(hipSetDevice(e->device));
   size_t off = 0;
   while (off < n) {
     const size_t piece = std::min<size_t>(n - off, PCM_CAP / 2);
-    int rc = push_common(e, pcm + off * ld, piece, ld, nch, 0, dev != 0);
+    int rc = push_common(g, pcm + off * ld, piece, ld, nch, 0, dev != 0);
     if (rc) return rc;
     off += piece;
   }
@@ -697,37 +857,39 @@ int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld,
 
 int aero_run(aero_engine *e) {
   if (!e) return AERO_E_INVALID;
-  HIPCHK(hipSetDevice(e->device));
   return run_impl(e, 0);
 }
 
 int aero_flush(aero_engine *e) {
   if (!e) return AERO_E_INVALID;
-  HIPCHK(hipSetDevice(e->device));
   return run_impl(e, 1);
 }
 
 int aero_pop_softbits(aero_engine *e, int ch, int16_t *dst, size_t cap, size_t *n) {
-  if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
-  return pop_vec(e->soft_hold[ch], dst, cap, n);
+  int c;
+  Group *g = route(e, ch, c);
+  if (!g) return AERO_E_INVALID;
+  return pop_vec(g->soft_hold[c], dst, cap, n);
 }
 
 int aero_pop_items(aero_engine *e, int ch, aero_acars_item *dst, size_t cap, size_t *n) {
-  if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  int c;
+  Group *g = route(e, ch, c);
+  if (!g) return AERO_E_INVALID;
   host_wait(e);
-  return pop_vec(e->host[ch]->items, dst, cap, n);
+  return pop_vec(g->host[c]->items, dst, cap, n);
 }
 
 int aero_pop_items_all(aero_engine *e, aero_acars_item *dst, int *ch, size_t cap, size_t *n) {
   if (!e || (cap && (!dst || !ch))) return AERO_E_INVALID;
   host_wait(e);
   size_t k = 0;
-  for (int c = 0; c < e->nch && k < cap; c++) {
-    auto &v = e->host[c]->items;
+  for (int gc = 0; gc < (int)e->chmap.size() && k < cap; gc++) {
+    auto &v = e->groups[e->chmap[gc].first]->host[e->chmap[gc].second]->items;
     const size_t m = std::min(cap - k, v.size());
     for (size_t i = 0; i < m; i++) {
       dst[k + i] = v[i];
-      ch[k + i] = c;
+      ch[k + i] = gc;
     }
     v.erase(v.begin(), v.begin() + m);
     k += m;
@@ -737,53 +899,80 @@ int aero_pop_items_all(aero_engine *e, aero_acars_item *dst, int *ch, size_t cap
 }
 
 int aero_pop_hops(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n) {
-  if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  int c;
+  Group *g = route(e, ch, c);
+  if (!g) return AERO_E_INVALID;
   size_t k = 0;
-  int rc = pop_vec(e->hop_hold[ch], dst, cap_records * 6, &k);
+  int rc = pop_vec(g->hop_hold[c], dst, cap_records * 6, &k);
   if (n) *n = k / 6;
   return rc;
 }
 
 int aero_pop_pt(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n) {
-  if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  int c;
+  Group *g = route(e, ch, c);
+  if (!g) return AERO_E_INVALID;
   size_t k = 0;
-  int rc = pop_vec(e->pt_hold[ch], dst, cap_records * 2, &k);
+  int rc = pop_vec(g->pt_hold[c], dst, cap_records * 2, &k);
   if (n) *n = k / 2;
   return rc;
 }
 
 int aero_pop_blocks(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
-  if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  int c;
+  Group *g = route(e, ch, c);
+  if (!g) return AERO_E_INVALID;
   host_wait(e);
-  return pop_vec(e->blk_hold[ch], dst, cap, n);
+  return pop_vec(g->blk_hold[c], dst, cap, n);
 }
 
 int aero_pop_frames(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
-  if (!e || ch < 0 || ch >= e->nch) return AERO_E_INVALID;
+  int c;
+  Group *g = route(e, ch, c);
+  if (!g) return AERO_E_INVALID;
   host_wait(e);
-  return pop_vec(e->frame_hold[ch], dst, cap, n);
+  return pop_vec(g->frame_hold[c], dst, cap, n);
 }
 
 int aero_timing(aero_engine *e, const char *name, double *ms, long *launches) {
   if (!e || !name) return AERO_E_INVALID;
-  ev_collect(e);
-  auto it = e->timing.find(name);
-  if (ms) *ms = it == e->timing.end() ? 0.0 : it->second.ms;
-  if (launches) *launches = it == e->timing.end() ? 0 : it->second.launches;
+  double tms = 0;
+  long tl = 0;
+  for (auto &g : e->groups) {
+    if (!g) continue;
+    ev_collect(g.get());
+    auto it = g->timing.find(name);
+    if (it != g->timing.end()) {
+      tms += it->second.ms;
+      tl += it->second.launches;
+    }
+  }
+  if (ms) *ms = tms;
+  if (launches) *launches = tl;
   return AERO_OK;
 }
 
 void aero_timing_reset(aero_engine *e) {
   if (!e) return;
-  ev_collect(e);
-  e->timing.clear();
+  for (auto &g : e->groups)
+    if (g) {
+      ev_collect(g.get());
+      g->timing.clear();
+    }
 }
 
-uint64_t aero_samples_processed(aero_engine *e) { return e ? e->processed : 0; }
+uint64_t aero_samples_processed(aero_engine *e) {
+  uint64_t s = 0;
+  if (e)
+    for (auto &g : e->groups)
+      if (g) s += g->processed;
+  return s;
+}
 
 int aero_sync(aero_engine *e) {
   if (!e) return AERO_E_INVALID;
-  HIPCHK(hipStreamSynchronize(e->st));
+  for (auto &g : e->groups)
+    if (g) HIPCHK(hipStreamSynchronize(g->st));
   host_wait(e);
   return AERO_OK;
 }
@@ -791,13 +980,14 @@ int aero_sync(aero_engine *e) {
 int aero_device_math(aero_engine *e, int fn, const double *x, const double *y, double *out, size_t n) {
   if (!e || !x || !y || !out) return AERO_E_INVALID;
   HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = e->groups[MODE_OQPSK]->st;
   double *d = nullptr;
   HIPCHK(hipMalloc(&d, 3 * n * sizeof(double) + 64));
   HIPCHK(hipMemcpy(d, x, n * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d + n, y, n * 8, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(math_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->st, fn, d, d + n, d + 2 * n, n);
+  hipLaunchKernelGGL(math_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, fn, d, d + n, d + 2 * n, n);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(e->st));
+  HIPCHK(hipStreamSynchronize(st));
   HIPCHK(hipMemcpy(out, d + 2 * n, n * 8, hipMemcpyDeviceToHost));
   HIPCHK(hipFree(d));
   return AERO_OK;

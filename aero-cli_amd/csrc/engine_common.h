@@ -33,6 +33,39 @@ constexpr int DL2_LEN = 4987;         // DelayLine setLength(4992-6) (aerol.cpp:
 constexpr int VIT_MAX = 5078;         // 62 overlap + 4992 + 24 pad
 constexpr int JOB_OUT = 328;          // 312 infofield + len + mask + formatid + channel
 
+// channel kinds (one engine group per kind; aero_channel_cfg.bitrate)
+enum Mode : int { MODE_OQPSK = 0, MODE_MSK600 = 1, MODE_MSK1200 = 2, MODE_COUNT = 3 };
+
+// continuous MSK (MskDemodulator as Decoder configures it, decode/decode.cpp:142-150,
+// decode/mskdemodulator.cpp:94-218): fb stays 600, Fs 12000 / 24000
+template <int M>
+struct MskK;
+template <>
+struct MskK<MODE_MSK600> {
+  static constexpr int FS = 12000, SPS = 20, BITRATE = 600, LEAVER = 6, WG = 256;
+};
+template <>
+struct MskK<MODE_MSK1200> {
+  static constexpr int FS = 24000, SPS = 40, BITRATE = 1200, LEAVER = 9, WG = 128;
+};
+constexpr int MSK_NFFT = 8192;          // coarsefreqest_fft_power 13 (mskdemodulator.h:26)
+constexpr int MSK_HOP = 2048;           // 75 % overlap (mskdemodulator.cpp:289-291)
+constexpr int MSK_MSEMA = 600;          // msema = MovingAverage(600) (mskdemodulator.cpp:57)
+constexpr int MSK_BLOCK_MAX = 9 * 64;   // 576
+constexpr int MSK_DL2_LEN = 571;        // dl2.setLength(576 - 6) (aerol.cpp:979,988)
+
+// per-mode geometry shared by the host layout and the kernels
+struct ModeGeom {
+  int fs, nfft, hop, agc_len, ntaps, marg_len, dt_len, ms_len, dsm_len, d8_len, block, leaver, dl2_len, y_lo,
+      y_hi, soft_group;
+};
+inline ModeGeom mode_geom(int m) {
+  if (m == MODE_OQPSK) return {48000, 16384, 4096, 192000, 55, 800, 401, 400, 0, 0, 4992, 78, 4987, 2815, 13568, 32};
+  // MSK: y[] bins the fold search reads: round(+-lockingbw/hzperbin + nfft/2) +- (expectedpeakbin + 1)
+  if (m == MODE_MSK600) return {12000, 8192, 2048, 12000, 40, 20, 11, 600, 21, 11, 384, 6, 571, 3276, 4915, 12};
+  return {24000, 8192, 2048, 24000, 80, 40, 21, 600, 41, 21, 576, 9, 571, 3686, 4505, 12};
+}
+
 // double state fields
 enum DS : int {
   DS_M2_PTR, DS_M2_STEP, DS_M2_FREQ,
@@ -48,6 +81,7 @@ enum DS : int {
   DS_MARG_SUM, DS_PM_SUM, DS_MS_SUM,
   DS_MSE,
   DS_PTD_RE, DS_PTD_IM, DS_S2L_RE, DS_S2L_IM,
+  DS_DIFF_LAST,   // MSK DiffDecode::lastsoftstate (decode/DSP.cpp:517-520)
   DS_COUNT
 };
 
@@ -63,6 +97,8 @@ enum IS : int {
   IS_RI, IS_CNTR, IS_GSL, IS_UWI, IS_UWR, IS_UWI_INV, IS_UWR_INV,
   IS_FRAMEINFO, IS_LASTFRAMEINFO, IS_FORMATID, IS_DATACD, IS_DATACDCD,
   IS_SCR_POS, IS_BLKBUF, IS_HAS_OVERLAP, IS_DL2_PTR,
+  IS_MSK_PD,      // MSK PreambleDetector shift register (aerol.cpp:716-725)
+  IS_BLK_SINCE_CLEAR,  // blocks appended to the infofield since cntr == 0
   IS_COUNT
 };
 
@@ -75,6 +111,7 @@ enum LS : int {
   LS_SOFT_P,      // soft bits produced
   LS_SOFT_C,      // soft bits consumed by AeroL
   LS_PT_N,        // pt trace records
+  LS_EVENTS,      // MSK symbol events (ring pointer of marg / dt / msema)
   LS_COUNT
 };
 
@@ -84,32 +121,36 @@ struct DevTables {
   const double2 *tw;       // [NFFT] forward twiddles   decode/jfft.cpp:41-53
   const double2 *twi;      // [NFFT] inverse twiddles
   const uint8_t *scr;      // [5000] scrambler bits      decode/aerol.h:408-427
-  const double *taps;      // [NTAPS] RRC taps           decode/DSP.h:325-351
+  const double *taps;      // [ntaps] RRC (OQPSK) / half-sine matched filter (MSK)
 };
 
 struct DevState {
   int C;                   // channel stride
+  int mode;                // Mode
+  ModeGeom g;              // ring and block sizes of this group
   double *ds;              // [DS_COUNT][C]
   int *is;                 // [IS_COUNT][C]
   long long *ls;           // [LS_COUNT][C]
   double *fir;             // [2*NTAPS][C] transposed-FIR partial sums
-  double *agc;             // [AGC_LEN][C]
-  double *marg;            // [C][MARG_LEN]
-  double2 *dt;             // [C][DT_LEN]
-  double *pm, *ms;         // [C][MSE_LEN] each
+  double *agc;             // [agc_len][C]
+  double2 *dsm;            // MSK delayedsmpl ring [dsm_len][C] (time-major, slot = n % len)
+  double *d8;              // MSK delayt8 ring [d8_len][C] (time-major)
+  double *marg;            // [C][marg_len]
+  double2 *dt;             // [C][dt_len]
+  double *pm, *ms;         // [C][ms_len] each (MSK: ms = msema)
   int16_t *pcm;            // [PCM_CAP][C] input ring (time-major)
   long long pcm_cap;       // power of 2
-  uint32_t *cring;         // [C][NFFT] coarse ring: cis index | pcm << 16
-  double *y;               // [C][Y_LEN] coarse smoothing state
+  uint32_t *cring;         // [C][nfft] coarse ring: cis index | pcm << 16
+  double *y;               // [C][y_hi - y_lo + 1] coarse smoothing state
   uint8_t *soft;           // [C][SOFT_RING]
   double2 *pt;             // [C][pt_cap] (trace only)
   long long pt_cap;
   double *hops;            // [C][hop_cap][6] per-run hop trace
   int hop_cap;
   int *hop_n;              // [C]
-  uint8_t *block;          // [C][2][BLOCK] double-buffered interleaver block
+  uint8_t *block;          // [C][2][block] double-buffered interleaver block
   uint8_t *overlap;        // [C][64]
-  uint8_t *dl2;            // [C][DL2_LEN]
+  uint8_t *dl2;            // [C][dl2_len]
   int *jobs;               // [C] job list: channel | (buf << 24)
   int *njobs;              // [1]
   uint8_t *jobout;         // [C][JOB_OUT]

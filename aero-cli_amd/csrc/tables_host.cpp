@@ -89,6 +89,32 @@ bool host_delay(double fractdelay, DelayDesc &d) {
   return true;
 }
 
+bool host_delay_uniform(double fractdelay, int &size, int &age_old, int &age_new, double &w, double &omw) {
+  size = (int)std::ceil(fractdelay) + 1;
+  for (int p = 0; p < size; p++) {
+    double dptr = ((double)p) - fractdelay;
+    while (std::floor(dptr) < 0) dptr += ((double)size);
+    const int iptr = (int)std::floor(dptr);
+    const double weighting = dptr - ((double)iptr);
+    const int a_old = ((p - iptr) % size + size) % size;
+    const int a_new = ((p - (iptr + 1) % size) % size + size) % size;
+    if (p == 0) {
+      age_old = a_old;
+      age_new = a_new;
+      w = weighting;
+      omw = (1.0 - weighting);
+    } else if (a_old != age_old || a_new != age_new || memcmp(&w, &weighting, 8)) {
+      return false;
+    }
+  }
+  return true;
+}
+
+void host_msk_taps(int sps, double *taps) {
+  const double SamplesPerSymbol = sps;
+  for (int i = 0; i < 2 * sps; i++) taps[i] = sin(M_PI * i / (2.0 * SamplesPerSymbol)) / (2.0 * SamplesPerSymbol);
+}
+
 void host_scrambler(uint8_t *pre) {  // AeroLScrambler::AeroLScrambler (decode/aerol.h:408-427)
   int st[15] = {1, 1, 0, 1, 0, 0, 1, 0, 1, 0, 1, 1, 0, 0, 1};
   for (int a = 0; a < 5000; a++) {
@@ -107,5 +133,10 @@ void aero_host_tables(double *cis, double *tw, double *twi, double *taps, int *n
   aero::host_cis(cis);
   aero::host_twiddles(16384, tw, twi);
   *ntaps = aero::host_rrc(1.0, 55, 48000, 10500 / 2, taps);
+}
+/* MSK groups: 8192-point twiddles and the 2*sps-tap matched filter */
+void aero_host_msk_tables(int sps, double *tw, double *twi, double *taps) {
+  aero::host_twiddles(8192, tw, twi);
+  aero::host_msk_taps(sps, taps);
 }
 }

@@ -13,6 +13,10 @@ void host_cis(double *cis);                                     // [19999][2] (c
 void host_twiddles(int nfft, double *tw, double *twi);          // [nfft][2] each
 int host_rrc(double alpha, int firsize, double samplerate, double symbol_freq, double *points);
 bool host_delay(double fractdelay, DelayDesc &d);
+// Delay<double> of any length whose weights do not depend on the write pointer
+bool host_delay_uniform(double fractdelay, int &size, int &age_old, int &age_new, double &w, double &omw);
+// MskDemodulator matched filter, 2*sps taps (decode/mskdemodulator.cpp:126-133)
+void host_msk_taps(int sps, double *taps);
 void host_scrambler(uint8_t *pre);                              // [5000]
 
 }  // namespace aero

@@ -47,9 +47,10 @@ typedef struct {
 } aero_engine_cfg;
 
 typedef struct {
-  int bitrate;            /* 10500 (600/1200 -> AERO_E_INVALID this round)   */
+  int bitrate;            /* 10500 (OQPSK), 600 or 1200 (MSK); decode/decode.h:42 */
   int burst;              /* 0 (burst mode -> AERO_E_INVALID this round)     */
-  uint32_t fs;            /* 48000 for 10500 bps (decode/decode.cpp:145)     */
+  uint32_t fs;            /* 48000 / 12000 / 24000 for 10500 / 600 / 1200 bps
+                             (decode/decode.cpp:145, 152-159)                 */
   int disable_reassembly; /* 1: items are ACARSfragmentsignal (decode.cpp:233) */
 } aero_channel_cfg;
 
@@ -77,13 +78,17 @@ void aero_engine_destroy(aero_engine *e);
 int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out);
 
 /* One ZMQ message == one call: Decoder::audioReceived ->
- * OqpskDemodulator::dataReceived (decode/decode.cpp:352,
- * decode/oqpskdemodulator.cpp:624-630).  pcm: int16 LE real samples. */
+ * OqpskDemodulator::dataReceived / MskDemodulator::dataReceived
+ * (decode/decode.cpp:352, decode/oqpskdemodulator.cpp:624-630,
+ * decode/mskdemodulator.cpp:472-481).  pcm: int16 LE real samples.  An MSK
+ * channel refuses a rate other than its own (AERO_E_RATE): the reference
+ * would re-apply its settings at the new rate. */
 int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t fs);
 
 /* Lockstep batch push for channels [0, nch): pcm is time-major, n samples
  * per channel, sample t of channel c at pcm[t*ld + c].  dev != 0: pcm is a
- * HIP device pointer (inputs already resident in HBM). */
+ * HIP device pointer (inputs already resident in HBM).  Channels [0, nch)
+ * must be of one kind (bit rate). */
 int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld, int nch, int dev);
 
 /* Runs the batched kernels for every channel over all pushed samples that
@@ -91,8 +96,9 @@ int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld,
 int aero_run(aero_engine *e);
 int aero_flush(aero_engine *e);
 
-/* Soft bits delivered to AeroL (groups of 32, 0..255;
- * decode/oqpskdemodulator.cpp:534-540).  Needs AERO_F_TRACE_SOFT. */
+/* Soft bits delivered to AeroL (groups of 32 for OQPSK, 12 for MSK, 0..255;
+ * decode/oqpskdemodulator.cpp:534-540, decode/mskdemodulator.cpp:404-407).
+ * Needs AERO_F_TRACE_SOFT. */
 int aero_pop_softbits(aero_engine *e, int ch, int16_t *dst, size_t cap, size_t *n);
 
 /* ACARSItems emitted on ACARSsignal (or ACARSfragmentsignal with

@@ -1915,6 +1915,10 @@ void oracle_twiddles(int nfft, int inverse, double *dst) {
     dst[2 * i + 1] = t[i].imag();
   }
 }
+void oracle_msk_taps(int sps, double *dst) {
+  const double SamplesPerSymbol = sps;  // mskdemodulator.cpp:126-133
+  for (int i = 0; i < 2 * sps; i++) dst[i] = sin(M_PI * i / (2.0 * SamplesPerSymbol)) / (2.0 * SamplesPerSymbol);
+}
 void oracle_fft(double *x, int nfft, int inverse) {
   JFFT j;
   j.init(nfft);

@@ -67,6 +67,7 @@ void oracle_deinterleave_perm(int N, int *src_index_of_dst);
 void oracle_rrc_design(double alpha, int firsize, double fs, double symfreq, double *dst);
 void oracle_cis_table(double *dst); /* 19999 x (cos, sin) */
 void oracle_twiddles(int nfft, int inverse, double *dst);
+void oracle_msk_taps(int sps, double *dst); /* MskDemodulator matched filter, 2*sps taps */
 
 /* raw JFFT-order transform for the FFT parity test (in place, nfft complex) */
 void oracle_fft(double *x, int nfft, int inverse);

@@ -111,6 +111,7 @@ class Oracle:
             L.oracle_cis_table.argtypes = [ctypes.c_void_p]
             L.oracle_twiddles.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
             L.oracle_fft.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+            L.oracle_msk_taps.argtypes = [ctypes.c_int, ctypes.c_void_p]
             cls._lib = L
         return cls._lib
 

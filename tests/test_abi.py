@@ -66,3 +66,20 @@ def test_engine_tables_match_oracle(engine_lib, cpu_libs):
     assert n.value == 55
     for a, b in ((cis, ocis), (tw, otw), (twi, otwi), (taps, otaps)):
         assert np.array_equal(a.view(np.int64), b.view(np.int64))
+
+
+@pytest.mark.parametrize('sps', [20, 40])
+def test_engine_msk_tables_match_oracle(engine_lib, cpu_libs, sps):
+    """MSK group tables (8192-point twiddles, 2*sps-tap half-sine matched
+    filter, decode/mskdemodulator.cpp:126-133) == the oracle's."""
+    L = engine_lib
+    tw, twi, taps = np.zeros(2 * 8192), np.zeros(2 * 8192), np.zeros(2 * sps)
+    L.aero_host_msk_tables(ctypes.c_int(sps), tw.ctypes.data_as(ctypes.c_void_p), twi.ctypes.data_as(ctypes.c_void_p),
+                           taps.ctypes.data_as(ctypes.c_void_p))
+    O = tl.Oracle.lib()
+    otw, otwi, otaps = np.zeros_like(tw), np.zeros_like(twi), np.zeros_like(taps)
+    O.oracle_twiddles(8192, 0, otw.ctypes.data)
+    O.oracle_twiddles(8192, 1, otwi.ctypes.data)
+    O.oracle_msk_taps(sps, otaps.ctypes.data)
+    for a, b in ((tw, otw), (twi, otwi), (taps, otaps)):
+        assert np.array_equal(a.view(np.int64), b.view(np.int64))
