@@ -246,8 +246,10 @@ class Engine:
     def drain_items(self, lines=False, cap=4096):
         """Pops the items of every channel (aero_pop_items_all).  Returns the
         count, or (channel, canonical line) pairs with lines=True."""
-        arr = (AcarsItem * cap)()
-        chs = (ctypes.c_int * cap)()
+        if getattr(self, '_drain_cap', 0) != cap:
+            self._drain_buf = ((AcarsItem * cap)(), (ctypes.c_int * cap)())
+            self._drain_cap = cap
+        arr, chs = self._drain_buf
         total, out = 0, []
         while True:
             n = ctypes.c_size_t()

@@ -259,8 +259,11 @@ __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, in
   __shared__ uint8_t obits[HALF + 64];
   __shared__ uint8_t dl[HALF];
   __shared__ uint8_t info[320];
-  const int job = blockIdx.x;
-  if (job >= *S.njobs) return;
+  // grid-stride over the jobs of this pass (the job count stays on the device,
+  // so the host launches without waiting for the framing kernel)
+  const int njobs = *S.njobs;
+  for (int job = blockIdx.x; job < njobs; job += gridDim.x) {
+  __syncthreads();  // LDS of the previous job fully consumed
   const int lane = threadIdx.x;
   const int4 jd = reinterpret_cast<const int4 *>(S.jobs)[job];
   const int c = jd.x, buf = jd.y & 1, first = (jd.y >> 1) & 1, reset = (jd.y >> 2) & 1, clear = (jd.y >> 3) & 1;
@@ -419,6 +422,7 @@ __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, in
     o[2] = formatid;
     o[3] = c | (reset << 30);
   }
+  }  // job loop
 }
 
 void launch_frame(hipStream_t st, int mode, const DevState &S, int nch) {
@@ -431,8 +435,11 @@ void launch_frame(hipStream_t st, int mode, const DevState &S, int nch) {
     hipLaunchKernelGGL(frame_msk_kernel<MODE_MSK1200>, g, b, 0, st, S, nch);
 }
 
+// max_jobs: an upper bound of the pass's job count (the count itself is read
+// on the device); the grid is capped, blocks stride over the jobs
 void launch_viterbi(hipStream_t st, int mode, const DevState &S, const DevTables &T, int max_jobs, int trace) {
   if (max_jobs <= 0) return;
+  max_jobs = max_jobs < 16384 ? max_jobs : 16384;
   if (mode == MODE_OQPSK)
     hipLaunchKernelGGL((viterbi_kernel<BLOCK, DL2_LEN>), dim3(max_jobs), dim3(64), 0, st, S, T, trace);
   else if (mode == MODE_MSK600)

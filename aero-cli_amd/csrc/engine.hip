@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <chrono>
+#include <deque>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -210,7 +211,33 @@ struct Group {
   // scratch
   int16_t *d_scratch = nullptr;
   size_t scratch_cap = 0;
-  std::vector<uint8_t> h_jobout, h_dbg;
+  std::vector<uint8_t> h_dbg;
+  // Asynchronous frame hand-off.  A pass that demodulates writes its Viterbi
+  // job records into one of NSLOT device slots; the records and the job count
+  // go back by an async copy into pinned memory, and the host SU/ACARS work
+  // for them starts once that copy's event has completed, while the GPU runs
+  // on.  aero_run therefore never waits for the GPU.
+  struct JobSlot {
+    uint8_t *d_out = nullptr;   // [C][JOB_OUT] (device)
+    int *d_n = nullptr;         // job count (device)
+    uint8_t *h_out = nullptr;   // pinned copy of the first `copied` records
+    int *h_n = nullptr;         // pinned copy of the count
+    int copied = 0;
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+  };
+  static constexpr int NSLOT = 4;
+  JobSlot slot[NSLOT];
+  std::deque<int> pending_slots;
+  int next_slot = 0, max_jobs_seen = 0;
+  // pinned staging for host->device counters and PCM (reused once its event completed)
+  static constexpr int NPIN = 4;
+  long long *pin_avail[NPIN] = {};
+  hipEvent_t pin_ev[NPIN] = {};
+  int next_pin = 0;
+  int16_t *pin_pcm = nullptr;
+  size_t pin_pcm_cap = 0;
+  hipEvent_t pin_pcm_ev = nullptr;
   std::map<std::string, TimingSlot> timing;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending_ev;
   uint64_t processed = 0;
@@ -374,26 +401,30 @@ bool su_crc_ok(const uint8_t *su) {
   return calc == rec;
 }
 
-// Frame records of a pass -> host SU/ACARS work on the worker pool
-// (asynchronous; host_wait() joins it).
-int collect_after_pass(Group *e, int njobs) {
+// Host SU/ACARS work for one completed job slot, on the worker pool
+// (asynchronous; host_wait() joins it).  Slots are handled in launch order,
+// and the pool finishes one slot's work before it starts the next, so a
+// channel's frames keep their order.
+int process_slot(Group *e, int si) {
+  auto &sl = e->slot[si];
   const int C = e->C, nch = e->nch;
-  if (njobs <= 0) return AERO_OK;
-  e->h_jobout.resize((size_t)njobs * JOB_OUT);
-  HIPCHK(hipMemcpyAsync(e->h_jobout.data(), e->S.jobout, (size_t)njobs * JOB_OUT, hipMemcpyDeviceToHost, e->st));
+  const int njobs = *sl.h_n;
+  e->max_jobs_seen = std::max(e->max_jobs_seen, njobs);
+  HOST_TIMER(e, "host_frames");
+  e->hpool->wait();  // previous slot's frames first (per-channel order)
+  e->h_jobs_task.resize((size_t)std::max(njobs, 1) * JOB_OUT);
+  if (njobs > 0) memcpy(e->h_jobs_task.data(), sl.h_out, (size_t)std::min(njobs, sl.copied) * JOB_OUT);
+  if (njobs > sl.copied)  // more jobs than the async copy covered: the slot's device records are intact
+    HIPCHK(hipMemcpy(e->h_jobs_task.data() + (size_t)sl.copied * JOB_OUT, sl.d_out + (size_t)sl.copied * JOB_OUT,
+                     (size_t)(njobs - sl.copied) * JOB_OUT, hipMemcpyDeviceToHost));
+  sl.pending = false;
   const bool blocks = (e->flags & AERO_F_TRACE_BLOCKS) != 0;
   if (blocks) {
-    e->h_dbg.resize((size_t)2500 * C);
-    HIPCHK(hipMemcpyAsync(e->h_dbg.data(), e->S.blocks_dbg, e->h_dbg.size(), hipMemcpyDeviceToHost, e->st));
+    // traces run synchronously (run_group waited for this slot): blocks_dbg is this pass's
+    e->h_dbg_task.resize((size_t)2500 * C);
+    HIPCHK(hipMemcpy(e->h_dbg_task.data(), e->S.blocks_dbg, e->h_dbg_task.size(), hipMemcpyDeviceToHost));
   }
-  {
-    HOST_TIMER(e, "host_wait_jobs");
-    HIPCHK(hipStreamSynchronize(e->st));
-  }
-  HOST_TIMER(e, "host_frames");
-  e->hpool->wait();  // previous pass's frames first (per-channel order)
-  std::swap(e->h_jobs_task, e->h_jobout);
-  std::swap(e->h_dbg_task, e->h_dbg);
+  if (njobs <= 0) return AERO_OK;
   const bool msk = e->mode != MODE_OQPSK;
   // channels partitioned over workers (c % T): a channel's frames stay in
   // queue order and no two workers share state
@@ -449,6 +480,22 @@ int collect_after_pass(Group *e, int njobs) {
     }
   };
   e->hpool->submit(work, std::max(1, std::min(njobs / 64, nch)));
+  return AERO_OK;
+}
+
+// hands completed slots (all of them when `wait`) to the host workers, in order
+int poll_slots(Group *e, bool wait) {
+  while (!e->pending_slots.empty()) {
+    const int si = e->pending_slots.front();
+    if (wait) {
+      HOST_TIMER(e, "host_wait_jobs");
+      HIPCHK(hipEventSynchronize(e->slot[si].ev));
+    } else if (hipEventQuery(e->slot[si].ev) != hipSuccess) {
+      break;
+    }
+    e->pending_slots.pop_front();
+    if (int rc = process_slot(e, si)) return rc;
+  }
   return AERO_OK;
 }
 
@@ -512,6 +559,7 @@ int run_group(Group *e, int flush) {
   HIPCHK(hipSetDevice(e->device));
   HOST_TIMER(e, "host_run");
   if (int rc = flush_pending_init(e)) return rc;
+  if (int rc = poll_slots(e, false)) return rc;
   const int tflags = AERO_F_TRACE_PT | AERO_F_TRACE_BLOCKS | AERO_F_TRACE_SOFT | AERO_F_TRACE_HOPS;
   const bool trace = (e->flags & tflags) != 0;
   const long long HOPN = e->g.hop;
@@ -542,39 +590,53 @@ int run_group(Group *e, int flush) {
       launch_coarse(e->st, e->mode, e->S, e->T, e->nch);
       ev_end(e, b);
     }
-    if (progress) {
-      ev_begin(e, "demod", a, b);
-      if (e->mode == MODE_OQPSK)
-        launch_demod(e->st, e->S, e->T, e->nch, flush, (e->flags & AERO_F_TRACE_PT) != 0);
-      else
-        launch_demod_msk(e->st, e->mode, e->S, e->T, e->nch, flush);
-      ev_end(e, b);
-    }
-    HIPCHK(hipMemsetAsync(e->S.njobs, 0, sizeof(int), e->st));
-    ev_begin(e, "frame", a, b);
-    launch_frame(e->st, e->mode, e->S, e->nch);
+    if (!progress) continue;  // no new soft bits: framing has nothing to do
+    ev_begin(e, "demod", a, b);
+    if (e->mode == MODE_OQPSK)
+      launch_demod(e->st, e->S, e->T, e->nch, flush, (e->flags & AERO_F_TRACE_PT) != 0);
+    else
+      launch_demod_msk(e->st, e->mode, e->S, e->T, e->nch, flush);
     ev_end(e, b);
-    int njobs = 0;
-    HIPCHK(hipMemcpyAsync(&njobs, e->S.njobs, sizeof(int), hipMemcpyDeviceToHost, e->st));
-    {
-      HOST_TIMER(e, "host_wait_njobs");
-      HIPCHK(hipStreamSynchronize(e->st));
+    // framing + Viterbi into the next job slot (at most one job per channel per pass)
+    const int si = e->next_slot;
+    e->next_slot = (si + 1) % Group::NSLOT;
+    auto &sl = e->slot[si];
+    if (sl.pending) {  // four passes old: long done, hand it over first
+      if (int rc = poll_slots(e, true)) return rc;
     }
-    if (njobs > 0) {
-      ev_begin(e, "viterbi", a, b);
-      launch_viterbi(e->st, e->mode, e->S, e->T, njobs, (e->flags & AERO_F_TRACE_BLOCKS) ? 1 : 0);
-      ev_end(e, b);
-    }
+    DevState S2 = e->S;
+    S2.njobs = sl.d_n;
+    S2.jobout = sl.d_out;
+    HIPCHK(hipMemsetAsync(sl.d_n, 0, sizeof(int), e->st));
+    ev_begin(e, "frame", a, b);
+    launch_frame(e->st, e->mode, S2, e->nch);
+    ev_end(e, b);
+    ev_begin(e, "viterbi", a, b);
+    launch_viterbi(e->st, e->mode, S2, e->T, e->nch, (e->flags & AERO_F_TRACE_BLOCKS) ? 1 : 0);
+    ev_end(e, b);
     HIPCHK(hipGetLastError());
-    int rc = collect_after_pass(e, njobs);
-    if (rc) return rc;
-    if (trace) {
-      rc = collect_traces(e);
-      if (rc) return rc;
+    // async hand-off: the count plus the records the job count is likely to need
+    sl.copied = std::min(e->nch, e->max_jobs_seen + e->max_jobs_seen / 4 + 256);
+    HIPCHK(hipMemcpyAsync(sl.h_n, sl.d_n, sizeof(int), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipMemcpyAsync(sl.h_out, sl.d_out, (size_t)sl.copied * JOB_OUT, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipEventRecord(sl.ev, e->st));
+    sl.pending = true;
+    e->pending_slots.push_back(si);
+    if (trace) {  // parity traces: synchronous, pass by pass
+      if (int rc = poll_slots(e, true)) return rc;
+      if (int rc = collect_traces(e)) return rc;
     }
   }
+  return AERO_OK;
+}
+
+// waits for the group's GPU work and hands every completed slot over
+int drain_group(Group *e) {
+  HIPCHK(hipSetDevice(e->device));
   HIPCHK(hipStreamSynchronize(e->st));
-  ev_collect(e);
+  if (int rc = poll_slots(e, true)) return rc;
+  if (e->flags & (AERO_F_TRACE_PT | AERO_F_TRACE_SOFT | AERO_F_TRACE_HOPS))
+    if (int rc = collect_traces(e)) return rc;
   return AERO_OK;
 }
 
@@ -584,7 +646,19 @@ int run_impl(aero_engine *e, int flush) {
       int rc = run_group(g.get(), flush);
       if (rc) return rc;
     }
+  if (flush)  // aero_flush returns with every output of the pushed samples available
+    for (auto &g : e->groups)
+      if (g) {
+        int rc = drain_group(g.get());
+        if (rc) return rc;
+      }
   return AERO_OK;
+}
+
+// non-blocking: completed slots go to the host workers
+void poll_all(aero_engine *e) {
+  for (auto &g : e->groups)
+    if (g) (void)poll_slots(g.get(), false);
 }
 
 template <class T>
@@ -614,6 +688,18 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
   HIPCHK(hipMemset(e->pool, 0, bytes));
   layout(e->S, e->T, mode, e->C, e->flags, reinterpret_cast<char *>(e->pool));
   HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
+  for (auto &sl : e->slot) {
+    if (hipMalloc(&sl.d_out, (size_t)JOB_OUT * e->C) != hipSuccess) return AERO_E_NOMEM;
+    if (hipMalloc(&sl.d_n, 64) != hipSuccess) return AERO_E_NOMEM;
+    if (hipHostMalloc(&sl.h_out, (size_t)JOB_OUT * e->C) != hipSuccess) return AERO_E_NOMEM;
+    if (hipHostMalloc(&sl.h_n, 64) != hipSuccess) return AERO_E_NOMEM;
+    HIPCHK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+  }
+  for (int k = 0; k < Group::NPIN; k++) {
+    if (hipHostMalloc(&e->pin_avail[k], sizeof(long long) * e->C) != hipSuccess) return AERO_E_NOMEM;
+    HIPCHK(hipEventCreateWithFlags(&e->pin_ev[k], hipEventDisableTiming));
+  }
+  HIPCHK(hipEventCreateWithFlags(&e->pin_pcm_ev, hipEventDisableTiming));
   const int nfft = e->g.nfft;
   std::vector<double> cis(2 * WTSIZE), tw(2 * nfft), twi(2 * nfft), taps(128, 0.0);
   std::vector<uint8_t> scr(5000);
@@ -675,6 +761,19 @@ void group_destroy(Group *e) {
   if (!e) return;
   if (e->st) hipStreamSynchronize(e->st);
   ev_collect(e);
+  for (auto &sl : e->slot) {
+    if (sl.d_out) (void)hipFree(sl.d_out);
+    if (sl.d_n) (void)hipFree(sl.d_n);
+    if (sl.h_out) (void)hipHostFree(sl.h_out);
+    if (sl.h_n) (void)hipHostFree(sl.h_n);
+    if (sl.ev) (void)hipEventDestroy(sl.ev);
+  }
+  for (int k = 0; k < Group::NPIN; k++) {
+    if (e->pin_avail[k]) (void)hipHostFree(e->pin_avail[k]);
+    if (e->pin_ev[k]) (void)hipEventDestroy(e->pin_ev[k]);
+  }
+  if (e->pin_pcm) (void)hipHostFree(e->pin_pcm);
+  if (e->pin_pcm_ev) (void)hipEventDestroy(e->pin_pcm_ev);
   if (e->d_scratch) (void)hipFree(e->d_scratch);
   if (e->pool) (void)hipFree(e->pool);
   if (e->st) (void)hipStreamDestroy(e->st);
@@ -701,15 +800,28 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
   }
   const int16_t *dsrc = src;
   if (!dev) {
+    // the caller's buffer is copied before returning: into pinned staging
+    // (after the previous copy out of it has completed), then async to HBM
     const size_t need = n * ld;
+    HIPCHK(hipEventSynchronize(e->pin_pcm_ev));
     if (need > e->scratch_cap) {
       if (e->d_scratch) (void)hipFree(e->d_scratch);
       e->d_scratch = nullptr;
       e->scratch_cap = 0;
+      HIPCHK(hipStreamSynchronize(e->st));
       HIPCHK(hipMalloc(&e->d_scratch, need * sizeof(int16_t)));
       e->scratch_cap = need;
     }
-    HIPCHK(hipMemcpyAsync(e->d_scratch, src, need * sizeof(int16_t), hipMemcpyHostToDevice, e->st));
+    if (need > e->pin_pcm_cap) {
+      if (e->pin_pcm) (void)hipHostFree(e->pin_pcm);
+      e->pin_pcm = nullptr;
+      e->pin_pcm_cap = 0;
+      HIPCHK(hipHostMalloc(&e->pin_pcm, need * sizeof(int16_t)));
+      e->pin_pcm_cap = need;
+    }
+    memcpy(e->pin_pcm, src, need * sizeof(int16_t));
+    HIPCHK(hipMemcpyAsync(e->d_scratch, e->pin_pcm, need * sizeof(int16_t), hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipEventRecord(e->pin_pcm_ev, e->st));
     dsrc = e->d_scratch;
   }
   const long long start = e->avail[c0];
@@ -721,10 +833,14 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
                      dsrc, (long long)n, (long long)ld, nch, c0, start);
   HIPCHK(hipGetLastError());
   for (int j = 0; j < nch; j++) e->avail[c0 + j] += (long long)n;
-  // device copy of the counters
-  std::vector<long long> av(e->avail.begin() + c0, e->avail.begin() + c0 + nch);
-  HIPCHK(hipMemcpyAsync(e->S.ls + (size_t)LS_AVAIL * e->C + c0, av.data(), 8 * nch, hipMemcpyHostToDevice, e->st));
-  HIPCHK(hipStreamSynchronize(e->st));
+  // device copy of the counters, from pinned staging (stream-ordered before the next demod)
+  const int k = e->next_pin;
+  e->next_pin = (k + 1) % Group::NPIN;
+  HIPCHK(hipEventSynchronize(e->pin_ev[k]));
+  memcpy(e->pin_avail[k], e->avail.data() + c0, 8 * (size_t)nch);
+  HIPCHK(hipMemcpyAsync(e->S.ls + (size_t)LS_AVAIL * e->C + c0, e->pin_avail[k], 8 * nch, hipMemcpyHostToDevice,
+                        e->st));
+  HIPCHK(hipEventRecord(e->pin_ev[k], e->st));
   return AERO_OK;
 }
 
@@ -772,6 +888,8 @@ int aero_engine_create(const aero_engine_cfg *cfg, aero_engine **out) {
 void aero_engine_destroy(aero_engine *e) {
   if (!e) return;
   hipSetDevice(e->device);
+  for (auto &g : e->groups)
+    if (g) (void)drain_group(g.get());
   host_wait(e);
   for (auto &g : e->groups) group_destroy(g.get());
   delete e;
@@ -876,19 +994,21 @@ int aero_pop_items(aero_engine *e, int ch, aero_acars_item *dst, size_t cap, siz
   int c;
   Group *g = route(e, ch, c);
   if (!g) return AERO_E_INVALID;
+  poll_all(e);
   host_wait(e);
   return pop_vec(g->host[c]->items, dst, cap, n);
 }
 
 int aero_pop_items_all(aero_engine *e, aero_acars_item *dst, int *ch, size_t cap, size_t *n) {
   if (!e || (cap && (!dst || !ch))) return AERO_E_INVALID;
+  poll_all(e);
   host_wait(e);
   size_t k = 0;
   for (int gc = 0; gc < (int)e->chmap.size() && k < cap; gc++) {
     auto &v = e->groups[e->chmap[gc].first]->host[e->chmap[gc].second]->items;
     const size_t m = std::min(cap - k, v.size());
-    for (size_t i = 0; i < m; i++) {
-      dst[k + i] = v[i];
+    for (size_t i = 0; i < m; i++) {  // msg bytes past msg_len are left unspecified
+      memcpy(&dst[k + i], &v[i], offsetof(aero_acars_item, msg) + v[i].msg_len);
       ch[k + i] = gc;
     }
     v.erase(v.begin(), v.begin() + m);
@@ -972,7 +1092,10 @@ uint64_t aero_samples_processed(aero_engine *e) {
 int aero_sync(aero_engine *e) {
   if (!e) return AERO_E_INVALID;
   for (auto &g : e->groups)
-    if (g) HIPCHK(hipStreamSynchronize(g->st));
+    if (g) {
+      int rc = drain_group(g.get());
+      if (rc) return rc;
+    }
   host_wait(e);
   return AERO_OK;
 }

@@ -107,7 +107,12 @@ int aero_pop_items(aero_engine *e, int ch, aero_acars_item *dst, size_t cap, siz
 
 /* Items of every channel in one call (channel order, then emission order);
  * ch[i] receives item i's channel.  For hosts that serve many VFOs from one
- * engine: one call per aero_run instead of one per channel. */
+ * engine: one call per aero_run instead of one per channel.  Only the first
+ * msg_len bytes of each msg are written.
+ *
+ * aero_run is asynchronous: it enqueues the GPU work and returns.  The pop
+ * calls return what has completed so far (in order); aero_flush and
+ * aero_sync return only when every pushed sample's outputs are available. */
 int aero_pop_items_all(aero_engine *e, aero_acars_item *dst, int *ch, size_t cap, size_t *n);
 
 /* Diagnostics used by the parity tests and the bench.
