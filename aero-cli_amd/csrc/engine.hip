@@ -238,6 +238,16 @@ struct Group {
   int16_t *pin_pcm = nullptr;
   size_t pin_pcm_cap = 0;
   hipEvent_t pin_pcm_ev = nullptr;
+  // device-pointer pushes: the caller's buffer is copied (side stream, the
+  // host waits for that copy only) into one of two staging buffers, which the
+  // compute stream's scatter then reads; a buffer is refilled only after the
+  // scatter that read it has run
+  hipStream_t st_in = nullptr;
+  hipEvent_t ev_in = nullptr;
+  int16_t *d_stage[2] = {};
+  size_t stage_cap[2] = {};
+  hipEvent_t ev_stage_used[2] = {};
+  int next_stage = 0;
   std::map<std::string, TimingSlot> timing;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending_ev;
   uint64_t processed = 0;
@@ -700,6 +710,9 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
     HIPCHK(hipEventCreateWithFlags(&e->pin_ev[k], hipEventDisableTiming));
   }
   HIPCHK(hipEventCreateWithFlags(&e->pin_pcm_ev, hipEventDisableTiming));
+  HIPCHK(hipStreamCreateWithFlags(&e->st_in, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
+  for (auto &ev : e->ev_stage_used) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   const int nfft = e->g.nfft;
   std::vector<double> cis(2 * WTSIZE), tw(2 * nfft), twi(2 * nfft), taps(128, 0.0);
   std::vector<uint8_t> scr(5000);
@@ -774,6 +787,13 @@ void group_destroy(Group *e) {
   }
   if (e->pin_pcm) (void)hipHostFree(e->pin_pcm);
   if (e->pin_pcm_ev) (void)hipEventDestroy(e->pin_pcm_ev);
+  if (e->st_in) hipStreamSynchronize(e->st_in);
+  for (int b = 0; b < 2; b++) {
+    if (e->d_stage[b]) (void)hipFree(e->d_stage[b]);
+    if (e->ev_stage_used[b]) (void)hipEventDestroy(e->ev_stage_used[b]);
+  }
+  if (e->ev_in) (void)hipEventDestroy(e->ev_in);
+  if (e->st_in) (void)hipStreamDestroy(e->st_in);
   if (e->d_scratch) (void)hipFree(e->d_scratch);
   if (e->pool) (void)hipFree(e->pool);
   if (e->st) (void)hipStreamDestroy(e->st);
@@ -823,6 +843,24 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
     HIPCHK(hipMemcpyAsync(e->d_scratch, e->pin_pcm, need * sizeof(int16_t), hipMemcpyHostToDevice, e->st));
     HIPCHK(hipEventRecord(e->pin_pcm_ev, e->st));
     dsrc = e->d_scratch;
+  } else {
+    const size_t need = ((n - 1) * ld + nch) * sizeof(int16_t);
+    const int b = e->next_stage;
+    e->next_stage ^= 1;
+    if (need > e->stage_cap[b]) {
+      HIPCHK(hipStreamSynchronize(e->st));
+      if (e->d_stage[b]) (void)hipFree(e->d_stage[b]);
+      e->d_stage[b] = nullptr;
+      e->stage_cap[b] = 0;
+      HIPCHK(hipMalloc(&e->d_stage[b], need));
+      e->stage_cap[b] = need;
+    }
+    HIPCHK(hipStreamWaitEvent(e->st_in, e->ev_stage_used[b], 0));
+    HIPCHK(hipMemcpyAsync(e->d_stage[b], src, need, hipMemcpyDeviceToDevice, e->st_in));
+    HIPCHK(hipEventRecord(e->ev_in, e->st_in));
+    HIPCHK(hipEventSynchronize(e->ev_in));  // the caller's buffer is free again
+    dsrc = e->d_stage[b];
+    HIPCHK(hipStreamWaitEvent(e->st, e->ev_in, 0));
   }
   const long long start = e->avail[c0];
   for (int j = 1; j < nch; j++)
@@ -832,6 +870,7 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
   hipLaunchKernelGGL(pcm_scatter_kernel, dim3(grid), dim3(256), 0, e->st, e->S.pcm, e->C, (long long)PCM_CAP - 1,
                      dsrc, (long long)n, (long long)ld, nch, c0, start);
   HIPCHK(hipGetLastError());
+  if (dev) HIPCHK(hipEventRecord(e->ev_stage_used[e->next_stage ^ 1], e->st));
   for (int j = 0; j < nch; j++) e->avail[c0 + j] += (long long)n;
   // device copy of the counters, from pinned staging (stream-ordered before the next demod)
   const int k = e->next_pin;

@@ -27,9 +27,22 @@ for p in (os.path.join(ROOT, 'aero-cli_amd'), os.path.join(ROOT, 'tests')):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-HOP = 4096
-FS = 48000
-BYTES_PER_SAMPLE = 18.22   # 2 B int16 in + 16 B AGC ring r/w + 0.22 B soft bits out
+# per channel kind: hop (samples per step), input rate, SURVEY.md §8(d) algorithmic
+# bytes per input sample, synthetic carrier range, CPU-baseline signal seconds
+MODES = {
+    # 2 B int16 in + 16 B AGC ring r/w (192000-deep, cannot stay on chip) + 0.22 B soft bits out
+    'oqpsk10500': dict(bitrate=10500, hop=4096, fs=48000, bytes=18.22, kernel='demod_oqpsk_kernel', timing='demod',
+                       metric='Msamples/s demod+Viterbi, 10500bps OQPSK, 1/2/4/8 GPU; ACARS frames bit-exact vs ref',
+                       cpu_seconds=240.0, config='C2'),
+    # 2 B int16 in + 0.05 B soft bits out
+    'msk600': dict(bitrate=600, hop=2048, fs=12000, bytes=2.05, kernel='demod_msk_kernel<1>', timing='msk600_demod',
+                   metric='Msamples/s demod+Viterbi, 600bps MSK (C3); ACARS frames bit-exact vs ref',
+                   cpu_seconds=2400.0, config='C3'),
+    # 2 B int16 in + 0.025 B soft bits out (fb stays 600 at 24 kHz, decode/decode.cpp:142-150)
+    'msk1200': dict(bitrate=1200, hop=2048, fs=24000, bytes=2.025, kernel='demod_msk_kernel<2>',
+                    timing='msk1200_demod', metric='Msamples/s demod+Viterbi, 1200bps MSK; ACARS frames bit-exact vs ref',
+                    cpu_seconds=1200.0, config='C3 (1200 variant)'),
+}
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6    # MI355X vector FP64 (spec)
 
@@ -37,11 +50,14 @@ FP64_PEAK_TFLOPS = 78.6    # MI355X vector FP64 (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--mode', default='oqpsk10500', choices=sorted(MODES),
+                    help='channel kind (default: the BASELINE.json headline, C2 10500-bps OQPSK)')
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=48, help='hops before timing (hunter scan + lock)')
     ap.add_argument('--channels', type=int, default=65536, help='VFO channels per GPU (one lane each: 65536 fill the 1024 SIMDs at one wave each)')
     ap.add_argument('--pool', type=int, default=64, help='distinct synthetic streams per GPU')
-    ap.add_argument('--cpu-seconds', type=float, default=240.0, help='signal seconds per CPU-baseline process (~10 s CPU each)')
+    ap.add_argument('--cpu-seconds', type=float, default=None,
+                    help='signal seconds per CPU-baseline process (default per mode: ~5-10 s CPU each)')
     ap.add_argument('--cpu-procs', type=int, default=8)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'pmc_demod.json'),
@@ -49,43 +65,53 @@ def parse():
     return ap.parse_args()
 
 
-def make_pool(n_streams, length, seed0):
+def synth_one(M, seconds, seed, k=0, lead_in=0):
+    import aero_testlib as tl
+    if M['bitrate'] == 10500:
+        # SURVEY.md §8(d): seed 0xAE20+k, carrier 12000 + 37.5 + 0.5 k Hz, Eb/N0 12 dB
+        return tl.synth(seconds=seconds, seed=seed, carrier=12037.5 + 0.5 * (k % 64), ebn0=12.0, phase0=0.1 * k,
+                        lead_in=lead_in)
+    # MSK: carriers inside the first coarse-search window (mixer centre 0 Hz, +-450 Hz)
+    return tl.synth_msk(seconds=seconds, bitrate=M['bitrate'], baud=600, seed=seed, carrier=300.0 + 2.0 * (k % 64),
+                        ebn0=12.0, phase0=0.1 * k, lead_in=lead_in)
+
+
+def make_pool(M, n_streams, length, seed0):
     import aero_testlib as tl
     tl.build_cpu_only() if not os.path.exists(tl.SYNTH_SO) else None
 
     def one(k):
-        # SURVEY.md §8(d): seed 0xAE20+k, carrier 12000 + 37.5 + 0.5 k Hz, Eb/N0 12 dB
-        return tl.synth(seconds=length / FS, seed=seed0 + k, carrier=12037.5 + 0.5 * (k % 64), ebn0=12.0,
-                        phase0=0.1 * k, lead_in=0)
+        return synth_one(M, length / M['fs'], seed0 + k, k)
     with cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as ex:
         return np.stack(list(ex.map(one, range(n_streams))))
 
 
-def cpu_baseline(seconds, procs):
+def cpu_baseline(M, seconds, procs):
     """The oracle (CPU port of the reference path) on host cores, one process
     per channel as aero-decode is deployed (one VFO per process); bounded
     sample: each process decodes `seconds` of its own synthetic stream."""
     import multiprocessing as mp
     ctx = mp.get_context('fork')
     with ctx.Pool(procs) as p:
-        res = p.map(_cpu_one, [(seconds, 0xBE00 + k) for k in range(procs)])
+        res = p.map(_cpu_one, [(M, seconds, 0xBE00 + k) for k in range(procs)])
     total = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     cpu = sum(r[1] for r in res)
     return {'value': round(total / wall / 1e6, 4), 'unit': 'Msamples/s', 'cores': procs, 'kind': 'port',
-            'sample': '%d processes x %.0f s of synthetic 10500-bps P-channel (48 kHz int16) through '
+            'sample': '%d processes x %.0f s of synthetic %d-bps P-channel (%d Hz int16) through '
                       'oracle/liboracle.so (demod + coarse + hunter + AeroL + Viterbi + ACARS), '
-                      '12000-sample messages; %.1f s CPU total' % (procs, seconds, cpu),
+                      '%d-sample messages; %.1f s CPU total' % (procs, seconds, M['bitrate'], M['fs'], M['fs'] // 4,
+                                                             cpu),
             'per_core_msps': round(total / cpu / 1e6, 4)}
 
 
 def _cpu_one(arg):
-    seconds, seed = arg
+    M, seconds, seed = arg
     import aero_testlib as tl
-    pcm = tl.synth(seconds=seconds, seed=seed, carrier=12037.5, ebn0=12.0)
-    o = tl.Oracle()
+    pcm = synth_one(M, seconds, seed, lead_in=1000)
+    o = tl.Oracle(bitrate=M['bitrate'])
     t = time.perf_counter()
-    o.push_chunked(pcm, 12000)
+    o.push_chunked(pcm, M['fs'] // 4)
     return len(pcm), time.perf_counter() - t
 
 
@@ -95,15 +121,17 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
     import shard
+    M = MODES[a.mode]
+    HOP, FS = M['hop'], M['fs']
     C, P = a.channels, a.pool
     steps_total = a.warmup + a.steps
     span = steps_total * HOP
     offsets = shard.channel_offsets(C, P, rank)
-    pool_host = make_pool(P, span + int(offsets.max()) + 1, 0xAE20 + 1000 * rank)
+    pool_host = make_pool(M, P, span + int(offsets.max()) + 1, 0xAE20 + 1000 * rank)
     # CPU baseline first, in worker processes forked before this process touches the GPU
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(a.cpu_seconds, a.cpu_procs)
+        cpu = cpu_baseline(M, a.cpu_seconds or M['cpu_seconds'], a.cpu_procs)
 
     import torch
     import torch.distributed as dist
@@ -120,7 +148,7 @@ def main():
 
     eng = ae.Engine(max_channels=C, device=local, flags=ae.F_TIMING)
     for _ in range(C):
-        eng.open_channel(10500, FS)
+        eng.open_channel(M['bitrate'], FS)
     # warmup: hunter scan, AFC and lock (untimed)
     for s in range(a.warmup):
         x = step_input(s)
@@ -155,32 +183,35 @@ def main():
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed, samples = float(tmax[0]), float(t[1])
-    kt = {k: eng.timing(k) for k in ('demod', 'coarse', 'frame', 'viterbi')}
+    pre = M['timing'][:-len('demod')]
+    kt = {k: eng.timing(pre + k) for k in ('demod', 'coarse', 'frame', 'viterbi')}
     ht = {k: eng.timing(k) for k in ('host_push', 'host_run', 'host_wait_njobs', 'host_wait_jobs', 'host_frames')}
     if rank == 0:
         value = samples / elapsed / 1e6
         dm_ms, dm_n = kt['demod']
         per_launch_s = dm_ms / 1e3 / max(dm_n, 1)
         samples_per_launch = C * HOP
-        achieved = BYTES_PER_SAMPLE * samples_per_launch / per_launch_s / 1e9
+        achieved = M['bytes'] * samples_per_launch / per_launch_s / 1e9
         traffic = None
-        if os.path.exists(a.pmc):
+        if a.mode == 'oqpsk10500' and os.path.exists(a.pmc):
             try:
                 traffic = json.load(open(a.pmc)).get('hbm_bytes_per_launch')
             except Exception:
                 traffic = None
         out = {
-            'metric': 'Msamples/s demod+Viterbi, 10500bps OQPSK, 1/2/4/8 GPU; ACARS frames bit-exact vs ref',
+            'metric': M['metric'],
             'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world, 'steps': a.steps,
             'warmup': a.warmup, 'ms_per_step': round(elapsed / a.steps * 1e3, 3), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
-            'config': {'workload': 'C2 x %d: independent single-VFO 10500-bps continuous OQPSK P-channels '
-                                   'per GPU, 48 kHz int16, one 4096-sample hop per step' % C,
+            'config': {'workload': '%s x %d: independent single-VFO %d-bps continuous %s P-channels '
+                                   'per GPU, %d Hz int16, one %d-sample hop per step' % (
+                                       M['config'], C, M['bitrate'], 'OQPSK' if M['bitrate'] == 10500 else 'MSK',
+                                       FS, HOP),
                        'channels_per_gpu': C, 'total_channels': C * world, 'hop_samples': HOP,
                        'parallelism': 'channel-sharded x%d' % world},
-            'roofline': {'bound': 'hbm', 'kernel': 'demod_oqpsk_kernel', 'achieved': round(achieved, 2),
+            'roofline': {'bound': 'hbm', 'kernel': M['kernel'], 'achieved': round(achieved, 2),
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
-                         'traffic': traffic, 'bytes_per_sample': BYTES_PER_SAMPLE,
+                         'traffic': traffic, 'bytes_per_sample': M['bytes'],
                          'avg_launch_ms': round(per_launch_s * 1e3, 3)},
             'kernel_ms_per_step': {k: round(v[0] / max(a.steps, 1), 3) for k, v in kt.items()},
             'acars_items': items,
