@@ -1037,6 +1037,201 @@ struct Parser {
   }
 };
 
+/* ------------------------------------------------- R/T channels (burst) */
+// RISUItem / RISUData (decode/aerol.h:125-135, decode/aerol.cpp:8-119)
+struct RISUItem : ISUItem {
+  int SEQINDICATOR = 0, SUTYPE = 0, filledarray = 0;
+  void clear() {
+    ISUItem::clear();
+    SEQINDICATOR = SUTYPE = filledarray = 0;
+  }
+};
+struct RISUData {
+  std::vector<RISUItem> isuitems;
+  RISUItem anisuitem, lastvalidisuitem;
+  int find(const RISUItem &a) {
+    if (a.SUTYPE > 11) return -1;
+    if (a.SUTYPE < 1) return -1;
+    for (size_t i = 0; i < isuitems.size(); i++)
+      if (a.GESID == isuitems[i].GESID && a.AESID == isuitems[i].AESID && a.QNO == isuitems[i].QNO &&
+          a.REFNO == isuitems[i].REFNO)
+        return (int)i;
+    return -1;
+  }
+  bool update(const std::string &data) {
+    for (size_t i = 0; i < isuitems.size(); i++) {  // deleteoldisuitems
+      isuitems[i].count++;
+      if (isuitems[i].count > 10) {
+        isuitems.erase(isuitems.begin() + i);
+        i--;
+      }
+    }
+    int byte1 = (uint8_t)data[0], byte2 = (uint8_t)data[1], byte3 = (uint8_t)data[2];
+    int byte4 = (uint8_t)data[3], byte5 = (uint8_t)data[4], byte6 = (uint8_t)data[5];
+    anisuitem.clear();
+    anisuitem.SEQINDICATOR = ((byte1 & 0xF0) >> 4);
+    anisuitem.SUTYPE = byte1 & 0x0F;
+    anisuitem.QNO = ((byte2 & 0xF0) >> 4);
+    anisuitem.REFNO = byte2 & 0x07;
+    anisuitem.AESID = byte3 << 16 | byte4 << 8 | byte5;
+    anisuitem.GESID = byte6;
+    int idx = find(anisuitem);
+    if (idx < 0) {
+      isuitems.push_back(anisuitem);
+      idx = (int)isuitems.size() - 1;
+    }
+    RISUItem *p = &isuitems[idx];
+    p->count = 0;
+    int SUTotal = 0, SUindex = 0;
+    switch (anisuitem.SEQINDICATOR) {
+      case 1: SUTotal = 1; SUindex = 0; break;
+      case 2: SUTotal = 2; SUindex = 0; break;
+      case 3: SUTotal = 2; SUindex = 1; break;
+      case 4: SUTotal = 3; SUindex = 0; break;
+      case 5: SUTotal = 3; SUindex = 1; break;
+      case 6: SUTotal = 3; SUindex = 2; break;
+      default: break;
+    }
+    int BytesInSU = 0;
+    if ((anisuitem.SUTYPE >= 1) && (anisuitem.SUTYPE <= 11)) BytesInSU = anisuitem.SUTYPE;
+    bool SignalingInfoSU = anisuitem.SUTYPE == 15;
+    int thisnum = 11 * SUTotal - 11 + BytesInSU;
+    if (thisnum > 0) {
+      if (p->userdata.size() == 0) p->userdata.resize(thisnum);
+      if (thisnum < (int)p->userdata.size()) p->userdata.resize(thisnum);
+    }
+    if (!SignalingInfoSU) {
+      for (int i = 0 - 1 + 7; i < BytesInSU - 1 + 7; i++) {
+        // Qt5 QByteRef grows the array on an out-of-range write (zero-filled here)
+        const size_t at = (size_t)(i + 11 * SUindex + 1 - 7);
+        if (at >= p->userdata.size()) p->userdata.resize(at + 1, '\0');
+        p->userdata[at] = data[i];
+      }
+      p->filledarray |= (1 << SUindex);
+    } else
+      p->userdata.clear();
+    if ((SignalingInfoSU) || ((p->filledarray == 7) && (SUTotal == 3)) ||
+        ((p->filledarray == 3) && (SUTotal == 2)) || ((p->filledarray == 1) && (SUTotal == 1))) {
+      lastvalidisuitem = *p;
+      isuitems.erase(isuitems.begin() + idx);
+      return true;
+    }
+    return false;
+  }
+};
+
+// AeroLcrc16::calcusingbitsandcheck (decode/aerol.h:273-307)
+bool crc_bits_check(const int *bits, int numberofbits) {
+  uint16_t crc_rec = 0;
+  for (int i = numberofbits - 1; i >= numberofbits - 16; i--) {
+    crc_rec <<= 1;
+    crc_rec |= bits[i];
+  }
+  numberofbits -= 16;
+  uint16_t crc = 0xFFFF;
+  for (int i = 0; i < numberofbits; i++) {
+    int crc_bit = crc & 1;
+    crc >>= 1;
+    if (crc_bit ^ bits[i]) crc = crc ^ 0x8408;
+  }
+  crc = ~crc;
+  return crc_rec == crc;
+}
+
+// RTChannelDeleaveFECScram, OQPSK update() (decode/aerol.h:548-612, 755-836):
+// after 320 soft bits and every 192 after, deinterleave (64 x blockptr/64),
+// Viterbi-decode the whole block (Decode_soft, jconvolutionalcodec.cpp:88-119),
+// descramble and test the R packet (19-byte CRC) or the T packet (6-byte
+// header CRC + every 12-byte SU CRC)
+struct RTChannel {
+  enum { OK_R = 3, OK_T = 5, Bad = 0, Test_Failed = 32, Nothing = 8, FULL = 16 };
+  std::vector<int> block = std::vector<int>(64 * 95, 0);
+  int blockptr = 0, lastpacketstate = Nothing, numberofsus = 0;
+  std::vector<int> deconvol;
+  std::string infofield;
+  std::vector<int> *pre_state = nullptr;
+  std::vector<uint8_t> *tests_out = nullptr;    // trace: per test (blockptr, result)
+  std::vector<uint8_t> *packets_out = nullptr;  // trace: per OK packet (kind, len, infofield)
+  int resetblockptr() {
+    blockptr = 0;
+    if (lastpacketstate == Test_Failed) {
+      lastpacketstate = Nothing;
+      return Bad;
+    }
+    lastpacketstate = Nothing;
+    return Nothing;
+  }
+  void packintobytes() {
+    infofield.clear();
+    int charptr = 0;
+    uint8_t ch = 0;
+    for (size_t h = 0; h < deconvol.size(); h++) {
+      ch |= deconvol[h] * 128;
+      charptr++;
+      charptr %= 8;
+      if (charptr == 0) {
+        infofield += (char)ch;
+        ch = 0;
+      } else
+        ch >>= 1;
+    }
+  }
+  int test() {
+    const int cols = blockptr / 64;
+    std::vector<uint8_t> del(blockptr);
+    int k = 0;
+    for (int j = 0; j < cols; j++)
+      for (int i = 0; i < 64; i++) del[k++] = (uint8_t)block[((i * 27) % 64) * cols + j];
+    std::vector<uint8_t> decoded(blockptr / 2 + 1, 0);
+    viterbi().decode_soft(del.data(), blockptr, decoded.data());
+    const int dbits = blockptr / 2;
+    deconvol.assign(dbits, 0);
+    for (int b = 0; b < dbits; b++) deconvol[b] = (decoded[b / 8] >> (7 - (b % 8))) & 1;
+    for (int b = 0; b < dbits; b++) deconvol[b] ^= (*pre_state)[b];  // scrambler reset + update
+    if (blockptr == 64 * 5) {
+      if (!crc_bits_check(deconvol.data(), 8 * 19)) return lastpacketstate = Test_Failed;
+      packintobytes();
+      blockptr = (int)block.size();
+      return lastpacketstate = OK_R;
+    }
+    if (!crc_bits_check(deconvol.data(), 8 * 6)) {
+      if (blockptr >= (int)block.size()) return lastpacketstate = Bad;
+      return lastpacketstate = Test_Failed;
+    }
+    numberofsus = 1 + (blockptr - (64 * 5)) / (64 * 3);
+    for (int i = 0; i < numberofsus; i++) {
+      if (!crc_bits_check(deconvol.data() + (8 * 6) + (8 * 12) * i, 8 * 12)) {
+        if (blockptr >= (int)block.size()) return lastpacketstate = Bad;
+        return lastpacketstate = Test_Failed;
+      }
+    }
+    packintobytes();
+    infofield.pop_back();  // chop(1)
+    blockptr = (int)block.size();
+    return lastpacketstate = OK_T;
+  }
+  int update(int bit) {
+    if (blockptr >= (int)block.size()) return FULL;
+    block[blockptr] = bit;
+    blockptr++;
+    if (((blockptr - (64 * 5)) % (64 * 3)) == 0) {
+      const int at = blockptr;
+      const int r = test();
+      if (tests_out) {
+        const uint32_t rec[2] = {(uint32_t)at, (uint32_t)r};
+        tests_out->insert(tests_out->end(), (const uint8_t *)rec, (const uint8_t *)rec + 8);
+      }
+      if (packets_out && (r == OK_R || r == OK_T)) {
+        const uint32_t rec[2] = {(uint32_t)(r == OK_R ? 'R' : 'T'), (uint32_t)infofield.size()};
+        packets_out->insert(packets_out->end(), (const uint8_t *)rec, (const uint8_t *)rec + 8);
+        packets_out->insert(packets_out->end(), infofield.begin(), infofield.end());
+      }
+      return r;
+    }
+    return Nothing;
+  }
+};
+
 /* ------------------------------------------------------- AeroL P-channel */
 struct AeroL {
   // AeroL::setSettings(fb, burstmode=false) (decode/aerol.cpp:960-1039):
@@ -1064,6 +1259,10 @@ struct AeroL {
   std::string infofield;
   ISUData isudata;
   Parser parser;
+  // burst mode (AeroL::setSettings(10500, true), aerol.cpp:966-971,1031-1038)
+  bool burstmode = false;
+  RTChannel rt;
+  RISUData risudata;
   // outputs
   std::vector<uint8_t> *blocks_out = nullptr, *frames_out = nullptr;
 
@@ -1085,6 +1284,40 @@ struct AeroL {
     }
     block.assign(leaverN * 64, 0);
     pre_state = scrambler_table();
+    rt.pre_state = &pre_state;
+  }
+  void setBurst() {  // 10500 burst: UW tolerance 4, a burst lasts at most 1 s of bits
+    burstmode = true;
+    uw_imag.tollerence = 4;
+    uw_real.tollerence = 4;
+    TotalNumberOfBits = 10500;
+  }
+
+  // R / T packet results (decode/aerol.cpp:1240-1460; only what emits items)
+  void rt_result(int result) {
+    if (result == RTChannel::OK_R) {
+      const std::string &inf = rt.infofield;
+      if ((((uint8_t)inf[1]) & 0x08) == 0x08) {  // User_data_ISU_SSU_R_channel
+        if (risudata.update(inf.substr(0, 17))) {
+          parser.downlink = burstmode;
+          parser.parse(risudata.lastvalidisuitem);
+        }
+      }
+    } else if (result == RTChannel::OK_T) {
+      const std::string &inf = rt.infofield;
+      for (int k = 0; k < rt.numberofsus; k++) {
+        int message = (uint8_t)inf[6 + k * 12];
+        if ((message & 0xC0) == 0xC0) message = -1;
+        if (message == 0x71) {
+          isudata.update(inf.substr(6 + k * 12, 10));
+        } else if (message == -1) {
+          if (isudata.update(inf.substr(6 + k * 12, 10))) {
+            parser.downlink = burstmode;
+            parser.parse(isudata.lastvalidisuitem);
+          }
+        }
+      }
+    }
   }
 
   std::vector<int> decode_continuous(const std::vector<uint8_t> &deleaved) {
@@ -1279,6 +1512,11 @@ struct AeroL {
             gotsync_last = false;
           }
         }
+        // 10500 burst: the UW must follow the start-of-packet marker by
+        // about 80 bits (aerol.cpp:1123-1129)
+        if (gotsync && burstmode) {
+          if (abs(muw - 80) > 150) gotsync = false;
+        }
         if ((realimag && uw_imag.inverted) || (!realimag && uw_real.inverted)) {
           bit = 1 - bit;
           if (soft_bit > 128)
@@ -1292,6 +1530,14 @@ struct AeroL {
         if (cntr == 0) {
           frameinfo = bit;
           infofield.clear();
+          if (burstmode) {  // R/T: no header, dummy one (aerol.cpp:1217-1229)
+            formatid = 1;
+            supfrmaker = 0;
+            framecounter1 = 0;
+            framecounter2 = 0;
+            cntr = 16;
+            rt.resetblockptr();
+          }
         } else {
           frameinfo <<= 1;
           frameinfo |= bit;
@@ -1306,7 +1552,9 @@ struct AeroL {
         framecounter1 = (frameinfo >> 4) & 0x000F;
         framecounter2 = (frameinfo >> 0) & 0x000F;
       }
-      if (cntr >= 16) {
+      if (cntr >= 16 && burstmode) {
+        rt_result(rt.update(soft_bit));
+      } else if (cntr >= 16) {
         if (cntr == 16) blockcnt = -1;
         int idx = (cntr - BitsInHeader) % (int)block.size();
         if (idx < 0) idx = 0;
@@ -1349,7 +1597,7 @@ struct AeroL {
         }
       }
       if (gotsync) {
-        if (cntr + 1 != TotalNumberOfBits) isudata.reset();
+        if (!burstmode && cntr + 1 != TotalNumberOfBits) isudata.reset();
         cntr = -1;
         datacd = true;
         datacdcountdown = 12;
@@ -1358,6 +1606,12 @@ struct AeroL {
       if (cntr + 1 == TotalNumberOfBits) {
         scr_pos = 0;
         cntr = -1;
+        if (burstmode) {  // end of the burst window: stop this call (aerol.cpp:2018-2029)
+          cntr = 1000000000;
+          datacd = false;
+          datacdcountdown = 0;
+          return;
+        }
       }
     }
   }
@@ -1811,6 +2065,502 @@ struct Msk {
   }
 };
 
+/* ------------------------------------------- burst OQPSK demodulator */
+// TMovingAverage<std::complex<double>> (decode/DSP.h:159-213)
+struct TMovingAverageC {
+  int MASz = 10, MAPtr = 0;
+  cpx MASum = 0, Val = 0;
+  std::vector<cpx> buf;
+  void setLength(int n) {
+    MASz = n;
+    MASum = 0;
+    buf.assign(n, cpx(0, 0));
+    MAPtr = 0;
+    Val = 0;
+  }
+  cpx UpdateSigned(cpx sig) {
+    MASum = MASum - buf[MAPtr];
+    MASum = MASum + (sig);
+    buf[MAPtr] = (sig);
+    MAPtr++;
+    MAPtr %= MASz;
+    Val = MASum / ((double)MASz);
+    return Val;
+  }
+};
+
+// Delay<std::complex<double>> (decode/DSP.h:355-390)
+struct DelayC {
+  std::vector<cpx> buff;
+  int buffptr = 0;
+  double fractdelay = 1;
+  void setdelay(double fd) {
+    fractdelay = fd;
+    int buffsize = (int)std::ceil(fractdelay) + 1;
+    buff.assign(buffsize, cpx(0, 0));
+    buffptr = 0;
+  }
+  cpx update(cpx sig) {
+    buff[buffptr] = sig;
+    double dptr = ((double)buffptr) - fractdelay;
+    buffptr++;
+    buffptr %= (int)buff.size();
+    while (std::floor(dptr) < 0) dptr += ((double)buff.size());
+    int iptr = (int)std::floor(dptr);
+    double weighting = dptr - ((double)iptr);
+    cpx older = buff[iptr];
+    iptr++;
+    iptr %= (int)buff.size();
+    cpx newer = buff[iptr];
+    return (weighting * newer + (1.0 - weighting) * older);
+  }
+};
+
+// DelayThing<T> (decode/DSP.h:446-486)
+template <class T>
+struct DelayThingT {
+  std::vector<T> buffer;
+  int buffer_ptr = 0, buffer_sz = 0;
+  DelayThingT() { setLength(12); }
+  void setLength(int length) {  // QVector::resize keeps the (zero) contents
+    length++;
+    buffer.resize(length, T(0));
+    buffer_ptr = 0;
+    buffer_sz = (int)buffer.size();
+  }
+  void update(T &data) {
+    buffer[buffer_ptr] = data;
+    buffer_ptr++;
+    buffer_ptr %= buffer_sz;
+    data = buffer[buffer_ptr];
+  }
+  T update_dont_touch(T data) {
+    buffer[buffer_ptr] = data;
+    buffer_ptr++;
+    buffer_ptr %= buffer_sz;
+    return buffer[buffer_ptr];
+  }
+  int findmaxpos(T &maxval) {
+    int maxpos = 0;
+    maxval = buffer[buffer_ptr];
+    for (int i = 0; i < buffer_sz; i++) {
+      if (buffer[buffer_ptr] > maxval) {
+        maxval = buffer[buffer_ptr];
+        maxpos = i;
+      }
+      buffer_ptr++;
+      buffer_ptr %= buffer_sz;
+    }
+    return maxpos;
+  }
+};
+
+// PeakDetector (decode/DSP.h:491-566)
+struct PeakDetector {
+  DelayThingT<double> d1, d2, d3;
+  double lastdy = 0, threshold = 0.25, maxval = 0;
+  int cntdown = 0, maxcntdown = 0, maxpos = 0, maxposcntdown = -1;
+  void setSettings(int length, double _threshold) {
+    d1.setLength(length * 2);
+    d2.setLength(length);
+    lastdy = 0;
+    maxcntdown = 2 * length;
+    cntdown = maxcntdown;
+    threshold = _threshold;
+    maxposcntdown = -1;
+    d3.setLength(2 * length);
+  }
+  PeakDetector() { setSettings((int)(9.14 * 128.0 / 2.0), 0.25); }
+  bool update(double &val) {
+    double val2 = d3.update_dont_touch(val);
+    double dy = val - d1.update_dont_touch(val);
+    d2.update(val);
+    if ((!cntdown) && (val > threshold) && ((lastdy >= 0 && dy < 0))) {
+      cntdown = maxcntdown;
+      maxval = 0;
+      maxpos = d3.findmaxpos(maxval);
+      maxposcntdown = maxpos;
+    }
+    if (cntdown > 0) cntdown--;
+    lastdy = dy;
+    val = val2;
+    if (!maxposcntdown) {
+      maxposcntdown--;
+      return true;
+    }
+    if (maxposcntdown > 0) maxposcntdown--;
+    return false;
+  }
+};
+
+// QJHilbertFilter on JFastFir (decode/DSP.cpp:730-761, decode/jfft.cpp:322-374,
+// 445-495): 2048-tap analytic-signal kernel, overlap-add in 8192-point blocks
+struct HilbertFir {
+  JFFT fft;
+  std::vector<cpx> kernel, sigspace, remainder;
+  int nfft = 0, sigspace_ptr = 0, signal_non_zero_size = 0, remainder_size = 0;
+  HilbertFir() {
+    const int N = 2048;
+    std::vector<cpx> k;
+    for (int i = 0; i < N; i++) {
+      if (i == N / 2) {
+        k.push_back(cpx(-1, 0));
+        continue;
+      }
+      if ((i % 2) == 0) {
+        k.push_back(cpx(0, 0));
+        continue;
+      }
+      k.push_back(cpx(0, (2.0 / ((double)N)) / (std::tan(M_PI * (((double)i) / ((double)N) - 0.5)))));
+    }
+    const int kernel_non_zero_size = N;
+    nfft = 1;
+    while (nfft < 4 * kernel_non_zero_size) nfft <<= 1;
+    kernel = k;
+    kernel.resize(nfft, cpx(0, 0));
+    sigspace.assign(nfft, cpx(0, 0));
+    sigspace_ptr = 0;
+    signal_non_zero_size = nfft + 1 - kernel_non_zero_size;
+    remainder_size = nfft - signal_non_zero_size;
+    remainder.assign(remainder_size, cpx(0, 0));
+    fft.init(nfft);
+    fft.fft(kernel.data(), false);
+  }
+  cpx update(cpx in_val) {
+    if (sigspace_ptr >= signal_non_zero_size) {
+      fft.fft(sigspace.data(), false);
+      for (int k = 0; k < nfft; ++k) sigspace[k] *= kernel[k];
+      fft.fft(sigspace.data(), true);
+      for (int k = 0; k < remainder_size; ++k) {
+        sigspace[k] += remainder[k];
+        remainder[k] = sigspace[signal_non_zero_size + k];
+        sigspace[signal_non_zero_size + k] = 0;
+      }
+      sigspace_ptr = 0;
+    }
+    cpx out_val = sigspace[sigspace_ptr];
+    sigspace[sigspace_ptr] = in_val;
+    sigspace_ptr++;
+    return out_val;
+  }
+};
+
+// FFTrWrapper<double>(32768) -> JFFT::fft_real on a 16384-point complex FFT
+// (decode/fftrwrapper.cpp:13-36, decode/jfft.cpp:54-90), kissfft scaling on
+struct FFTr {
+  JFFT fft;
+  int nfft = 0;  // complex size
+  std::vector<cpx> DA, DB;
+  explicit FFTr(int N) {
+    nfft = N / 2;
+    fft.init(nfft);
+    cpx imag = cpx(0, 1);
+    DA.resize(nfft);
+    DB.resize(nfft);
+    for (int i = 0; i < nfft; i++) {
+      DA[i] = 0.5 * (1.0 - imag * std::exp(-2.0 * imag * M_PI * ((double)i) / ((double)(2 * nfft))));
+      DB[i] = 0.5 * (1.0 + imag * std::exp(-2.0 * imag * M_PI * ((double)i) / ((double)(2 * nfft))));
+    }
+  }
+  void transform(const std::vector<double> &real, std::vector<cpx> &out) {
+    const int NpN = nfft << 1;
+    std::vector<cpx> F(nfft);
+    for (int i = 0; i < nfft; ++i) F[i] = cpx(real[2 * i], real[2 * i + 1]);
+    fft.fft(F.data(), false);
+    out.assign(NpN, cpx(0, 0));
+    out[0] = F[0] * DA[0] + DB[0] * std::conj(F[0]);
+    out[nfft] = F[0] * DB[0] + DA[0] * std::conj(F[0]);
+    for (int i = 1; i < nfft; ++i) {
+      out[i] = F[i] * DA[i] + DB[i] * std::conj(F[(nfft - i)]);
+      out[NpN - i] = std::conj(out[i]);
+    }
+    for (int i = NpN / 2 + 1; i < NpN; i++) out[i] = 0;  // kissfft_scaling
+  }
+};
+
+// BurstOqpskDemodulator (decode/burstoqpskdemodulator.cpp:5-703) as Decoder
+// configures it (decode/decode.cpp:131-136: default Settings, zmqAudio, AFC
+// on, CPUReduce off; the hunter is disabled for burst, decode.cpp:175).
+// OQPSKEbNoMeasure, the spectrum and scatter buffers are output-dead (their
+// signals are unconnected) and not run.  rotator_freq, never initialised by
+// the reference before the first trident detection, is 0.
+struct BurstOqpsk {
+  const double Fs = 48000, fb = 10500, lockingbw = 10500, signalthreshold = 0.6;
+  const double SamplesPerSymbol = 2.0 * 48000.0 / 10500.0;
+  const cpx imag = cpx(0, 1);
+  double mse = 100;
+  bool insertpreamble = false;
+  WaveTable mixer2, st_osc, st_osc_ref, st_osc_quarter;
+  AGC agc, agc2;
+  HilbertFir hfir;
+  DelayC bt_d1;
+  Delay bt_ma_diff;
+  TMovingAverageC bt_ma1;
+  MovingAverage mav1{1170};
+  PeakDetector pdet;
+  DelayThingT<cpx> d1;
+  DelayThingT<double> d2;
+  std::vector<double> tridentbuffer;
+  int tridentbuffer_ptr = 0, tridentbuffer_sz = 0;
+  FFTr fftr{4096 * 4 * 2};
+  FIR fir_re, fir_im;
+  Delay delays, delayt41, delayt42, delayt8, a1;
+  IIR st_iir_resonator;
+  double ee = 0.4;
+  cpx symboltone_averotator = 1, rotator = 1, symboltone_rotator = 1, pt_d = 0, sig2_last = 0;
+  double rotator_freq = 0;
+  MovingAverage msema{128};
+  int startstopstart = 0, yui = 0, startstop = -1, cntr = 0;
+  double vol_gain = 1;
+  std::vector<short> RxDataBits;
+  AeroL aerol{10500};
+  long long nsamples = 0;
+  std::vector<uint8_t> soft_out;  // delivered soft bits (marker as 0xFF00 is lost: see soft16)
+  std::vector<int16_t> soft16;
+  std::vector<double> hops, pts;  // hops: per trident check (sample, detected, carrier Hz, gain, maxval, bin)
+  bool trace_pt = false;
+
+  BurstOqpsk() {
+    trig();
+    aerol.setBurst();
+    mixer2.SetFreq(8000, 48000);  // setSettings: freq_center 8000 (burstoqpskdemodulator.h:33)
+    st_osc.SetFreq(fb, (int)Fs);
+    st_osc_ref.SetFreq(fb, (int)Fs);
+    st_osc_quarter.SetFreq(fb / 4.0, (int)Fs);
+    agc.init(1, Fs);
+    agc2.init(SamplesPerSymbol * 64.0 / Fs, Fs);
+    bt_d1.setdelay(1.0 * SamplesPerSymbol);
+    bt_ma1.setLength(qRound(128.0 * SamplesPerSymbol));
+    mav1 = MovingAverage((int)(SamplesPerSymbol * 128));
+    bt_ma_diff.setdelay(SamplesPerSymbol * 128);
+    d1.setLength((int)(SamplesPerSymbol * 128.0 * 2.5 - 190));
+    tridentbuffer_sz = qRound((256.0 + 16.0 + 16.0) * SamplesPerSymbol);
+    tridentbuffer.assign(tridentbuffer_sz, 0.0);
+    tridentbuffer_ptr = 0;
+    d2.setLength(tridentbuffer_sz);
+    pdet.setSettings((int)(SamplesPerSymbol * 128.0 / 2.0), 0.2);
+    a1.setdelay(SamplesPerSymbol / 2.0);
+    startstopstart = SamplesPerSymbol * (1050);
+    std::vector<double> rrc = rrc_design(1, 55, Fs, fb / 2.0);
+    fir_re.init(rrc);
+    fir_im.init(rrc);
+    delays.setdelay(1);
+    delayt41.setdelay(SamplesPerSymbol / 4.0);
+    delayt42.setdelay(SamplesPerSymbol / 4.0);
+    delayt8.setdelay(SamplesPerSymbol / 8.0);
+    st_iir_resonator.b[0] = 0.0048847995518126464;
+    st_iir_resonator.b[1] = 0;
+    st_iir_resonator.b[2] = -0.0048847995518126464;
+    st_iir_resonator.a[0] = 1;
+    st_iir_resonator.a[1] = -0.3882746897971619;
+    st_iir_resonator.a[2] = 0.99023040089637471;
+    st_iir_resonator.init();
+  }
+
+  void trident_check() {  // burstoqpskdemodulator.cpp:343-440
+    const int L = qRound(128.0 * SamplesPerSymbol);
+    std::vector<double> in(32768, 0.0);
+    std::vector<cpx> out_base, out_top;
+    for (int k = 0; k < L; k++) in[k] = tridentbuffer[k];
+    fftr.transform(in, out_base);
+    std::fill(in.begin(), in.end(), 0.0);
+    for (int k = 0; k < L; k++) in[k] = tridentbuffer[L + k];
+    fftr.transform(in, out_top);
+    const int NB = (int)out_base.size();
+    std::vector<double> out_abs_diff(NB / 2);
+    for (int i = 0; i < NB / 2; i++) out_abs_diff[i] = (std::abs(out_top[i]) - std::abs(out_base[i]));
+    double hzperbin = Fs / ((double)NB);
+    double binpeakspacing = (0.25 * fb) / hzperbin;
+    int b = qRound(binpeakspacing);
+    int firstbin = b, lstbin = NB / 2 - b;
+    double maxval = out_abs_diff[firstbin - b] + out_abs_diff[firstbin + b] - out_abs_diff[firstbin];
+    double maxvalbin = firstbin;
+    for (int i = firstbin; i < lstbin; i++) {
+      double testval = out_abs_diff[i - b] + out_abs_diff[i + b] - out_abs_diff[i];
+      if (testval > maxval) {
+        maxval = testval;
+        maxvalbin = i;
+      }
+    }
+    double minval = std::abs(out_base[0]);
+    double minvalbin = 0;
+    for (int i = 0; i < NB / 2; i++) {
+      if ((std::abs(out_base[i])) > minval) {
+        minval = std::abs(out_base[i]);
+        minvalbin = i;
+      }
+    }
+    const bool det = (maxval > 500.0) && (fabs((((double)(maxvalbin - minvalbin))) * hzperbin) < 20.0);
+    if (det) {
+      double carrierphase = std::arg(out_base[(int)minvalbin]) - (M_PI / 4.0);
+      mixer2.SetFreq(hzperbin * minvalbin);
+      mixer2.SetPhaseDeg((180.0 / M_PI) * carrierphase);
+      vol_gain = 1.4142 * 500.0 / minval;
+      st_osc.SetFreq(st_osc_ref.GetFreqHz());
+      st_osc.SetPhaseDeg(0);
+      st_osc_ref.SetPhaseDeg(0);
+      st_iir_resonator.init();
+      startstop = startstopstart;
+      cntr = 0;
+      rotator = 1;
+      insertpreamble = true;
+      rotator_freq = 0;
+      symboltone_averotator = 1;
+      mse = 0;
+      msema = MovingAverage(128);
+    }
+    hops.push_back((double)nsamples);
+    hops.push_back(det ? 1.0 : 0.0);
+    hops.push_back(mixer2.GetFreqHz());
+    hops.push_back(vol_gain);
+    hops.push_back(maxval);
+    hops.push_back(minvalbin);
+  }
+
+  void emit(const std::vector<short> &bits) {
+    for (short v : bits) {
+      soft16.push_back(v);
+      if (v >= 0) soft_out.push_back((uint8_t)v);
+    }
+    aerol.decode(bits.data(), (int)bits.size());
+  }
+
+  void writeData(const short *ptr, int n) {  // writeDataSlot (:262-703), one call per message
+    const double lastmse = mse;
+    for (int i = 0; i < n; i++, ptr++, nsamples++) {
+      cpx cval = hfir.update(cpx(((double)(*ptr)) / 32768.0, 0));
+      agc.Update(std::abs(cval));
+      cval *= agc.AGCVal;
+      cpx cval_d = d1.update_dont_touch(cval);
+      double val_to_demod = (d2.update_dont_touch(std::real(cval_d)));
+      double fastarm = std::abs(bt_ma1.UpdateSigned(cval * std::conj(bt_d1.update(cval))));
+      fastarm = mav1.UpdateSigned(fastarm);
+      fastarm -= bt_ma_diff.update(fastarm);
+      if (fastarm < 0) fastarm = 0;
+      double bt_sig = fastarm * fastarm;
+      if (bt_sig > 500) bt_sig = 500;
+      if (pdet.update(bt_sig)) tridentbuffer_ptr = 0;
+      if (tridentbuffer_ptr < tridentbuffer_sz) {
+        tridentbuffer[tridentbuffer_ptr] = std::real(cval_d);
+        tridentbuffer_ptr++;
+      } else if (tridentbuffer_ptr == tridentbuffer_sz) {
+        tridentbuffer_ptr++;
+        trident_check();
+      }
+      cpx cval_dd = mixer2.WTCISValue() * (vol_gain * val_to_demod);
+      cpx sig2 = cpx(fir_re.FIRUpdateAndProcess(cval_dd.real()), fir_im.FIRUpdateAndProcess(cval_dd.imag()));
+      if (startstop > 0) {
+        startstop--;
+        if (cntr < 1000000) cntr++;
+        if (mse < 0.75) startstop = startstopstart;
+      }
+      if (startstop == 0) startstop--;
+      if ((cntr > ((256 - 10) * SamplesPerSymbol)) && insertpreamble) {
+        RxDataBits.push_back(-1);
+        insertpreamble = false;
+      }
+      if ((cntr > SamplesPerSymbol * (128 + 10)) && (cntr < ((256 - 10) * SamplesPerSymbol))) {
+        double progress = (((double)cntr) - (SamplesPerSymbol * (128 + 10))) /
+                          (((256 - 10) * SamplesPerSymbol) - (SamplesPerSymbol * (128 + 10)));
+        cpx symboltone_pt = sig2 * symboltone_rotator * imag;
+        double er = std::tanh(symboltone_pt.imag()) * (symboltone_pt.real());
+        symboltone_rotator = symboltone_rotator * std::exp(imag * er * 0.01);
+        symboltone_averotator = symboltone_averotator * 0.95 + 0.05 * symboltone_rotator;
+        symboltone_pt = cpx((symboltone_pt.real()), a1.update(symboltone_pt.real()));
+        double st_err = std::arg((st_osc_quarter.WTCISValue()) * std::conj(symboltone_pt));
+        st_err *= 1.5 * (1.0 - progress * progress);
+        st_osc_quarter.AdvanceFractionOfWave(-(1.0 / (2.0 * M_PI)) * st_err * 0.1);
+        st_osc.SetPhaseDeg((360.0 * st_osc_quarter.WTptr / ((double)WTSIZE)) * 4.0 + (360.0 * ee));
+      }
+      sig2 *= symboltone_averotator;
+      rotator = rotator * std::exp(imag * rotator_freq);
+      sig2 *= rotator;
+      double sig2abs = std::abs(sig2);
+      sig2 *= agc2.Update(sig2abs);
+      double abval = std::abs(sig2);
+      if (abval > 2.84) sig2 = (2.84 / abval) * sig2;
+      double st_diff = delays.update(abval * abval) - (abval * abval);
+      double st_d1out = delayt41.update(st_diff);
+      double st_d2out = delayt42.update(st_d1out);
+      double st_eta = (st_d2out - st_diff) * st_d1out;
+      st_iir_resonator.update(st_eta);
+      if (cntr > SamplesPerSymbol * (128 + 128)) st_eta = st_iir_resonator.y;
+      cpx st_m1 = cpx(st_eta, -delayt8.update(st_eta));
+      cpx st_out = st_osc.WTCISValue() * st_m1;
+      double st_angle_error = std::arg(st_out);
+      if (cntr > SamplesPerSymbol * (128 + 64)) {
+        st_osc.IncreseFreqHz(-st_angle_error * 0.00000001);
+        st_osc.AdvanceFractionOfWave(-st_angle_error * 0.01 / 360.0);
+      }
+      if (st_osc.GetFreqHz() < (st_osc_ref.GetFreqHz() - 0.1)) st_osc.SetFreq((st_osc_ref.GetFreqHz() - 0.1));
+      if (st_osc.GetFreqHz() > (st_osc_ref.GetFreqHz() + 0.1)) st_osc.SetFreq((st_osc_ref.GetFreqHz() + 0.1));
+      if (st_osc.IfHavePassedPoint(ee)) {
+        double pt_last = st_osc.FractionOfSampleItPassesBy;
+        double pt_this = 1.0 - pt_last;
+        cpx pt = pt_this * sig2 + pt_last * sig2_last;
+        double twospeed =
+            -4.0 * ((std::fmod((360.0 * st_osc_quarter.WTptr / ((double)WTSIZE)) * 2.0 + (360.0 * ee * 0.5), 360.0) /
+                     360.0) -
+                    (0.34046 + 0.4111 * ee));
+        bool even = true;
+        if (twospeed < 0) even = false;
+        yui++;
+        yui %= 2;
+        if (cntr < ((128 + 128) * SamplesPerSymbol)) {
+          if ((even && yui == 1) || (!even && yui == 0)) {
+            yui++;
+            yui %= 2;
+          }
+        }
+        if (!yui)
+          pt_d = pt;
+        else {
+          cpx pt_qpsk = cpx(pt.real(), pt_d.imag());
+          double ct_xt = tanh(pt.imag()) * pt.real();
+          double ct_xt_d = tanh(pt_d.real()) * pt_d.imag();
+          double ct_ec = ct_xt_d - ct_xt;
+          if (ct_ec > M_PI) ct_ec = M_PI;
+          if (ct_ec < -M_PI) ct_ec = -M_PI;
+          if (ct_ec > M_PI_2) ct_ec = M_PI_2;
+          if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
+          if (cntr > ((128 + 10) * SamplesPerSymbol)) {
+            rotator = rotator * std::exp(imag * ct_ec * 0.1);
+            if (cntr > ((128 + 10) * SamplesPerSymbol)) rotator_freq = rotator_freq + ct_ec * 0.0001;
+          }
+          if (trace_pt) {
+            pts.push_back(pt_qpsk.real());
+            pts.push_back(pt_qpsk.imag());
+          }
+          if (cntr > ((128 + 10) * SamplesPerSymbol)) {
+            double tda = (fabs(pt_qpsk.real()) - 1.0);
+            double tdb = (fabs(pt_qpsk.imag()) - 1.0);
+            mse = msema.Update((tda * tda) + (tdb * tdb));
+          }
+          if (startstop > 0) {
+            int ibit = qRound(0.75 * pt_qpsk.imag() * 127.0 + 128.0);
+            if (ibit > 255) ibit = 255;
+            if (ibit < 0) ibit = 0;
+            RxDataBits.push_back((short)(uint8_t)ibit);
+            ibit = qRound(0.75 * pt_qpsk.real() * 127.0 + 128.0);
+            if (ibit > 255) ibit = 255;
+            if (ibit < 0) ibit = 0;
+            RxDataBits.push_back((short)(uint8_t)ibit);
+            if (RxDataBits.size() >= 32) {
+              if (mse < signalthreshold || lastmse < signalthreshold) emit(RxDataBits);
+              RxDataBits.clear();
+            }
+          }
+        }
+      }
+      sig2_last = sig2;
+      mixer2.WTnextFrame();
+      st_osc.WTnextFrame();
+      st_osc_ref.WTnextFrame();
+      st_osc_quarter.WTnextFrame();
+    }
+  }
+};
+
 template <class T>
 size_t copy_out(const std::vector<T> &v, T *dst, size_t cap) {
   size_t n = std::min(cap, v.size());
@@ -1823,12 +2573,13 @@ size_t copy_out(const std::vector<T> &v, T *dst, size_t cap) {
 struct oracle_chan {
   std::unique_ptr<Oqpsk> oq;
   std::unique_ptr<Msk> msk;
-  std::vector<uint8_t> blocks, frames;
+  std::unique_ptr<BurstOqpsk> bq;
+  std::vector<uint8_t> blocks, frames, rt_tests, rt_packets;
   std::string items;
-  AeroL &aerol() { return oq ? oq->aerol : msk->aerol; }
-  const std::vector<uint8_t> &soft() const { return oq ? oq->soft_out : msk->soft_out; }
-  const std::vector<double> &hops() const { return oq ? oq->hops : msk->hops; }
-  const std::vector<double> &pts() const { return oq ? oq->pts : msk->pts; }
+  AeroL &aerol() { return oq ? oq->aerol : (msk ? msk->aerol : bq->aerol); }
+  const std::vector<uint8_t> &soft() const { return oq ? oq->soft_out : (msk ? msk->soft_out : bq->soft_out); }
+  const std::vector<double> &hops() const { return oq ? oq->hops : (msk ? msk->hops : bq->hops); }
+  const std::vector<double> &pts() const { return oq ? oq->pts : (msk ? msk->pts : bq->pts); }
 };
 
 extern "C" {
@@ -1837,7 +2588,16 @@ oracle_chan *oracle_create(int bitrate, int flags) {
   if (bitrate != 10500 && bitrate != 600 && bitrate != 1200) return nullptr;
   oracle_chan *c = new oracle_chan();
   const bool tp = (flags & ORACLE_TRACE_PT) != 0;
-  if (bitrate == 10500) {
+  if (flags & ORACLE_BURST) {
+    if (bitrate != 10500) {
+      delete c;
+      return nullptr;
+    }
+    c->bq.reset(new BurstOqpsk());
+    c->bq->trace_pt = tp;
+    c->bq->aerol.rt.tests_out = &c->rt_tests;
+    c->bq->aerol.rt.packets_out = &c->rt_packets;
+  } else if (bitrate == 10500) {
     c->oq.reset(new Oqpsk());
     c->oq->trace_pt = tp;
   } else {
@@ -1854,10 +2614,18 @@ int oracle_push(oracle_chan *c, const int16_t *pcm, size_t n) {
   if (!n) return 0;
   if (c->oq)
     c->oq->writeData(pcm, (int)n);
-  else
+  else if (c->msk)
     c->msk->writeData(pcm, (int)n);
+  else
+    c->bq->writeData(pcm, (int)n);
   return 0;
 }
+size_t oracle_softbits16(const oracle_chan *c, int16_t *dst, size_t cap) {
+  static const std::vector<int16_t> none;
+  return copy_out(c->bq ? c->bq->soft16 : none, dst, cap);
+}
+size_t oracle_rt_tests(const oracle_chan *c, uint8_t *dst, size_t cap) { return copy_out(c->rt_tests, dst, cap); }
+size_t oracle_rt_packets(const oracle_chan *c, uint8_t *dst, size_t cap) { return copy_out(c->rt_packets, dst, cap); }
 size_t oracle_softbits(const oracle_chan *c, uint8_t *dst, size_t cap) {
   return copy_out(c->soft(), dst, cap);
 }

@@ -26,6 +26,7 @@ typedef struct oracle_chan oracle_chan;
 
 /* flags */
 #define ORACLE_TRACE_PT 1 /* record every rotated pt_qpsk (re,im) */
+#define ORACLE_BURST 2    /* burst mode (aero-decode --burst; 10500 only) */
 
 oracle_chan *oracle_create(int bitrate, int flags);
 void oracle_destroy(oracle_chan *c);
@@ -36,6 +37,12 @@ int oracle_push(oracle_chan *c, const int16_t *pcm, size_t n);
 
 /* Soft bits delivered to AeroL (groups of 32, decode/oqpskdemodulator.cpp:534-540). */
 size_t oracle_softbits(const oracle_chan *c, uint8_t *dst, size_t cap);
+/* burst: delivered soft bits including the -1 start-of-packet markers */
+size_t oracle_softbits16(const oracle_chan *c, int16_t *dst, size_t cap);
+/* burst: every R/T test (uint32 blockptr, uint32 result code) in order */
+size_t oracle_rt_tests(const oracle_chan *c, uint8_t *dst, size_t cap);
+/* burst: per decoded R/T packet: uint32 kind ('R'/'T'), uint32 length, infofield bytes */
+size_t oracle_rt_packets(const oracle_chan *c, uint8_t *dst, size_t cap);
 
 /* Per coarse-estimate hop, 6 doubles: sample index, freq_offset_est emitted,
  * mixer2 freq, mixer_center freq (after the slot ran), mse, signal flag. */

@@ -80,6 +80,32 @@ def synth_msk(seconds=10.0, bitrate=600, seed=0xAE40, carrier=1800.0, ebn0=12.0,
     return pcm
 
 
+def synth_burst(seconds=10.0, seed=0xAE50, carrier=12000.0, ebn0=14.0, amplitude=0.25, phase0=0.3, lead_in=24000,
+                return_packets=False):
+    """int16 48 kHz PCM of 10500-bps burst OQPSK R/T packets (SURVEY.md §8(d)
+    C4 input) + the transmitted packets [(kind 'R'/'T', bytes)]."""
+    global _synth
+    if _synth is None:
+        _synth = ctypes.CDLL(SYNTH_SO)
+    _synth.aero_synth_burst.restype = ctypes.c_size_t
+    n = int(48000 * seconds)
+    pcm = np.zeros(n, dtype=np.int16)
+    cap = int(seconds + 4) * 400
+    buf = np.zeros(cap, dtype=np.uint8)
+    npk = ctypes.c_size_t()
+    cfg = SynthCfg(48000.0, carrier, phase0, amplitude, ebn0, seed, 0.6, lead_in)
+    used = _synth.aero_synth_burst(ctypes.byref(cfg), pcm.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n),
+                                   buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(cap), ctypes.byref(npk))
+    if not return_packets:
+        return pcm
+    pk, i = [], 0
+    while i < used:
+        kind, ln = np.frombuffer(buf[i:i + 8].tobytes(), np.uint32)
+        pk.append((chr(kind), bytes(buf[i + 8:i + 8 + ln])))
+        i += 8 + int(ln)
+    return pcm, pk
+
+
 class Oracle:
     """One reference channel (a whole `aero-decode -b <bitrate>` instance)."""
     _lib = None
@@ -112,13 +138,16 @@ class Oracle:
             L.oracle_twiddles.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
             L.oracle_fft.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
             L.oracle_msk_taps.argtypes = [ctypes.c_int, ctypes.c_void_p]
+            for f in ('oracle_softbits16', 'oracle_rt_tests', 'oracle_rt_packets'):
+                getattr(L, f).restype = ctypes.c_size_t
+                getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
             cls._lib = L
         return cls._lib
 
-    def __init__(self, trace_pt=False, bitrate=10500):
+    def __init__(self, trace_pt=False, bitrate=10500, burst=False):
         self.L = self.lib()
         self.bitrate = bitrate
-        self.h = self.L.oracle_create(bitrate, 1 if trace_pt else 0)
+        self.h = self.L.oracle_create(bitrate, (1 if trace_pt else 0) | (2 if burst else 0))
         assert self.h, 'oracle_create(%d) failed' % bitrate
 
     def __del__(self):
@@ -142,6 +171,19 @@ class Oracle:
 
     def softbits(self):
         return self._get(self.L.oracle_softbits, np.uint8)
+
+    def softbits16(self):
+        """burst: delivered soft bits with the -1 start-of-packet markers"""
+        return self._get(self.L.oracle_softbits16, np.int16)
+
+    def rt_tests(self):
+        """burst: (blockptr, result code) of every R/T test"""
+        return self._get(self.L.oracle_rt_tests, np.uint32).reshape(-1, 2)
+
+    def rt_packets(self):
+        """burst: [(kind 'R'/'T', infofield bytes)] of every decoded R/T packet"""
+        raw = self._get(self.L.oracle_rt_packets, np.uint8)
+        return parse_rt_packets(raw)
 
     def hops(self):
         return self._get(self.L.oracle_hops, np.float64, 6)
@@ -171,4 +213,14 @@ def frame_records(raw):
         L = int(np.frombuffer(r[312:316].tobytes(), np.uint32)[0])
         m = int(np.frombuffer(r[316:320].tobytes(), np.uint32)[0])
         out.append((bytes(r[:L]), m))
+    return out
+
+
+def parse_rt_packets(raw):
+    raw = np.asarray(raw, dtype=np.uint8)
+    out, i = [], 0
+    while i < len(raw):
+        kind, ln = np.frombuffer(raw[i:i + 8].tobytes(), np.uint32)
+        out.append((chr(kind), bytes(raw[i + 8:i + 8 + int(ln)])))
+        i += 8 + int(ln)
     return out

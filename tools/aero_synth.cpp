@@ -19,6 +19,7 @@
  * Not part of the product path: tests/ and bench.py use it to make inputs.
  */
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -413,4 +414,235 @@ extern "C" size_t aero_synth_msk(const aero_synth_cfg *cfg, int bitrate, int bau
     pcm[n] = (int16_t)v;
   }
   return nframes;
+}
+
+/* ------------------------------------------------------------------ bursts
+ * 10500-bps burst OQPSK (R / T channels, aero-decode --burst): per burst
+ * 128 symbols of unmodulated carrier, 128 symbols of symbol tone, the UW on
+ * both arms, then one R or T packet (decode/aerol.h:755-836 inverted):
+ *   R: 17 bytes (RISU user-data SU, decode/aerol.cpp:32-119) + CRC = 152 bits
+ *   T: 4-byte header + CRC, then S >= 2 SUs of 10 bytes + CRC (0x71 ISU + SSUs)
+ * -> LSB-first bits, scrambled from 0, zero-padded to blockptr/2 - 6 bits, six
+ * zero flush bits, K=7 {109,79} encoding (libcorrect, decode/jconvolutionalcodec.cpp:88-119)
+ * -> 64 x (blockptr/64) interleaver, blockptr = 320 + 192 (S - 1).
+ * Bursts are 1-3 s apart.  packets[] receives, per
+ * burst, 2 x uint32 (kind 'R'/'T', byte count) + the packet bytes (<= 392). */
+namespace {
+struct BurstTx {
+  Tx tx;
+  unsigned risu_ref = 0;
+  explicit BurstTx(const aero_synth_cfg &c) : tx(c) {}
+
+  std::vector<uint8_t> acars_ud(unsigned aes, int maxtext) {
+    char reg[8];
+    snprintf(reg, sizeof reg, ".N%05u", (unsigned)(aes % 100000));
+    static const char *labels[] = {"H1", "SA", "_d", "Q0", "B6", "10", "5Z", "AA"};
+    const char *label = labels[tx.rng.below(8)];
+    std::string text = tx.rand_text(1 + tx.rng.below(maxtext));
+    std::vector<uint8_t> ud = {0xFF, 0xFF, odd(0x01), odd('2')};
+    for (int i = 0; i < 7; i++) ud.push_back(odd(i < (int)strlen(reg) ? reg[i] : '.'));
+    ud.push_back(odd(0x15));
+    ud.push_back(odd(label[0]));
+    ud.push_back(odd(label[1]));
+    ud.push_back(odd((uint8_t)('A' + tx.rng.below(26))));
+    ud.push_back(odd(0x02));
+    for (char ch : text) ud.push_back(odd((uint8_t)ch));
+    ud.push_back(0x83);
+    ud.push_back((uint8_t)tx.rng.below(256));
+    ud.push_back((uint8_t)tx.rng.below(256));
+    ud.push_back(0x7F);
+    return ud;
+  }
+
+  // queued packets (bytes incl. CRCs) + kind
+  std::vector<std::pair<char, std::vector<uint8_t>>> pending;
+
+  void refill() {
+    unsigned aes = tx.aes_pool[tx.rng.below(8)];
+    uint8_t ges = (uint8_t)(0x80 + tx.rng.below(8));
+    const double u = tx.rng.uniform();
+    if (u < 0.35) {
+      // a one-SU R user-data packet (SEQINDICATOR 1): too short for ACARS,
+      // ParserISU reports it as a non-ACARS item (decode/aerol.cpp:471-488)
+      uint8_t b[19] = {0};
+      const int nb = 1 + tx.rng.below(11);
+      b[0] = (uint8_t)((1 << 4) | nb);
+      b[1] = (uint8_t)((tx.rng.below(16) << 4) | 0x08 | (risu_ref++ & 7));
+      b[2] = (uint8_t)(aes >> 16);
+      b[3] = (uint8_t)(aes >> 8);
+      b[4] = (uint8_t)aes;
+      b[5] = ges;
+      for (int i = 0; i < 11; i++) b[6 + i] = (uint8_t)tx.rng.below(256);
+      const uint16_t c = crc16(b, 17);
+      b[17] = c & 0xFF;
+      b[18] = c >> 8;
+      pending.push_back({'R', std::vector<uint8_t>(b, b + 19)});
+    } else if (u < 0.55) {
+      // one ACARS message over three R bursts: SEQINDICATOR 4/5/6, 11 + 11 + r bytes
+      std::vector<uint8_t> ud = acars_ud(aes, 13);
+      while (ud.size() < 23) ud.insert(ud.end() - 4, odd('X'));  // keep the third SU non-empty
+      const int r = (int)ud.size() - 22;
+      const uint8_t qno = (uint8_t)tx.rng.below(16), ref = (uint8_t)(risu_ref++ & 7);
+      for (int k = 0; k < 3; k++) {
+        const int nb = k < 2 ? 11 : r;
+        uint8_t b[19] = {0};
+        b[0] = (uint8_t)(((4 + k) << 4) | nb);
+        b[1] = (uint8_t)((qno << 4) | 0x08 | ref);
+        b[2] = (uint8_t)(aes >> 16);
+        b[3] = (uint8_t)(aes >> 8);
+        b[4] = (uint8_t)aes;
+        b[5] = ges;
+        for (int i = 0; i < 11; i++) b[6 + i] = i < nb ? ud[11 * k + i] : (uint8_t)tx.rng.below(256);
+        const uint16_t c = crc16(b, 17);
+        b[17] = c & 0xFF;
+        b[18] = c >> 8;
+        pending.push_back({'R', std::vector<uint8_t>(b, b + 19)});
+      }
+    } else {
+      // T packet: header + 0x71 ISU + SSUs (ISUData, decode/aerol.cpp:158-227)
+      std::vector<uint8_t> ud = acars_ud(aes, 40);
+      tx.queue.clear();
+      // reuse the P-channel ISU/SSU builder on this message's user data
+      const int rest = (int)ud.size() - 2;
+      const int m = (rest + 7) / 8;
+      const int r = rest - 8 * (m - 1);
+      const uint8_t qno = (uint8_t)tx.rng.below(16), ref = (uint8_t)(tx.refno++ & 0x0F);
+      std::vector<uint8_t> pkt;
+      uint8_t hdr[4] = {(uint8_t)(aes >> 16), (uint8_t)(aes >> 8), (uint8_t)aes, ges};
+      pkt.insert(pkt.end(), hdr, hdr + 4);
+      uint16_t c = crc16(hdr, 4);
+      pkt.push_back(c & 0xFF);
+      pkt.push_back(c >> 8);
+      uint8_t isu[10] = {0x71, (uint8_t)(aes >> 16), (uint8_t)(aes >> 8), (uint8_t)aes, ges,
+                         (uint8_t)((qno << 4) | ref), (uint8_t)(m & 0x3F), (uint8_t)(r << 4), ud[0], ud[1]};
+      SU s = make_su(isu);
+      pkt.insert(pkt.end(), s.b, s.b + 12);
+      size_t p = 2;
+      for (int q = m - 1; q >= 0; q--) {
+        uint8_t ssu[10] = {(uint8_t)(0xC0 | q), (uint8_t)((qno << 4) | ref), 0, 0, 0, 0, 0, 0, 0, 0};
+        const int nb = q == 0 ? r : 8;
+        for (int i = 0; i < nb; i++) ssu[2 + i] = ud[p++];
+        for (int i = nb; i < 8; i++) ssu[2 + i] = (uint8_t)tx.rng.below(256);
+        s = make_su(ssu);
+        pkt.insert(pkt.end(), s.b, s.b + 12);
+      }
+      pending.push_back({'T', pkt});
+    }
+  }
+
+  // channel bits of the next burst's packet part (after the UW)
+  std::vector<int> next_packet(char &kind, std::vector<uint8_t> &bytes) {
+    if (pending.empty()) refill();
+    kind = pending.front().first;
+    bytes = pending.front().second;
+    pending.erase(pending.begin());
+    const int nbytes = (int)bytes.size();
+    const int S = kind == 'T' ? (nbytes - 6) / 12 : 1;
+    const int blockptr = kind == 'R' ? 320 : 320 + 192 * (S - 1);
+    const int dbits = blockptr / 2;
+    std::vector<int> in(dbits, 0);
+    for (int h = 0; h < 8 * nbytes && h < dbits - 6; h++) in[h] = ((bytes[h / 8] >> (h % 8)) & 1) ^ tx.scr[h];
+    for (int h = 8 * nbytes; h < dbits - 6; h++) in[h] = tx.scr[h];  // decodes to zero pad bits
+    std::vector<int> coded(blockptr);
+    unsigned reg = 0;
+    for (int t = 0; t < dbits; t++) {
+      reg = ((reg << 1) | (unsigned)in[t]) & 127;
+      coded[2 * t] = __builtin_popcount(reg & 109) & 1;
+      coded[2 * t + 1] = __builtin_popcount(reg & 79) & 1;
+    }
+    const int cols = blockptr / 64;
+    std::vector<int> blk(blockptr);
+    for (int j = 0; j < cols; j++)
+      for (int i = 0; i < 64; i++) blk[tx.perm[i] * cols + j] = coded[j * 64 + i];
+    return blk;
+  }
+};
+}  // namespace
+
+extern "C" size_t aero_synth_burst(const aero_synth_cfg *cfg, int16_t *pcm, size_t nsamples, uint8_t *packets,
+                                   size_t packets_cap, size_t *npackets) {
+  BurstTx bt(*cfg);
+  const double Fs = cfg->fs, Ts = Fs / 5250.0;
+  const int SPAN = 8, OS = 256;
+  std::vector<double> tab(2 * SPAN * OS + 2);
+  double energy = 0;
+  for (size_t i = 0; i < tab.size(); i++) tab[i] = rrc1((double)i / OS - SPAN);
+  for (int i = 0; i < 2 * SPAN * OS; i++) energy += tab[i] * tab[i];
+  energy /= OS;
+  auto pulse = [&](double x) {
+    double p = (x + SPAN) * OS;
+    if (p <= 0 || p >= 2 * SPAN * OS) return 0.0;
+    int ip = (int)p;
+    double f = p - ip;
+    return tab[ip] * (1 - f) + tab[ip + 1] * f;
+  };
+  // symbol streams over the whole recording; 0 = silence
+  const size_t nsym = (size_t)(nsamples / Ts) + 2 * SPAN + 4;
+  std::vector<double> qs(nsym, 0.0), is(nsym, 0.0);
+  size_t k = (size_t)(cfg->lead_in / Ts), np = 0, used = 0;
+  while (true) {
+    char kind;
+    std::vector<uint8_t> bytes;
+    std::vector<int> pk = bt.next_packet(kind, bytes);
+    const size_t len = 256 + 32 + pk.size() / 2 + 16;
+    if (k + len + 2 * SPAN >= nsym) break;
+    for (int s = 0; s < 128; s++) qs[k + s] = is[k + s] = 1.0;  // carrier
+    // symbol tone: Q alternates, I stays (of the four I/Q alternation patterns
+    // this is the one BurstOqpskDemodulator's x4 symbol-tone PLL and arm
+    // resolution lock to on every burst, burstoqpskdemodulator.cpp:466-493, 551-569)
+    for (int s = 0; s < 128; s++) {
+      qs[k + 128 + s] = (s & 1) ? -1.0 : 1.0;
+      is[k + 128 + s] = 1.0;
+    }
+    size_t at = k + 256;
+    const uint32_t uw = 0xE15AE893u;
+    for (int j = 0; j < 32; j++, at++) qs[at] = is[at] = ((uw >> (31 - j)) & 1) ? 1.0 : -1.0;
+    for (size_t b = 0; b < pk.size(); b += 2, at++) {
+      qs[at] = pk[b] ? 1.0 : -1.0;
+      is[at] = pk[b + 1] ? 1.0 : -1.0;
+    }
+    for (int s = 0; s < 16; s++, at++) {
+      qs[at] = bt.tx.rng.below(2) ? 1.0 : -1.0;
+      is[at] = bt.tx.rng.below(2) ? 1.0 : -1.0;
+    }
+    if (packets && used + 8 + bytes.size() <= packets_cap) {
+      uint32_t h[2] = {(uint32_t)kind, (uint32_t)bytes.size()};
+      memcpy(packets + used, h, 8);
+      memcpy(packets + used + 8, bytes.data(), bytes.size());
+      used += 8 + bytes.size();
+    }
+    np++;
+    // next burst 1-3 s later
+    k += (size_t)((1.0 + 2.0 * bt.tx.rng.uniform()) * 5250.0);
+  }
+  if (npackets) *npackets = np;
+  double A = cfg->amplitude;
+  double P = A * A * (2.0 * energy) / 2.0;
+  double sigma = 0;
+  if (cfg->ebn0_db < 99) {
+    double Eb = P / 10500.0;
+    double N0 = Eb / pow(10.0, cfg->ebn0_db / 10.0);
+    sigma = sqrt(N0 / 2.0 * Fs);
+  }
+  Rng nrng(cfg->seed ^ 0xA5A5A5A55A5A5A5AULL);
+  const double w = 2.0 * M_PI * cfg->carrier_hz / Fs;
+  for (size_t n = 0; n < nsamples; n++) {
+    const double t = (double)n / Ts;
+    long long k0 = (long long)floor(t) - SPAN, k1 = (long long)floor(t) + SPAN + 1;
+    if (k0 < 0) k0 = 0;
+    if (k1 >= (long long)nsym) k1 = (long long)nsym - 1;
+    double I = 0, Q = 0;
+    for (long long kk = k0; kk <= k1; kk++) {
+      if (qs[kk] != 0.0) Q += qs[kk] * pulse(t - (double)kk);
+      if (is[kk] != 0.0) I += is[kk] * pulse(t - (double)kk - 0.5);
+    }
+    const double ph = w * (double)n + cfg->phase0;
+    double x = A * (I * cos(ph) + Q * sin(ph));
+    if (sigma > 0) x += sigma * nrng.gauss();
+    double v = floor(x * 32768.0 + 0.5);
+    if (v > 32767) v = 32767;
+    if (v < -32768) v = -32768;
+    pcm[n] = (int16_t)v;
+  }
+  return used;
 }
