@@ -58,7 +58,26 @@ class AcarsItem(ctypes.Structure):
                 ('msg_len', ctypes.c_uint32), ('msg', ctypes.c_char * 3584)]
 
 
-# every entry point declared in include/aero_engine.h (tests/test_abi.py checks the header)
+class ChanCfg(ctypes.Structure):
+    _fields_ = [('device', ctypes.c_int), ('sample_rate', ctypes.c_int), ('center_frequency', ctypes.c_int),
+                ('mix_offset', ctypes.c_int), ('correct_dc_bias', ctypes.c_int), ('max_blocks', ctypes.c_int),
+                ('flags', ctypes.c_int)]
+
+
+class ChanMain(ctypes.Structure):
+    _fields_ = [('frequency', ctypes.c_int), ('out_rate', ctypes.c_int), ('compress_scale', ctypes.c_int),
+                ('publish', ctypes.c_int)]
+
+
+class ChanVfo(ctypes.Structure):
+    _fields_ = [('frequency', ctypes.c_int), ('data_rate', ctypes.c_int), ('out_rate', ctypes.c_int),
+                ('filter_bandwidth', ctypes.c_int), ('gain', ctypes.c_float), ('skip', ctypes.c_int)]
+
+
+CHAN_F_HOST_OUT = 0x1
+
+
+# every entry point declared in include/aero_engine.h and include/aero_chan.h (tests/test_abi.py checks the header)
 _SIGS = {
     'aero_engine_create': (ctypes.c_int, [ctypes.POINTER(EngineCfg), ctypes.POINTER(ctypes.c_void_p)]),
     'aero_engine_destroy': (None, [ctypes.c_void_p]),
@@ -67,6 +86,8 @@ _SIGS = {
                                      ctypes.c_uint32]),
     'aero_push_pcm_batch': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
                                            ctypes.c_int, ctypes.c_int]),
+    'aero_push_pcm_dev': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_uint32]),
     'aero_run': (ctypes.c_int, [ctypes.c_void_p]),
     'aero_flush': (ctypes.c_int, [ctypes.c_void_p]),
     'aero_pop_softbits': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
@@ -91,6 +112,23 @@ _SIGS = {
     'aero_device_math': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_size_t]),
     'aero_strerror': (ctypes.c_char_p, [ctypes.c_int]),
+    # include/aero_chan.h
+    'aero_chan_create': (ctypes.c_int, [ctypes.POINTER(ChanCfg), ctypes.POINTER(ChanMain), ctypes.c_int,
+                                        ctypes.POINTER(ChanVfo), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    'aero_chan_destroy': (None, [ctypes.c_void_p]),
+    'aero_chan_block_len': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
+    'aero_chan_vfo_info': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    'aero_chan_main_info': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    'aero_chan_push': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]),
+    'aero_chan_run': (ctypes.c_int, [ctypes.c_void_p]),
+    'aero_chan_sync': (ctypes.c_int, [ctypes.c_void_p]),
+    'aero_chan_vfo_output': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                            ctypes.POINTER(ctypes.c_size_t)]),
+    'aero_chan_pop_audio': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.POINTER(ctypes.c_size_t)]),
+    'aero_chan_pop_iq': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.POINTER(ctypes.c_size_t)]),
+    'aero_chan_feed': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
 }
 
 _lib = None
@@ -192,6 +230,11 @@ class Engine:
         n, ld = pcm.shape
         _check(self.lib.aero_push_pcm_batch(self.h, pcm.ctypes.data, n, ld, nch or ld, 0), 'aero_push_pcm_batch')
 
+    def push_device(self, ch, ptr, n, fs=None):
+        """ptr: HIP device pointer of n int16 samples for channel ch."""
+        fs = fs or self._fs.get(ch, 48000)
+        _check(self.lib.aero_push_pcm_dev(self.h, ch, ctypes.c_void_p(ptr), n, fs), 'aero_push_pcm_dev')
+
     def push_batch_device(self, ptr, n, ld, nch):
         """ptr: HIP device pointer of int16 [n, ld] (e.g. torch tensor.data_ptr())."""
         _check(self.lib.aero_push_pcm_batch(self.h, ctypes.c_void_p(ptr), n, ld, nch, 1), 'aero_push_pcm_batch')
@@ -279,3 +322,170 @@ class Engine:
         _check(self.lib.aero_device_math(self.h, MATH_FN[fn], x.ctypes.data, y.ctypes.data, out.ctypes.data,
                                          x.size), 'aero_device_math')
         return out
+
+
+# ------------------------------------------------------------------ channeliser
+def vfo_out_rate(data_rate, out_rate=0):
+    """[vfos] out_rate default by data_rate (publish/publisher.cpp:164-176)."""
+    if out_rate or not data_rate:
+        return out_rate
+    return {600: 12000, 1200: 24000}.get(int(data_rate), 48000)
+
+
+def vfo_bitrate(data_rate):
+    """aero-decode bit rate of a [vfos] entry's audio (10500 unless 600/1200)."""
+    return int(data_rate) if int(data_rate) in (600, 1200) else 10500
+
+
+def parse_sdr_ini(text):
+    """SDRReceiver INI as QSettings reads it for aero-publish
+    (publish/publisher.cpp:55-227): returns (general, mains, vfos) dicts with
+    the keys the publisher uses; arrays are QSettings' [name] size=N,
+    i\\key=value entries."""
+    sections, cur = {}, 'General'
+    for raw in text.splitlines():
+        line = raw.strip()
+        if not line or line[0] in ';#':
+            continue
+        if line.startswith('[') and line.endswith(']'):
+            cur = line[1:-1]
+            continue
+        if '=' in line:
+            k, v = line.split('=', 1)
+            sections.setdefault(cur, {})[k.strip()] = v.strip()
+
+    def to_int(v):  # QVariant::toInt: 0 when the text is not an integer
+        try:
+            return int(v)
+        except (TypeError, ValueError):
+            return 0
+
+    def to_float(v):
+        try:
+            return float(v)
+        except (TypeError, ValueError):
+            return 0.0
+
+    def array(name):
+        sec = sections.get(name, {})
+        out = []
+        for i in range(1, to_int(sec.get('size')) + 1):
+            pre = '%d\\' % i
+            out.append({k[len(pre):]: v for k, v in sec.items() if k.startswith(pre)})
+        return out
+
+    g = sections.get('General', {})
+    general = dict(sample_rate=to_int(g.get('sample_rate')), center_frequency=to_int(g.get('center_frequency')),
+                   mix_offset=to_int(g.get('mix_offset')), correct_dc_bias=g.get('correct_dc_bias') == '1',
+                   zmq_address=g.get('zmq_address', ''))
+    mains = [dict(frequency=to_int(d.get('frequency')), out_rate=to_int(d.get('out_rate')),
+                  compress_scale=to_int(d.get('compress_scale')),
+                  publish=int(bool(d.get('zmq_address')) and bool(d.get('zmq_topic'))))
+             for d in array('main_vfos')]
+    vfos = [dict(frequency=to_int(d.get('frequency')), data_rate=to_int(d.get('data_rate')),
+                 out_rate=to_int(d.get('out_rate')), filter_bandwidth=to_int(d.get('filter_bandwidth')),
+                 gain=to_float(d.get('gain')), topic=d.get('topic', ''))
+            for d in array('vfos')]
+    return general, mains, vfos
+
+
+class Channeliser:
+    """aero-publish's channeliser on one GPU (include/aero_chan.h):
+    Publisher::loadSettings + demodData (publish/publisher.cpp:55-306) and
+    vfo::process (publish/vfo.cpp:154-313).  `mains` / `vfos` are the INI's
+    [main_vfos] / [vfos] entries (dicts as parse_sdr_ini returns); `skip`
+    marks [vfos] entries another process computes."""
+
+    def __init__(self, sample_rate, center_frequency, mains, vfos, mix_offset=0, correct_dc_bias=False,
+                 max_blocks=8, device=0, host_out=False, skip=None):
+        self.lib = load_library()
+        cfg = ChanCfg(device, int(sample_rate), int(center_frequency), int(mix_offset), int(bool(correct_dc_bias)),
+                      int(max_blocks), CHAN_F_HOST_OUT if host_out else 0)
+        m = (ChanMain * max(1, len(mains)))()
+        for i, d in enumerate(mains):
+            m[i] = ChanMain(int(d['frequency']), int(d.get('out_rate', 0)), int(d.get('compress_scale', 0)),
+                            int(d.get('publish', 0)))
+        v = (ChanVfo * max(1, len(vfos)))()
+        for i, d in enumerate(vfos):
+            v[i] = ChanVfo(int(d['frequency']), int(d.get('data_rate', 0)), int(d.get('out_rate', 0)),
+                           int(d.get('filter_bandwidth', 0)), float(d.get('gain', 0.0)),
+                           int(bool(skip[i])) if skip is not None else 0)
+        h = ctypes.c_void_p()
+        _check(self.lib.aero_chan_create(ctypes.byref(cfg), m, len(mains), v, len(vfos), ctypes.byref(h)),
+               'aero_chan_create')
+        self.h = h
+        self.nmain, self.nvfo = len(mains), len(vfos)
+        b = ctypes.c_int()
+        _check(self.lib.aero_chan_block_len(h, ctypes.byref(b)), 'aero_chan_block_len')
+        self.block_len = b.value
+
+    def close(self):
+        if self.h:
+            self.lib.aero_chan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def vfo_info(self, v):
+        i = (ctypes.c_int * 5)()
+        _check(self.lib.aero_chan_vfo_info(self.h, v, i), 'aero_chan_vfo_info')
+        return dict(main=i[0], out_rate=i[1], samples_per_block=i[2], halfbands=i[3], late=i[4])
+
+    def main_info(self, m):
+        i = (ctypes.c_int * 3)()
+        _check(self.lib.aero_chan_main_info(self.h, m, i), 'aero_chan_main_info')
+        return dict(out_rate=i[0], samples_per_block=i[1], halfbands=i[2])
+
+    def push(self, iq):
+        """iq: complex64 host samples, whole reads of block_len."""
+        iq = np.ascontiguousarray(iq, dtype=np.complex64)
+        nb = iq.size // self.block_len
+        if nb * self.block_len != iq.size:
+            raise ValueError('push whole reads of %d samples' % self.block_len)
+        _check(self.lib.aero_chan_push(self.h, iq.ctypes.data, nb, 0), 'aero_chan_push')
+
+    def push_device(self, ptr, nblocks):
+        """ptr: HIP device pointer of nblocks * block_len interleaved CF32 samples."""
+        _check(self.lib.aero_chan_push(self.h, ctypes.c_void_p(ptr), nblocks, 1), 'aero_chan_push')
+
+    def run(self):
+        _check(self.lib.aero_chan_run(self.h), 'aero_chan_run')
+
+    def sync(self):
+        _check(self.lib.aero_chan_sync(self.h), 'aero_chan_sync')
+
+    def output_device(self, v):
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        _check(self.lib.aero_chan_vfo_output(self.h, v, ctypes.byref(p), ctypes.byref(n)), 'aero_chan_vfo_output')
+        return p.value, n.value
+
+    def _pop(self, fn, i, dtype):
+        out, cap = [], 1 << 20
+        while True:
+            buf = np.empty(cap, dtype=dtype)
+            n = ctypes.c_size_t()
+            _check(fn(self.h, i, buf.ctypes.data, cap, ctypes.byref(n)), fn.__name__)
+            out.append(buf[:n.value].copy())
+            if n.value < cap:
+                return np.concatenate(out)
+
+    def audio(self, v):
+        return self._pop(self.lib.aero_chan_pop_audio, v, np.int16)
+
+    def iq(self, m):
+        return self._pop(self.lib.aero_chan_pop_iq, m, np.int8)
+
+    def feed(self, engine, channels):
+        """channels[v]: engine channel of [vfos] entry v, or -1."""
+        arr = (ctypes.c_int * max(1, self.nvfo))(*[int(c) for c in channels])
+        _check(self.lib.aero_chan_feed(self.h, engine.h, arr), 'aero_chan_feed')

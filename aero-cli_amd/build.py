@@ -29,7 +29,7 @@ FP = ['-ffp-contract=off', '-fno-fast-math']
 HIP_FLAGS = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH, '-munsafe-fp-atomics'] + FP
 CXX_FLAGS = ['-O2', '-std=c++17', '-fPIC', '-Wall'] + FP
 
-HIP_SRCS = ['demod_oqpsk.hip', 'demod_msk.hip', 'coarse.hip', 'aerol.hip', 'engine.hip']
+HIP_SRCS = ['demod_oqpsk.hip', 'demod_msk.hip', 'coarse.hip', 'aerol.hip', 'engine.hip', 'chan.hip']
 CXX_SRCS = ['tables_host.cpp', 'acars_host.cpp']
 
 
@@ -55,7 +55,7 @@ def build_engine(jobs=4, variant=None, defines=()):
     out = ENGINE_SO if variant is None else os.path.join(HERE, 'libaero_engine_%s.so' % variant)
     os.makedirs(bdir, exist_ok=True)
     headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith('.h')]
-    headers.append(os.path.join(ROOT, 'include', 'aero_engine.h'))
+    headers += [os.path.join(ROOT, 'include', h) for h in ('aero_engine.h', 'aero_chan.h')]
     dflags = ['-D' + d for d in defines]
     tasks, objs = [], []
     for s in HIP_SRCS + CXX_SRCS:

@@ -19,6 +19,7 @@
 
 #include "aero_math.h"
 #include "engine_common.h"
+#include "fft_dit.h"
 
 namespace aero {
 
@@ -45,98 +46,6 @@ struct CoarseK<MODE_MSK1200> {
   static constexpr int YLO = 3686, YHI = 4505;
   static constexpr double FS = 24000.0;
 };
-
-__device__ __forceinline__ int pad(int p) { return p + (p >> 4); }
-
-// position of value i of thread t in register phase PH (4 FFT stages per
-// phase; the last phase holds the LOG2N - 12 remaining stage bits in i's low bits)
-template <int LOG2N, int PH>
-__device__ __forceinline__ int epos(int t, int i) {
-  constexpr int LFT = LOG2N - 4, R = LOG2N - 12;
-  if (PH == 0) return (t << 4) | i;
-  if (PH == 1) return (t & 15) | (i << 4) | ((t >> 4) << 8);
-  if (PH == 2) return (t & 255) | (i << 8) | ((t >> 8) << 12);
-  return (t & ((1 << LFT) - 1)) | ((i >> R) << LFT) | ((i & ((1 << R) - 1)) << (LOG2N - R));
-}
-
-template <int LOG2N>
-__device__ __forceinline__ int bitrev(int p) { return (int)(__builtin_bitreverse32((uint32_t)p) >> (32 - LOG2N)); }
-
-// one radix-2 DIT stage of half-size n on the thread's 16 values;
-// `lb` is the bit of i that encodes the stage's position bit.
-// `t` is laundered at every stage/exchange so the compiler recomputes the
-// (cheap) per-thread positions instead of keeping hundreds of addresses live
-// across the three transforms (that is what spilled).
-__device__ __forceinline__ int fresh(int t) {
-  asm volatile("" : "+v"(t));
-  return t;
-}
-
-template <int LOG2N, int PH>
-__device__ __forceinline__ void stage(double2 (&x)[16], int t0, int lb, int n, const double2 *__restrict__ TW) {
-  const int t = fresh(t0);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    if (i & (1 << lb)) continue;
-    const int il = i | (1 << lb);
-    const int pk = epos<LOG2N, PH>(t, i);
-    const double2 w = TW[n - 1 + (pk & (n - 1))];
-    const double yr = w.x * x[il].x - w.y * x[il].y;
-    const double yi = w.x * x[il].y + w.y * x[il].x;
-    x[il].x = x[i].x - yr;
-    x[il].y = x[i].y - yi;
-    x[i].x = x[i].x + yr;
-    x[i].y = x[i].y + yi;
-  }
-}
-
-// move values from layout PH_FROM to PH_TO through LDS (re then im);
-// BR: the destination reads bit-reversed positions (start of a new transform)
-template <int LOG2N, int PH_FROM, int PH_TO, bool BR>
-__device__ __forceinline__ void exchange(double2 (&x)[16], int t0, double *lds) {
-#pragma unroll
-  for (int part = 0; part < 2; ++part) {
-    const int t = fresh(t0);
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 16; ++i) lds[pad(epos<LOG2N, PH_FROM>(t, i))] = part ? x[i].y : x[i].x;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      int p = epos<LOG2N, PH_TO>(t, i);
-      if (BR) p = bitrev<LOG2N>(p);
-      const double v = lds[pad(p)];
-      if (part)
-        x[i].y = v;
-      else
-        x[i].x = v;
-    }
-  }
-}
-
-// full JFFT::fft on values already loaded in bit-reversed order in layout 0;
-// leaves the natural-order result in layout 3
-template <int L>
-__device__ __forceinline__ void fft_dit(double2 (&x)[16], int t, double *lds, const double2 *__restrict__ TW) {
-  static_assert(L == 13 || L == 14, "register phases cover 13 or 14 stages");
-  stage<L, 0>(x, t, 0, 1, TW);
-  stage<L, 0>(x, t, 1, 2, TW);
-  stage<L, 0>(x, t, 2, 4, TW);
-  stage<L, 0>(x, t, 3, 8, TW);
-  exchange<L, 0, 1, false>(x, t, lds);
-  stage<L, 1>(x, t, 0, 16, TW);
-  stage<L, 1>(x, t, 1, 32, TW);
-  stage<L, 1>(x, t, 2, 64, TW);
-  stage<L, 1>(x, t, 3, 128, TW);
-  exchange<L, 1, 2, false>(x, t, lds);
-  stage<L, 2>(x, t, 0, 256, TW);
-  stage<L, 2>(x, t, 1, 512, TW);
-  stage<L, 2>(x, t, 2, 1024, TW);
-  stage<L, 2>(x, t, 3, 2048, TW);
-  exchange<L, 2, 3, false>(x, t, lds);
-  stage<L, 3>(x, t, 0, 4096, TW);
-  if (L == 14) stage<L, 3>(x, t, 1, 8192, TW);
-}
 
 __device__ __forceinline__ void set_freq1(double &freq, double &step, double f, double fs) {  // SetFreq (DSP.cpp:163-168)
   freq = f;

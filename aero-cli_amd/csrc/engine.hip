@@ -994,6 +994,23 @@ int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t
   return AERO_OK;
 }
 
+int aero_push_pcm_dev(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t fs) {
+  int c;
+  Group *g = route(e, ch, c);
+  if (!g || (!pcm && n)) return AERO_E_INVALID;
+  if (g->mode != MODE_OQPSK && fs != (uint32_t)g->g.fs) return AERO_E_RATE;
+  if (!n) return AERO_OK;
+  HIPCHK(hipSetDevice(e->device));
+  size_t off = 0;
+  while (off < n) {
+    const size_t piece = std::min<size_t>(n - off, PCM_CAP / 2);
+    int rc = push_common(g, pcm + off, piece, 1, 1, c, true);
+    if (rc) return rc;
+    off += piece;
+  }
+  return AERO_OK;
+}
+
 int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld, int nch, int dev) {
   if (!e || !pcm || nch <= 0 || nch > (int)e->chmap.size() || ld < (size_t)nch) return AERO_E_INVALID;
   // channels [0, nch) must be one kind, opened in order (local == engine index)

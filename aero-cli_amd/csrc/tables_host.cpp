@@ -9,6 +9,7 @@
 #include <cmath>
 #include <complex>
 #include <cstring>
+#include <vector>
 
 namespace aero {
 
@@ -125,9 +126,74 @@ void host_scrambler(uint8_t *pre) {  // AeroLScrambler::AeroLScrambler (decode/a
   }
 }
 
+/* ------------------------------------------ aero-publish channeliser (FP32) */
+int host_pub_osc_len(double sampleRate) { return (int)sampleRate; }
+
+// Oscillator::Oscillator (publish/oscillator.cpp:4-28): queue[i] is the
+// rotator after i+1 renormalised steps, in std::complex<float> as there
+void host_pub_osc(double sampleRate, double frequency, float *queue) {
+  typedef std::complex<float> cpxf;
+  const double anglePerSample = 2.0 * M_PI * frequency / sampleRate;
+  const cpxf rotation((float)cos(anglePerSample), (float)sin(anglePerSample));
+  cpxf v(1.0f, 0);
+  const int length = (int)sampleRate;
+  for (int i = 0; i < length; i++) {
+    v *= rotation;
+    const float norm = 1.95f - (v.real() * v.real() + v.imag() * v.imag());
+    v = v * norm;
+    queue[2 * i] = v.real();
+    queue[2 * i + 1] = v.imag();
+  }
+}
+
+// FIRHilbert::FIRHilbert (publish/dsp.cpp:181-215).  `sqrt` of the float sum
+// resolves to the float overload there (`using namespace std`, dsp.cpp:30).
+void host_pub_hilbert(int len, int Fs, float *points) {
+  std::vector<float> tempCoeffs(len);
+  float sumofsquares = 0;
+  for (int n = 0; n < len; n++) {
+    if (n == len / 2)
+      tempCoeffs[n] = 0;
+    else
+      tempCoeffs[n] = Fs / (M_PI * (n - len / 2)) * (1 - cos(M_PI * (n - len / 2)));
+    sumofsquares += tempCoeffs[n] * tempCoeffs[n];
+  }
+  const double gain = std::sqrt(sumofsquares);
+  for (int i = 0; i < len; i++) points[i] = tempCoeffs[len - i - 1] / gain;
+}
+
+// firfilter::low_pass with WIN_HAMMING (publish/firfilter.cpp:47-99, 186-193)
+int host_pub_low_pass(double gain, double fs, double cutoff, double tw, float *taps, int cap) {
+  int ntaps = (int)(53.0 * fs / (22.0 * tw));  // compute_ntaps, max_attenuation(HAMMING) = 53
+  if ((ntaps & 1) == 0) ntaps++;
+  if (ntaps > cap) return -1;
+  std::vector<float> w(ntaps);
+  const float Mf = static_cast<float>(ntaps - 1);
+  for (int n = 0; n < ntaps; n++) w[n] = 0.54 - 0.46 * cos((2 * M_PI * n) / Mf);
+  const int M = (ntaps - 1) / 2;
+  const double fwT0 = 2 * M_PI * cutoff / fs;
+  for (int n = -M; n <= M; n++) {
+    if (n == 0)
+      taps[n + M] = fwT0 / M_PI * w[n + M];
+    else
+      taps[n + M] = sin(n * fwT0) / (n * M_PI) * w[n + M];
+  }
+  double fmax = taps[0 + M];
+  for (int n = 1; n <= M; n++) fmax += 2 * taps[n + M];
+  gain /= fmax;
+  for (int i = 0; i < ntaps; i++) taps[i] *= gain;
+  return ntaps;
+}
+
 }  // namespace aero
 
 extern "C" {
+/* channeliser designs, for tests/test_abi.py (engine tables vs the oracle's) */
+void aero_host_pub_osc(double fs, double freq, float *queue) { aero::host_pub_osc(fs, freq, queue); }
+void aero_host_pub_hilbert(int len, int fs, float *points) { aero::host_pub_hilbert(len, fs, points); }
+int aero_host_pub_low_pass(double gain, double fs, double cutoff, double tw, float *taps, int cap) {
+  return aero::host_pub_low_pass(gain, fs, cutoff, tw, taps, cap);
+}
 /* exported for tests/test_tables.py: the engine's tables vs the oracle's */
 void aero_host_tables(double *cis, double *tw, double *twi, double *taps, int *ntaps) {
   aero::host_cis(cis);

@@ -19,4 +19,11 @@ bool host_delay_uniform(double fractdelay, int &size, int &age_old, int &age_new
 void host_msk_taps(int sps, double *taps);
 void host_scrambler(uint8_t *pre);                              // [5000]
 
+// aero-publish channeliser designs (publish/oscillator.cpp:4-28,
+// publish/dsp.cpp:181-215, publish/firfilter.cpp:47-99): FP32 as there
+int host_pub_osc_len(double sampleRate);
+void host_pub_osc(double sampleRate, double frequency, float *queue);  // [(int)sampleRate][2]
+void host_pub_hilbert(int len, int Fs, float *points);                 // [len]
+int host_pub_low_pass(double gain, double fs, double cutoff, double tw, float *taps, int cap);
+
 }  // namespace aero

@@ -1,8 +1,10 @@
 """Channel sharding across GPUs.
 
 VFO channels are independent streams: every rank owns a disjoint channel
-set and runs the whole decode path for it; the only inter-rank traffic is
-the benchmark's barrier and its max/sum timing reduction.
+set and runs the whole decode path for it.  For the C5 channeliser the one
+exchange step is the broadcast of each wideband read from the rank that
+received it (RCCL over xGMI); every rank then channelises and decodes only
+its own [vfos] entries (shard_vfos).
 """
 import numpy as np
 
@@ -28,3 +30,30 @@ def channel_offsets(n_channels, pool, rank=0):
     groups = max(1, n_channels // pool)
     g = np.arange(groups, dtype=np.int64)
     return ((g * 7919 + rank * 104729) % 65536).astype(np.int64)
+
+
+# decode cost per VFO by bit rate (a 10500 channel costs
+# about 5.6x a 600/1200 one on the CPU probe)
+VFO_COST = {600: 1.0, 1200: 1.0}
+
+
+def shard_vfos(vfos, world):
+    """Owner rank of every [vfos] entry: longest-processing-time-first over
+    the per-VFO decode cost, ties by index, so every rank derives the same map."""
+    costs = [VFO_COST.get(int(v.get('data_rate', 0)), 5.6) for v in vfos]
+    load = [0.0] * world
+    owner = [0] * len(vfos)
+    for i in sorted(range(len(vfos)), key=lambda i: (-costs[i], i)):
+        r = min(range(world), key=lambda r: (load[r], r))
+        owner[i] = r
+        load[r] += costs[i]
+    return owner
+
+
+def broadcast_reads(buf, src=0):
+    """The C5 exchange step: the wideband reads in `buf` (a CUDA tensor on
+    the NCCL/RCCL backend, a CPU tensor on gloo) go from rank `src` to all."""
+    import torch.distributed as dist
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.broadcast(buf, src=src)
+    return buf

@@ -91,6 +91,10 @@ int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t
  * must be of one kind (bit rate). */
 int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld, int nch, int dev);
 
+/* aero_push_pcm with pcm a HIP device pointer (e.g. channeliser audio already
+ * in HBM, aero_chan.h); the samples are copied before returning. */
+int aero_push_pcm_dev(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t fs);
+
 /* Runs the batched kernels for every channel over all pushed samples that
  * complete a coarse-estimate hop; aero_flush also processes the tail. */
 int aero_run(aero_engine *e);

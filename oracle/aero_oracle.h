@@ -79,6 +79,23 @@ void oracle_msk_taps(int sps, double *dst); /* MskDemodulator matched filter, 2*
 /* raw JFFT-order transform for the FFT parity test (in place, nfft complex) */
 void oracle_fft(double *x, int nfft, int inverse);
 
+/* aero-publish channeliser (pub_oracle.cpp).  mains: nmain x {frequency,
+ * out_rate, compress_scale, publish}; vfos: nvfo x {frequency, data_rate,
+ * out_rate, filter_bandwidth}; gains: the INI "gain" values.  NULL when the
+ * configuration is invalid. */
+typedef struct oracle_pub oracle_pub;
+oracle_pub *oracle_pub_create(int fs, int center, int mix_offset, int dcc, const int *mains, int nmain,
+                              const int *vfos, const float *gains, int nvfo);
+void oracle_pub_destroy(oracle_pub *o);
+int oracle_pub_block_len(const oracle_pub *o);
+void oracle_pub_process(oracle_pub *o, const float *iq, int nblocks); /* interleaved CF32 blocks */
+size_t oracle_pub_usb(const oracle_pub *o, int v, int16_t *dst, size_t cap);
+size_t oracle_pub_iq(const oracle_pub *o, int m, int8_t *dst, size_t cap);
+int oracle_pub_info(const oracle_pub *o, int v, int *info7);
+int oracle_pub_low_pass(double gain, double fs, double cutoff, double tw, float *dst, int cap);
+void oracle_pub_hilbert(int len, int fs, float *dst);
+void oracle_pub_osc(double fs, double freq, float *dst); /* (int)fs complex */
+
 #ifdef __cplusplus
 }
 #endif

@@ -224,3 +224,115 @@ def parse_rt_packets(raw):
         out.append((chr(kind), bytes(raw[i + 8:i + 8 + int(ln)])))
         i += 8 + int(ln)
     return out
+
+
+class OraclePublisher:
+    """oracle/pub_oracle.cpp: aero-publish's channeliser restated sample by
+    sample (the checker for aero-cli_amd/csrc/chan.hip)."""
+    _ready = False
+
+    @classmethod
+    def lib(cls):
+        L = Oracle.lib()
+        if not cls._ready:
+            c = ctypes
+            L.oracle_pub_create.restype = c.c_void_p
+            L.oracle_pub_create.argtypes = [c.c_int, c.c_int, c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_void_p,
+                                            c.c_void_p, c.c_int]
+            L.oracle_pub_destroy.argtypes = [c.c_void_p]
+            L.oracle_pub_block_len.argtypes = [c.c_void_p]
+            L.oracle_pub_block_len.restype = c.c_int
+            L.oracle_pub_process.argtypes = [c.c_void_p, c.c_void_p, c.c_int]
+            for f in ('oracle_pub_usb', 'oracle_pub_iq'):
+                getattr(L, f).argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_size_t]
+                getattr(L, f).restype = c.c_size_t
+            L.oracle_pub_info.argtypes = [c.c_void_p, c.c_int, c.c_void_p]
+            L.oracle_pub_low_pass.argtypes = [c.c_double, c.c_double, c.c_double, c.c_double, c.c_void_p, c.c_int]
+            L.oracle_pub_hilbert.argtypes = [c.c_int, c.c_int, c.c_void_p]
+            L.oracle_pub_osc.argtypes = [c.c_double, c.c_double, c.c_void_p]
+            cls._ready = True
+        return L
+
+    def __init__(self, sample_rate, center_frequency, mains, vfos, mix_offset=0, correct_dc_bias=False):
+        L = self.lib()
+        m = np.array([[d['frequency'], d.get('out_rate', 0), d.get('compress_scale', 0), d.get('publish', 0)]
+                      for d in mains], dtype=np.int32).reshape(-1, 4)
+        v = np.array([[d['frequency'], d.get('data_rate', 0), d.get('out_rate', 0), d.get('filter_bandwidth', 0)]
+                      for d in vfos], dtype=np.int32).reshape(-1, 4)
+        g = np.array([d.get('gain', 0.0) for d in vfos], dtype=np.float32)
+        self._keep = (m, v, g)
+        self.h = L.oracle_pub_create(sample_rate, center_frequency, mix_offset, int(bool(correct_dc_bias)),
+                                     m.ctypes.data, len(mains), v.ctypes.data, g.ctypes.data, len(vfos))
+        if not self.h:
+            raise ValueError('invalid publisher configuration')
+        self.block_len = L.oracle_pub_block_len(self.h)
+        self.nvfo, self.nmain = len(vfos), len(mains)
+
+    def __del__(self):
+        if getattr(self, 'h', None):
+            Oracle.lib().oracle_pub_destroy(self.h)
+            self.h = None
+
+    def process(self, iq):
+        iq = np.ascontiguousarray(iq, dtype=np.complex64)
+        nb = iq.size // self.block_len
+        assert nb * self.block_len == iq.size
+        Oracle.lib().oracle_pub_process(self.h, iq.ctypes.data, nb)
+
+    def usb(self, v):
+        L = Oracle.lib()
+        n = L.oracle_pub_usb(self.h, v, None, 0)
+        out = np.zeros(n, dtype=np.int16)
+        L.oracle_pub_usb(self.h, v, out.ctypes.data, n)
+        return out
+
+    def iq(self, m):
+        L = Oracle.lib()
+        n = L.oracle_pub_iq(self.h, m, None, 0)
+        out = np.zeros(n, dtype=np.int8)
+        L.oracle_pub_iq(self.h, m, out.ctypes.data, n)
+        return out
+
+    def info(self, v):
+        i = np.zeros(7, dtype=np.int32)
+        assert Oracle.lib().oracle_pub_info(self.h, v, i.ctypes.data) == 0
+        return dict(main=int(i[0]), out_rate=int(i[1]), samples_per_block=int(i[2]), halfbands=int(i[3]),
+                    late=int(i[4]), late_taps=int(i[5]), usb_taps=int(i[6]))
+
+
+def wideband(sample_rate, n, seed, tones=(), noise=0.05):
+    """Synthetic CF32 wideband: complex Gaussian noise plus (offset_hz,
+    amplitude) tones relative to the centre frequency."""
+    rng = np.random.default_rng(seed)
+    x = (rng.normal(0, noise, n) + 1j * rng.normal(0, noise, n)).astype(np.complex128)
+    t = np.arange(n) / float(sample_rate)
+    for f, a in tones:
+        x += a * np.exp(2j * np.pi * f * t)
+    return x.astype(np.complex64)
+
+
+# C5-like channeliser configurations (SURVEY.md §8(d) C5 stand-in): one per
+# SDR rate, exercising 2^k half-bands, late 1/5 and 1/6 decimation, the audio
+# low-pass, int16 wrap-around (gain 5000 %), and a main VFO with IQ output
+CENTER = 1545000000
+PUB_CONFIGS = {
+    'r1536k': dict(sample_rate=1536000, mains=[dict(frequency=CENTER - 300000, out_rate=192000),
+                                               dict(frequency=CENTER + 100000, out_rate=192000),
+                                               dict(frequency=CENTER + 600000, out_rate=192000, publish=1,
+                                                    compress_scale=2)],
+                   vfos=[dict(frequency=CENTER - 320000, data_rate=10500, gain=100.0),
+                         dict(frequency=CENTER - 265000, data_rate=600, filter_bandwidth=2500, gain=150.0),
+                         dict(frequency=CENTER + 60000, data_rate=1200, gain=80.0),
+                         dict(frequency=CENTER + 130000, data_rate=10500, gain=5000.0)],
+                   tones=[(-318500.0, 0.3), (-264000.0, 0.2), (61200.0, 0.25), (131000.0, 0.4), (600500.0, 0.5)]),
+    'r288k': dict(sample_rate=288000, mains=[dict(frequency=CENTER, out_rate=288000)],
+                  vfos=[dict(frequency=CENTER + 20000, data_rate=10500, gain=100.0),
+                        dict(frequency=CENTER - 50000, data_rate=600, gain=100.0, filter_bandwidth=3000),
+                        dict(frequency=CENTER + 90000, data_rate=1200, gain=100.0)],
+                  tones=[(21500.0, 0.3), (-49000.0, 0.2), (91000.0, 0.2)]),
+    'r1920k': dict(sample_rate=1920000, mains=[dict(frequency=CENTER, out_rate=240000)],
+                   vfos=[dict(frequency=CENTER - 40000, data_rate=10500, gain=100.0),
+                         dict(frequency=CENTER + 30000, data_rate=600, gain=100.0),
+                         dict(frequency=CENTER + 70000, data_rate=1200, gain=100.0, filter_bandwidth=4000)],
+                   tones=[(-38000.0, 0.3), (31000.0, 0.2), (72000.0, 0.2)]),
+}
