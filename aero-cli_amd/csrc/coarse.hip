@@ -146,11 +146,12 @@ __device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<in
 }
 
 template <int M>
-__global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4)) void coarse_kernel(DevState S, DevTables T, int nch) {
+__global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 13 ? 4 : 1) void coarse_kernel(DevState S, DevTables T, int nch) {
   using K = CoarseK<M>;
   constexpr int L = K::LOG2N, N = 1 << L, FT = N / 16, PADDED = N + N / 16;
   constexpr int YLEN = K::YHI - K::YLO + 1;
   __shared__ double lds[PADDED];
+  __shared__ double2 s_tw[TwLds<L>::LEN];
   __shared__ double red_v[FT / 64];
   __shared__ int red_i[FT / 64];
   const int c = blockIdx.x;
@@ -178,6 +179,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4)) void coarse_kernel(De
   }
   __syncthreads();
 
+  load_tw_lds<L>(s_tw, T.tw, t, FT);
   // ring words -> LDS (as uint32 in the first N*4 bytes)
   uint32_t *ring_lds = reinterpret_cast<uint32_t *>(lds);
   const uint32_t *ring = S.cring + (size_t)c * N;
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4)) void coarse_kernel(De
     }
   }
   // forward FFT
-  fft_dit<L>(x, t, lds, T.tw);
+  fft_dit<L, false>(x, t, lds, T.tw, s_tw);
   // boxcar: zero bins startbin..stopbin (coarsefreqestimate.cpp:143-146)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -208,7 +210,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4)) void coarse_kernel(De
   }
   // inverse FFT (JFFT scales by 1/N, FFTWrapper multiplies by N)
   exchange<L, 3, 0, true>(x, t, lds);
-  fft_dit<L>(x, t, lds, T.twi);
+  fft_dit<L, true>(x, t, lds, T.twi, s_tw);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     x[i].x *= (1.0 / ((double)N));
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4)) void coarse_kernel(De
     x[i] = make_double2(r, im);
   }
   exchange<L, 3, 0, true>(x, t, lds);
-  fft_dit<L>(x, t, lds, T.tw);
+  fft_dit<L, false>(x, t, lds, T.tw, s_tw);
   // fftshift + smoothing y = 0.9 y + 10 log10(max(|X|,1)) over the bins the fold reads:
   // |X| per bin to LDS first (keeps the log10 out of the register-heavy FFT scope)
   __syncthreads();

@@ -39,15 +39,34 @@ __device__ __forceinline__ int fresh(int t) {
   return t;
 }
 
-template <int LOG2N, int PH>
-__device__ __forceinline__ void stage(double2 (&x)[16], int t0, int lb, int n, const double2 *__restrict__ TW) {
+// Twiddles of the stages n <= TW_LDS<LOG2N> come from an LDS copy of the
+// forward table (fewer L2 round trips per stage).  An inverse transform
+// negates their imaginary parts: JFFT's inverse table is the forward one
+// conjugated bit for bit (mirrored std::exp arguments, decode/jfft.cpp:41-53;
+// tests/test_abi.py::test_twiddle_inverse_is_conjugate).
+template <int LOG2N>
+struct TwLds {
+  static constexpr int N = LOG2N >= 14 ? 512 : 256;  // largest stage served from LDS
+  static constexpr int LEN = 2 * N - 1;             // TW[0 .. 2N-2]
+};
+
+template <int LOG2N, int PH, bool INV>
+__device__ __forceinline__ void stage(double2 (&x)[16], int t0, int lb, int n, const double2 *__restrict__ TW,
+                                      const double2 *stw) {
   const int t = fresh(t0);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     if (i & (1 << lb)) continue;
     const int il = i | (1 << lb);
     const int pk = epos<LOG2N, PH>(t, i);
-    const double2 w = TW[n - 1 + (pk & (n - 1))];
+    const int widx = n - 1 + (pk & (n - 1));
+    double2 w;
+    if (n <= TwLds<LOG2N>::N) {
+      w = stw[widx];
+      if (INV) w.y = -w.y;
+    } else {
+      w = TW[widx];
+    }
     const double yr = w.x * x[il].x - w.y * x[il].y;
     const double yi = w.x * x[il].y + w.y * x[il].x;
     x[il].x = x[i].x - yr;
@@ -81,28 +100,36 @@ __device__ __forceinline__ void exchange(double2 (&x)[16], int t0, double *lds) 
   }
 }
 
-// full JFFT::fft on values already loaded in bit-reversed order in layout 0;
-// leaves the natural-order result in layout 3
+// copy of the forward twiddles the LDS-served stages use (all threads call it)
 template <int L>
-__device__ __forceinline__ void fft_dit(double2 (&x)[16], int t, double *lds, const double2 *__restrict__ TW) {
+__device__ __forceinline__ void load_tw_lds(double2 *stw, const double2 *__restrict__ TW, int t, int nthreads) {
+  for (int j = t; j < TwLds<L>::LEN; j += nthreads) stw[j] = TW[j];
+}
+
+// full JFFT::fft on values already loaded in bit-reversed order in layout 0;
+// leaves the natural-order result in layout 3.  TW: this direction's table;
+// stw: LDS copy of the forward table's first TwLds<L>::LEN entries.
+template <int L, bool INV>
+__device__ __forceinline__ void fft_dit(double2 (&x)[16], int t, double *lds, const double2 *__restrict__ TW,
+                                        const double2 *stw) {
   static_assert(L == 13 || L == 14, "register phases cover 13 or 14 stages");
-  stage<L, 0>(x, t, 0, 1, TW);
-  stage<L, 0>(x, t, 1, 2, TW);
-  stage<L, 0>(x, t, 2, 4, TW);
-  stage<L, 0>(x, t, 3, 8, TW);
+  stage<L, 0, INV>(x, t, 0, 1, TW, stw);
+  stage<L, 0, INV>(x, t, 1, 2, TW, stw);
+  stage<L, 0, INV>(x, t, 2, 4, TW, stw);
+  stage<L, 0, INV>(x, t, 3, 8, TW, stw);
   exchange<L, 0, 1, false>(x, t, lds);
-  stage<L, 1>(x, t, 0, 16, TW);
-  stage<L, 1>(x, t, 1, 32, TW);
-  stage<L, 1>(x, t, 2, 64, TW);
-  stage<L, 1>(x, t, 3, 128, TW);
+  stage<L, 1, INV>(x, t, 0, 16, TW, stw);
+  stage<L, 1, INV>(x, t, 1, 32, TW, stw);
+  stage<L, 1, INV>(x, t, 2, 64, TW, stw);
+  stage<L, 1, INV>(x, t, 3, 128, TW, stw);
   exchange<L, 1, 2, false>(x, t, lds);
-  stage<L, 2>(x, t, 0, 256, TW);
-  stage<L, 2>(x, t, 1, 512, TW);
-  stage<L, 2>(x, t, 2, 1024, TW);
-  stage<L, 2>(x, t, 3, 2048, TW);
+  stage<L, 2, INV>(x, t, 0, 256, TW, stw);
+  stage<L, 2, INV>(x, t, 1, 512, TW, stw);
+  stage<L, 2, INV>(x, t, 2, 1024, TW, stw);
+  stage<L, 2, INV>(x, t, 3, 2048, TW, stw);
   exchange<L, 2, 3, false>(x, t, lds);
-  stage<L, 3>(x, t, 0, 4096, TW);
-  if (L == 14) stage<L, 3>(x, t, 1, 8192, TW);
+  stage<L, 3, INV>(x, t, 0, 4096, TW, stw);
+  if (L == 14) stage<L, 3, INV>(x, t, 1, 8192, TW, stw);
 }
 
 
