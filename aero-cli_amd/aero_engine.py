@@ -104,6 +104,10 @@ _SIGS = {
                                        ctypes.POINTER(ctypes.c_size_t)]),
     'aero_pop_frames': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                        ctypes.POINTER(ctypes.c_size_t)]),
+    'aero_pop_rt_tests': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.POINTER(ctypes.c_size_t)]),
+    'aero_pop_rt_packets': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.POINTER(ctypes.c_size_t)]),
     'aero_timing': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_long)]),
     'aero_timing_reset': (None, [ctypes.c_void_p]),
@@ -263,6 +267,24 @@ class Engine:
 
     def softbits(self, ch):
         return self._pop(self.lib.aero_pop_softbits, ch, np.int16).astype(np.uint8)
+
+    def softbits16(self, ch):
+        """burst channels: delivered soft bits with -1 start-of-packet markers"""
+        return self._pop(self.lib.aero_pop_softbits, ch, np.int16)
+
+    def rt_tests(self, ch):
+        """burst channels: (blockptr, result code) of every R/T test"""
+        return self._pop(self.lib.aero_pop_rt_tests, ch, np.uint8).view(np.uint32).reshape(-1, 2)
+
+    def rt_packets(self, ch):
+        """burst channels: [(kind 'R'/'T', infofield bytes)] of every decoded R/T packet"""
+        raw = self._pop(self.lib.aero_pop_rt_packets, ch, np.uint8)
+        out, i = [], 0
+        while i < len(raw):
+            kind, ln = np.frombuffer(raw[i:i + 8].tobytes(), np.uint32)
+            out.append((chr(kind), bytes(raw[i + 8:i + 8 + int(ln)])))
+            i += 8 + int(ln)
+        return out
 
     def hops(self, ch):
         return self._pop(self.lib.aero_pop_hops, ch, np.float64, 6)

@@ -150,7 +150,7 @@ void PChannelHost::lookup_and_emit(const AcarsItem &in) {
   if (!fragments_only_) emit(p, false);
 }
 
-// ParserISU::parse (aerol.cpp:333-489), downlink = false on the P channel
+// ParserISU::parse (aerol.cpp:333-489); downlink is false on the P channel, true on R/T
 bool PChannelHost::parse(const IsuItem &isu) {
   if (isu.aesid == 0) return false;
   const std::string &ud = isu.userdata;
@@ -165,7 +165,7 @@ bool PChannelHost::parse(const IsuItem &isu) {
                        ((uint8_t)ud[15] == 0x83 || (uint8_t)ud[15] == 0x02);
   if (isacars) {
     an_ = AcarsItem();
-    an_.downlink = false;
+    an_.downlink = downlink_;
     an_.isu = isu;
     an_.mode = (uint8_t)ud[3] & 0x7F;
     an_.tak = (uint8_t)textish[11];
@@ -194,7 +194,7 @@ bool PChannelHost::parse(const IsuItem &isu) {
     return true;
   }
   an_ = AcarsItem();
-  an_.downlink = false;
+  an_.downlink = downlink_;
   an_.isu = isu;
   an_.nonacars = true;
   static const char *H = "0123456789ABCDEF";
@@ -273,6 +273,95 @@ void PChannelHost::frame(const uint8_t *info, int len, uint32_t okmask, int form
         break;
     }
     if (what) send_cassign(info, k, decline_prefix(su, k, formatid) + what);
+  }
+}
+
+// RISUData::update (decode/aerol.cpp:32-119) on the first 17 bytes of an R packet
+bool PChannelHost::risu_update(const uint8_t *d) {
+  for (size_t i = 0; i < risuitems_.size(); i++) {  // deleteoldisuitems
+    risuitems_[i].isu.count++;
+    if (risuitems_[i].isu.count > 10) {
+      risuitems_.erase(risuitems_.begin() + i);
+      i--;
+    }
+  }
+  const int byte1 = d[0], byte2 = d[1], byte3 = d[2], byte4 = d[3], byte5 = d[4], byte6 = d[5];
+  an_risu_ = RIsuItem();
+  an_risu_.seqind = ((byte1 & 0xF0) >> 4);
+  an_risu_.sutype = byte1 & 0x0F;
+  an_risu_.isu.qno = (uint8_t)((byte2 & 0xF0) >> 4);
+  an_risu_.isu.refno = (uint8_t)(byte2 & 0x07);
+  an_risu_.isu.aesid = (uint32_t)(byte3 << 16 | byte4 << 8 | byte5);
+  an_risu_.isu.gesid = (uint8_t)byte6;
+  int idx = -1;
+  if (an_risu_.sutype >= 1 && an_risu_.sutype <= 11)
+    for (size_t i = 0; i < risuitems_.size(); i++)
+      if (an_risu_.isu.gesid == risuitems_[i].isu.gesid && an_risu_.isu.aesid == risuitems_[i].isu.aesid &&
+          an_risu_.isu.qno == risuitems_[i].isu.qno && an_risu_.isu.refno == risuitems_[i].isu.refno) {
+        idx = (int)i;
+        break;
+      }
+  if (idx < 0) {
+    risuitems_.push_back(an_risu_);
+    idx = (int)risuitems_.size() - 1;
+  }
+  RIsuItem *p = &risuitems_[idx];
+  p->isu.count = 0;
+  int su_total = 0, su_index = 0;
+  switch (an_risu_.seqind) {
+    case 1: su_total = 1; su_index = 0; break;
+    case 2: su_total = 2; su_index = 0; break;
+    case 3: su_total = 2; su_index = 1; break;
+    case 4: su_total = 3; su_index = 0; break;
+    case 5: su_total = 3; su_index = 1; break;
+    case 6: su_total = 3; su_index = 2; break;
+    default: break;
+  }
+  int bytes_in_su = 0;
+  if ((an_risu_.sutype >= 1) && (an_risu_.sutype <= 11)) bytes_in_su = an_risu_.sutype;
+  const bool signaling = an_risu_.sutype == 15;
+  const int thisnum = 11 * su_total - 11 + bytes_in_su;
+  if (thisnum > 0) {
+    if (p->isu.userdata.size() == 0) p->isu.userdata.resize(thisnum);
+    if (thisnum < (int)p->isu.userdata.size()) p->isu.userdata.resize(thisnum);
+  }
+  if (!signaling) {
+    for (int i = 0 - 1 + 7; i < bytes_in_su - 1 + 7; i++) {
+      // QByteArray's operator[] grows the array on an out-of-range write
+      const size_t at = (size_t)(i + 11 * su_index + 1 - 7);
+      if (at >= p->isu.userdata.size()) p->isu.userdata.resize(at + 1, '\0');
+      p->isu.userdata[at] = (char)d[i];
+    }
+    p->filled |= (1 << su_index);
+  } else {
+    p->isu.userdata.clear();
+  }
+  if ((signaling) || ((p->filled == 7) && (su_total == 3)) || ((p->filled == 3) && (su_total == 2)) ||
+      ((p->filled == 1) && (su_total == 1))) {
+    risu_last_ = p->isu;
+    risuitems_.erase(risuitems_.begin() + idx);
+    return true;
+  }
+  return false;
+}
+
+void PChannelHost::rt_packet(bool r_packet, const uint8_t *info, int len, int nsus) {
+  downlink_ = true;
+  if (r_packet) {  // User_data_ISU_SSU_R_channel (aerol.cpp:1256-1290)
+    if (len >= 17 && (info[1] & 0x08) == 0x08 && risu_update(info)) parse(risu_last_);
+    return;
+  }
+  for (int k = 0; k < nsus; k++) {  // T channel SUs (aerol.cpp:1300-1460)
+    if (6 + k * 12 + 10 > len) break;
+    const uint8_t *su = info + 6 + k * 12;
+    int message = su[0];
+    if ((message & 0xC0) == 0xC0) message = -1;
+    bool missing;
+    if (message == 0x71) {
+      isu_update(su, missing);
+    } else if (message == -1) {
+      if (isu_update(su, missing)) parse(lastvalid_);
+    }
   }
 }
 

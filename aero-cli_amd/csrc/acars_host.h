@@ -36,9 +36,18 @@ class PChannelHost {
   // one GPU frame record: infofield bytes (len), crc-ok mask, format id
   void frame(const uint8_t *info, int len, uint32_t okmask, int formatid);
   void isu_reset() { isuitems_.clear(); }
+  // one decoded burst R/T packet (RTChannelDeleaveFECScram OK_R / OK_T):
+  // the R/T branch of AeroL::Decode (decode/aerol.cpp:1253-1460), items
+  // marked downlink (parser.downlink = burstmode)
+  void rt_packet(bool r_packet, const uint8_t *info, int len, int nsus);
   std::vector<aero_acars_item> items;
 
  private:
+  struct RIsuItem {  // RISUItem (decode/aerol.h:125-135)
+    IsuItem isu;
+    int seqind = 0, sutype = 0, filled = 0;
+  };
+  bool risu_update(const uint8_t *d);
   bool isu_update(const uint8_t *d, bool &missing);
   bool parse(const IsuItem &isu);
   bool defragment(AcarsItem &a);
@@ -48,6 +57,10 @@ class PChannelHost {
   void send_logon(const uint8_t *info, int k, const char *text);
 
   bool fragments_only_;
+  bool downlink_ = false;
+  std::vector<RIsuItem> risuitems_;
+  RIsuItem an_risu_;
+  IsuItem risu_last_;
   std::vector<IsuItem> isuitems_;
   IsuItem an_isu_, lastvalid_;
   AcarsItem an_;

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include "engine_common.h"
+#include "viterbi_dev.h"
 
 namespace aero {
 
@@ -234,22 +235,6 @@ __global__ __launch_bounds__(256) void frame_msk_kernel(DevState S, int nch) {
 }
 
 // ---------------------------------------------------------------- Viterbi
-__device__ __forceinline__ int conv_table(int r) {  // table[r]: bit j = parity(r & poly[j])
-  return (__builtin_popcount(r & 109) & 1) | ((__builtin_popcount(r & 79) & 1) << 1);
-}
-
-__device__ __forceinline__ int soft_dist(int hard, int a, int b) {  // metric_soft_distance_linear
-  const int x0 = (hard & 1) ? 255 : 0, x1 = (hard & 2) ? 255 : 0;
-  const int d0 = a - x0, d1 = b - x1;
-  return (d0 < 0 ? -d0 : d0) + (d1 < 0 ? -d1 : d1);
-}
-
-__device__ __forceinline__ int shfl_idx(int v, int src) {
-  return __builtin_amdgcn_ds_bpermute(src << 2, v);
-}
-
-constexpr int HCAP = 140, MINTB = 35, RENORM = 128;
-
 // BLK = interleaver block (N x 64 soft bits), N = BLK / 64; DL2 = dl2 length + 1
 template <int BLK, int DL2>
 __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, int trace) {
@@ -285,71 +270,7 @@ __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, in
   if (lane < 62) S.overlap[(size_t)c * 64 + lane] = sbuf[ov + BLK - 62 + lane];
 
   const int sets = nsoft / 2;
-  const int s = lane;
-  const int tab_lo = conv_table(s), tab_hi = conv_table(s | 64);
-  int m = 0;  // uint16 path metric of state s
-  // warmup (decode.c convolutional_decode_warmup): states reachable from 0
-  for (int i = 0; i < 6 && i < sets; ++i) {
-    const int a = sbuf[2 * i], b = sbuf[2 * i + 1];
-    const int prev = shfl_idx(m, s >> 1);
-    if (s < (2 << i)) m = (soft_dist(conv_table(s), a, b) + prev) & 0xFFFF;
-  }
-  int index = 0, len = 0, renorm = 0, outpos = 0;
-  auto search = [&](int skip) -> int {
-    // least metric among states s % skip == 0, lowest index on ties
-    int key = (s % skip == 0) ? ((m << 6) | s) : 0x7FFFFFFF;
-    for (int off = 32; off > 0; off >>= 1) {
-      const int o = __shfl_xor(key, off, 64);
-      key = o < key ? o : key;
-    }
-    return key & 63;
-  };
-  auto traceback = [&](int bestpath, int mintb) {
-    const int nout = len - mintb;
-    if (lane == 0) {
-      int idx = index;
-      for (int j = 0; j < len; ++j) {
-        idx = idx == 0 ? HCAP - 1 : idx - 1;
-        const int hb = (int)((hist[idx] >> bestpath) & 1ULL);
-        bestpath = (bestpath | (hb << 6)) >> 1;
-        if (j >= mintb) obits[outpos + (nout - 1 - (j - mintb))] = (uint8_t)hb;
-      }
-    }
-    outpos += nout;
-    len -= nout;
-    __syncthreads();
-  };
-  auto process = [&](int skip) {
-    index++;
-    if (index == HCAP) index = 0;
-    renorm++;
-    len++;
-    if (renorm == RENORM) {
-      renorm = 0;
-      const int best = search(skip);
-      const int mind = shfl_idx(m, best);
-      m = (m - mind) & 0xFFFF;
-      if (len == HCAP) traceback(best, MINTB);
-    } else if (len == HCAP) {
-      traceback(search(skip), MINTB);
-    }
-  };
-  for (int i = 6; i < sets; ++i) {
-    const int a = sbuf[2 * i], b = sbuf[2 * i + 1];
-    const bool tail = i >= sets - 6;
-    const int skip = tail ? (1 << (7 - (sets - i))) : 1;
-    const int m0 = shfl_idx(m, s >> 1), m1 = shfl_idx(m, (s >> 1) | 32);
-    const int e0 = (m0 + soft_dist(tab_lo, a, b)) & 0xFFFF;
-    const int e1 = (m1 + soft_dist(tab_hi, a, b)) & 0xFFFF;
-    const bool act = (s % skip) == 0;
-    const int h = (e0 <= e1) ? 0 : 1;
-    if (act) m = h ? e1 : e0;
-    const unsigned long long mask = __ballot(act && h);
-    if (lane == 0) hist[index] = mask;
-    __syncthreads();
-    process(skip);
-  }
-  traceback(0, 0);
+  viterbi_decode_wave(sbuf, nsoft, hist, obits, lane);
   // Decode_Continuous: keep decoded bits [25, 25 + BLK/2) clipped to size/2
   const int nbits = (sets - 25) < HALF ? (sets - 25) : HALF;
   if (trace) {

@@ -1,0 +1,969 @@
+/*
+ * burst.hip — burst-mode 10500-bps OQPSK on gfx950 (aero-decode --burst):
+ * BurstOqpskDemodulator::writeDataSlot (decode/burstoqpskdemodulator.cpp:262-703)
+ * and the burst branch of AeroL::Decode with RTChannelDeleaveFECScram
+ * (decode/aerol.cpp:1060-1240, decode/aerol.h:755-836).
+ *
+ *  hilbert_kernel      QJHilbertFilter on JFastFir (decode/DSP.cpp:730-761,
+ *                      decode/jfft.cpp:445-495): 8192-point overlap-add blocks of
+ *                      6145 samples, one workgroup per channel, into a
+ *                      time-major analytic-signal ring.
+ *  demod_burst_kernel  the per-sample recurrence, one channel per lane.  A lane
+ *                      stops where the reference runs its trident check
+ *                      (burstoqpskdemodulator.cpp:343-440) and resumes after
+ *                      trident_kernel has decided, at the same sample.
+ *  trident_kernel      FFTrWrapper<double>(32768) of both trident halves (a
+ *                      16384-point JFFT + split), |top| - |base|, the +-1792-bin
+ *                      trident search and the strongest base bin; one
+ *                      1024-thread workgroup per waiting channel.
+ *  frame_burst_kernel  AeroL burst framing (UW tolerance 4 within the muw window,
+ *                      dummy header, R/T block fill, tests at blockptr 320+192k).
+ *  rt_viterbi_kernel   one wave per R/T test: deinterleave 64 x blockptr/64 and
+ *                      Decode_soft of the whole block (jconvolutionalcodec.cpp:88-119).
+ * CRC checks and R/T packet handling run on the host (engine.hip).
+ *
+ * Bit-exactness rules as in demod_oqpsk.hip: -ffp-contract=off, reference
+ * operation order, GCC complex products, aero_math.h for libm.
+ */
+#include <hip/hip_runtime.h>
+
+#include "aero_math.h"
+#include "burst_common.h"
+#include "engine_common.h"
+#include "fft_dit.h"
+#include "viterbi_dev.h"
+
+namespace aero {
+
+namespace {
+
+constexpr double SPS = 2.0 * 48000.0 / 10500.0;  // SamplesPerSymbol
+constexpr uint32_t BUW = 0xE15AE893u;
+
+__constant__ double c_bsr_b[3];  // st_iir_resonator (burstoqpskdemodulator.cpp:220-227)
+__constant__ double c_bsr_a[3];
+
+__device__ __forceinline__ int b_cis_index(double WTptr) {  // WaveTable::WTCISValue (DSP.cpp:81-88)
+  int tint = (int)WTptr;
+  if (tint >= WTSIZE) tint = 0;
+  if (tint < 0) tint = WTSIZE - 1;
+  return tint;
+}
+
+__device__ __forceinline__ void b_nco_next(double &ptr, double &step) {  // WTnextFrame (DSP.cpp:71-79)
+  if (step < 0) step = 0;
+  ptr += step;
+  while (((int)ptr) >= WTSIZE) ptr -= WTSIZE;
+}
+
+__device__ __forceinline__ void b_set_freq(double &freq, double &step, double f) {  // SetFreq (DSP.cpp:163-168)
+  freq = f;
+  if (freq < 0) freq = 0;
+  step = (freq) * ((double)WTSIZE) / 48000.0;
+}
+
+__device__ __forceinline__ void b_set_phase_deg(double &ptr, double phase_deg) {  // SetPhaseDeg (DSP.cpp:177-187)
+  phase_deg = fmod(phase_deg, 360.0);
+  while (phase_deg < 0) phase_deg += 360.0;
+  ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+}
+
+__device__ __forceinline__ void b_advance(double &ptr, double frac) {  // AdvanceFractionOfWave (DSP.h:59-65)
+  ptr += frac * WTSIZE;
+  while (ptr >= WTSIZE) ptr -= WTSIZE;
+  while (ptr < 0) ptr += WTSIZE;
+}
+
+__device__ __forceinline__ int b_qround(double d) {  // qRound (Qt 5.9 qglobal.h:525)
+  return d >= 0.0 ? int(d + 0.5) : int(d - double(int(d - 1)) + 0.5) + int(d - 1);
+}
+
+// std::exp(complex(0 * y, y)) as glibc's cexp returns it: (cos y, sin y), or
+// (1, y) when |y| <= DBL_MIN
+__device__ __forceinline__ void b_cexp_i(double y, double &c, double &s) {
+  if (fabs(y) > 2.2250738585072014e-308) {
+    aero_sincos(y, s, c);
+  } else {
+    s = y;
+    c = 1.0;
+  }
+}
+
+// Delay<T>::update (DSP.h:365-384) on a time-major ring with per-pointer weights
+struct DlyRef {
+  const double *w, *omw;
+  const int *io;
+  int size;
+};
+__device__ __forceinline__ double dly_update(double *ring, int C, int &p, const DlyRef &d, double sig) {
+  ring[(size_t)p * C] = sig;
+  const int io = d.io[p], in = io + 1 == d.size ? 0 : io + 1;
+  const double older = ring[(size_t)io * C], newer = ring[(size_t)in * C];
+  const double w = d.w[p], om = d.omw[p];
+  p = p + 1 == d.size ? 0 : p + 1;
+  return (w * newer + om * older);
+}
+__device__ __forceinline__ double2 dly_update2(double2 *ring, int C, int &p, const DlyRef &d, double2 sig) {
+  ring[(size_t)p * C] = sig;
+  const int io = d.io[p], in = io + 1 == d.size ? 0 : io + 1;
+  const double2 older = ring[(size_t)io * C], newer = ring[(size_t)in * C];
+  const double w = d.w[p], om = d.omw[p];
+  p = p + 1 == d.size ? 0 : p + 1;
+  return make_double2(w * newer.x + om * older.x, w * newer.y + om * older.y);
+}
+
+__device__ __forceinline__ DlyRef dref(const BurstTables &T, int k) { return {T.dw[k], T.domw[k], T.dio[k], T.dsize[k]}; }
+
+}  // namespace
+
+// ------------------------------------------------------------ Hilbert FIR
+// Kernel spectrum: JFFT of the zero-padded 2048-tap kernel (JFastFir ctor).
+__global__ __launch_bounds__(512) void hk_spectrum_kernel(BurstTables T, double2 *hk) {
+  constexpr int L = 13, PADDED = HB_N + HB_N / 16;
+  __shared__ double lds[PADDED];
+  __shared__ double2 s_tw[TwLds<L>::LEN];
+  const int t = threadIdx.x;
+  load_tw_lds<L>(s_tw, T.tw8, t, 512);
+  __syncthreads();
+  double2 x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = T.hk_time[bitrev<L>(epos<L, 0>(t, i))];
+  fft_dit<L, false>(x, t, lds, T.tw8, s_tw);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) hk[epos<L, 3>(t, i)] = x[i];
+}
+
+// JFastFir::update (decode/jfft.cpp:445-495): for every complete block j of
+// 6145 inputs (pcm / 32768, 0): y = IFFT(FFT(block, zeros) * K) (JFFT scales
+// the inverse by 1/N); y[0 .. 2047) += previous remainder; outputs y[0 .. 6145)
+// are the analytic samples of inputs (j + 1) * 6145 + p; y[6145 ..) is the
+// next remainder.  Inputs 0 .. 6144 come out as zeros (the initial buffer).
+__global__ __launch_bounds__(512) void hilbert_kernel(BurstState S, BurstTables T, int nch) {
+  constexpr int L = 13, PADDED = HB_N + HB_N / 16;
+  __shared__ double lds[PADDED];
+  __shared__ double2 s_tw[TwLds<L>::LEN];
+  const int c = blockIdx.x, t = threadIdx.x;
+  if (c >= nch) return;
+  const int C = S.C;
+  load_tw_lds<L>(s_tw, T.tw8, t, 512);
+  __syncthreads();
+  long long j = S.ls[BL_HB_DONE * C + c];
+  const long long avail = S.ls[BL_AVAIL * C + c];
+  const long long capm = S.pcm_cap - 1;
+  double2 *rem = S.hb_rem + (size_t)c * HB_REM;
+  for (; (j + 1) * HB_SNZ <= avail; ++j) {
+    double2 x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int p = bitrev<L>(epos<L, 0>(t, i));
+      if (p < HB_SNZ) {
+        const long long s = j * HB_SNZ + p;
+        x[i] = make_double2(((double)S.pcm[(size_t)(s & capm) * C + c]) / 32768.0, 0.0);
+      } else {
+        x[i] = make_double2(0.0, 0.0);
+      }
+    }
+    fft_dit<L, false>(x, t, lds, T.tw8, s_tw);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {  // sigspace[k] *= kernel[k]
+      const double2 k = T.hk[epos<L, 3>(t, i)];
+      x[i] = make_double2(x[i].x * k.x - x[i].y * k.y, x[i].x * k.y + x[i].y * k.x);
+    }
+    exchange<L, 3, 0, true>(x, t, lds);
+    fft_dit<L, true>(x, t, lds, T.twi8, s_tw);
+    double2 r[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      x[i].x *= (1.0 / ((double)HB_N));
+      x[i].y *= (1.0 / ((double)HB_N));
+      const int p = epos<L, 3>(t, i);
+      r[i] = p < HB_REM ? rem[p] : make_double2(0.0, 0.0);
+    }
+    __syncthreads();  // every old remainder read before it is replaced
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int p = epos<L, 3>(t, i);
+      if (p < HB_SNZ) {
+        double2 y = x[i];
+        if (p < HB_REM) y = make_double2(y.x + r[i].x, y.y + r[i].y);
+        const long long s = (j + 1) * HB_SNZ + p;
+        S.ana[(size_t)(s & (ANA_LEN - 1)) * C + c] = y;
+      } else {
+        rem[p - HB_SNZ] = x[i];
+      }
+    }
+    __syncthreads();
+  }
+  if (t == 0) S.ls[BL_HB_DONE * C + c] = j;
+}
+
+// ----------------------------------------------------------------- demod
+constexpr int BD_BLOCK = 128;  // channels per workgroup: both RRC halves in LDS (110 KB)
+
+__global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, BurstTables T, int nch, int max_n,
+                                                               int trace) {
+  __shared__ double s_qre[NTAPS][BD_BLOCK];
+  __shared__ double s_qim[NTAPS][BD_BLOCK];
+  __shared__ double s_taps[NTAPS];
+  if (threadIdx.x < NTAPS) s_taps[threadIdx.x] = T.taps[threadIdx.x];
+  __syncthreads();
+  const int c = blockIdx.x * BD_BLOCK + threadIdx.x, col = threadIdx.x;
+  if (c >= nch) return;
+  const int C = S.C;
+  double *ds = S.ds + c;
+  int *is = S.is + c;
+  long long *ls = S.ls + c;
+  int pend = is[BI_PEND * C];
+  if (pend == 1) return;  // trident check outstanding
+  const long long n0 = ls[BL_NSAMP * C];
+  long long end = ls[BL_AVAIL * C];
+  if (end - n0 > max_n) end = n0 + max_n;
+  if (n0 >= end && pend != 2) return;
+
+  double m2_ptr = ds[BD_M2_PTR * C], m2_step = ds[BD_M2_STEP * C], m2_freq = ds[BD_M2_FREQ * C];
+  double so_ptr = ds[BD_SO_PTR * C], so_last = ds[BD_SO_LAST * C], so_step = ds[BD_SO_STEP * C];
+  double so_freq = ds[BD_SO_FREQ * C];
+  double q_ptr = ds[BD_Q_PTR * C], q_step = ds[BD_Q_STEP * C];
+  double agc_sum = ds[BD_AGC_SUM * C], agc2_sum = ds[BD_AGC2_SUM * C];
+  double ma1r = ds[BD_MA1_RE * C], ma1i = ds[BD_MA1_IM * C], mav1_sum = ds[BD_MAV1_SUM * C];
+  double pd_lastdy = ds[BD_PD_LASTDY * C], vol_gain = ds[BD_VOL_GAIN * C];
+  double srx1 = ds[BD_SR_X1 * C], srx2 = ds[BD_SR_X2 * C], sry1 = ds[BD_SR_Y1 * C], sry2 = ds[BD_SR_Y2 * C];
+  double ave_r = ds[BD_AVE_RE * C], ave_i = ds[BD_AVE_IM * C], rot_r = ds[BD_ROT_RE * C], rot_i = ds[BD_ROT_IM * C];
+  double str_r = ds[BD_STR_RE * C], str_i = ds[BD_STR_IM * C];
+  double ptd_r = ds[BD_PTD_RE * C], ptd_i = ds[BD_PTD_IM * C], s2l_r = ds[BD_S2L_RE * C], s2l_i = ds[BD_S2L_IM * C];
+  double rotf = ds[BD_ROTF * C], mse = ds[BD_MSE * C], lastmse = ds[BD_LASTMSE * C];
+  double msema_sum = ds[BD_MSEMA_SUM * C];
+  int agc_p = is[BI_AGC_P * C], agc2_p = is[BI_AGC2_P * C], d1_p = is[BI_D1_P * C], d2_p = is[BI_D2_P * C];
+  int ma1_p = is[BI_MA1_P * C], mav1_p = is[BI_MAV1_P * C];
+  int dlp[BDL_COUNT];
+#pragma unroll
+  for (int k = 0; k < BDL_COUNT; ++k) dlp[k] = is[(BI_DL_P0 + k) * C];
+  int pd1_p = is[BI_PD1_P * C], pd2_p = is[BI_PD2_P * C], pd3_p = is[BI_PD3_P * C];
+  int pd_cntdown = is[BI_PD_CNTDOWN * C], pd_maxposcd = is[BI_PD_MAXPOSCD * C];
+  int tri_ptr = is[BI_TRI_PTR * C], msema_p = is[BI_MSEMA_P * C];
+  int startstop = is[BI_STARTSTOP * C], cntr = is[BI_CNTR * C], insertpre = is[BI_INSERTPRE * C];
+  int yui = is[BI_YUI * C];
+  long long sp = ls[BL_SP * C], scommit = ls[BL_SCOMMIT * C];
+  const long long scons = ls[BL_SCONS * C];
+  long long chunk_h = ls[BL_CHUNK_H * C];
+  const long long chunk_n = ls[BL_CHUNK_N * C];
+  int hop_n = is[BI_HOP_N * C];
+#pragma unroll 1
+  for (int j = 0; j < NTAPS; ++j) {
+    s_qre[j][col] = S.fir[(size_t)j * C + c];
+    s_qim[j][col] = S.fir[(size_t)(NTAPS + j) * C + c];
+  }
+  int16_t *soft = S.soft + (size_t)c * B_SOFT_RING;
+  const long long *chunks = S.chunks + (size_t)c * CHUNK_RING;
+  const double PT = 0.4 * WTSIZE;  // IfHavePassedPoint(ee), ee = 0.4
+  const DlyRef dS = dref(T, BDL_S), d41 = dref(T, BDL_41), d42 = dref(T, BDL_42), d8 = dref(T, BDL_8);
+  const DlyRef dA1 = dref(T, BDL_A1), dBT = dref(T, BDL_BT), dMD = dref(T, BDL_MADIFF);
+
+  long long n = n0;
+  bool resume = pend == 2;
+  while (resume || n < end) {
+    double vtd;  // val_to_demod
+    if (!resume) {
+      if (sp - scons > B_SOFT_RING - 64) break;  // soft ring full: framing frees it next
+      // lastmse is captured at the start of every message (burstoqpskdemodulator.cpp:264)
+      while (chunk_h < chunk_n && chunks[chunk_h & (CHUNK_RING - 1)] == n) {
+        lastmse = mse;
+        chunk_h++;
+      }
+      const double2 a = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
+      double cr = a.x, ci = a.y;
+      {  // agc.Update(|cval|); cval *= AGCVal (:316-317)
+        const double av = aero_hypot(cr, ci);
+        double *ring = S.agc + (size_t)agc_p * C + c;
+        agc_sum = agc_sum - *ring;
+        agc_sum = agc_sum + fabs(av);
+        *ring = fabs(av);
+        agc_p = agc_p + 1 == B_AGC ? 0 : agc_p + 1;
+        double g = 1.414213562 / fmax(agc_sum / ((double)B_AGC), 0.000001);
+        g = fmax(g, 0.000001);
+        cr *= g;
+        ci *= g;
+      }
+      double2 cvd;  // d1.update_dont_touch(cval)
+      S.d1[(size_t)d1_p * C + c] = make_double2(cr, ci);
+      d1_p = d1_p + 1 == B_D1 ? 0 : d1_p + 1;
+      cvd = S.d1[(size_t)d1_p * C + c];
+      S.d2[(size_t)d2_p * C + c] = cvd.x;  // d2.update_dont_touch(real(cval_d))
+      d2_p = d2_p + 1 == B_D2 ? 0 : d2_p + 1;
+      vtd = S.d2[(size_t)d2_p * C + c];
+      double fastarm;
+      {  // burst-timing statistic (:326-339)
+        const double2 bd = dly_update2(reinterpret_cast<double2 *>(S.dl[BDL_BT]) + c, C, dlp[BDL_BT], dBT,
+                                       make_double2(cr, ci));
+        const double pr = cr * bd.x - ci * (-bd.y), pi = cr * (-bd.y) + ci * bd.x;  // cval * conj(bd)
+        double2 *mr = S.ma1 + (size_t)ma1_p * C + c;
+        const double2 old = *mr;
+        ma1r = ma1r - old.x;
+        ma1i = ma1i - old.y;
+        ma1r = ma1r + pr;
+        ma1i = ma1i + pi;
+        *mr = make_double2(pr, pi);
+        ma1_p = ma1_p + 1 == B_MA ? 0 : ma1_p + 1;
+        fastarm = aero_hypot(ma1r / ((double)B_MA), ma1i / ((double)B_MA));
+        double *mv = S.mav1 + (size_t)mav1_p * C + c;
+        mav1_sum = mav1_sum - *mv;
+        mav1_sum = mav1_sum + (fastarm);
+        *mv = fastarm;
+        mav1_p = mav1_p + 1 == B_MA ? 0 : mav1_p + 1;
+        fastarm = mav1_sum / ((double)B_MA);
+        fastarm -= dly_update(S.dl[BDL_MADIFF] + c, C, dlp[BDL_MADIFF], dMD, fastarm);
+        if (fastarm < 0) fastarm = 0;
+      }
+      double bt = fastarm * fastarm;
+      if (bt > 500) bt = 500;
+      {  // PeakDetector::update (DSP.h:491-566)
+        double val = bt;
+        double *r3 = S.pd3 + (size_t)pd3_p * C + c;
+        *r3 = val;
+        pd3_p = pd3_p + 1 == B_PD3 ? 0 : pd3_p + 1;
+        double *r1 = S.pd1 + (size_t)pd1_p * C + c;
+        *r1 = val;
+        pd1_p = pd1_p + 1 == B_PD1 ? 0 : pd1_p + 1;
+        const double dy = val - S.pd1[(size_t)pd1_p * C + c];
+        S.pd2[(size_t)pd2_p * C + c] = val;
+        pd2_p = pd2_p + 1 == B_PD2 ? 0 : pd2_p + 1;
+        val = S.pd2[(size_t)pd2_p * C + c];  // d2.update(val)
+        if ((!pd_cntdown) && (val > 0.2) && ((pd_lastdy >= 0 && dy < 0))) {
+          pd_cntdown = B_PD_MAXCD;
+          // d3.findmaxpos: first maximum, scanning from the oldest slot
+          int q = pd3_p, maxpos = 0;
+          double maxval = S.pd3[(size_t)q * C + c];
+          for (int i = 0; i < B_PD3; i++) {
+            const double v = S.pd3[(size_t)q * C + c];
+            if (v > maxval) {
+              maxval = v;
+              maxpos = i;
+            }
+            q = q + 1 == B_PD3 ? 0 : q + 1;
+          }
+          pd_maxposcd = maxpos;
+        }
+        if (pd_cntdown > 0) pd_cntdown--;
+        pd_lastdy = dy;
+        bool hit = false;
+        if (!pd_maxposcd) {
+          pd_maxposcd--;
+          hit = true;
+        } else if (pd_maxposcd > 0) {
+          pd_maxposcd--;
+        }
+        if (hit) tri_ptr = 0;
+      }
+      if (tri_ptr < B_TRI) {
+        S.tri[(size_t)c * B_TRI + tri_ptr] = cvd.x;
+        tri_ptr++;
+      } else if (tri_ptr == B_TRI) {
+        tri_ptr++;
+        ds[BD_RESUME_VAL * C] = vtd;
+        pend = 1;  // trident_kernel decides, this sample resumes after it
+        break;
+      }
+    } else {
+      vtd = ds[BD_RESUME_VAL * C];
+      // trident decision (burstoqpskdemodulator.cpp:393-411)
+      if (is[BI_TRI_DET * C]) {
+        const double carrierphase = aero_atan2(ds[BD_TRI_BIM * C], ds[BD_TRI_BRE * C]) - (M_PI / 4.0);
+        b_set_freq(m2_freq, m2_step, (48000.0 / 32768.0) * (double)is[BI_TRI_MINBIN * C]);
+        b_set_phase_deg(m2_ptr, (180.0 / M_PI) * carrierphase);
+        vol_gain = 1.4142 * 500.0 / ds[BD_TRI_MINVAL * C];
+        b_set_freq(so_freq, so_step, 10500.0);
+        b_set_phase_deg(so_ptr, 0);
+        srx1 = srx2 = sry1 = sry2 = 0;
+        startstop = B_STARTSTOP;
+        cntr = 0;
+        rot_r = 1;
+        rot_i = 0;
+        insertpre = 1;
+        rotf = 0;
+        ave_r = 1;
+        ave_i = 0;
+        mse = 0;
+        double *mm = S.msema + (size_t)c * B_MSEMA;
+        for (int k = 0; k < B_MSEMA; k++) mm[k] = 0;
+        msema_sum = 0;
+        msema_p = 0;
+      }
+      if (trace && hop_n < S.hop_cap) {
+        double *h = S.hops + ((size_t)c * S.hop_cap + hop_n) * 6;
+        h[0] = (double)n;
+        h[1] = is[BI_TRI_DET * C] ? 1.0 : 0.0;
+        h[2] = m2_freq;
+        h[3] = vol_gain;
+        h[4] = ds[BD_TRI_MAXVAL * C];
+        h[5] = (double)is[BI_TRI_MINBIN * C];
+      }
+      hop_n++;
+      resume = false;
+      pend = 0;
+    }
+    // ---- part B (:450-702)
+    double s2r, s2i;
+    {
+      const double2 m2 = T.cis[b_cis_index(m2_ptr)];
+      const double sc = vol_gain * vtd;
+      const double ddr = m2.x * sc, ddi = m2.y * sc;
+      // RRC, transposed form (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
+      s2r = s_qre[NTAPS - 1][col];
+      s2i = s_qim[NTAPS - 1][col];
+      for (int j = NTAPS - 1; j >= 1; --j) {
+        s_qre[j][col] = s_qre[j - 1][col] + s_taps[j] * ddr;
+        s_qim[j][col] = s_qim[j - 1][col] + s_taps[j] * ddi;
+      }
+      s_qre[0][col] = 0.0 + s_taps[0] * ddr;
+      s_qim[0][col] = 0.0 + s_taps[0] * ddi;
+    }
+    if (startstop > 0) {
+      startstop--;
+      if (cntr < 1000000) cntr++;
+      if (mse < 0.75) startstop = B_STARTSTOP;
+    }
+    if (startstop == 0) startstop--;
+    if ((cntr > ((256 - 10) * SPS)) && insertpre) {
+      soft[sp & (B_SOFT_RING - 1)] = B_SOFT_MARK;
+      sp++;
+      insertpre = 0;
+    }
+    if ((cntr > SPS * (128 + 10)) && (cntr < ((256 - 10) * SPS))) {  // symbol-tone PLL (:462-474)
+      const double progress =
+          (((double)cntr) - (SPS * (128 + 10))) / (((256 - 10) * SPS) - (SPS * (128 + 10)));
+      const double t1r = s2r * str_r - s2i * str_i, t1i = s2r * str_i + s2i * str_r;
+      const double spr = t1r * 0.0 - t1i * 1.0, spi = t1r * 1.0 + t1i * 0.0;  // * imag
+      const double er = aero_tanh(spi) * (spr);
+      double ec, es;
+      b_cexp_i(er * 0.01, ec, es);
+      const double nr = str_r * ec - str_i * es, ni = str_r * es + str_i * ec;
+      str_r = nr;
+      str_i = ni;
+      ave_r = ave_r * 0.95 + 0.05 * str_r;
+      ave_i = ave_i * 0.95 + 0.05 * str_i;
+      const double spi2 = dly_update(S.dl[BDL_A1] + c, C, dlp[BDL_A1], dA1, spr);
+      const double2 qv = T.cis[b_cis_index(q_ptr)];
+      const double er_r = qv.x * spr - qv.y * (-spi2), er_i = qv.x * (-spi2) + qv.y * spr;
+      double st_err = aero_atan2(er_i, er_r);
+      st_err *= 1.5 * (1.0 - progress * progress);
+      b_advance(q_ptr, -(1.0 / (2.0 * M_PI)) * st_err * 0.1);
+      b_set_phase_deg(so_ptr, (360.0 * q_ptr / ((double)WTSIZE)) * 4.0 + (360.0 * 0.4));
+    }
+    {  // sig2 *= symboltone_averotator; rotator *= exp(i rotator_freq); sig2 *= rotator
+      const double ar = s2r * ave_r - s2i * ave_i, ai = s2r * ave_i + s2i * ave_r;
+      double ec, es;
+      b_cexp_i(rotf, ec, es);
+      const double rr = rot_r * ec - rot_i * es, ri = rot_r * es + rot_i * ec;
+      rot_r = rr;
+      rot_i = ri;
+      s2r = ar * rot_r - ai * rot_i;
+      s2i = ar * rot_i + ai * rot_r;
+    }
+    {  // agc2 (AGC(SPS*64/Fs)) and clip (:478-481)
+      const double sa = aero_hypot(s2r, s2i);
+      double *ring = S.agc2 + (size_t)agc2_p * C + c;
+      agc2_sum = agc2_sum - *ring;
+      agc2_sum = agc2_sum + fabs(sa);
+      *ring = fabs(sa);
+      agc2_p = agc2_p + 1 == B_AGC2 ? 0 : agc2_p + 1;
+      double g = 1.414213562 / fmax(agc2_sum / ((double)B_AGC2), 0.000001);
+      g = fmax(g, 0.000001);
+      s2r *= g;
+      s2i *= g;
+    }
+    const double abval = aero_hypot(s2r, s2i);
+    if (abval > 2.84) {
+      const double k = 2.84 / abval;
+      s2r = k * s2r;
+      s2i = k * s2i;
+    }
+    {  // symbol timing (:482-496)
+      const double st_diff = dly_update(S.dl[BDL_S] + c, C, dlp[BDL_S], dS, abval * abval) - (abval * abval);
+      const double st_d1out = dly_update(S.dl[BDL_41] + c, C, dlp[BDL_41], d41, st_diff);
+      const double st_d2out = dly_update(S.dl[BDL_42] + c, C, dlp[BDL_42], d42, st_d1out);
+      double st_eta = (st_d2out - st_diff) * st_d1out;
+      {  // st_iir_resonator.update(st_eta)
+        double y = 0;
+        y += srx2 * c_bsr_b[2];
+        y += srx1 * c_bsr_b[1];
+        y += st_eta * c_bsr_b[0];
+        y -= sry2 * c_bsr_a[2];
+        y -= sry1 * c_bsr_a[1];
+        srx2 = srx1;
+        srx1 = st_eta;
+        sry2 = sry1;
+        sry1 = y;
+        if (cntr > SPS * (128 + 128)) st_eta = y;
+      }
+      const double m1r = st_eta, m1i = -dly_update(S.dl[BDL_8] + c, C, dlp[BDL_8], d8, st_eta);
+      const double2 so = T.cis[b_cis_index(so_ptr)];
+      const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
+      const double st_angle_error = aero_atan2(oim, ore);
+      if (cntr > SPS * (128 + 64)) {
+        b_set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
+        b_advance(so_ptr, -st_angle_error * 0.01 / 360.0);
+      }
+      if (so_freq < (10500.0 - 0.1)) b_set_freq(so_freq, so_step, (10500.0 - 0.1));
+      if (so_freq > (10500.0 + 0.1)) b_set_freq(so_freq, so_step, (10500.0 + 0.1));
+    }
+    {  // IfHavePassedPoint(ee) (DSP.cpp:222-238) and the symbol step (:497-554)
+      double tl = so_last - PT, tw = so_ptr - PT;
+      if (tl < 0.0) tl += WTSIZE;
+      if (tw < 0.0) tw += WTSIZE;
+      if ((tl > 3.0 * WTSIZE / 4.0) && (tw < 1.0 * WTSIZE / 4.0)) {
+        const double pt_last = tw / so_step;
+        const double pt_this = 1.0 - pt_last;
+        const double ptr_ = pt_this * s2r + pt_last * s2l_r, pti = pt_this * s2i + pt_last * s2l_i;
+        const double twospeed =
+            -4.0 * ((fmod((360.0 * q_ptr / ((double)WTSIZE)) * 2.0 + (360.0 * 0.4 * 0.5), 360.0) / 360.0) -
+                    (0.34046 + 0.4111 * 0.4));
+        const bool even = !(twospeed < 0);
+        yui++;
+        yui %= 2;
+        if (cntr < ((128 + 128) * SPS)) {
+          if ((even && yui == 1) || (!even && yui == 0)) {
+            yui++;
+            yui %= 2;
+          }
+        }
+        if (!yui) {
+          ptd_r = ptr_;
+          ptd_i = pti;
+        } else {
+          const double qr = ptr_, qi = ptd_i;  // pt_qpsk
+          const double ct_xt = aero_tanh(pti) * ptr_;
+          const double ct_xt_d = aero_tanh(ptd_r) * ptd_i;
+          double ct_ec = ct_xt_d - ct_xt;
+          if (ct_ec > M_PI) ct_ec = M_PI;
+          if (ct_ec < -M_PI) ct_ec = -M_PI;
+          if (ct_ec > M_PI_2) ct_ec = M_PI_2;
+          if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
+          if (cntr > ((128 + 10) * SPS)) {
+            double ec, es;
+            b_cexp_i(ct_ec * 0.1, ec, es);
+            const double rr = rot_r * ec - rot_i * es, ri = rot_r * es + rot_i * ec;
+            rot_r = rr;
+            rot_i = ri;
+            rotf = rotf + ct_ec * 0.0001;
+          }
+          if (cntr > ((128 + 10) * SPS)) {  // msema.Update (DSP.cpp:405-416)
+            const double tda = (fabs(qr) - 1.0), tdb = (fabs(qi) - 1.0);
+            const double v = (tda * tda) + (tdb * tdb);
+            double *mm = S.msema + (size_t)c * B_MSEMA;
+            msema_sum = msema_sum - mm[msema_p];
+            msema_sum = msema_sum + fabs(v);
+            mm[msema_p] = fabs(v);
+            msema_p = msema_p + 1 == B_MSEMA ? 0 : msema_p + 1;
+            mse = msema_sum / ((double)B_MSEMA);
+          }
+          if (startstop > 0) {
+            int ibit = b_qround(0.75 * qi * 127.0 + 128.0);
+            if (ibit > 255) ibit = 255;
+            if (ibit < 0) ibit = 0;
+            soft[sp & (B_SOFT_RING - 1)] = (int16_t)ibit;
+            sp++;
+            ibit = b_qround(0.75 * qr * 127.0 + 128.0);
+            if (ibit > 255) ibit = 255;
+            if (ibit < 0) ibit = 0;
+            soft[sp & (B_SOFT_RING - 1)] = (int16_t)ibit;
+            sp++;
+            if (sp - scommit >= 32) {  // RxDataBits emitted or dropped as a group (:548-551)
+              if (mse < 0.6 || lastmse < 0.6) {
+                soft[(sp - 1) & (B_SOFT_RING - 1)] |= B_SOFT_LAST;
+                scommit = sp;
+              } else {
+                sp = scommit;
+              }
+            }
+          }
+        }
+      }
+    }
+    s2l_r = s2r;
+    s2l_i = s2i;
+    b_nco_next(m2_ptr, m2_step);
+    so_last = so_ptr;
+    b_nco_next(so_ptr, so_step);
+    b_nco_next(q_ptr, q_step);
+    n++;
+  }
+  // state back
+#pragma unroll 1
+  for (int j = 0; j < NTAPS; ++j) {
+    S.fir[(size_t)j * C + c] = s_qre[j][col];
+    S.fir[(size_t)(NTAPS + j) * C + c] = s_qim[j][col];
+  }
+  ds[BD_M2_PTR * C] = m2_ptr;
+  ds[BD_M2_STEP * C] = m2_step;
+  ds[BD_M2_FREQ * C] = m2_freq;
+  ds[BD_SO_PTR * C] = so_ptr;
+  ds[BD_SO_LAST * C] = so_last;
+  ds[BD_SO_STEP * C] = so_step;
+  ds[BD_SO_FREQ * C] = so_freq;
+  ds[BD_Q_PTR * C] = q_ptr;
+  ds[BD_Q_STEP * C] = q_step;
+  ds[BD_AGC_SUM * C] = agc_sum;
+  ds[BD_AGC2_SUM * C] = agc2_sum;
+  ds[BD_MA1_RE * C] = ma1r;
+  ds[BD_MA1_IM * C] = ma1i;
+  ds[BD_MAV1_SUM * C] = mav1_sum;
+  ds[BD_PD_LASTDY * C] = pd_lastdy;
+  ds[BD_VOL_GAIN * C] = vol_gain;
+  ds[BD_SR_X1 * C] = srx1;
+  ds[BD_SR_X2 * C] = srx2;
+  ds[BD_SR_Y1 * C] = sry1;
+  ds[BD_SR_Y2 * C] = sry2;
+  ds[BD_AVE_RE * C] = ave_r;
+  ds[BD_AVE_IM * C] = ave_i;
+  ds[BD_ROT_RE * C] = rot_r;
+  ds[BD_ROT_IM * C] = rot_i;
+  ds[BD_STR_RE * C] = str_r;
+  ds[BD_STR_IM * C] = str_i;
+  ds[BD_PTD_RE * C] = ptd_r;
+  ds[BD_PTD_IM * C] = ptd_i;
+  ds[BD_S2L_RE * C] = s2l_r;
+  ds[BD_S2L_IM * C] = s2l_i;
+  ds[BD_ROTF * C] = rotf;
+  ds[BD_MSE * C] = mse;
+  ds[BD_LASTMSE * C] = lastmse;
+  ds[BD_MSEMA_SUM * C] = msema_sum;
+  is[BI_AGC_P * C] = agc_p;
+  is[BI_AGC2_P * C] = agc2_p;
+  is[BI_D1_P * C] = d1_p;
+  is[BI_D2_P * C] = d2_p;
+  is[BI_MA1_P * C] = ma1_p;
+  is[BI_MAV1_P * C] = mav1_p;
+#pragma unroll
+  for (int k = 0; k < BDL_COUNT; ++k) is[(BI_DL_P0 + k) * C] = dlp[k];
+  is[BI_PD1_P * C] = pd1_p;
+  is[BI_PD2_P * C] = pd2_p;
+  is[BI_PD3_P * C] = pd3_p;
+  is[BI_PD_CNTDOWN * C] = pd_cntdown;
+  is[BI_PD_MAXPOSCD * C] = pd_maxposcd;
+  is[BI_TRI_PTR * C] = tri_ptr;
+  is[BI_MSEMA_P * C] = msema_p;
+  is[BI_STARTSTOP * C] = startstop;
+  is[BI_CNTR * C] = cntr;
+  is[BI_INSERTPRE * C] = insertpre;
+  is[BI_YUI * C] = yui;
+  is[BI_PEND * C] = pend;
+  is[BI_HOP_N * C] = hop_n;
+  ls[BL_NSAMP * C] = n;
+  ls[BL_SP * C] = sp;
+  ls[BL_SCOMMIT * C] = scommit;
+  ls[BL_CHUNK_H * C] = chunk_h;
+}
+
+// --------------------------------------------------------- trident check
+// burstoqpskdemodulator.cpp:343-392 for every channel waiting on it
+__global__ __launch_bounds__(1024) void trident_kernel(BurstState S, BurstTables T, int nch) {
+  constexpr int L = 14, N = TRI_N, FT = N / 16, PADDED = N + N / 16;
+  __shared__ double lds[PADDED];
+  __shared__ double2 s_tw[TwLds<L>::LEN];
+  __shared__ double red_v[FT / 64];
+  __shared__ int red_i[FT / 64];
+  __shared__ double2 s_best;
+  const int c = blockIdx.x, t = threadIdx.x;
+  if (c >= nch) return;
+  const int C = S.C;
+  if (S.is[BI_PEND * C + c] != 1) return;  // uniform per workgroup
+  load_tw_lds<L>(s_tw, T.tw16, t, FT);
+  const double *tb = S.tri + (size_t)c * B_TRI;
+  double *absb = S.tri_abs + (size_t)c * N;
+  // block reduction: larger value, then smaller index
+  auto reduce = [&](double v, int idx, double &bv, int &bi) {
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ov = __shfl_down(v, off, 64);
+      const int oi = __shfl_down(idx, off, 64);
+      if (ov > v || (ov == v && oi < idx)) {
+        v = ov;
+        idx = oi;
+      }
+    }
+    __syncthreads();
+    if ((t & 63) == 0) {
+      red_v[t >> 6] = v;
+      red_i[t >> 6] = idx;
+    }
+    __syncthreads();
+    bv = red_v[0];
+    bi = red_i[0];
+    for (int w = 1; w < FT / 64; ++w)
+      if (red_v[w] > bv || (red_v[w] == bv && red_i[w] < bi)) {
+        bv = red_v[w];
+        bi = red_i[w];
+      }
+  };
+  double minval = 0;
+  int minbin = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    // FFTrWrapper: F[i] = (real[2i], real[2i+1]) of the 32768 reals (1170 trident samples, zeros)
+    const int off = pass ? B_TRI_HALF : 0;
+    double2 x[16];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int j = bitrev<L>(epos<L, 0>(t, i));
+      const double a = 2 * j < B_TRI_HALF ? tb[off + 2 * j] : 0.0;
+      const double b = 2 * j + 1 < B_TRI_HALF ? tb[off + 2 * j + 1] : 0.0;
+      x[i] = make_double2(a, b);
+    }
+    fft_dit<L, false>(x, t, lds, T.tw16, s_tw);
+    // out[i] = F[i] * DA[i] + DB[i] * conj(F[(N - i) % N])
+    double2 g[16];
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 16; ++i) lds[pad(epos<L, 3>(t, i))] = part ? x[i].y : x[i].x;
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const double v = lds[pad((N - epos<L, 3>(t, i)) & (N - 1))];
+        if (part)
+          g[i].y = v;
+        else
+          g[i].x = v;
+      }
+    }
+    __syncthreads();
+    double lv = -1.0;
+    int li = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int p = epos<L, 3>(t, i);
+      const double2 da = T.da[p], db = T.db[p];
+      const double ar = x[i].x * da.x - x[i].y * da.y, ai = x[i].x * da.y + x[i].y * da.x;
+      const double br = db.x * g[i].x - db.y * (-g[i].y), bi = db.x * (-g[i].y) + db.y * g[i].x;
+      const double orr = ar + br, oi = ai + bi;
+      const double ab = aero_hypot(orr, oi);
+      x[i] = make_double2(orr, oi);
+      if (pass == 0) {
+        absb[p] = ab;
+        if (ab > lv || (ab == lv && p < li)) {
+          lv = ab;
+          li = p;
+        }
+      } else {
+        lds[pad(p)] = ab - absb[p];  // out_abs_diff
+      }
+    }
+    if (pass == 0) {
+      // strongest base bin, first on ties (:377-383)
+      double bv;
+      int bi;
+      reduce(lv, li, bv, bi);
+      minval = bv;
+      minbin = bi;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (epos<L, 3>(t, i) == minbin) s_best = x[i];
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  // trident search: testval(i) = d[i-b] + d[i+b] - d[i], i in [b, N - b), b = 1792 (:369-376)
+  constexpr int B = 1792;
+  double lv = -1e308;
+  int li = 0x7fffffff;
+  for (int i = B + t; i < N - B; i += FT) {
+    const double tv = lds[pad(i - B)] + lds[pad(i + B)] - lds[pad(i)];
+    if (tv > lv) {
+      lv = tv;
+      li = i;
+    }
+  }
+  double maxval;
+  int maxbin;
+  reduce(lv, li, maxval, maxbin);
+  if (t == 0) {
+    const double hzperbin = 48000.0 / 32768.0;
+    const int det = (maxval > 500.0) && (fabs((((double)maxbin - (double)minbin)) * hzperbin) < 20.0);
+    S.is[BI_TRI_DET * C + c] = det;
+    S.is[BI_TRI_MINBIN * C + c] = minbin;
+    S.is[BI_TRI_MAXBIN * C + c] = maxbin;
+    S.ds[BD_TRI_MINVAL * C + c] = minval;
+    S.ds[BD_TRI_MAXVAL * C + c] = maxval;
+    S.ds[BD_TRI_BRE * C + c] = s_best.x;
+    S.ds[BD_TRI_BIM * C + c] = s_best.y;
+    S.is[BI_PEND * C + c] = 2;
+  }
+}
+
+// -------------------------------------------------------- AeroL framing
+// AeroL::Decode, burst branch (decode/aerol.cpp:1060-1240, 2014-2030): the
+// start-of-packet marker resets muw; the phase-invariant UW detectors take 4
+// bit errors and must fire within |muw - 80| <= 150; a sync starts a packet
+// with a dummy header (cntr jumps to 16) and every soft bit then fills the
+// R/T block, tested at blockptr = 320 + 192 k (C remainder: also at 128); a
+// burst window ends after 10500 bits, dropping the rest of that group.
+// A lane stops before a new packet would overwrite the block of tests it
+// queued this pass, and after RT_TESTS_PER_PASS tests.
+__global__ __launch_bounds__(256) void frame_burst_kernel(BurstState S, int nch) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nch) return;
+  const int C = S.C;
+  int *is = S.is + c;
+  long long *ls = S.ls + c;
+  const long long E = ls[BL_SCOMMIT * C];
+  long long q = ls[BL_SCONS * C];
+  if (q >= E) return;
+  int realimag = is[BI_RI * C], muw = is[BI_MUW * C], cntr = is[BI_FCNTR * C], gsl = is[BI_GSL * C];
+  uint32_t uwi = (uint32_t)is[BI_UWI * C], uwr = (uint32_t)is[BI_UWR * C];
+  int inv_i = is[BI_UWI_INV * C], inv_r = is[BI_UWR_INV * C];
+  int datacd = is[BI_DATACD * C], blockptr = is[BI_BLOCKPTR * C], burst = is[BI_BURST_ID * C];
+  int skip = is[BI_SKIP_GROUP * C];
+  const int16_t *soft = S.soft + (size_t)c * B_SOFT_RING;
+  uint8_t *blk = S.rtblock + (size_t)c * RT_BLOCK;
+  int emitted = 0;
+  for (; q < E; ++q) {
+    const int e = soft[q & (B_SOFT_RING - 1)];
+    const bool last = (e & B_SOFT_LAST) != 0;
+    const int v = e & 0x1FF;
+    if (skip) {
+      if (last) skip = 0;
+      continue;
+    }
+    if (v == B_SOFT_MARK) {
+      muw = 0;
+      continue;
+    }
+    if ((cntr == -1 && emitted) || emitted >= RT_TESTS_PER_PASS) break;
+    int bit = v >= 128 ? 1 : 0, soft_bit = v;
+    if (muw < 100000) muw++;
+    realimag++;
+    realimag %= 2;
+    int gotsync;
+    if (cntr > 4992 - 68 || cntr <= 0 || !datacd) {
+      uint32_t &reg = realimag ? uwi : uwr;
+      int &inv = realimag ? inv_i : inv_r;
+      reg = (reg << 1) | (uint32_t)bit;
+      const int xs = __builtin_popcount(reg ^ BUW);
+      int g = 0;
+      if (xs >= 32 - 4) {
+        inv = 1;
+        g = 1;
+      } else if (xs <= 4) {
+        inv = 0;
+        g = 1;
+      }
+      gotsync = g;
+      if (!gsl) {
+        gsl = gotsync;
+        gotsync = 0;
+      } else
+        gsl = 0;
+    } else {
+      gotsync = 0;
+      gsl = 0;
+    }
+    if (gotsync && abs(muw - 80) > 150) gotsync = 0;
+    if (realimag ? inv_i : inv_r) {
+      bit = 1 - bit;
+      if (soft_bit != 128) soft_bit = 255 - soft_bit;
+    }
+    if (cntr < 1000000000) cntr++;
+    if (cntr == 0) {  // dummy header, rtchanneldeleavefecscram.resetblockptr()
+      cntr = 16;
+      blockptr = 0;
+      burst++;
+    }
+    if (cntr >= 16 && blockptr < RT_BLOCK) {  // RTChannelDeleaveFECScram::update
+      blk[blockptr] = (uint8_t)soft_bit;
+      blockptr++;
+      if (((blockptr - (64 * 5)) % (64 * 3)) == 0) {
+        const int j = atomicAdd(S.njobs, 1);
+        reinterpret_cast<int4 *>(S.jobs)[j] = make_int4(c, blockptr, burst, 0);
+        emitted++;
+      }
+    }
+    if (gotsync) {
+      cntr = -1;
+      datacd = 1;
+    }
+    if (cntr + 1 == 10500) {  // end of the burst window: Decode returns
+      cntr = 1000000000;
+      datacd = 0;
+      if (!last) skip = 1;
+    }
+  }
+  ls[BL_SCONS * C] = q;
+  is[BI_RI * C] = realimag;
+  is[BI_MUW * C] = muw;
+  is[BI_FCNTR * C] = cntr;
+  is[BI_GSL * C] = gsl;
+  is[BI_UWI * C] = (int)uwi;
+  is[BI_UWR * C] = (int)uwr;
+  is[BI_UWI_INV * C] = inv_i;
+  is[BI_UWR_INV * C] = inv_r;
+  is[BI_DATACD * C] = datacd;
+  is[BI_BLOCKPTR * C] = blockptr;
+  is[BI_BURST_ID * C] = burst;
+  is[BI_SKIP_GROUP * C] = skip;
+}
+
+// one wave per R/T test: del[j*64 + i] = block[((i*27) % 64) * cols + j],
+// Decode_soft over blockptr soft values, decoded bits MSB-first
+__global__ __launch_bounds__(64) void rt_viterbi_kernel(BurstState S) {
+  __shared__ uint8_t sbuf[RT_BLOCK];
+  __shared__ unsigned long long hist[HCAP];
+  __shared__ uint8_t obits[RT_BLOCK / 2 + 64];
+  const int njobs = *S.njobs;
+  const int lane = threadIdx.x;
+  for (int job = blockIdx.x; job < njobs; job += gridDim.x) {
+    __syncthreads();
+    const int4 jd = reinterpret_cast<const int4 *>(S.jobs)[job];
+    const int c = jd.x, bp = jd.y, cols = bp / 64;
+    const uint8_t *blk = S.rtblock + (size_t)c * RT_BLOCK;
+    for (int k = lane; k < bp; k += 64) {
+      const int j = k / 64, i = k % 64;
+      sbuf[k] = blk[((i * 27) % 64) * cols + j];
+    }
+    for (int k = lane; k < RT_BLOCK / 2 + 64; k += 64) obits[k] = 0;
+    __syncthreads();
+    viterbi_decode_wave(sbuf, bp, hist, obits, lane);
+    uint8_t *out = S.jobout + (size_t)job * RT_JOB_OUT;
+    const int nbits = bp / 2;
+    if (lane == 0) *reinterpret_cast<int4 *>(out) = make_int4(c, bp, jd.z, nbits);
+    for (int b = lane; b < (nbits + 7) / 8; b += 64) {
+      int v = 0;
+      for (int m = 0; m < 8; ++m)
+        if (8 * b + m < nbits) v |= obits[8 * b + m] << (7 - m);
+      out[16 + b] = (uint8_t)v;
+    }
+  }
+}
+
+// ------------------------------------------------------------ launchers
+void burst_upload_constants(const double *sr_b, const double *sr_a) {
+  hipMemcpyToSymbol(HIP_SYMBOL(c_bsr_b), sr_b, sizeof(double) * 3);
+  hipMemcpyToSymbol(HIP_SYMBOL(c_bsr_a), sr_a, sizeof(double) * 3);
+}
+
+void launch_hk_spectrum(hipStream_t st, const BurstTables &T, double2 *hk) {
+  hipLaunchKernelGGL(hk_spectrum_kernel, dim3(1), dim3(512), 0, st, T, hk);
+}
+
+void launch_hilbert(hipStream_t st, const BurstState &S, const BurstTables &T, int nch) {
+  hipLaunchKernelGGL(hilbert_kernel, dim3(nch), dim3(512), 0, st, S, T, nch);
+}
+
+void launch_demod_burst(hipStream_t st, const BurstState &S, const BurstTables &T, int nch, int max_n, int trace) {
+  hipLaunchKernelGGL(demod_burst_kernel, dim3((nch + BD_BLOCK - 1) / BD_BLOCK), dim3(BD_BLOCK), 0, st, S, T, nch,
+                     max_n, trace);
+}
+
+void launch_trident(hipStream_t st, const BurstState &S, const BurstTables &T, int nch) {
+  hipLaunchKernelGGL(trident_kernel, dim3(nch), dim3(1024), 0, st, S, T, nch);
+}
+
+void launch_frame_burst(hipStream_t st, const BurstState &S, int nch) {
+  hipLaunchKernelGGL(frame_burst_kernel, dim3((nch + 255) / 256), dim3(256), 0, st, S, nch);
+}
+
+void launch_rt_viterbi(hipStream_t st, const BurstState &S, int max_jobs) {
+  const int g = max_jobs < 16384 ? (max_jobs > 0 ? max_jobs : 1) : 16384;
+  hipLaunchKernelGGL(rt_viterbi_kernel, dim3(g), dim3(64), 0, st, S);
+}
+
+}  // namespace aero

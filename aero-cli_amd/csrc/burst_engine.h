@@ -1,0 +1,26 @@
+// burst_engine.h — the burst-mode group's entry points for engine.hip
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../include/aero_engine.h"
+
+namespace aero {
+
+struct BurstGroup;
+int burst_group_create(int device, int flags, int max_channels, BurstGroup **out);
+void burst_group_destroy(BurstGroup *g);
+int burst_open(BurstGroup *g, bool disable_reassembly, int *local);
+int burst_push(BurstGroup *g, int c, const int16_t *pcm, size_t n, bool dev, bool msg_start);
+int burst_run(BurstGroup *g, int flush);
+int burst_sync(BurstGroup *g);
+int burst_pop_soft(BurstGroup *g, int c, int16_t *dst, size_t cap, size_t *n);
+int burst_pop_hops(BurstGroup *g, int c, double *dst, size_t cap_records, size_t *n);
+int burst_pop_tests(BurstGroup *g, int c, uint8_t *dst, size_t cap, size_t *n);
+int burst_pop_packets(BurstGroup *g, int c, uint8_t *dst, size_t cap, size_t *n);
+std::vector<aero_acars_item> &burst_items(BurstGroup *g, int c);
+uint64_t burst_processed(const BurstGroup *g);
+
+}  // namespace aero

@@ -1,0 +1,502 @@
+/*
+ * burst_engine.hip — host side of the burst-mode 10500-bps OQPSK group
+ * (aero-decode --burst, decode/decode.cpp:131-136, 175): device layout and
+ * initial state (BurstOqpskDemodulator ctor + setSettings,
+ * decode/burstoqpskdemodulator.cpp:5-232; AeroL::setSettings(10500, burst),
+ * decode/aerol.cpp:960-1039), one message per push (the lastmse gate makes
+ * burst output depend on message boundaries, burstoqpskdemodulator.cpp:264,
+ * 685), the pass loop over the kernels of burst.hip, and the R/T test results:
+ * descrambling, CRC checks and packet handling of
+ * RTChannelDeleaveFECScram::test (decode/aerol.h:755-836) and the R/T branch
+ * of AeroL::Decode (decode/aerol.cpp:1240-1460).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "../../include/aero_engine.h"
+#include "acars_host.h"
+#include "burst_common.h"
+#include "burst_engine.h"
+#include "engine_common.h"
+#include "tables_host.h"
+
+namespace aero {
+
+void burst_upload_constants(const double *sr_b, const double *sr_a);
+void launch_hk_spectrum(hipStream_t st, const BurstTables &T, double2 *hk);
+void launch_hilbert(hipStream_t st, const BurstState &S, const BurstTables &T, int nch);
+void launch_demod_burst(hipStream_t st, const BurstState &S, const BurstTables &T, int nch, int max_n, int trace);
+void launch_trident(hipStream_t st, const BurstState &S, const BurstTables &T, int nch);
+void launch_frame_burst(hipStream_t st, const BurstState &S, int nch);
+void launch_rt_viterbi(hipStream_t st, const BurstState &S, int max_jobs);
+
+namespace {
+
+#define BCHK(x)                                                                        \
+  do {                                                                                 \
+    hipError_t err__ = (x);                                                            \
+    if (err__ != hipSuccess) {                                                         \
+      fprintf(stderr, "aero_engine(burst): %s failed: %s\n", #x, hipGetErrorString(err__)); \
+      return AERO_E_HIP;                                                               \
+    }                                                                                  \
+  } while (0)
+
+constexpr long long B_PCM_CAP = 32768;
+constexpr int B_HOP_CAP = 256;
+constexpr int DEMOD_ROUNDS = 8;  // demod / trident alternations per pass
+
+__global__ void b_scatter_kernel(int16_t *ring, int C, long long capm, const int16_t *src, long long n, int c,
+                                 long long start) {
+  for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x)
+    ring[((start + k) & capm) * C + c] = src[k];
+}
+
+template <class T>
+T *carve(char *&p, size_t count) {
+  T *r = reinterpret_cast<T *>(p);
+  p += (count * sizeof(T) + 255) & ~size_t(255);
+  return r;
+}
+
+// AeroLcrc16::calcusingbitsandcheck (decode/aerol.h:273-307)
+bool crc_bits_check(const int *bits, int numberofbits) {
+  uint16_t crc_rec = 0;
+  for (int i = numberofbits - 1; i >= numberofbits - 16; i--) {
+    crc_rec <<= 1;
+    crc_rec |= bits[i];
+  }
+  numberofbits -= 16;
+  uint16_t crc = 0xFFFF;
+  for (int i = 0; i < numberofbits; i++) {
+    const int crc_bit = crc & 1;
+    crc >>= 1;
+    if (crc_bit ^ bits[i]) crc = crc ^ 0x8408;
+  }
+  crc = ~crc;
+  return crc_rec == crc;
+}
+
+// RTChannelDeleaveFECScram::packintobytes: LSB first
+std::vector<uint8_t> pack_bits(const std::vector<int> &bits) {
+  std::vector<uint8_t> out;
+  int charptr = 0;
+  uint8_t ch = 0;
+  for (size_t h = 0; h < bits.size(); h++) {
+    ch |= bits[h] * 128;
+    charptr++;
+    charptr %= 8;
+    if (charptr == 0) {
+      out.push_back(ch);
+      ch = 0;
+    } else {
+      ch >>= 1;
+    }
+  }
+  return out;
+}
+
+}  // namespace
+
+struct BurstGroup {
+  int device = 0, flags = 0, C = 0, nch = 0;
+  hipStream_t st = nullptr;
+  BurstState S{};
+  BurstTables T{};
+  void *pool = nullptr;
+  std::vector<long long> avail, chunk_n;
+  std::vector<std::unique_ptr<PChannelHost>> host;
+  std::vector<int> ok_burst;
+  std::vector<std::vector<int16_t>> soft_hold;
+  std::vector<long long> soft_seen;
+  std::vector<std::vector<double>> hop_hold;
+  std::vector<int> hops_seen;
+  std::vector<std::vector<uint8_t>> tests_hold, packets_hold;
+  std::vector<uint8_t> scr;
+  int16_t *d_scratch = nullptr;
+  size_t scratch_cap = 0;
+  uint64_t processed = 0;
+  long long last_work = -1;
+  std::vector<long long> hb_base;  // first sample the Hilbert stage still needs (host mirror)
+  std::vector<int> since_run;      // messages pushed since the last run (message-start ring)
+};
+
+namespace {
+
+size_t burst_layout(BurstState &S, BurstTables &T, int C, char *base, double2 **hk_out) {
+  char *p = base;
+  S.C = C;
+  S.ds = carve<double>(p, (size_t)BD_COUNT * C);
+  S.is = carve<int>(p, (size_t)BI_COUNT * C);
+  S.ls = carve<long long>(p, (size_t)BL_COUNT * C);
+  S.fir = carve<double>(p, (size_t)2 * NTAPS * C);
+  S.ana = carve<double2>(p, (size_t)ANA_LEN * C);
+  S.pcm = carve<int16_t>(p, (size_t)B_PCM_CAP * C);
+  S.pcm_cap = B_PCM_CAP;
+  S.hb_rem = carve<double2>(p, (size_t)HB_REM * C);
+  S.agc = carve<double>(p, (size_t)B_AGC * C);
+  S.agc2 = carve<double>(p, (size_t)B_AGC2 * C);
+  S.d1 = carve<double2>(p, (size_t)B_D1 * C);
+  S.d2 = carve<double>(p, (size_t)B_D2 * C);
+  S.ma1 = carve<double2>(p, (size_t)B_MA * C);
+  S.mav1 = carve<double>(p, (size_t)B_MA * C);
+  for (int k = 0; k < BDL_COUNT; k++)  // sizes <= 1172 (bt_ma_diff); BDL_BT holds double2
+    S.dl[k] = carve<double>(p, (size_t)(k == BDL_BT ? 2 : 1) * 1172 * C);
+  S.pd1 = carve<double>(p, (size_t)B_PD1 * C);
+  S.pd2 = carve<double>(p, (size_t)B_PD2 * C);
+  S.pd3 = carve<double>(p, (size_t)B_PD3 * C);
+  S.tri = carve<double>(p, (size_t)B_TRI * C);
+  S.msema = carve<double>(p, (size_t)B_MSEMA * C);
+  S.chunks = carve<long long>(p, (size_t)CHUNK_RING * C);
+  S.soft = carve<int16_t>(p, (size_t)B_SOFT_RING * C);
+  S.hop_cap = B_HOP_CAP;
+  S.hops = carve<double>(p, (size_t)B_HOP_CAP * 6 * C);
+  S.rtblock = carve<uint8_t>(p, (size_t)RT_BLOCK * C);
+  S.jobs = carve<int>(p, (size_t)4 * RT_TESTS_PER_PASS * C);
+  S.njobs = carve<int>(p, 16);
+  S.jobout = carve<uint8_t>(p, (size_t)RT_JOB_OUT * RT_TESTS_PER_PASS * C);
+  S.tri_abs = carve<double>(p, (size_t)TRI_N * C);
+  T.cis = carve<double2>(p, WTSIZE);
+  T.tw8 = carve<double2>(p, 8192);
+  T.twi8 = carve<double2>(p, 8192);
+  T.tw16 = carve<double2>(p, 16384);
+  double2 *hk = carve<double2>(p, HB_N);
+  T.hk = hk;
+  if (hk_out) *hk_out = hk;
+  T.hk_time = carve<double2>(p, HB_N);
+  T.da = carve<double2>(p, TRI_N);
+  T.db = carve<double2>(p, TRI_N);
+  T.taps = carve<double>(p, 64);
+  for (int k = 0; k < BDL_COUNT; k++) {
+    T.dw[k] = carve<double>(p, 1172);
+    T.domw[k] = carve<double>(p, 1172);
+    T.dio[k] = carve<int>(p, 1172);
+  }
+  return (size_t)(p - base);
+}
+
+template <class V>
+int h2d(const V *dst, const std::vector<V> &src) {
+  BCHK(hipMemcpy((void *)dst, src.data(), src.size() * sizeof(V), hipMemcpyHostToDevice));
+  return AERO_OK;
+}
+
+int run_once(BurstGroup *g, bool trace, bool &progress) {
+  const int nch = g->nch;
+  progress = false;
+  launch_hilbert(g->st, g->S, g->T, nch);
+  for (int r = 0; r < DEMOD_ROUNDS; r++) {
+    launch_demod_burst(g->st, g->S, g->T, nch, (int)B_PCM_CAP, trace ? 1 : 0);
+    launch_trident(g->st, g->S, g->T, nch);
+  }
+  BCHK(hipMemsetAsync(g->S.njobs, 0, sizeof(int), g->st));
+  launch_frame_burst(g->st, g->S, nch);
+  launch_rt_viterbi(g->st, g->S, nch * RT_TESTS_PER_PASS);
+  BCHK(hipGetLastError());
+  int njobs = 0;
+  BCHK(hipMemcpyAsync(&njobs, g->S.njobs, sizeof(int), hipMemcpyDeviceToHost, g->st));
+  std::vector<long long> ls((size_t)BL_COUNT * g->C);
+  BCHK(hipMemcpyAsync(ls.data(), g->S.ls, ls.size() * 8, hipMemcpyDeviceToHost, g->st));
+  BCHK(hipStreamSynchronize(g->st));
+  std::vector<uint8_t> jobs((size_t)std::max(njobs, 1) * RT_JOB_OUT);
+  if (njobs > 0)
+    BCHK(hipMemcpy(jobs.data(), g->S.jobout, (size_t)njobs * RT_JOB_OUT, hipMemcpyDeviceToHost));
+  // R/T tests in emission order (a channel's tests come from one lane, in order)
+  std::vector<int> bits, deconvol;
+  for (int j = 0; j < njobs; j++) {
+    const uint8_t *rec = jobs.data() + (size_t)j * RT_JOB_OUT;
+    int h[4];
+    memcpy(h, rec, 16);
+    const int c = h[0], bp = h[1], burst = h[2], nbits = h[3];
+    if (c < 0 || c >= nch || burst == g->ok_burst[c]) continue;  // packet already decoded: the block is FULL
+    deconvol.assign(nbits, 0);
+    for (int b = 0; b < nbits; b++) deconvol[b] = ((rec[16 + b / 8] >> (7 - (b % 8))) & 1) ^ g->scr[b];
+    enum { OK_R = 3, OK_T = 5, Bad = 0, Test_Failed = 32 };
+    int result, nsus = 0;
+    std::vector<uint8_t> info;
+    if (bp == 64 * 5) {
+      if (!crc_bits_check(deconvol.data(), 8 * 19)) {
+        result = Test_Failed;
+      } else {
+        info = pack_bits(deconvol);
+        result = OK_R;
+      }
+    } else if (!crc_bits_check(deconvol.data(), 8 * 6)) {
+      result = bp >= RT_BLOCK ? Bad : Test_Failed;
+    } else {
+      nsus = 1 + (bp - (64 * 5)) / (64 * 3);
+      result = OK_T;
+      for (int i = 0; i < nsus; i++)
+        if (!crc_bits_check(deconvol.data() + (8 * 6) + (8 * 12) * i, 8 * 12)) {
+          result = bp >= RT_BLOCK ? Bad : Test_Failed;
+          break;
+        }
+      if (result == OK_T) {
+        info = pack_bits(deconvol);
+        if (!info.empty()) info.pop_back();  // infofield.chop(1)
+      }
+    }
+    if (g->flags & AERO_F_TRACE_FRAMES) {
+      const uint32_t t2[2] = {(uint32_t)bp, (uint32_t)result};
+      g->tests_hold[c].insert(g->tests_hold[c].end(), (const uint8_t *)t2, (const uint8_t *)t2 + 8);
+    }
+    if (result == OK_R || result == OK_T) {
+      g->ok_burst[c] = burst;
+      if (g->flags & AERO_F_TRACE_FRAMES) {
+        const uint32_t p2[2] = {(uint32_t)(result == OK_R ? 'R' : 'T'), (uint32_t)info.size()};
+        auto &ph = g->packets_hold[c];
+        ph.insert(ph.end(), (const uint8_t *)p2, (const uint8_t *)p2 + 8);
+        ph.insert(ph.end(), info.begin(), info.end());
+      }
+      g->host[c]->rt_packet(result == OK_R, info.data(), (int)info.size(), nsus);
+    }
+  }
+  // traces: committed soft entries (with the start-of-packet markers) and trident records
+  if (g->flags & AERO_F_TRACE_SOFT) {
+    std::vector<int16_t> ring;
+    for (int c = 0; c < nch; c++) {
+      const long long com = ls[(size_t)BL_SCOMMIT * g->C + c];
+      if (com <= g->soft_seen[c]) continue;
+      if (ring.empty()) {
+        ring.resize((size_t)B_SOFT_RING * nch);
+        BCHK(hipMemcpy(ring.data(), g->S.soft, ring.size() * 2, hipMemcpyDeviceToHost));
+      }
+      for (long long k = g->soft_seen[c]; k < com; k++) {
+        const int e = ring[(size_t)c * B_SOFT_RING + (k & (B_SOFT_RING - 1))] & 0x1FF;
+        g->soft_hold[c].push_back(e == B_SOFT_MARK ? (int16_t)-1 : (int16_t)e);
+      }
+      g->soft_seen[c] = com;
+    }
+  }
+  if (g->flags & AERO_F_TRACE_HOPS) {  // trident records of this pass, then the counters restart
+    std::vector<int> hn(nch);
+    BCHK(hipMemcpy(hn.data(), g->S.is + (size_t)BI_HOP_N * g->C, sizeof(int) * nch, hipMemcpyDeviceToHost));
+    std::vector<double> hops;
+    for (int c = 0; c < nch; c++) {
+      if (hn[c] <= 0) continue;
+      if (hn[c] > B_HOP_CAP) return AERO_E_FULL;
+      if (hops.empty()) {
+        hops.resize((size_t)B_HOP_CAP * 6 * nch);
+        BCHK(hipMemcpy(hops.data(), g->S.hops, hops.size() * 8, hipMemcpyDeviceToHost));
+      }
+      g->hop_hold[c].insert(g->hop_hold[c].end(), hops.begin() + (size_t)c * B_HOP_CAP * 6,
+                            hops.begin() + ((size_t)c * B_HOP_CAP + hn[c]) * 6);
+    }
+    BCHK(hipMemset(g->S.is + (size_t)BI_HOP_N * g->C, 0, sizeof(int) * nch));
+  }
+  // more passes while any channel has samples or committed soft bits left
+  long long work = 0;
+  for (int c = 0; c < nch; c++) {
+    work += (g->avail[c] - ls[(size_t)BL_NSAMP * g->C + c]) +
+            (ls[(size_t)BL_SCOMMIT * g->C + c] - ls[(size_t)BL_SCONS * g->C + c]);
+  }
+  progress = work > 0 && (work != g->last_work || njobs > 0);
+  g->last_work = work;
+  return AERO_OK;
+}
+
+}  // namespace
+
+int burst_group_create(int device, int flags, int max_channels, BurstGroup **out) {
+  std::unique_ptr<BurstGroup> g(new BurstGroup());
+  g->device = device;
+  g->flags = flags;
+  g->C = (max_channels + 63) & ~63;
+  BurstState S{};
+  BurstTables T{};
+  const size_t bytes = burst_layout(S, T, g->C, nullptr, nullptr) + 4096;
+  if (hipMalloc(&g->pool, bytes) != hipSuccess) return AERO_E_NOMEM;
+  BCHK(hipMemset(g->pool, 0, bytes));
+  double2 *hk = nullptr;
+  burst_layout(g->S, g->T, g->C, reinterpret_cast<char *>(g->pool), &hk);
+  BCHK(hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking));
+  // tables (host glibc, g++-compiled: tables_host.cpp)
+  std::vector<double> cis(2 * WTSIZE), tw8(2 * 8192), twi8(2 * 8192), tw16(2 * 16384), twi16(2 * 16384);
+  host_cis(cis.data());
+  host_twiddles(8192, tw8.data(), twi8.data());
+  host_twiddles(16384, tw16.data(), twi16.data());
+  std::vector<double> hk_time(2 * HB_N), da(2 * TRI_N), db(2 * TRI_N), taps(64, 0.0);
+  host_hilbert_kernel(hk_time.data());
+  host_fftr_split(TRI_N, da.data(), db.data());
+  if (host_rrc(1.0, 55, 48000, 10500 / 2.0, taps.data()) != NTAPS) return AERO_E_INVALID;
+  if (int rc = h2d((const double *)g->T.cis, cis)) return rc;
+  if (int rc = h2d((const double *)g->T.tw8, tw8)) return rc;
+  if (int rc = h2d((const double *)g->T.twi8, twi8)) return rc;
+  if (int rc = h2d((const double *)g->T.tw16, tw16)) return rc;
+  if (int rc = h2d((const double *)g->T.hk_time, hk_time)) return rc;
+  if (int rc = h2d((const double *)g->T.da, da)) return rc;
+  if (int rc = h2d((const double *)g->T.db, db)) return rc;
+  if (int rc = h2d(g->T.taps, taps)) return rc;
+  // Delay<> instances (burstoqpskdemodulator.cpp:186-196, 213-216)
+  const double fds[BDL_COUNT] = {1.0, (2.0 * 48000.0 / 10500.0) / 4.0, (2.0 * 48000.0 / 10500.0) / 4.0,
+                                 (2.0 * 48000.0 / 10500.0) / 8.0, (2.0 * 48000.0 / 10500.0) / 2.0,
+                                 1.0 * (2.0 * 48000.0 / 10500.0), (2.0 * 48000.0 / 10500.0) * 128};
+  for (int k = 0; k < BDL_COUNT; k++) {
+    std::vector<double> w(1172), omw(1172);
+    std::vector<int> io(1172);
+    const int size = host_delay_table(fds[k], w.data(), omw.data(), io.data(), 1172);
+    if (size <= 0) return AERO_E_INVALID;
+    g->T.dsize[k] = size;
+    if (int rc = h2d(g->T.dw[k], w)) return rc;
+    if (int rc = h2d(g->T.domw[k], omw)) return rc;
+    if (int rc = h2d(g->T.dio[k], io)) return rc;
+  }
+  const double sr_b[3] = {0.0048847995518126464, 0, -0.0048847995518126464};
+  const double sr_a[3] = {1, -0.3882746897971619, 0.99023040089637471};
+  burst_upload_constants(sr_b, sr_a);
+  launch_hk_spectrum(g->st, g->T, hk);
+  BCHK(hipGetLastError());
+  BCHK(hipStreamSynchronize(g->st));
+  g->scr.resize(5000);
+  host_scrambler(g->scr.data());
+  *out = g.release();
+  return AERO_OK;
+}
+
+void burst_group_destroy(BurstGroup *g) {
+  if (!g) return;
+  if (g->st) (void)hipStreamSynchronize(g->st);
+  if (g->d_scratch) (void)hipFree(g->d_scratch);
+  if (g->pool) (void)hipFree(g->pool);
+  if (g->st) (void)hipStreamDestroy(g->st);
+  delete g;
+}
+
+int burst_open(BurstGroup *g, bool disable_reassembly, int *local) {
+  if (g->nch >= g->C) return AERO_E_FULL;
+  const int c = g->nch;
+  const int C = g->C;
+  // BurstOqpskDemodulator ctor + setSettings (burstoqpskdemodulator.cpp:5-232) and AeroL burst state
+  std::vector<double> ds(BD_COUNT, 0.0);
+  std::vector<int> is(BI_COUNT, 0);
+  ds[BD_M2_FREQ] = 8000;  // freq_center (burstoqpskdemodulator.h:33)
+  ds[BD_M2_STEP] = (8000.0) * ((double)WTSIZE) / ((float)48000);
+  ds[BD_SO_FREQ] = 10500;
+  ds[BD_SO_STEP] = (10500.0) * ((double)WTSIZE) / ((float)48000);
+  ds[BD_Q_STEP] = (10500.0 / 4.0) * ((double)WTSIZE) / ((float)48000);
+  ds[BD_VOL_GAIN] = 1;
+  ds[BD_AVE_RE] = ds[BD_ROT_RE] = ds[BD_STR_RE] = 1;
+  ds[BD_MSE] = 100;
+  ds[BD_LASTMSE] = 100;
+  is[BI_PD_CNTDOWN] = B_PD_MAXCD;
+  is[BI_PD_MAXPOSCD] = -1;
+  is[BI_STARTSTOP] = -1;
+  is[BI_FCNTR] = 1000000000;
+  for (int f = 0; f < BD_COUNT; f++) BCHK(hipMemcpy(g->S.ds + (size_t)f * C + c, &ds[f], 8, hipMemcpyHostToDevice));
+  for (int f = 0; f < BI_COUNT; f++) BCHK(hipMemcpy(g->S.is + (size_t)f * C + c, &is[f], 4, hipMemcpyHostToDevice));
+  g->nch++;
+  g->avail.push_back(0);
+  g->chunk_n.push_back(0);
+  g->host.emplace_back(new PChannelHost(disable_reassembly));
+  g->ok_burst.push_back(-1);
+  g->soft_hold.emplace_back();
+  g->soft_seen.push_back(0);
+  g->hop_hold.emplace_back();
+  g->hops_seen.push_back(0);
+  g->tests_hold.emplace_back();
+  g->packets_hold.emplace_back();
+  g->hb_base.push_back(0);
+  g->since_run.push_back(0);
+  *local = c;
+  return AERO_OK;
+}
+
+int burst_run(BurstGroup *g, int flush) {
+  (void)flush;  // every pushed sample is processed (burst output depends on message boundaries only)
+  if (!g || !g->nch) return AERO_OK;
+  BCHK(hipSetDevice(g->device));
+  const bool trace = (g->flags & (AERO_F_TRACE_HOPS | AERO_F_TRACE_SOFT)) != 0;
+  g->last_work = -1;
+  for (int guard = 0; guard < 100000; guard++) {
+    bool more = false;
+    if (int rc = run_once(g, trace, more)) return rc;
+    if (!more) break;
+  }
+  for (int c = 0; c < g->nch; c++) {
+    g->hb_base[c] = (g->avail[c] / HB_SNZ) * HB_SNZ;
+    g->since_run[c] = 0;
+  }
+  return AERO_OK;
+}
+
+// one message (Decoder::audioReceived -> BurstOqpskDemodulator::dataReceived)
+int burst_push(BurstGroup *g, int c, const int16_t *pcm, size_t n, bool dev, bool msg_start) {
+  if (!n) return AERO_OK;
+  BCHK(hipSetDevice(g->device));
+  const int C = g->C;
+  if ((long long)n > B_PCM_CAP / 2) return AERO_E_FULL;  // one message is at most 16384 samples here
+  // never outrun the PCM ring (the Hilbert stage reads from hb_base on) or
+  // the message-start ring: process what is pending first
+  if (g->avail[c] + (long long)n - g->hb_base[c] > B_PCM_CAP - 2 || g->since_run[c] >= CHUNK_RING - 1)
+    if (int rc = burst_run(g, 0)) return rc;
+  const int16_t *src = pcm;
+  if (!dev) {
+    if (n > g->scratch_cap) {
+      if (g->d_scratch) (void)hipFree(g->d_scratch);
+      g->d_scratch = nullptr;
+      g->scratch_cap = 0;
+      BCHK(hipMalloc(&g->d_scratch, n * sizeof(int16_t)));
+      g->scratch_cap = n;
+    }
+    BCHK(hipMemcpyAsync(g->d_scratch, pcm, n * sizeof(int16_t), hipMemcpyHostToDevice, g->st));
+    src = g->d_scratch;
+  }
+  const long long start = g->avail[c];
+  const int grid = (int)std::min<long long>(((long long)n + 255) / 256, 4096);
+  hipLaunchKernelGGL(b_scatter_kernel, dim3(grid), dim3(256), 0, g->st, g->S.pcm, C, B_PCM_CAP - 1, src,
+                     (long long)n, c, start);
+  BCHK(hipGetLastError());
+  // message start (lastmse capture) and the new pushed count
+  if (msg_start) {
+    const long long k = g->chunk_n[c];
+    BCHK(hipMemcpyAsync(g->S.chunks + (size_t)c * CHUNK_RING + (k & (CHUNK_RING - 1)), &start, 8,
+                        hipMemcpyHostToDevice, g->st));
+    g->chunk_n[c] = k + 1;
+    g->since_run[c]++;
+  }
+  g->avail[c] = start + (long long)n;
+  BCHK(hipMemcpyAsync(g->S.ls + (size_t)BL_CHUNK_N * C + c, &g->chunk_n[c], 8, hipMemcpyHostToDevice, g->st));
+  BCHK(hipMemcpyAsync(g->S.ls + (size_t)BL_AVAIL * C + c, &g->avail[c], 8, hipMemcpyHostToDevice, g->st));
+  BCHK(hipStreamSynchronize(g->st));  // the host values copied above and the caller's buffer are free again
+  g->processed += n;
+  return AERO_OK;
+}
+
+template <class T>
+static int pop_v(std::vector<T> &v, T *dst, size_t cap, size_t *n) {
+  const size_t k = std::min(cap, v.size());
+  if (dst && k) memcpy(dst, v.data(), k * sizeof(T));
+  if (n) *n = k;
+  v.erase(v.begin(), v.begin() + k);
+  return AERO_OK;
+}
+
+int burst_pop_soft(BurstGroup *g, int c, int16_t *dst, size_t cap, size_t *n) {
+  return pop_v(g->soft_hold[c], dst, cap, n);
+}
+int burst_pop_hops(BurstGroup *g, int c, double *dst, size_t cap_records, size_t *n) {
+  size_t k = 0;
+  int rc = pop_v(g->hop_hold[c], dst, cap_records * 6, &k);
+  if (n) *n = k / 6;
+  return rc;
+}
+int burst_pop_tests(BurstGroup *g, int c, uint8_t *dst, size_t cap, size_t *n) {
+  return pop_v(g->tests_hold[c], dst, cap, n);
+}
+int burst_pop_packets(BurstGroup *g, int c, uint8_t *dst, size_t cap, size_t *n) {
+  return pop_v(g->packets_hold[c], dst, cap, n);
+}
+std::vector<aero_acars_item> &burst_items(BurstGroup *g, int c) { return g->host[c]->items; }
+uint64_t burst_processed(const BurstGroup *g) { return g ? g->processed : 0; }
+int burst_sync(BurstGroup *g) {
+  if (!g) return AERO_OK;
+  BCHK(hipStreamSynchronize(g->st));
+  return AERO_OK;
+}
+
+}  // namespace aero

@@ -31,6 +31,7 @@
 
 #include "../../include/aero_engine.h"
 #include "acars_host.h"
+#include "burst_engine.h"
 #include "aero_math.h"
 #include "engine_common.h"
 #include "tables_host.h"
@@ -255,9 +256,12 @@ struct Group {
   std::vector<uint8_t> h_jobs_task, h_dbg_task;  // buffers owned by the running host task
 };
 
+constexpr int MODE_BURST = MODE_COUNT;  // chmap kind of burst-mode channels (burst_engine.hip)
+
 struct aero_engine {
   int device = 0, flags = 0, max_channels = 0;
   std::unique_ptr<Group> groups[MODE_COUNT];
+  BurstGroup *burst = nullptr;
   std::vector<std::pair<int, int>> chmap;  // engine channel -> (mode, local index)
   std::unique_ptr<HostPool> hpool;
   std::map<std::string, TimingSlot> timing;  // engine-level host sections
@@ -650,7 +654,15 @@ int drain_group(Group *e) {
   return AERO_OK;
 }
 
+// engine channel -> burst-group index, or -1
+int route_burst(aero_engine *e, int ch) {
+  if (!e || ch < 0 || ch >= (int)e->chmap.size() || e->chmap[ch].first != MODE_BURST) return -1;
+  return e->chmap[ch].second;
+}
+
 int run_impl(aero_engine *e, int flush) {
+  if (e->burst)
+    if (int rc = burst_run(e->burst, flush)) return rc;
   for (auto &g : e->groups)
     if (g) {
       int rc = run_group(g.get(), flush);
@@ -801,7 +813,7 @@ void group_destroy(Group *e) {
 
 // engine channel -> (group, local index); nullptr if out of range
 Group *route(aero_engine *e, int ch, int &local) {
-  if (!e || ch < 0 || ch >= (int)e->chmap.size()) return nullptr;
+  if (!e || ch < 0 || ch >= (int)e->chmap.size() || e->chmap[ch].first == MODE_BURST) return nullptr;
   local = e->chmap[ch].second;
   return e->groups[e->chmap[ch].first].get();
 }
@@ -931,12 +943,23 @@ void aero_engine_destroy(aero_engine *e) {
     if (g) (void)drain_group(g.get());
   host_wait(e);
   for (auto &g : e->groups) group_destroy(g.get());
+  if (e->burst) burst_group_destroy(e->burst);
   delete e;
 }
 
 int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) {
   if (!e || !cfg || !ch_out) return AERO_E_INVALID;
-  if (cfg->burst) return AERO_E_INVALID;  // burst modes: not built this round
+  if (cfg->burst) {  // aero-decode --burst: 10500 bps OQPSK (burst MSK is not built)
+    if (cfg->bitrate != 10500 || cfg->fs != 48000) return AERO_E_INVALID;
+    HIPCHK(hipSetDevice(e->device));
+    if (!e->burst)
+      if (int rc = burst_group_create(e->device, e->flags, e->max_channels, &e->burst)) return rc;
+    int local;
+    if (int rc = burst_open(e->burst, cfg->disable_reassembly != 0, &local)) return rc;
+    *ch_out = (int)e->chmap.size();
+    e->chmap.push_back({MODE_BURST, local});
+    return AERO_OK;
+  }
   int mode;
   if (cfg->bitrate == 10500 && cfg->fs == 48000)
     mode = MODE_OQPSK;
@@ -973,7 +996,22 @@ int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) 
   return AERO_OK;
 }
 
+// burst: one message = one BurstOqpskDemodulator::writeDataSlot call; pieces
+// of a long message keep its single message start
+int push_burst(aero_engine *e, int b, const int16_t *pcm, size_t n, bool dev) {
+  HIPCHK(hipSetDevice(e->device));
+  size_t off = 0;
+  while (off < n) {
+    const size_t piece = std::min<size_t>(n - off, 16384);
+    if (int rc = burst_push(e->burst, b, pcm + off, piece, dev, off == 0)) return rc;
+    off += piece;
+  }
+  return AERO_OK;
+}
+
 int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t fs) {
+  const int b = route_burst(e, ch);
+  if (b >= 0) return (pcm || !n) ? push_burst(e, b, pcm, n, false) : AERO_E_INVALID;  // rate only logged (:626-628)
   int c;
   Group *g = route(e, ch, c);
   if (!g || (!pcm && n)) return AERO_E_INVALID;
@@ -995,6 +1033,8 @@ int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t
 }
 
 int aero_push_pcm_dev(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t fs) {
+  const int b = route_burst(e, ch);
+  if (b >= 0) return (pcm || !n) ? push_burst(e, b, pcm, n, true) : AERO_E_INVALID;
   int c;
   Group *g = route(e, ch, c);
   if (!g || (!pcm && n)) return AERO_E_INVALID;
@@ -1015,6 +1055,7 @@ int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld,
   if (!e || !pcm || nch <= 0 || nch > (int)e->chmap.size() || ld < (size_t)nch) return AERO_E_INVALID;
   // channels [0, nch) must be one kind, opened in order (local == engine index)
   const int mode = e->chmap[0].first;
+  if (mode == MODE_BURST) return AERO_E_INVALID;  // burst channels take one message per call
   for (int j = 0; j < nch; j++)
     if (e->chmap[j].first != mode || e->chmap[j].second != j) return AERO_E_INVALID;
   Group *g = e->groups[mode].get();
@@ -1040,6 +1081,8 @@ int aero_flush(aero_engine *e) {
 }
 
 int aero_pop_softbits(aero_engine *e, int ch, int16_t *dst, size_t cap, size_t *n) {
+  const int b = route_burst(e, ch);
+  if (b >= 0) return burst_pop_soft(e->burst, b, dst, cap, n);
   int c;
   Group *g = route(e, ch, c);
   if (!g) return AERO_E_INVALID;
@@ -1047,6 +1090,8 @@ int aero_pop_softbits(aero_engine *e, int ch, int16_t *dst, size_t cap, size_t *
 }
 
 int aero_pop_items(aero_engine *e, int ch, aero_acars_item *dst, size_t cap, size_t *n) {
+  const int b = route_burst(e, ch);
+  if (b >= 0) return pop_vec(burst_items(e->burst, b), dst, cap, n);
   int c;
   Group *g = route(e, ch, c);
   if (!g) return AERO_E_INVALID;
@@ -1061,7 +1106,8 @@ int aero_pop_items_all(aero_engine *e, aero_acars_item *dst, int *ch, size_t cap
   host_wait(e);
   size_t k = 0;
   for (int gc = 0; gc < (int)e->chmap.size() && k < cap; gc++) {
-    auto &v = e->groups[e->chmap[gc].first]->host[e->chmap[gc].second]->items;
+    auto &v = e->chmap[gc].first == MODE_BURST ? burst_items(e->burst, e->chmap[gc].second)
+                                               : e->groups[e->chmap[gc].first]->host[e->chmap[gc].second]->items;
     const size_t m = std::min(cap - k, v.size());
     for (size_t i = 0; i < m; i++) {  // msg bytes past msg_len are left unspecified
       memcpy(&dst[k + i], &v[i], offsetof(aero_acars_item, msg) + v[i].msg_len);
@@ -1075,6 +1121,8 @@ int aero_pop_items_all(aero_engine *e, aero_acars_item *dst, int *ch, size_t cap
 }
 
 int aero_pop_hops(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n) {
+  const int b = route_burst(e, ch);
+  if (b >= 0) return burst_pop_hops(e->burst, b, dst, cap_records, n);
   int c;
   Group *g = route(e, ch, c);
   if (!g) return AERO_E_INVALID;
@@ -1085,6 +1133,10 @@ int aero_pop_hops(aero_engine *e, int ch, double *dst, size_t cap_records, size_
 }
 
 int aero_pop_pt(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n) {
+  if (route_burst(e, ch) >= 0) {  // not produced by burst channels
+    if (n) *n = 0;
+    return AERO_OK;
+  }
   int c;
   Group *g = route(e, ch, c);
   if (!g) return AERO_E_INVALID;
@@ -1095,6 +1147,10 @@ int aero_pop_pt(aero_engine *e, int ch, double *dst, size_t cap_records, size_t 
 }
 
 int aero_pop_blocks(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
+  if (route_burst(e, ch) >= 0) {  // not produced by burst channels
+    if (n) *n = 0;
+    return AERO_OK;
+  }
   int c;
   Group *g = route(e, ch, c);
   if (!g) return AERO_E_INVALID;
@@ -1103,11 +1159,27 @@ int aero_pop_blocks(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n)
 }
 
 int aero_pop_frames(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
+  if (route_burst(e, ch) >= 0) {  // not produced by burst channels
+    if (n) *n = 0;
+    return AERO_OK;
+  }
   int c;
   Group *g = route(e, ch, c);
   if (!g) return AERO_E_INVALID;
   host_wait(e);
   return pop_vec(g->frame_hold[c], dst, cap, n);
+}
+
+int aero_pop_rt_tests(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
+  const int b = route_burst(e, ch);
+  if (b < 0) return AERO_E_INVALID;
+  return burst_pop_tests(e->burst, b, dst, cap, n);
+}
+
+int aero_pop_rt_packets(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
+  const int b = route_burst(e, ch);
+  if (b < 0) return AERO_E_INVALID;
+  return burst_pop_packets(e->burst, b, dst, cap, n);
 }
 
 int aero_timing(aero_engine *e, const char *name, double *ms, long *launches) {
@@ -1139,14 +1211,18 @@ void aero_timing_reset(aero_engine *e) {
 
 uint64_t aero_samples_processed(aero_engine *e) {
   uint64_t s = 0;
-  if (e)
+  if (e) {
     for (auto &g : e->groups)
       if (g) s += g->processed;
+    s += burst_processed(e->burst);
+  }
   return s;
 }
 
 int aero_sync(aero_engine *e) {
   if (!e) return AERO_E_INVALID;
+  if (e->burst)
+    if (int rc = burst_sync(e->burst)) return rc;
   for (auto &g : e->groups)
     if (g) {
       int rc = drain_group(g.get());

@@ -126,6 +126,59 @@ void host_scrambler(uint8_t *pre) {  // AeroLScrambler::AeroLScrambler (decode/a
   }
 }
 
+
+// Delay<T>::update (decode/DSP.h:365-384) for every write pointer p: the slot
+// of the older sample and the weights (weighting, 1 - weighting).  Returns the
+// ring size ceil(fd) + 1, or -1 when it exceeds cap.
+int host_delay_table(double fractdelay, double *w, double *omw, int *iold, int cap) {
+  const int size = (int)std::ceil(fractdelay) + 1;
+  if (size > cap) return -1;
+  for (int p = 0; p < size; p++) {
+    double dptr = ((double)p) - fractdelay;
+    while (std::floor(dptr) < 0) dptr += ((double)size);
+    const int iptr = (int)std::floor(dptr);
+    const double weighting = dptr - ((double)iptr);
+    w[p] = weighting;
+    omw[p] = (1.0 - weighting);
+    iold[p] = iptr;
+  }
+  return size;
+}
+
+// FFTrWrapper split tables DA/DB (decode/fftrwrapper.cpp:13-24, JFFT::init
+// real path decode/jfft.cpp:54-67), nfft = complex FFT size
+void host_fftr_split(int nfft, double *da, double *db) {
+  typedef std::complex<double> cpx;
+  const cpx imag = cpx(0, 1);
+  for (int i = 0; i < nfft; i++) {
+    const cpx a = 0.5 * (1.0 - imag * std::exp(-2.0 * imag * M_PI * ((double)i) / ((double)(2 * nfft))));
+    const cpx b = 0.5 * (1.0 + imag * std::exp(-2.0 * imag * M_PI * ((double)i) / ((double)(2 * nfft))));
+    da[2 * i] = a.real();
+    da[2 * i + 1] = a.imag();
+    db[2 * i] = b.real();
+    db[2 * i + 1] = b.imag();
+  }
+}
+
+// QJHilbertFilter's 2048-tap analytic-signal kernel (decode/DSP.cpp:730-761)
+// zero-padded to the 8192-point JFastFir block (decode/jfft.cpp:322-374)
+void host_hilbert_kernel(double *k) {
+  typedef std::complex<double> cpx;
+  const int N = 2048;
+  memset(k, 0, sizeof(double) * 2 * 8192);
+  for (int i = 0; i < N; i++) {
+    cpx v;
+    if (i == N / 2)
+      v = cpx(-1, 0);
+    else if ((i % 2) == 0)
+      v = cpx(0, 0);
+    else
+      v = cpx(0, (2.0 / ((double)N)) / (std::tan(M_PI * (((double)i) / ((double)N) - 0.5))));
+    k[2 * i] = v.real();
+    k[2 * i + 1] = v.imag();
+  }
+}
+
 /* ------------------------------------------ aero-publish channeliser (FP32) */
 int host_pub_osc_len(double sampleRate) { return (int)sampleRate; }
 
@@ -188,6 +241,9 @@ int host_pub_low_pass(double gain, double fs, double cutoff, double tw, float *t
 }  // namespace aero
 
 extern "C" {
+/* burst tables, for tests/test_abi.py */
+void aero_host_fftr_split(int nfft, double *da, double *db) { aero::host_fftr_split(nfft, da, db); }
+void aero_host_hilbert_kernel(double *k) { aero::host_hilbert_kernel(k); }
 /* channeliser designs, for tests/test_abi.py (engine tables vs the oracle's) */
 void aero_host_pub_osc(double fs, double freq, float *queue) { aero::host_pub_osc(fs, freq, queue); }
 void aero_host_pub_hilbert(int len, int fs, float *points) { aero::host_pub_hilbert(len, fs, points); }

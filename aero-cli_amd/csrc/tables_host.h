@@ -19,6 +19,12 @@ bool host_delay_uniform(double fractdelay, int &size, int &age_old, int &age_new
 void host_msk_taps(int sps, double *taps);
 void host_scrambler(uint8_t *pre);                              // [5000]
 
+// burst OQPSK: Delay<T> per-pointer weights and older slot, FFTrWrapper split
+// tables, the Hilbert fast-FIR kernel (time domain, 8192 complex)
+int host_delay_table(double fractdelay, double *w, double *omw, int *iold, int cap);
+void host_fftr_split(int nfft, double *da, double *db);  // [nfft][2] each
+void host_hilbert_kernel(double *k);                    // [8192][2]
+
 // aero-publish channeliser designs (publish/oscillator.cpp:4-28,
 // publish/dsp.cpp:181-215, publish/firfilter.cpp:47-99): FP32 as there
 int host_pub_osc_len(double sampleRate);

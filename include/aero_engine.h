@@ -48,7 +48,7 @@ typedef struct {
 
 typedef struct {
   int bitrate;            /* 10500 (OQPSK), 600 or 1200 (MSK); decode/decode.h:42 */
-  int burst;              /* 0 (burst mode -> AERO_E_INVALID this round)     */
+  int burst;              /* 1: aero-decode --burst (10500 bps OQPSK only)    */
   uint32_t fs;            /* 48000 / 12000 / 24000 for 10500 / 600 / 1200 bps
                              (decode/decode.cpp:145, 152-159)                 */
   int disable_reassembly; /* 1: items are ACARSfragmentsignal (decode.cpp:233) */
@@ -129,6 +129,12 @@ int aero_pop_hops(aero_engine *e, int ch, double *dst, size_t cap_records, size_
 int aero_pop_pt(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n);
 int aero_pop_blocks(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
 int aero_pop_frames(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
+/* Burst channels (AERO_F_TRACE_FRAMES): every R/T test (uint32 blockptr,
+ * uint32 RTChannelDeleaveFECScram result) and every decoded R/T packet
+ * (uint32 'R'/'T', uint32 length, the infofield bytes), in order
+ * (decode/aerol.h:755-836). */
+int aero_pop_rt_tests(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
+int aero_pop_rt_packets(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
 
 /* Timing (AERO_F_TIMING): kernel names {"demod","coarse","frame","viterbi"}
  * give summed device milliseconds (HIP events) and launch counts; host

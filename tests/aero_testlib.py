@@ -178,7 +178,7 @@ class Oracle:
 
     def rt_tests(self):
         """burst: (blockptr, result code) of every R/T test"""
-        return self._get(self.L.oracle_rt_tests, np.uint32).reshape(-1, 2)
+        return self._get(self.L.oracle_rt_tests, np.uint8).view(np.uint32).reshape(-1, 2)
 
     def rt_packets(self):
         """burst: [(kind 'R'/'T', infofield bytes)] of every decoded R/T packet"""
