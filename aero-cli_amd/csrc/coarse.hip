@@ -226,6 +226,12 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   fft_dit<L, false>(x, t, lds, T.tw, s_tw);
   // fftshift + smoothing y = 0.9 y + 10 log10(max(|X|,1)) over the bins the fold reads:
   // |X| per bin to LDS first (keeps the log10 out of the register-heavy FFT scope)
+  // the y history (HBM) is read three iterations ahead of its update, the
+  // first loads overlapping the |X| work below
+  double *yg = S.y + (size_t)c * YLEN;
+  const int yreset = S.is[IS_YRESET * C + c];
+  auto yload = [&](int k) { return (k < YLEN && !yreset) ? yg[k] : 20.0; };
+  double yp0 = yload(t), yp1 = yload(t + FT);
   __syncthreads();
   double *ylds = lds;  // [YLEN]
 #pragma unroll
@@ -233,17 +239,17 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     const int yi = epos<L, 3>(t, i) ^ (N / 2);
     if (yi >= K::YLO && yi <= K::YHI) ylds[yi - K::YLO] = aero_hypot(x[i].x, x[i].y);
   }
+  double yp2 = yload(t + 2 * FT);
   __syncthreads();
-  {
-    double *yg = S.y + (size_t)c * YLEN;
-    const int yreset = S.is[IS_YRESET * C + c];
 #pragma unroll 1
-    for (int k = t; k < YLEN; k += FT) {
-      const double yold = yreset ? 20.0 : yg[k];
-      const double ynew = yold * 0.9 + 0.1 * 10 * aero_log10(fmax(ylds[k], 1.0));
-      yg[k] = ynew;
-      ylds[k] = ynew;
-    }
+  for (int k = t; k < YLEN; k += FT) {
+    const double yold = yp0;
+    yp0 = yp1;
+    yp1 = yp2;
+    yp2 = yload(k + 3 * FT);
+    const double ynew = yold * 0.9 + 0.1 * 10 * aero_log10(fmax(ylds[k], 1.0));
+    yg[k] = ynew;
+    ylds[k] = ynew;
   }
   __syncthreads();
   // fold search (coarsefreqestimate.cpp:166-185): first strict maximum above 0

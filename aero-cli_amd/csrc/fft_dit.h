@@ -50,30 +50,57 @@ struct TwLds {
   static constexpr int LEN = 2 * N - 1;             // TW[0 .. 2N-2]
 };
 
+// twiddles of one stage's 8 butterflies (the values i with bit lb clear, in
+// order).  epos(t, i) = epos(t, 0) | epos(0, i) with disjoint bits, so the
+// index splits into a per-thread base plus a compile-time offset per value;
+// duplicate indices (stages whose n spans fewer than 8 of the thread's
+// butterflies) are the same load and fold away.
 template <int LOG2N, int PH, bool INV>
-__device__ __forceinline__ void stage(double2 (&x)[16], int t0, int lb, int n, const double2 *__restrict__ TW,
-                                      const double2 *stw) {
+__device__ __forceinline__ void tw_load(double2 (&w)[8], int t0, int lb, int n, const double2 *__restrict__ TW,
+                                        const double2 *stw) {
   const int t = fresh(t0);
+  const int wbase = n - 1 + (epos<LOG2N, PH>(t, 0) & (n - 1));
+  int j = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (i & (1 << lb)) continue;
+    const int widx = wbase + (epos<LOG2N, PH>(0, i) & (n - 1));
+    if (n <= TwLds<LOG2N>::N) {
+      w[j] = stw[widx];
+      if (INV) w[j].y = -w[j].y;
+    } else {
+      w[j] = TW[widx];
+    }
+    ++j;
+  }
+}
+
+// the stage's radix-2 DIT butterflies with JFFT's operand order
+// (decode/jfft.cpp:176-204): y = w * x[il]; x[il] = x[i] - y; x[i] = x[i] + y
+__device__ __forceinline__ void bfly(double2 (&x)[16], int lb, const double2 (&w)[8]) {
+  int j = 0;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     if (i & (1 << lb)) continue;
     const int il = i | (1 << lb);
-    const int pk = epos<LOG2N, PH>(t, i);
-    const int widx = n - 1 + (pk & (n - 1));
-    double2 w;
-    if (n <= TwLds<LOG2N>::N) {
-      w = stw[widx];
-      if (INV) w.y = -w.y;
-    } else {
-      w = TW[widx];
-    }
-    const double yr = w.x * x[il].x - w.y * x[il].y;
-    const double yi = w.x * x[il].y + w.y * x[il].x;
+    const double yr = w[j].x * x[il].x - w[j].y * x[il].y;
+    const double yi = w[j].x * x[il].y + w[j].y * x[il].x;
     x[il].x = x[i].x - yr;
     x[il].y = x[i].y - yi;
     x[i].x = x[i].x + yr;
     x[i].y = x[i].y + yi;
+    ++j;
   }
+}
+
+// one radix-2 DIT stage of half-size n on the thread's 16 values; `lb` is the
+// bit of i that encodes the stage's position bit
+template <int LOG2N, int PH, bool INV>
+__device__ __forceinline__ void stage(double2 (&x)[16], int t, int lb, int n, const double2 *__restrict__ TW,
+                                      const double2 *stw) {
+  double2 w[8];
+  tw_load<LOG2N, PH, INV>(w, t, lb, n, TW, stw);
+  bfly(x, lb, w);
 }
 
 // move values from layout PH_FROM to PH_TO through LDS (re then im);
@@ -83,15 +110,22 @@ __device__ __forceinline__ void exchange(double2 (&x)[16], int t0, double *lds) 
 #pragma unroll
   for (int part = 0; part < 2; ++part) {
     const int t = fresh(t0);
+    // pad(A | B) = pad(A) + pad(B) for bit-disjoint A = epos(t, 0), B = epos(0, i)
+    // (bit reversal permutes bits, so it keeps them disjoint): one base address
+    // per thread, the per-value part is an immediate offset
+    double *wb = lds + pad(epos<LOG2N, PH_FROM>(t, 0));
+    int rp = epos<LOG2N, PH_TO>(t, 0);
+    if (BR) rp = bitrev<LOG2N>(rp);
+    const double *rb = lds + pad(rp);
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 16; ++i) lds[pad(epos<LOG2N, PH_FROM>(t, i))] = part ? x[i].y : x[i].x;
+    for (int i = 0; i < 16; ++i) wb[pad(epos<LOG2N, PH_FROM>(0, i))] = part ? x[i].y : x[i].x;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      int p = epos<LOG2N, PH_TO>(t, i);
+      int p = epos<LOG2N, PH_TO>(0, i);
       if (BR) p = bitrev<LOG2N>(p);
-      const double v = lds[pad(p)];
+      const double v = rb[pad(p)];
       if (part)
         x[i].y = v;
       else
@@ -122,14 +156,36 @@ __device__ __forceinline__ void fft_dit(double2 (&x)[16], int t, double *lds, co
   stage<L, 1, INV>(x, t, 1, 32, TW, stw);
   stage<L, 1, INV>(x, t, 2, 64, TW, stw);
   stage<L, 1, INV>(x, t, 3, 128, TW, stw);
-  exchange<L, 1, 2, false>(x, t, lds);
-  stage<L, 2, INV>(x, t, 0, 256, TW, stw);
-  stage<L, 2, INV>(x, t, 1, 512, TW, stw);
-  stage<L, 2, INV>(x, t, 2, 1024, TW, stw);
-  stage<L, 2, INV>(x, t, 3, 2048, TW, stw);
-  exchange<L, 2, 3, false>(x, t, lds);
-  stage<L, 3, INV>(x, t, 0, 4096, TW, stw);
-  if (L == 14) stage<L, 3, INV>(x, t, 1, 8192, TW, stw);
+  // the stages past TwLds read their twiddles from L2: each stage's loads are
+  // issued one stage (or one LDS exchange) ahead of its butterflies, so their
+  // latency overlaps work instead of stalling every wave of the workgroup
+  double2 wa[8], wb[8];
+  if (L == 14) {
+    tw_load<L, 2, INV>(wa, t, 2, 1024, TW, stw);
+    exchange<L, 1, 2, false>(x, t, lds);
+    stage<L, 2, INV>(x, t, 0, 256, TW, stw);
+    stage<L, 2, INV>(x, t, 1, 512, TW, stw);
+    tw_load<L, 2, INV>(wb, t, 3, 2048, TW, stw);
+    bfly(x, 2, wa);
+    bfly(x, 3, wb);
+    tw_load<L, 3, INV>(wa, t, 0, 4096, TW, stw);
+    exchange<L, 2, 3, false>(x, t, lds);
+    tw_load<L, 3, INV>(wb, t, 1, 8192, TW, stw);
+    bfly(x, 0, wa);
+    bfly(x, 1, wb);
+  } else {
+    tw_load<L, 2, INV>(wa, t, 1, 512, TW, stw);
+    exchange<L, 1, 2, false>(x, t, lds);
+    stage<L, 2, INV>(x, t, 0, 256, TW, stw);
+    tw_load<L, 2, INV>(wb, t, 2, 1024, TW, stw);
+    bfly(x, 1, wa);
+    tw_load<L, 2, INV>(wa, t, 3, 2048, TW, stw);
+    bfly(x, 2, wb);
+    tw_load<L, 3, INV>(wb, t, 0, 4096, TW, stw);
+    bfly(x, 3, wa);
+    exchange<L, 2, 3, false>(x, t, lds);
+    bfly(x, 0, wb);
+  }
 }
 
 
