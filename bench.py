@@ -33,15 +33,15 @@ MODES = {
     # 2 B int16 in + 16 B AGC ring r/w (192000-deep, cannot stay on chip) + 0.22 B soft bits out
     'oqpsk10500': dict(bitrate=10500, hop=4096, fs=48000, bytes=18.22, kernel='demod_oqpsk_kernel', timing='demod',
                        metric='Msamples/s demod+Viterbi, 10500bps OQPSK, 1/2/4/8 GPU; ACARS frames bit-exact vs ref',
-                       cpu_seconds=240.0, config='C2'),
+                       cpu_seconds=240.0, config='C2', flops=1300.0),
     # 2 B int16 in + 0.05 B soft bits out
     'msk600': dict(bitrate=600, hop=2048, fs=12000, bytes=2.05, kernel='demod_msk_kernel<1>', timing='msk600_demod',
                    metric='Msamples/s demod+Viterbi, 600bps MSK (C3); ACARS frames bit-exact vs ref',
-                   cpu_seconds=2400.0, config='C3'),
+                   cpu_seconds=2400.0, config='C3', flops=1050.0),
     # 2 B int16 in + 0.025 B soft bits out (fb stays 600 at 24 kHz, decode/decode.cpp:142-150)
     'msk1200': dict(bitrate=1200, hop=2048, fs=24000, bytes=2.025, kernel='demod_msk_kernel<2>',
                     timing='msk1200_demod', metric='Msamples/s demod+Viterbi, 1200bps MSK; ACARS frames bit-exact vs ref',
-                    cpu_seconds=1200.0, config='C3 (1200 variant)'),
+                    cpu_seconds=1200.0, config='C3 (1200 variant)', flops=1050.0),
 }
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6    # MI355X vector FP64 (spec)
@@ -213,6 +213,11 @@ def main():
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
                          'traffic': traffic, 'bytes_per_sample': M['bytes'],
                          'avg_launch_ms': round(per_launch_s * 1e3, 3)},
+            # SURVEY §8(d) / BASELINE.md: the path is FP64-VALU bound, so the whole-path FP64
+            # rate (algorithmic flop per input sample x samples/s) is reported beside the HBM one
+            'fp64_roofline': {'flop_per_sample': M['flops'], 'achieved': round(value * 1e6 * M['flops'] / 1e12, 3),
+                              'peak': FP64_PEAK_TFLOPS * world, 'unit': 'TFLOP/s',
+                              'frac': round(value * 1e6 * M['flops'] / 1e12 / (FP64_PEAK_TFLOPS * world), 5)},
             'kernel_ms_per_step': {k: round(v[0] / max(a.steps, 1), 3) for k, v in kt.items()},
             'acars_items': items,
             'host_ms_per_step': {k: round(v[0] / max(a.steps, 1), 3) for k, v in ht.items()},
