@@ -13,7 +13,13 @@
 
 namespace aero {
 
-__device__ __forceinline__ int pad(int p) { return p + (p >> 4); }
+// LDS padding of the transposes: one double per 32 (one 64-bank row of
+// dwords).  Contiguous 32-lane accesses (layouts 2, 3) stay conflict-free and
+// the stride-16 ones (layout 0) spread over all banks; it is additive over
+// bit-disjoint parts, which the base + immediate-offset addressing needs.
+// (p + p/16 left 2-way conflicts on layouts 2/3 and the bit-reversed reads:
+// SQ_LDS_BANK_CONFLICT ~= SQ_ACTIVE_INST_LDS on coarse_kernel.)
+__device__ __forceinline__ int pad(int p) { return p + (p >> 5); }
 
 // position of value i of thread t in register phase PH (4 FFT stages per
 // phase; the last phase holds the LOG2N - 12 remaining stage bits in i's low bits)
