@@ -180,10 +180,11 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   __syncthreads();
 
   load_tw_lds<L>(s_tw, T.tw, t, FT);
-  // ring words -> LDS (as uint32 in the first N*4 bytes)
+  // ring words -> LDS (uint32, one pad word per 16: the bit-reversed gather
+  // below reads 16-word strides, which would hit 4 of the 64 banks unpadded)
   uint32_t *ring_lds = reinterpret_cast<uint32_t *>(lds);
   const uint32_t *ring = S.cring + (size_t)c * N;
-  for (int j = t; j < N; j += FT) ring_lds[j] = ring[j];
+  for (int j = t; j < N; j += FT) ring_lds[j + (j >> 4)] = ring[j];
   __syncthreads();
   double2 x[16];
   const long long s0 = nk - (N - 1);  // sample of snapshot element 0 (oqpskdemodulator.cpp:359-365)
@@ -194,7 +195,8 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     if (s < 0 || s < zero_before) {
       x[i] = make_double2(0.0, 0.0);
     } else {
-      const uint32_t w = ring_lds[s & (N - 1)];
+      const int q = (int)(s & (N - 1));
+      const uint32_t w = ring_lds[q + (q >> 4)];
       const double dval = ((double)(int16_t)(w >> 16)) / 32768.0;
       const double2 cs = T.cis[w & 0xFFFF];
       x[i] = make_double2(cs.x * dval, cs.y * dval);
