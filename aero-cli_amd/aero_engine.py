@@ -112,6 +112,7 @@ _SIGS = {
                                    ctypes.POINTER(ctypes.c_long)]),
     'aero_timing_reset': (None, [ctypes.c_void_p]),
     'aero_samples_processed': (ctypes.c_uint64, [ctypes.c_void_p]),
+    'aero_stat': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]),
     'aero_sync': (ctypes.c_int, [ctypes.c_void_p]),
     'aero_device_math': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_size_t]),
@@ -138,15 +139,42 @@ _SIGS = {
 _lib = None
 
 
+def _torch_hip_runtime():
+    """Paths of the HIP/HSA runtime copies a PyTorch-ROCm wheel bundles
+    (torch/lib), or [] when torch is not installed.  Found without importing
+    torch (no HIP initialisation happens here)."""
+    import importlib.util
+    spec = importlib.util.find_spec('torch')
+    if spec is None or not spec.origin:
+        return []
+    tlib = os.path.join(os.path.dirname(spec.origin), 'lib')
+    return [p for p in (os.path.join(tlib, 'libhsa-runtime64.so'), os.path.join(tlib, 'libamdhip64.so'))
+            if os.path.exists(p)]
+
+
 def load_library(path=None):
     """Loads libaero_engine.so (or $AERO_ENGINE_SO, an experimental build of
-    the same sources); raises when the HIP build is missing."""
+    the same sources); raises when the HIP build is missing.
+
+    One HIP runtime per process: the PyTorch-ROCm wheel bundles its own
+    libamdhip64 / libhsa-runtime64 (SONAME libamdhip64.so.7, the same as
+    /opt/rocm's, which the engine links).  Loaded after torch, the engine
+    binds to torch's copy by SONAME; loaded first, it would pull in
+    /opt/rocm's copy and torch would then load a second runtime from
+    torch/lib, and a device pointer allocated by one runtime is unknown to
+    the other (aero_push_pcm_dev / aero_chan_push(dev) fail).  So torch's
+    copy, when torch is installed, is loaded first by its absolute path:
+    torch's later load of the same file reuses it (same inode) and the engine
+    binds to it by SONAME, in either import order.  Without torch (the C++
+    host) the engine uses /opt/rocm's runtime."""
     global _lib
     if _lib is not None:
         return _lib
     path = path or os.environ.get('AERO_ENGINE_SO') or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError('libaero_engine.so not built (%s); run aero-cli_amd/build.py' % path)
+    for rt in _torch_hip_runtime():
+        ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
     lib = ctypes.CDLL(path)
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)
@@ -333,6 +361,12 @@ class Engine:
 
     def timing_reset(self):
         self.lib.aero_timing_reset(self.h)
+
+    def stat(self, name):
+        """aero_stat counter: 'viterbi_jobs', 'frames' or 'su_crc_ok'."""
+        v = ctypes.c_uint64()
+        _check(self.lib.aero_stat(self.h, name.encode(), ctypes.byref(v)), 'aero_stat')
+        return int(v.value)
 
     def samples_processed(self):
         return int(self.lib.aero_samples_processed(self.h))

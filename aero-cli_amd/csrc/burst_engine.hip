@@ -303,7 +303,8 @@ int run_once(BurstGroup *g, bool trace, bool &progress) {
 }  // namespace
 
 int burst_group_create(int device, int flags, int max_channels, BurstGroup **out) {
-  std::unique_ptr<BurstGroup> g(new BurstGroup());
+  // every early return below releases what was already allocated
+  std::unique_ptr<BurstGroup, void (*)(BurstGroup *)> g(new BurstGroup(), burst_group_destroy);
   g->device = device;
   g->flags = flags;
   g->C = (max_channels + 63) & ~63;

@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "../../include/aero_chan.h"
+#include "engine_internal.h"
 #include "tables_host.h"
 
 using aero::host_pub_hilbert;
@@ -277,7 +278,7 @@ struct aero_chan {
   float2 *in = nullptr, *avept = nullptr;
   int pending = 0, last_nblk = 0, parity = 0;
   hipStream_t st = nullptr;
-  hipEvent_t ev_jobs = nullptr, ev_pin = nullptr, ev_in = nullptr;
+  hipEvent_t ev_jobs = nullptr, ev_pin = nullptr, ev_in = nullptr, ev_out = nullptr;
   std::vector<void *> dmem;
   char *d_jobs = nullptr, *h_jobs = nullptr;
   size_t jobs_cap = 0;
@@ -541,6 +542,7 @@ void destroy_impl(aero_chan *c) {
   if (c->ev_jobs) (void)hipEventDestroy(c->ev_jobs);
   if (c->ev_pin) (void)hipEventDestroy(c->ev_pin);
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+  if (c->ev_out) (void)hipEventDestroy(c->ev_out);
   if (c->st) (void)hipStreamDestroy(c->st);
 }
 
@@ -652,6 +654,7 @@ int aero_chan_create(const aero_chan_cfg *cfg, const aero_chan_main *mains, int 
   CHK(hipEventCreateWithFlags(&c->ev_jobs, hipEventDisableTiming));
   CHK(hipEventCreateWithFlags(&c->ev_pin, hipEventDisableTiming));
   CHK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
+  CHK(hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming));
   if (int rc = dalloc(c.get(), c->in, (size_t)cfg->max_blocks * c->B)) return rc;
   if (int rc = dalloc(c.get(), c->avept, 1)) return rc;
   for (auto &m : c->mains)
@@ -707,6 +710,13 @@ int aero_chan_push(aero_chan *c, const float *iq, size_t nblocks, int dev) {
   if (!c || (!iq && nblocks)) return AERO_E_INVALID;
   CHK(hipSetDevice(c->cfg.device));
   const size_t blk = (size_t)c->B * 2;  // floats per read
+  // without host output an implicit batch would overwrite the previous
+  // batch's device audio before aero_chan_feed / aero_chan_vfo_output read
+  // it: refuse the push whole instead (with host output every batch is kept)
+  if (!(c->cfg.flags & AERO_CHAN_F_HOST_OUT) && (size_t)c->pending + nblocks > (size_t)c->cfg.max_blocks)
+    return AERO_E_FULL;
+  if (dev && nblocks)
+    if (int rc = check_dev_ptr(iq)) return rc;
   size_t done = 0;
   while (done < nblocks) {
     if (c->pending == c->cfg.max_blocks)
@@ -771,13 +781,23 @@ int aero_chan_pop_iq(aero_chan *c, int m, int8_t *dst, size_t cap, size_t *n) {
 int aero_chan_feed(aero_chan *c, aero_engine *e, const int *ch) {
   if (!c || !e || !ch) return AERO_E_INVALID;
   CHK(hipSetDevice(c->cfg.device));
-  CHK(hipStreamSynchronize(c->st));
+  // one gather launch per channel kind, ordered after this batch's audio by
+  // an event; the next batch waits for it on this stream (no host wait)
+  std::vector<int> chs;
+  std::vector<const int16_t *> src;
+  std::vector<size_t> n;
+  std::vector<uint32_t> fs;
   for (size_t v = 0; v < c->subs.size(); v++) {
     const Vfo &s = c->subs[v];
     if (ch[v] < 0 || !s.active || !c->last_nblk) continue;
-    if (int rc = aero_push_pcm_dev(e, ch[v], s.out16, (size_t)c->last_nblk * s.S, (uint32_t)s.out_rate)) return rc;
+    chs.push_back(ch[v]);
+    src.push_back(s.out16);
+    n.push_back((size_t)c->last_nblk * s.S);
+    fs.push_back((uint32_t)s.out_rate);
   }
-  return AERO_OK;
+  if (chs.empty()) return AERO_OK;
+  CHK(hipEventRecord(c->ev_out, c->st));
+  return aero_engine_feed_dev(e, (int)chs.size(), chs.data(), src.data(), n.data(), fs.data(), c->ev_out, c->st);
 }
 
 }  // extern "C"

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <chrono>
 #include <deque>
 #include <condition_variable>
@@ -34,6 +35,7 @@
 #include "burst_engine.h"
 #include "aero_math.h"
 #include "engine_common.h"
+#include "engine_internal.h"
 #include "tables_host.h"
 
 namespace aero {
@@ -74,6 +76,20 @@ __global__ void pcm_scatter_kernel(int16_t *ring, int C, long long capm, const i
     const int j = (int)(k - t * nch);
     ring[((start + t) & capm) * C + c0 + j] = src[t * ld + j];
   }
+}
+
+// one feed item: a device PCM run for one channel (aero_chan_feed)
+struct GatherJob {
+  const int16_t *src;
+  long long n, start, avail_after;
+  int c, pad;
+};
+
+__global__ void pcm_gather_kernel(int16_t *ring, int C, long long capm, long long *avail, const GatherJob *jobs) {
+  const GatherJob j = jobs[blockIdx.y];
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < j.n; t += (long long)gridDim.x * blockDim.x)
+    ring[((j.start + t) & capm) * C + j.c] = j.src[t];
+  if (blockIdx.x == 0 && threadIdx.x == 0) avail[j.c] = j.avail_after;  // LS_AVAIL row
 }
 
 __global__ void math_kernel(int fn, const double *x, const double *y, double *out, size_t n) {
@@ -189,6 +205,7 @@ class HostPool {
 // One group per channel kind (Mode): its own device pool, stream, tables and
 // kernels.  aero_engine routes every channel to its kind's group.
 struct Group {
+  ~Group();  // releases every device/host resource (also on a failed group_create)
   int mode = MODE_OQPSK;
   ModeGeom g{};
   int device = 0, flags = 0, C = 0, nch = 0;
@@ -249,9 +266,17 @@ struct Group {
   size_t stage_cap[2] = {};
   hipEvent_t ev_stage_used[2] = {};
   int next_stage = 0;
+  // aero_chan_feed job tables (pinned -> device, reused once their event completed)
+  GatherJob *pin_gjobs[NPIN] = {}, *d_gjobs[NPIN] = {};
+  hipEvent_t gjob_ev[NPIN] = {};
+  int next_gjob = 0;
+  hipEvent_t ev_feed_done = nullptr;
   std::map<std::string, TimingSlot> timing;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending_ev;
   uint64_t processed = 0;
+  // aero_stat counters: Viterbi jobs handed back, frames delivered to the
+  // SU/ACARS host, SUs whose CRC checked
+  std::atomic<uint64_t> st_jobs{0}, st_frames{0}, st_su_ok{0};
   int init_lo = 0;  // channels [init_lo, nch) await device state init
   std::vector<uint8_t> h_jobs_task, h_dbg_task;  // buffers owned by the running host task
 };
@@ -439,6 +464,7 @@ int process_slot(Group *e, int si) {
     HIPCHK(hipMemcpy(e->h_dbg_task.data(), e->S.blocks_dbg, e->h_dbg_task.size(), hipMemcpyDeviceToHost));
   }
   if (njobs <= 0) return AERO_OK;
+  e->st_jobs += (uint64_t)njobs;
   const bool msk = e->mode != MODE_OQPSK;
   // channels partitioned over workers (c % T): a channel's frames stay in
   // queue order and no two workers share state
@@ -481,6 +507,8 @@ int process_slot(Group *e, int si) {
         flen = meta[0];
       }
       if (flen >= 0) {
+        e->st_frames++;
+        e->st_su_ok += (uint64_t)__builtin_popcount(mask);
         e->host[c]->frame(info, flen, mask, meta[2]);
         if (e->flags & AERO_F_TRACE_FRAMES) {
           uint8_t rec[320] = {0};
@@ -694,7 +722,7 @@ int pop_vec(std::vector<T> &v, T *dst, size_t cap, size_t *n) {
 
 // group tables and kernel constants (host glibc, g++-compiled: tables_host.cpp)
 int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
-  std::unique_ptr<Group> e(new Group());
+  std::unique_ptr<Group> e(new Group());  // ~Group releases what an early return leaves allocated
   e->mode = mode;
   e->g = mode_geom(mode);
   e->device = E->device;
@@ -797,6 +825,12 @@ void group_destroy(Group *e) {
     if (e->pin_avail[k]) (void)hipHostFree(e->pin_avail[k]);
     if (e->pin_ev[k]) (void)hipEventDestroy(e->pin_ev[k]);
   }
+  for (int k = 0; k < Group::NPIN; k++) {
+    if (e->pin_gjobs[k]) (void)hipHostFree(e->pin_gjobs[k]);
+    if (e->d_gjobs[k]) (void)hipFree(e->d_gjobs[k]);
+    if (e->gjob_ev[k]) (void)hipEventDestroy(e->gjob_ev[k]);
+  }
+  if (e->ev_feed_done) (void)hipEventDestroy(e->ev_feed_done);
   if (e->pin_pcm) (void)hipHostFree(e->pin_pcm);
   if (e->pin_pcm_ev) (void)hipEventDestroy(e->pin_pcm_ev);
   if (e->st_in) hipStreamSynchronize(e->st_in);
@@ -811,6 +845,12 @@ void group_destroy(Group *e) {
   if (e->st) (void)hipStreamDestroy(e->st);
 }
 
+}  // namespace
+
+Group::~Group() { group_destroy(this); }
+
+namespace {
+
 // engine channel -> (group, local index); nullptr if out of range
 Group *route(aero_engine *e, int ch, int &local) {
   if (!e || ch < 0 || ch >= (int)e->chmap.size() || e->chmap[ch].first == MODE_BURST) return nullptr;
@@ -818,8 +858,27 @@ Group *route(aero_engine *e, int ch, int &local) {
   return e->groups[e->chmap[ch].first].get();
 }
 
+}  // namespace
+
+// A device pointer this process's HIP runtime does not know (e.g. allocated
+// by a second runtime copy loaded into the process, aero_engine.py
+// load_library) cannot be copied from: refuse it loudly.
+int check_dev_ptr(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    fprintf(stderr, "aero_engine: %p is not a device pointer of this process's HIP runtime\n", p);
+    return AERO_E_INVALID;
+  }
+  return AERO_OK;
+}
+
+namespace {
+
 int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int c0, bool dev) {
   HOST_TIMER(e, "host_push");
+  if (dev)
+    if (int rc = check_dev_ptr(src)) return rc;
   if (int rc = flush_pending_init(e)) return rc;
   // keep the ring from overrunning unprocessed samples
   for (int j = 0; j < nch; j++) {
@@ -845,7 +904,13 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
       e->scratch_cap = need;
     }
     if (need > e->pin_pcm_cap) {
-      if (e->pin_pcm) (void)hipHostFree(e->pin_pcm);
+      for (int k = 0; k < Group::NPIN; k++) {
+    if (e->pin_gjobs[k]) (void)hipHostFree(e->pin_gjobs[k]);
+    if (e->d_gjobs[k]) (void)hipFree(e->d_gjobs[k]);
+    if (e->gjob_ev[k]) (void)hipEventDestroy(e->gjob_ev[k]);
+  }
+  if (e->ev_feed_done) (void)hipEventDestroy(e->ev_feed_done);
+  if (e->pin_pcm) (void)hipHostFree(e->pin_pcm);
       e->pin_pcm = nullptr;
       e->pin_pcm_cap = 0;
       HIPCHK(hipHostMalloc(&e->pin_pcm, need * sizeof(int16_t)));
@@ -892,6 +957,62 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
   HIPCHK(hipMemcpyAsync(e->S.ls + (size_t)LS_AVAIL * e->C + c0, e->pin_avail[k], 8 * nch, hipMemcpyHostToDevice,
                         e->st));
   HIPCHK(hipEventRecord(e->pin_ev[k], e->st));
+  return AERO_OK;
+}
+
+// Channeliser -> decoder hand-off without a host wait (aero_chan_feed): the
+// group's stream waits for the producer's audio (event `ready`), one gather
+// launch copies every item into the PCM rings and sets the channels' pushed
+// counters, and the producer's stream then waits for that launch before it
+// may overwrite the audio.  items: (local channel, device source, samples).
+int feed_group(Group *e, const std::vector<std::pair<int, std::pair<const int16_t *, size_t>>> &items,
+               hipEvent_t ready, hipStream_t producer) {
+  HOST_TIMER(e, "host_push");
+  if (items.empty()) return AERO_OK;
+  if (int rc = flush_pending_init(e)) return rc;
+  for (auto &it : items) {  // keep the ring from overrunning unprocessed samples
+    const int c = it.first;
+    const long long n = (long long)it.second.second;
+    if (n > PCM_CAP / 2) return AERO_E_FULL;
+    if (e->avail[c] + n - e->nsamp[c] > PCM_CAP - 2) {
+      if (int rc = run_group(e, 0)) return rc;
+      if (e->avail[c] + n - e->nsamp[c] > PCM_CAP - 2) return AERO_E_FULL;
+    }
+  }
+  const int k = e->next_gjob;
+  e->next_gjob = (k + 1) % Group::NPIN;
+  if (!e->pin_gjobs[k]) {
+    if (hipHostMalloc(&e->pin_gjobs[k], sizeof(GatherJob) * e->C) != hipSuccess) return AERO_E_NOMEM;
+    if (hipMalloc(&e->d_gjobs[k], sizeof(GatherJob) * e->C) != hipSuccess) return AERO_E_NOMEM;
+    HIPCHK(hipEventCreateWithFlags(&e->gjob_ev[k], hipEventDisableTiming));
+  }
+  if (!e->ev_feed_done) HIPCHK(hipEventCreateWithFlags(&e->ev_feed_done, hipEventDisableTiming));
+  HIPCHK(hipEventSynchronize(e->gjob_ev[k]));  // the table NPIN feeds ago has been read
+  if ((int)items.size() > e->C) return AERO_E_INVALID;
+  long long mx = 0;
+  for (size_t i = 0; i < items.size(); i++) {
+    const int c = items[i].first;
+    const long long n = (long long)items[i].second.second;
+    GatherJob &j = e->pin_gjobs[k][i];
+    j.src = items[i].second.first;
+    j.n = n;
+    j.start = e->avail[c];
+    j.avail_after = e->avail[c] + n;
+    j.c = c;
+    j.pad = 0;
+    e->avail[c] += n;
+    mx = std::max(mx, n);
+  }
+  HIPCHK(hipMemcpyAsync(e->d_gjobs[k], e->pin_gjobs[k], sizeof(GatherJob) * items.size(), hipMemcpyHostToDevice,
+                        e->st));
+  HIPCHK(hipEventRecord(e->gjob_ev[k], e->st));
+  HIPCHK(hipStreamWaitEvent(e->st, ready, 0));
+  const unsigned gx = (unsigned)std::max<long long>(1, std::min<long long>((mx + 255) / 256, 64));
+  hipLaunchKernelGGL(pcm_gather_kernel, dim3(gx, (unsigned)items.size()), dim3(256), 0, e->st, e->S.pcm, e->C,
+                     (long long)PCM_CAP - 1, e->S.ls + (size_t)LS_AVAIL * e->C, (const GatherJob *)e->d_gjobs[k]);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e->ev_feed_done, e->st));
+  HIPCHK(hipStreamWaitEvent(producer, e->ev_feed_done, 0));
   return AERO_OK;
 }
 
@@ -942,7 +1063,7 @@ void aero_engine_destroy(aero_engine *e) {
   for (auto &g : e->groups)
     if (g) (void)drain_group(g.get());
   host_wait(e);
-  for (auto &g : e->groups) group_destroy(g.get());
+  for (auto &g : e->groups) g.reset();
   if (e->burst) burst_group_destroy(e->burst);
   delete e;
 }
@@ -1209,6 +1330,26 @@ void aero_timing_reset(aero_engine *e) {
     }
 }
 
+int aero_stat(aero_engine *e, const char *name, uint64_t *value) {
+  if (!e || !name || !value) return AERO_E_INVALID;
+  host_wait(e);  // counters of frames the host workers are still handling
+  uint64_t v = 0;
+  const std::string n(name);
+  for (auto &g : e->groups) {
+    if (!g) continue;
+    if (n == "viterbi_jobs")
+      v += g->st_jobs.load();
+    else if (n == "frames")
+      v += g->st_frames.load();
+    else if (n == "su_crc_ok")
+      v += g->st_su_ok.load();
+    else
+      return AERO_E_INVALID;
+  }
+  *value = v;
+  return AERO_OK;
+}
+
 uint64_t aero_samples_processed(aero_engine *e) {
   uint64_t s = 0;
   if (e) {
@@ -1249,3 +1390,29 @@ int aero_device_math(aero_engine *e, int fn, const double *x, const double *y, d
 }
 
 }  // extern "C"
+
+// aero_chan_feed's entry into the engine (engine_internal.h)
+int aero_engine_feed_dev(aero_engine *e, int nitems, const int *ch, const int16_t *const *src, const size_t *n,
+                         const uint32_t *fs, hipEvent_t ready, hipStream_t producer) {
+  if (!e || nitems < 0 || (nitems && (!ch || !src || !n || !fs))) return AERO_E_INVALID;
+  HIPCHK(hipSetDevice(e->device));
+  std::vector<std::pair<int, std::pair<const int16_t *, size_t>>> per[MODE_COUNT];
+  for (int i = 0; i < nitems; i++) {
+    if (!n[i]) continue;
+    const int b = route_burst(e, ch[i]);
+    if (b >= 0) {  // burst channels keep one message per call (synchronous copy)
+      HIPCHK(hipEventSynchronize(ready));
+      if (int rc = push_burst(e, b, src[i], n[i], true)) return rc;
+      continue;
+    }
+    int c;
+    Group *g = route(e, ch[i], c);
+    if (!g || !src[i]) return AERO_E_INVALID;
+    if (g->mode != MODE_OQPSK && fs[i] != (uint32_t)g->g.fs) return AERO_E_RATE;
+    per[g->mode].push_back({c, {src[i], n[i]}});
+  }
+  for (int m = 0; m < MODE_COUNT; m++)
+    if (!per[m].empty())
+      if (int rc = feed_group(e->groups[m].get(), per[m], ready, producer)) return rc;
+  return AERO_OK;
+}

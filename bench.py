@@ -45,6 +45,16 @@ MODES = {
 }
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6    # MI355X vector FP64 (spec)
+# Untimed pre-roll before the warmup steps: the hunter's scan and the carrier
+# lock take ~30 hops on the synthetic streams; 48 hops leave every channel
+# locked (mse < threshold) however small --warmup is, so the timed steps
+# always run the locked path (soft bits -> frames -> Viterbi -> ACARS)
+PREROLL_HOPS = 48
+# CPU-baseline calibration: the oracle's
+# per-core rate on the survey container's Intel Xeon (8 vCPU) against the
+# reference's own -O2 build probed on that same host
+CALIBRATION = {'oqpsk10500': {'port_msps_per_core': 0.967, 'reference_msps_per_core': 0.996},
+               'msk600': {'port_msps_per_core': 1.114, 'reference_msps_per_core': 1.387}}
 
 
 def parse():
@@ -53,15 +63,19 @@ def parse():
     ap.add_argument('--mode', default='oqpsk10500', choices=sorted(MODES),
                     help='channel kind (default: the BASELINE.json headline, C2 10500-bps OQPSK)')
     ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=48, help='hops before timing (hunter scan + lock)')
+    ap.add_argument('--warmup', type=int, default=5,
+                    help='untimed steps after the fixed %d-hop lock-in pre-roll' % PREROLL_HOPS)
     ap.add_argument('--channels', type=int, default=65536, help='VFO channels per GPU (one lane each: 65536 fill the 1024 SIMDs at one wave each)')
     ap.add_argument('--pool', type=int, default=64, help='distinct synthetic streams per GPU')
     ap.add_argument('--cpu-seconds', type=float, default=None,
                     help='signal seconds per CPU-baseline process (default per mode: ~5-10 s CPU each)')
-    ap.add_argument('--cpu-procs', type=int, default=8)
+    ap.add_argument('--cpu-procs', type=int, default=None,
+                    help='CPU-baseline processes (default: the host cores this process may use, at most 16 = '
+                         'the GPU box CPU share)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'pmc_demod.json'),
-                    help='rocprofv3 PMC summary for the roofline traffic field')
+    ap.add_argument('--pmc', default=None,
+                    help='rocprofv3 PMC summary for the roofline traffic field (default profiles/pmc_<mode>.json; '
+                         'used only when it was captured at this mode and channel count)')
     return ap.parse_args()
 
 
@@ -86,10 +100,31 @@ def make_pool(M, n_streams, length, seed0):
         return np.stack(list(ex.map(one, range(n_streams))))
 
 
-def cpu_baseline(M, seconds, procs):
+def host_cores():
+    """Cores this process may run on, capped at the GPU box's per-GPU CPU
+    share (16): os.cpu_count() there reports the whole machine."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_model():
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
+def cpu_baseline(mode, M, seconds, procs):
     """The oracle (CPU port of the reference path) on host cores, one process
     per channel as aero-decode is deployed (one VFO per process); bounded
-    sample: each process decodes `seconds` of its own synthetic stream."""
+    sample: each process decodes `seconds` of its own synthetic stream.  The
+    1-core figure is samples per CPU-second of the same runs."""
     import multiprocessing as mp
     ctx = mp.get_context('fork')
     with ctx.Pool(procs) as p:
@@ -97,12 +132,16 @@ def cpu_baseline(M, seconds, procs):
     total = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     cpu = sum(r[1] for r in res)
-    return {'value': round(total / wall / 1e6, 4), 'unit': 'Msamples/s', 'cores': procs, 'kind': 'port',
-            'sample': '%d processes x %.0f s of synthetic %d-bps P-channel (%d Hz int16) through '
-                      'oracle/liboracle.so (demod + coarse + hunter + AeroL + Viterbi + ACARS), '
-                      '%d-sample messages; %.1f s CPU total' % (procs, seconds, M['bitrate'], M['fs'], M['fs'] // 4,
-                                                             cpu),
-            'per_core_msps': round(total / cpu / 1e6, 4)}
+    out = {'value': round(total / wall / 1e6, 4), 'unit': 'Msamples/s', 'cores': procs, 'kind': 'port',
+           'sample': '%d processes x %.0f s of synthetic %d-bps P-channel (%d Hz int16) through '
+                     'oracle/liboracle.so (demod + coarse + hunter + AeroL + Viterbi + ACARS), '
+                     '%d-sample messages; %.1f s CPU total' % (procs, seconds, M['bitrate'], M['fs'], M['fs'] // 4,
+                                                            cpu),
+           'one_core_msps': round(total / cpu / 1e6, 4), 'cpu_model': cpu_model(),
+           'host_cpus_visible': os.cpu_count()}
+    if mode in CALIBRATION:
+        out['calibration'] = dict(CALIBRATION[mode], host='survey container Intel Xeon, 8 vCPU, 1 thread')
+    return out
 
 
 def _cpu_one(arg):
@@ -115,8 +154,43 @@ def _cpu_one(arg):
     return len(pcm), time.perf_counter() - t
 
 
+def spawn_ranks(n):
+    """--gpus N without a launcher: one child process per GPU with the
+    torch.distributed env a launcher would set (rendezvous on 127.0.0.1).
+    This process never touches the GPU; it exits with the worst child code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+def pmc_traffic(path, mode, channels):
+    """HBM bytes per dominant-kernel launch from a rocprofv3 PMC capture of
+    this same bench configuration (scripts/pmc_bench.sh); None otherwise."""
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    cfg = d.get('config', {})
+    if cfg.get('mode') != mode or int(cfg.get('channels', -1)) != channels:
+        return None, None
+    return d.get('hbm_bytes_per_launch'), os.path.relpath(path, ROOT)
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and 'RANK' not in os.environ:
+        sys.exit(spawn_ranks(a.gpus))
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
@@ -124,14 +198,15 @@ def main():
     M = MODES[a.mode]
     HOP, FS = M['hop'], M['fs']
     C, P = a.channels, a.pool
-    steps_total = a.warmup + a.steps
+    pre = PREROLL_HOPS + a.warmup  # untimed hops: lock-in pre-roll + warmup
+    steps_total = pre + a.steps
     span = steps_total * HOP
     offsets = shard.channel_offsets(C, P, rank)
     pool_host = make_pool(M, P, span + int(offsets.max()) + 1, 0xAE20 + 1000 * rank)
     # CPU baseline first, in worker processes forked before this process touches the GPU
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(M, a.cpu_seconds or M['cpu_seconds'], a.cpu_procs)
+        cpu = cpu_baseline(a.mode, M, a.cpu_seconds or M['cpu_seconds'], a.cpu_procs or host_cores())
 
     import torch
     import torch.distributed as dist
@@ -149,18 +224,20 @@ def main():
     eng = ae.Engine(max_channels=C, device=local, flags=ae.F_TIMING)
     for _ in range(C):
         eng.open_channel(M['bitrate'], FS)
-    # warmup: hunter scan, AFC and lock (untimed)
-    for s in range(a.warmup):
+    # pre-roll (hunter scan, AFC and lock) + warmup, untimed
+    for s in range(pre):
         x = step_input(s)
         torch.cuda.synchronize()
         eng.push_batch_device(x.data_ptr(), HOP, C, C)
         eng.run()
         eng.drain_items()
-    timed_inputs = [step_input(a.warmup + s) for s in range(a.steps)]
+    timed_inputs = [step_input(pre + s) for s in range(a.steps)]
     eng.sync()
+    eng.drain_items()
     torch.cuda.synchronize()
     eng.timing_reset()
     s0 = eng.samples_processed()
+    st0 = {k: eng.stat(k) for k in ('viterbi_jobs', 'frames', 'su_crc_ok')}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -177,14 +254,19 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     samples = eng.samples_processed() - s0
-    t = torch.tensor([elapsed, float(samples)], dtype=torch.float64, device='cuda')
+    stats = {k: eng.stat(k) - v for k, v in st0.items()}
+    stats['acars_items'] = items
+    keys = sorted(stats)
+    t = torch.tensor([elapsed, float(samples)] + [float(stats[k]) for k in keys], dtype=torch.float64,
+                     device='cuda')
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed, samples = float(tmax[0]), float(t[1])
-    pre = M['timing'][:-len('demod')]
-    kt = {k: eng.timing(pre + k) for k in ('demod', 'coarse', 'frame', 'viterbi')}
+        stats = {k: int(t[2 + i]) for i, k in enumerate(keys)}
+    tag = M['timing'][:-len('demod')]
+    kt = {k: eng.timing(tag + k) for k in ('demod', 'coarse', 'frame', 'viterbi')}
     ht = {k: eng.timing(k) for k in ('host_push', 'host_run', 'host_wait_njobs', 'host_wait_jobs', 'host_frames')}
     if rank == 0:
         value = samples / elapsed / 1e6
@@ -192,16 +274,13 @@ def main():
         per_launch_s = dm_ms / 1e3 / max(dm_n, 1)
         samples_per_launch = C * HOP
         achieved = M['bytes'] * samples_per_launch / per_launch_s / 1e9
-        traffic = None
-        if a.mode == 'oqpsk10500' and os.path.exists(a.pmc):
-            try:
-                traffic = json.load(open(a.pmc)).get('hbm_bytes_per_launch')
-            except Exception:
-                traffic = None
+        traffic, traffic_src = pmc_traffic(a.pmc or os.path.join(ROOT, 'profiles', 'pmc_%s.json' % a.mode),
+                                           a.mode, C)
         out = {
             'metric': M['metric'],
             'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world, 'steps': a.steps,
-            'warmup': a.warmup, 'ms_per_step': round(elapsed / a.steps * 1e3, 3), 'higher_is_better': True,
+            'warmup': a.warmup, 'preroll_hops': PREROLL_HOPS, 'ms_per_step': round(elapsed / a.steps * 1e3, 3),
+            'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
             'config': {'workload': '%s x %d: independent single-VFO %d-bps continuous %s P-channels '
                                    'per GPU, %d Hz int16, one %d-sample hop per step' % (
@@ -211,7 +290,7 @@ def main():
                        'parallelism': 'channel-sharded x%d' % world},
             'roofline': {'bound': 'hbm', 'kernel': M['kernel'], 'achieved': round(achieved, 2),
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
-                         'traffic': traffic, 'bytes_per_sample': M['bytes'],
+                         'traffic': traffic, 'traffic_source': traffic_src, 'bytes_per_sample': M['bytes'],
                          'avg_launch_ms': round(per_launch_s * 1e3, 3)},
             # SURVEY §8(d) / BASELINE.md: the path is FP64-VALU bound, so the whole-path FP64
             # rate (algorithmic flop per input sample x samples/s) is reported beside the HBM one
@@ -219,13 +298,17 @@ def main():
                               'peak': FP64_PEAK_TFLOPS * world, 'unit': 'TFLOP/s',
                               'frac': round(value * 1e6 * M['flops'] / 1e12 / (FP64_PEAK_TFLOPS * world), 5)},
             'kernel_ms_per_step': {k: round(v[0] / max(a.steps, 1), 3) for k, v in kt.items()},
-            'acars_items': items,
+            'timed_region': stats,
             'host_ms_per_step': {k: round(v[0] / max(a.steps, 1), 3) for k, v in ht.items()},
         }
         if cpu is not None:
             out['cpu_baseline'] = cpu
             out['vs_cpu'] = round(value / cpu['value'], 1)
         print(json.dumps(out), flush=True)
+        if stats['viterbi_jobs'] <= 0 or stats['acars_items'] <= 0:
+            # the metric names demod + Viterbi: a timed region without decoded frames measured something else
+            print('bench: timed region decoded no Viterbi jobs / ACARS items (%s)' % stats, file=sys.stderr)
+            sys.exit(3)
     eng.close()
     if world > 1:
         dist.destroy_process_group()

@@ -78,8 +78,11 @@ int aero_chan_vfo_info(aero_chan *c, int v, int *info5);
 int aero_chan_main_info(aero_chan *c, int m, int *info3);
 
 /* nblocks whole reads of interleaved CF32 (SOAPY_SDR_CF32, publisher.cpp:254);
- * dev != 0: a HIP device pointer.  Copied before returning; a batch runs
- * when max_blocks reads are pending. */
+ * dev != 0: a HIP device pointer.  Copied before returning.  At most
+ * max_blocks reads may be pending between two aero_chan_run calls: a push
+ * beyond that returns AERO_E_FULL (nothing of the excess is taken), except
+ * with AERO_CHAN_F_HOST_OUT, where the full batch runs first and its
+ * outputs are kept for aero_chan_pop_*. */
 int aero_chan_push(aero_chan *c, const float *iq, size_t nblocks, int dev);
 /* processes the pending reads (asynchronous; aero_chan_sync waits) */
 int aero_chan_run(aero_chan *c);

@@ -144,6 +144,12 @@ int aero_pop_rt_packets(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t
 int aero_timing(aero_engine *e, const char *name, double *ms, long *launches);
 void aero_timing_reset(aero_engine *e);
 
+/* Continuous-channel counters since creation: "viterbi_jobs" (blocks the
+ * GPU Viterbi decoded and handed back), "frames" (frames delivered to the
+ * SU/ACARS host), "su_crc_ok" (SUs whose CRC-16 checked).  Joins the
+ * asynchronous host frame work first.  AERO_E_INVALID for another name. */
+int aero_stat(aero_engine *e, const char *name, uint64_t *value);
+
 /* Total input samples demodulated across channels since creation. */
 uint64_t aero_samples_processed(aero_engine *e);
 

@@ -64,7 +64,7 @@ def test_oracle_regression_fixture(cpu_libs, k):
 
 
 @pytest.mark.gpu
-def test_engine_matches_golden_digests():
+def test_engine_matches_golden_digests(engine_lib, cpu_libs):
     import aero_engine as ae
     fx = _load('oracle_regression.json')
     eng = ae.Engine(max_channels=len(fx), flags=ae.F_TRACE_SOFT)

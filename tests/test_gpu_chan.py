@@ -14,15 +14,6 @@ import aero_testlib as tl
 
 pytestmark = pytest.mark.gpu
 
-# torch's HIP runtime must come up before the engine's (device-pointer test):
-# initialise it at collection, ahead of every test's library calls
-try:
-    import torch
-    if torch.cuda.is_available():
-        torch.cuda.init()
-except ImportError:
-    pass
-
 C = tl.CENTER
 
 

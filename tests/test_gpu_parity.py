@@ -123,3 +123,22 @@ def test_many_channels_multiple_waves(engine_lib):
         assert np.array_equal(eng.softbits(chans[k]), o.softbits()), 'channel %d soft bits differ' % k
         assert eng.items(chans[k]) == o.item_lines('A'), 'channel %d items differ' % k
     eng.close()
+
+
+@pytest.mark.gpu
+def test_documented_channel_config_per_bitrate(engine_lib):
+    """INTEGRATION.md's binding: aero_channel_open with the rate each bit
+    rate's audio arrives at (decode/decode.cpp:145, 152-159) for every
+    aero-decode bit rate, and AERO_E_INVALID for a mismatched rate."""
+    import ctypes
+    import aero_engine as ae
+    eng = ae.Engine(max_channels=4)
+    lib = ae.load_library()
+    for bitrate in (10500, 600, 1200):
+        fs = 12000 if bitrate == 600 else (24000 if bitrate == 1200 else 48000)
+        cfg = ae.ChannelCfg(bitrate, 0, fs, 0)
+        ch = ctypes.c_int()
+        assert lib.aero_channel_open(eng.h, ctypes.byref(cfg), ctypes.byref(ch)) == ae.AERO_OK, bitrate
+        bad = ae.ChannelCfg(bitrate, 0, 48000 if bitrate != 10500 else 12000, 0)
+        assert lib.aero_channel_open(eng.h, ctypes.byref(bad), ctypes.byref(ch)) == ae.AERO_E_INVALID, bitrate
+    eng.close()
