@@ -113,6 +113,8 @@ _SIGS = {
     'aero_timing_reset': (None, [ctypes.c_void_p]),
     'aero_samples_processed': (ctypes.c_uint64, [ctypes.c_void_p]),
     'aero_stat': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]),
+    'aero_channel_stat': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p,
+                                         ctypes.POINTER(ctypes.c_int64)]),
     'aero_sync': (ctypes.c_int, [ctypes.c_void_p]),
     'aero_device_math': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_size_t]),
@@ -366,6 +368,12 @@ class Engine:
         """aero_stat counter: 'viterbi_jobs', 'frames' or 'su_crc_ok'."""
         v = ctypes.c_uint64()
         _check(self.lib.aero_stat(self.h, name.encode(), ctypes.byref(v)), 'aero_stat')
+        return int(v.value)
+
+    def channel_stat(self, ch, name):
+        """aero_channel_stat: 'hunter_scans' or 'freq_center'."""
+        v = ctypes.c_int64()
+        _check(self.lib.aero_channel_stat(self.h, ch, name.encode(), ctypes.byref(v)), 'aero_channel_stat')
         return int(v.value)
 
     def samples_processed(self):

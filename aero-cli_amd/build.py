@@ -99,11 +99,62 @@ def build_oracle():
     return os.path.join(ORACLE_DIR, 'liboracle.so')
 
 
+HOST = os.path.join(HERE, 'host')
+BIN = os.path.join(HERE, 'bin')
+HOST_COMMON = ['qstr.cpp', 'output.cpp', 'forwarder.cpp', 'zmq_dl.cpp']
+# the host binaries: drop-in aero-decode / aero-publish over the engine's C ABI
+HOST_BINS = {'aero-decode': ['aero_decode.cpp']}
+TOOL_BINS = {'zmq_pcm_pub': os.path.join(ROOT, 'tools', 'zmq_pcm_pub.cpp')}
+
+
+def build_host(jobs=4):
+    """aero-cli_amd/bin/<binary>: C++17 over include/aero_engine.h, linked
+    to libaero_engine.so through an $ORIGIN rpath; libzmq is dlopen'ed."""
+    os.makedirs(BIN, exist_ok=True)
+    hdrs = [os.path.join(HOST, h) for h in os.listdir(HOST) if h.endswith('.h')]
+    hdrs += [os.path.join(ROOT, 'include', 'aero_engine.h'), os.path.join(ROOT, 'include', 'aero_chan.h')]
+    bdir = os.path.join(BUILD, 'host')
+    os.makedirs(bdir, exist_ok=True)
+    objs = {}
+    tasks = []
+    for s in HOST_COMMON + sum(HOST_BINS.values(), []):
+        src, obj = os.path.join(HOST, s), os.path.join(bdir, s + '.o')
+        objs[s] = obj
+        if _stale(obj, [src] + hdrs):
+            tasks.append(['g++', '-O2', '-std=c++17', '-Wall', '-fPIC', '-c', src, '-o', obj])
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for f in [ex.submit(_run, t) for t in tasks]:
+            f.result()
+    out = []
+    for name, srcs in HOST_BINS.items():
+        exe = os.path.join(BIN, name)
+        deps = [objs[s] for s in HOST_COMMON + srcs] + [ENGINE_SO]
+        if _stale(exe, deps):
+            _run(['g++', '-o', exe] + [objs[s] for s in srcs + HOST_COMMON] +
+                 [ENGINE_SO, '-Wl,-rpath,$ORIGIN/..', '-ldl', '-lpthread'])
+        out.append(exe)
+    # the formatter alone (no engine, no GPU): libaero_host.so
+    so = os.path.join(BIN, 'libaero_host.so')
+    capi = os.path.join(HOST, 'host_capi.cpp')
+    if _stale(so, [capi, objs['qstr.cpp'], objs['output.cpp']] + hdrs):
+        _run(['g++', '-O2', '-std=c++17', '-Wall', '-fPIC', '-shared', '-o', so, capi, objs['qstr.cpp'],
+              objs['output.cpp']])
+    out.append(so)
+    for name, src in TOOL_BINS.items():
+        exe = os.path.join(ROOT, 'tools', name)
+        if _stale(exe, [src, os.path.join(HOST, 'zmq_dl.cpp'), os.path.join(HOST, 'zmq_dl.h')]):
+            _run(['g++', '-O2', '-std=c++17', '-Wall', '-I', HOST, '-o', exe, src, objs['zmq_dl.cpp'], '-ldl'])
+        out.append(exe)
+    return out
+
+
 def build_all(jobs=4):
     build_oracle()
     build_synth()
     build_mathhost()
-    return build_engine(jobs)
+    so = build_engine(jobs)
+    build_host(jobs)
+    return so
 
 
 if __name__ == '__main__':
@@ -111,9 +162,10 @@ if __name__ == '__main__':
     ap.add_argument('--engine', action='store_true')
     ap.add_argument('--synth', action='store_true')
     ap.add_argument('--oracle', action='store_true')
+    ap.add_argument('--host', action='store_true')
     ap.add_argument('-j', type=int, default=4)
     a = ap.parse_args()
-    if not (a.engine or a.synth or a.oracle):
+    if not (a.engine or a.synth or a.oracle or a.host):
         print(build_all(a.j))
         sys.exit(0)
     if a.oracle:
@@ -122,3 +174,5 @@ if __name__ == '__main__':
         print(build_synth())
     if a.engine:
         print(build_engine(a.j))
+    if a.host:
+        print(build_host(a.j))

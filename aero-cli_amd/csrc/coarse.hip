@@ -23,6 +23,14 @@
 
 namespace aero {
 
+#ifdef AERO_X_OCML  // timing experiment only (see demod_oqpsk.hip)
+#define CO_HYPOT ::hypot
+#define CO_LOG10 ::log10
+#else
+#define CO_HYPOT aero_hypot
+#define CO_LOG10 aero_log10
+#endif
+
 // Geometry of one channel's coarse estimate (decode/coarsefreqestimate.cpp:39-76
 // with the settings each demodulator applies).  OQPSK: setSettings(14, 10500,
 // 10500, 48000); MSK: setSettings(13, 900, 600, Fs).
@@ -203,7 +211,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     }
   }
   // forward FFT
-  fft_dit<L, false>(x, t, lds, T.tw, s_tw);
+  fft_dit<L, false, true>(x, t, lds, T.tw, s_tw);
   // boxcar: zero bins startbin..stopbin (coarsefreqestimate.cpp:143-146)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -212,7 +220,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   }
   // inverse FFT (JFFT scales by 1/N, FFTWrapper multiplies by N)
   exchange<L, 3, 0, true>(x, t, lds);
-  fft_dit<L, true>(x, t, lds, T.twi, s_tw);
+  fft_dit<L, true, true>(x, t, lds, T.twi, s_tw);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     x[i].x *= (1.0 / ((double)N));
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     x[i] = make_double2(r, im);
   }
   exchange<L, 3, 0, true>(x, t, lds);
-  fft_dit<L, false>(x, t, lds, T.tw, s_tw);
+  fft_dit<L, false, true>(x, t, lds, T.tw, s_tw);
   // fftshift + smoothing y = 0.9 y + 10 log10(max(|X|,1)) over the bins the fold reads:
   // |X| per bin to LDS first (keeps the log10 out of the register-heavy FFT scope)
   // the y history (HBM) is read three iterations ahead of its update, the
@@ -239,7 +247,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int yi = epos<L, 3>(t, i) ^ (N / 2);
-    if (yi >= K::YLO && yi <= K::YHI) ylds[yi - K::YLO] = aero_hypot(x[i].x, x[i].y);
+    if (yi >= K::YLO && yi <= K::YHI) ylds[yi - K::YLO] = CO_HYPOT(x[i].x, x[i].y);
   }
   double yp2 = yload(t + 2 * FT);
   __syncthreads();
@@ -249,7 +257,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     yp0 = yp1;
     yp1 = yp2;
     yp2 = yload(k + 3 * FT);
-    const double ynew = yold * 0.9 + 0.1 * 10 * aero_log10(fmax(ylds[k], 1.0));
+    const double ynew = yold * 0.9 + 0.1 * 10 * CO_LOG10(fmax(ylds[k], 1.0));
     yg[k] = ynew;
     ylds[k] = ynew;
   }

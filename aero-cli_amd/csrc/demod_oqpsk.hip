@@ -26,6 +26,26 @@
 
 namespace aero {
 
+// Timing experiments only (never in the product build): AERO_X_OCML swaps
+// the bit-exact libm for the device ocml one, AERO_X_DIVMUL turns divisions
+// by constants into multiplications, to price those parts of the loop.
+#ifdef AERO_X_OCML
+#define DM_HYPOT ::hypot
+#define DM_ATAN2 ::atan2
+#define DM_TANH ::tanh
+#define DM_SINCOS(x, s, c) ::sincos(x, &(s), &(c))
+#else
+#define DM_HYPOT aero_hypot
+#define DM_ATAN2 aero_atan2
+#define DM_TANH aero_tanh
+#define DM_SINCOS(x, s, c) aero_sincos(x, s, c)
+#endif
+#ifdef AERO_X_DIVMUL
+#define DM_DIVC(a, c) ((a) * (1.0 / (c)))
+#else
+#define DM_DIVC(a, c) ((a) / (c))
+#endif
+
 __constant__ double c_taps[NTAPS];
 __constant__ DelayDesc c_dly[4];  // delays(1), delayt41(T/4), delayt42(T/4), delayt8(T/8)
 __constant__ double c_sr_b[3];    // st resonator (oqpskdemodulator.cpp:218-223)
@@ -49,7 +69,7 @@ __device__ __forceinline__ void nco_next(double &ptr, double &step) {  // WTnext
 __device__ __forceinline__ void set_freq(double &freq, double &step, double f) {  // SetFreq (DSP.cpp:163-168)
   freq = f;
   if (freq < 0) freq = 0;
-  step = (freq) * ((double)WTSIZE) / 48000.0;
+  step = DM_DIVC((freq) * ((double)WTSIZE), 48000.0);
 }
 
 // Delay<double>::update (DSP.h:365-384) as a shift register: h[0] is the
@@ -257,13 +277,13 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
         S.agc[(size_t)agc_ptr * C + c] = fabs(dab);
         agc_ptr++;
         if (agc_ptr == AGC_LEN) agc_ptr = 0;
-        double g = 1.414213562 / fmax(agc_sum / ((double)AGC_LEN), 0.000001);
+        double g = 1.414213562 / fmax(DM_DIVC(agc_sum, ((double)AGC_LEN)), 0.000001);
         g = fmax(g, 0.000001);
         s2r *= g;
         s2i *= g;
       }
       // clipping (:408-410)
-      const double ab = aero_hypot(s2r, s2i);
+      const double ab = DM_HYPOT(s2r, s2i);
       if (ab > 2.84) {
         const double k = 2.84 / ab;
         s2r = k * s2r;
@@ -277,9 +297,9 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       st_eta = iir3(srx1, srx2, sry1, sry2, c_sr_b, c_sr_a, st_eta);
       const double m1r = st_eta, m1i = -delay_tap<3, 2, 1>(d8, c_dly[3], st_eta);
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
-      const double st_angle_error = aero_atan2(oim, ore);
+      const double st_angle_error = DM_ATAN2(oim, ore);
       set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
-      so_ptr += (-st_angle_error * 0.01 / 360.0) * WTSIZE;
+      so_ptr += DM_DIVC(-st_angle_error * 0.01, 360.0) * WTSIZE;
       while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
       while (so_ptr < 0) so_ptr += WTSIZE;
       if (so_freq < (10500.0 - 0.1)) set_freq(so_freq, so_step, (10500.0 - 0.1));
@@ -366,8 +386,8 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       double m2_freq = s_pd[PD_M2_FREQ][pair];
       double qr = pr, qi = ptd_im;  // pt_qpsk
       // carrier tracking (:456-470)
-      const double ct_xt = aero_tanh(pi) * pr;
-      const double ct_xt_d = aero_tanh(ptd_re) * ptd_im;
+      const double ct_xt = DM_TANH(pi) * pr;
+      const double ct_xt_d = DM_TANH(ptd_re) * ptd_im;
       double ct_ec = ct_xt_d - ct_xt;
       if (ct_ec > M_PI) ct_ec = M_PI;
       if (ct_ec < -M_PI) ct_ec = -M_PI;
@@ -388,14 +408,14 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       marg[marg_p] = ct_ec;
       marg_p++;
       marg_p %= MARG_LEN;
-      const double mval = marg_sum / ((double)MARG_LEN);
+      const double mval = DM_DIVC(marg_sum, ((double)MARG_LEN));
       // dt.update (DSP.h:456-461): slot p written, slot p+1 read
       dtb[dt_p] = make_double2(qr, qi);
       dt_p = dt_rp;
       qr = dv.x;
       qi = dv.y;
       double rs, rc;
-      aero_sincos(mval, rs, rc);
+      DM_SINCOS(mval, rs, rc);
       const double rr = qr * rc - qi * rs, ri = qr * rs + qi * rc;
       qr = rr;
       qi = ri;
@@ -406,13 +426,13 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       }
       // MSEcalc::Update (DSP.cpp:449-461)
       {
-        const double av = aero_hypot(qr, qi);
+        const double av = DM_HYPOT(qr, qi);
         pm_sum = pm_sum - pm_old;
         pm_sum = pm_sum + fabs(av);
         pmb[pm_p] = fabs(av);
         pm_p++;
         pm_p %= MSE_LEN;
-        double mu = pm_sum / ((double)MSE_LEN);
+        double mu = DM_DIVC(pm_sum, ((double)MSE_LEN));
         if (mu < 0.000001) mu = 0.000001;
         const double tr = (1.4142135623730951 * qr) / mu, ti = (1.4142135623730951 * qi) / mu;
         const double tda = (fabs(tr) - 1.0), tdb = (fabs(ti) - 1.0);
@@ -422,7 +442,7 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
         msb[ms_p] = fabs(v);
         ms_p++;
         ms_p %= MSE_LEN;
-        mse = ms_sum / ((double)MSE_LEN);
+        mse = DM_DIVC(ms_sum, ((double)MSE_LEN));
       }
       if (mse < 0.65) {  // soft bits, imag first (:516-530)
         int ibit = qround(0.75 * qi * 127.0 + 128.0);

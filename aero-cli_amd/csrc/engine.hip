@@ -271,6 +271,7 @@ struct Group {
   hipEvent_t gjob_ev[NPIN] = {};
   int next_gjob = 0;
   hipEvent_t ev_feed_done = nullptr;
+  void *pin_stat = nullptr;  // aero_channel_stat staging
   std::map<std::string, TimingSlot> timing;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending_ev;
   uint64_t processed = 0;
@@ -750,6 +751,7 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
     HIPCHK(hipEventCreateWithFlags(&e->pin_ev[k], hipEventDisableTiming));
   }
   HIPCHK(hipEventCreateWithFlags(&e->pin_pcm_ev, hipEventDisableTiming));
+  if (hipHostMalloc(&e->pin_stat, 64) != hipSuccess) return AERO_E_NOMEM;
   HIPCHK(hipStreamCreateWithFlags(&e->st_in, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
   for (auto &ev : e->ev_stage_used) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -831,6 +833,7 @@ void group_destroy(Group *e) {
     if (e->gjob_ev[k]) (void)hipEventDestroy(e->gjob_ev[k]);
   }
   if (e->ev_feed_done) (void)hipEventDestroy(e->ev_feed_done);
+  if (e->pin_stat) (void)hipHostFree(e->pin_stat);
   if (e->pin_pcm) (void)hipHostFree(e->pin_pcm);
   if (e->pin_pcm_ev) (void)hipEventDestroy(e->pin_pcm_ev);
   if (e->st_in) hipStreamSynchronize(e->st_in);
@@ -910,6 +913,7 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
     if (e->gjob_ev[k]) (void)hipEventDestroy(e->gjob_ev[k]);
   }
   if (e->ev_feed_done) (void)hipEventDestroy(e->ev_feed_done);
+  if (e->pin_stat) (void)hipHostFree(e->pin_stat);
   if (e->pin_pcm) (void)hipHostFree(e->pin_pcm);
       e->pin_pcm = nullptr;
       e->pin_pcm_cap = 0;
@@ -1347,6 +1351,39 @@ int aero_stat(aero_engine *e, const char *name, uint64_t *value) {
       return AERO_E_INVALID;
   }
   *value = v;
+  return AERO_OK;
+}
+
+int aero_channel_stat(aero_engine *e, int ch, const char *name, int64_t *value) {
+  if (!e || !name || !value) return AERO_E_INVALID;
+  const std::string n(name);
+  if (route_burst(e, ch) >= 0) {  // the hunter is disabled in burst mode (decode/decode.cpp:175)
+    if (n != "hunter_scans" && n != "freq_center") return AERO_E_INVALID;
+    *value = 0;
+    return AERO_OK;
+  }
+  int c;
+  Group *g = route(e, ch, c);
+  if (!g) return AERO_E_INVALID;
+  HIPCHK(hipSetDevice(e->device));
+  if (int rc = flush_pending_init(g)) return rc;
+  if (n == "hunter_scans") {
+    int v = 0;
+    HIPCHK(hipMemcpyAsync(g->pin_stat, g->S.is + (size_t)IS_HUNT_SCANS * g->C + c, sizeof(int),
+                          hipMemcpyDeviceToHost, g->st));
+    HIPCHK(hipStreamSynchronize(g->st));
+    memcpy(&v, g->pin_stat, sizeof v);
+    *value = v;
+  } else if (n == "freq_center") {
+    double v = 0;
+    HIPCHK(hipMemcpyAsync(g->pin_stat, g->S.ds + (size_t)DS_MC_FREQ * g->C + c, sizeof(double),
+                          hipMemcpyDeviceToHost, g->st));
+    HIPCHK(hipStreamSynchronize(g->st));
+    memcpy(&v, g->pin_stat, sizeof v);
+    *value = (int64_t)v;
+  } else {
+    return AERO_E_INVALID;
+  }
   return AERO_OK;
 }
 

@@ -146,17 +146,63 @@ __device__ __forceinline__ void load_tw_lds(double2 *stw, const double2 *__restr
   for (int j = t; j < TwLds<L>::LEN; j += nthreads) stw[j] = TW[j];
 }
 
+// A stage of register phase 0: epos(t, i) = (t << 4) | i, so the twiddle
+// index k = i & (n - 1) is a compile-time constant per value and the k == 0
+// butterflies (twiddle TW[n - 1] = exp(0) = (1, +-0) exactly) skip the
+// multiply: 1*x - (+-0)*y == x for every nonzero x, so the results differ
+// from JFFT's at most in the sign of an exact zero, which no later add,
+// product, hypot or square can turn into a different nonzero value.
+template <int LOG2N, bool INV, int LB>
+__device__ __forceinline__ void stage0(double2 (&x)[16], int t0, const double2 *__restrict__ TW,
+                                       const double2 *stw) {
+  constexpr int n = 1 << LB;
+#ifdef AERO_X_NOTRIV
+  stage<LOG2N, 0, INV>(x, t0, LB, n, TW, stw);
+#else
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (i & n) continue;
+    const int il = i | n;
+    const int k = i & (n - 1);
+    double yr, yi;
+    if (k == 0) {
+      yr = x[il].x;
+      yi = x[il].y;
+    } else {
+      double2 w = stw[n - 1 + k];  // n <= 8: the LDS copy of the forward table
+      if (INV) w.y = -w.y;
+      yr = w.x * x[il].x - w.y * x[il].y;
+      yi = w.x * x[il].y + w.y * x[il].x;
+    }
+    x[il].x = x[i].x - yr;
+    x[il].y = x[i].y - yi;
+    x[i].x = x[i].x + yr;
+    x[i].y = x[i].y + yi;
+  }
+#endif
+}
+
 // full JFFT::fft on values already loaded in bit-reversed order in layout 0;
 // leaves the natural-order result in layout 3.  TW: this direction's table;
 // stw: LDS copy of the forward table's first TwLds<L>::LEN entries.
-template <int L, bool INV>
+// SKIP1: skip the exact-(1, +-0) twiddle multiplies of phase 0 (stage0);
+// only for callers whose outputs are magnitudes / squares (coarse.hip), as
+// the sign of an exact zero may differ from JFFT's.
+template <int L, bool INV, bool SKIP1 = false>
 __device__ __forceinline__ void fft_dit(double2 (&x)[16], int t, double *lds, const double2 *__restrict__ TW,
                                         const double2 *stw) {
   static_assert(L == 13 || L == 14, "register phases cover 13 or 14 stages");
-  stage<L, 0, INV>(x, t, 0, 1, TW, stw);
-  stage<L, 0, INV>(x, t, 1, 2, TW, stw);
-  stage<L, 0, INV>(x, t, 2, 4, TW, stw);
-  stage<L, 0, INV>(x, t, 3, 8, TW, stw);
+  if (SKIP1) {
+    stage0<L, INV, 0>(x, t, TW, stw);
+    stage0<L, INV, 1>(x, t, TW, stw);
+    stage0<L, INV, 2>(x, t, TW, stw);
+    stage0<L, INV, 3>(x, t, TW, stw);
+  } else {
+    stage<L, 0, INV>(x, t, 0, 1, TW, stw);
+    stage<L, 0, INV>(x, t, 1, 2, TW, stw);
+    stage<L, 0, INV>(x, t, 2, 4, TW, stw);
+    stage<L, 0, INV>(x, t, 3, 8, TW, stw);
+  }
   exchange<L, 0, 1, false>(x, t, lds);
   stage<L, 1, INV>(x, t, 0, 16, TW, stw);
   stage<L, 1, INV>(x, t, 1, 32, TW, stw);

@@ -150,6 +150,12 @@ void aero_timing_reset(aero_engine *e);
  * asynchronous host frame work first.  AERO_E_INVALID for another name. */
 int aero_stat(aero_engine *e, const char *name, uint64_t *value);
 
+/* Per-channel state: "hunter_scans" (full SignalHunter scans without a
+ * signal, decode/hunter.cpp:31-37 -- aero-decode's --no-signal-exit),
+ * "freq_center" (the mixer centre in Hz after the last coarse hop).  Waits
+ * for the channel's queued GPU work. */
+int aero_channel_stat(aero_engine *e, int ch, const char *name, int64_t *value);
+
 /* Total input samples demodulated across channels since creation. */
 uint64_t aero_samples_processed(aero_engine *e);
 

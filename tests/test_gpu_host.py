@@ -1,0 +1,192 @@
+"""The drop-in aero-decode host (aero-cli_amd/bin/aero-decode) end to end on
+the GPU: synthetic P-channel PCM published over ZeroMQ in aero-publish's wire
+format (tools/zmq_pcm_pub, [topic][u32 rate][int16 PCM] in 12000-sample
+messages) -> ZMQ SUB -> engine -> console lines in --format jsondump, a TCP
+forwarder in text and a UDP forwarder in jaero.  Every line must equal the
+oracle's ACARS items for the same PCM, formatted by the Qt-pinned formatter
+(tests/test_host_output.py), at a pinned wall clock."""
+import ctypes
+import os
+import re
+import signal
+import socket
+import subprocess
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import aero_testlib as tl
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, 'aero-cli_amd', 'bin')
+PUB = os.path.join(ROOT, 'tools', 'zmq_pcm_pub')
+FIXED_MS = 1714558496789
+STATION = 'GPU-TEST'
+
+
+def free_port(kind=socket.SOCK_STREAM):
+    with socket.socket(socket.AF_INET, kind) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def parse_line(line):
+    """oracle / engine canonical item line -> aero_acars_item"""
+    import aero_engine as ae
+    f = dict(kv.split('=', 1) for kv in line.split()[1:])
+    it = ae.AcarsItem()
+    it.aesid, it.gesid = int(f['aes'], 16), int(f['ges'], 16)
+    it.qno, it.refno, it.mode = int(f['qno'], 16), int(f['refno'], 16), int(f['mode'], 16)
+    it.tak, it.bi = int(f['tak'], 16), int(f['bi'], 16)
+    it.nonacars, it.downlink, it.valid = int(f['nonacars']), int(f['downlink']), int(f['valid'])
+    it.hastext, it.moretocome = int(f['hastext']), int(f['more'])
+    it.fragment = 1 if line.startswith('F') else 0
+    lab, reg, msg = bytes.fromhex(f['label']), bytes.fromhex(f['reg']), bytes.fromhex(f['msg'])
+    it.label_len, it.reg_len, it.msg_len = len(lab), len(reg), len(msg)
+    it.label, it.reg = lab, reg
+    ctypes.memmove(ctypes.addressof(it) + ae.AcarsItem.msg.offset, msg, len(msg))
+    return it
+
+
+def expected(lines, fmt_id):
+    L = ctypes.CDLL(os.path.join(BIN, 'libaero_host.so'))
+    L.aero_host_format.restype = ctypes.c_long
+    L.aero_host_format.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong,
+                                   ctypes.c_char_p, ctypes.c_size_t]
+    out = []
+    for ln in lines:
+        it = parse_line(ln)
+        buf = ctypes.create_string_buffer(65536)
+        n = L.aero_host_format(fmt_id, STATION.encode(), 0, ctypes.byref(it), FIXED_MS, buf, len(buf))
+        out.append(buf.raw[:n].decode())
+    return out
+
+
+class TcpSink(threading.Thread):
+    def __init__(self):
+        super().__init__(daemon=True)
+        self.srv = socket.socket()
+        self.srv.bind(('127.0.0.1', 0))
+        self.srv.listen(4)
+        self.port = self.srv.getsockname()[1]
+        self.data = b''
+
+    def run(self):
+        self.srv.settimeout(120)
+        try:
+            conn, _ = self.srv.accept()
+        except OSError:
+            return
+        conn.settimeout(120)
+        while True:
+            try:
+                b = conn.recv(65536)
+            except OSError:
+                break
+            if not b:
+                break
+            self.data += b
+
+
+class UdpSink(threading.Thread):
+    def __init__(self):
+        super().__init__(daemon=True)
+        self.s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        self.s.bind(('127.0.0.1', 0))
+        self.port = self.s.getsockname()[1]
+        self.msgs = []
+
+    def run(self):
+        self.s.settimeout(1.0)
+        self.stop = False
+        while not self.stop:
+            try:
+                self.msgs.append(self.s.recv(65536))
+            except OSError:
+                continue
+
+
+def _start_decoder(args, env):
+    p = subprocess.Popen([os.path.join(BIN, 'aero-decode')] + args, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         env=dict(os.environ, AERO_DECODE_FIXED_TIME_MS=str(FIXED_MS), **env))
+    lines = []
+
+    def pump():
+        for raw in p.stderr:
+            lines.append(raw.decode('utf-8', 'replace').rstrip('\n'))
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    t0 = time.time()
+    while not any('Listening for samples' in l for l in lines):
+        assert p.poll() is None, '\n'.join(lines)
+        assert time.time() - t0 < 120, 'decoder did not start'
+        time.sleep(0.1)
+    return p, lines, th
+
+
+def test_zmq_to_acars_json_end_to_end(engine_lib, cpu_libs, tmp_path):
+    import build
+    build.build_host()
+    pcm = tl.synth(seconds=20.0, seed=0xAE70, carrier=12041.0, ebn0=12.0)
+    ref = tl.Oracle()
+    ref.push_chunked(pcm, 12000)
+    want = ref.item_lines('A')
+    assert len(want) >= 5
+    f = tmp_path / 'vfo.pcm'
+    pcm.astype('<i2').tofile(str(f))
+    port = free_port()
+    tcp, udp = TcpSink(), UdpSink()
+    tcp.start()
+    udp.start()
+    dec, lines, th = _start_decoder(
+        ['-p', 'tcp://127.0.0.1:%d' % port, '-t', 'VFO01', '-b', '10500', '--format', 'jsondump', '-s', STATION,
+         '-v', '-f', 'text=tcp://127.0.0.1:%d,jaero=udp://127.0.0.1:%d' % (tcp.port, udp.port)], {})
+    try:
+        r = subprocess.run([PUB, '--bind', 'tcp://127.0.0.1:%d' % port, '--topic', 'VFO01', '--rate', '48000',
+                            '--chunk', '12000', '--wait-ms', '1500', str(f)], capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr
+        time.sleep(2.0)
+    finally:
+        dec.send_signal(signal.SIGTERM)
+        rc = dec.wait(timeout=120)
+    th.join(timeout=10)
+    tcp.join(timeout=10)
+    udp.stop = True
+    udp.join(timeout=5)
+    assert rc == 0, '\n'.join(lines[-20:])
+    console = [l for l in lines if l.startswith('{')]
+    assert console == expected(want, 3)
+    assert tcp.data.decode('latin-1').splitlines() == [s for s in expected(want, 1)]
+    assert [m.decode('latin-1').rstrip('\n') for m in udp.msgs] == expected(want, 2)
+
+
+def test_no_signal_exit(engine_lib, tmp_path):
+    """--no-signal-exit: a full hunter scan without a signal ends the decoder
+    (decode/decode.cpp:418-427; 4 x 15 hops of 4096 samples at 10500 bps)."""
+    import build
+    build.build_host()
+    rng = np.random.default_rng(5)
+    noise = (rng.normal(0, 300, 48000 * 8)).astype('<i2')
+    f = tmp_path / 'noise.pcm'
+    noise.tofile(str(f))
+    port = free_port()
+    dec, lines, th = _start_decoder(['-p', 'tcp://127.0.0.1:%d' % port, '-t', 'VFO07', '-b', '10500', '-s', 'X',
+                                     '--no-signal-exit', '-v'], {})
+    try:
+        subprocess.run([PUB, '--bind', 'tcp://127.0.0.1:%d' % port, '--topic', 'VFO07', '--rate', '48000',
+                        '--chunk', '4800', '--pace-ms', '30', '--wait-ms', '1500', str(f)], capture_output=True,
+                       timeout=120)
+        rc = dec.wait(timeout=60)
+    finally:
+        if dec.poll() is None:
+            dec.kill()
+    th.join(timeout=10)
+    text = '\n'.join(lines)
+    assert 'Scanned entire VFO bandwidth and could not find a signal.' in text
+    assert 'Exiting because of no signal' in text
+    assert rc == 0
