@@ -121,7 +121,7 @@ def build_host(jobs=4):
         src, obj = os.path.join(HOST, s), os.path.join(bdir, s + '.o')
         objs[s] = obj
         if _stale(obj, [src] + hdrs):
-            tasks.append(['g++', '-O2', '-std=c++17', '-Wall', '-fPIC', '-c', src, '-o', obj])
+            tasks.append(['g++', '-O2', '-g', '-std=c++17', '-Wall', '-fPIC', '-c', src, '-o', obj])
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         for f in [ex.submit(_run, t) for t in tasks]:
             f.result()
@@ -131,7 +131,7 @@ def build_host(jobs=4):
         deps = [objs[s] for s in HOST_COMMON + srcs] + [ENGINE_SO]
         if _stale(exe, deps):
             _run(['g++', '-o', exe] + [objs[s] for s in srcs + HOST_COMMON] +
-                 [ENGINE_SO, '-Wl,-rpath,$ORIGIN/..', '-ldl', '-lpthread'])
+                 [ENGINE_SO, '-Wl,-rpath,$ORIGIN/..', '-rdynamic', '-ldl', '-lpthread'])
         out.append(exe)
     # the formatter alone (no engine, no GPU): libaero_host.so
     so = os.path.join(BIN, 'libaero_host.so')

@@ -907,14 +907,7 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
       e->scratch_cap = need;
     }
     if (need > e->pin_pcm_cap) {
-      for (int k = 0; k < Group::NPIN; k++) {
-    if (e->pin_gjobs[k]) (void)hipHostFree(e->pin_gjobs[k]);
-    if (e->d_gjobs[k]) (void)hipFree(e->d_gjobs[k]);
-    if (e->gjob_ev[k]) (void)hipEventDestroy(e->gjob_ev[k]);
-  }
-  if (e->ev_feed_done) (void)hipEventDestroy(e->ev_feed_done);
-  if (e->pin_stat) (void)hipHostFree(e->pin_stat);
-  if (e->pin_pcm) (void)hipHostFree(e->pin_pcm);
+      if (e->pin_pcm) (void)hipHostFree(e->pin_pcm);
       e->pin_pcm = nullptr;
       e->pin_pcm_cap = 0;
       HIPCHK(hipHostMalloc(&e->pin_pcm, need * sizeof(int16_t)));

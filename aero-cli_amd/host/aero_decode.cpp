@@ -15,6 +15,7 @@
  *    reference's synchronous chain has no tail to flush);
  *  - libacars enrichment (`parsed`) is absent (libacars is not in the image).
  */
+#include <execinfo.h>
 #include <signal.h>
 #include <unistd.h>
 
@@ -46,6 +47,16 @@ using namespace aerohost;
 namespace {
 
 std::atomic<int> g_running{0};
+
+// a crash prints the native stack before the default action (diagnostics)
+void on_fatal(int sig) {
+  void *bt[64];
+  const int n = backtrace(bt, 64);
+  fprintf(stderr, "aero-decode: fatal signal %d\n", sig);
+  backtrace_symbols_fd(bt, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
 
 void on_signal(int sig) {
   if (sig == SIGINT || sig == SIGTERM) g_running.store(0);  // handleInterrupt / handleTerminate
@@ -292,6 +303,9 @@ int main(int argc, char **argv) {
   sigaction(SIGINT, &sa, nullptr);
   sigaction(SIGTERM, &sa, nullptr);
   signal(SIGHUP, SIG_IGN);  // handleHup: nothing to do
+  signal(SIGSEGV, on_fatal);
+  signal(SIGBUS, on_fatal);
+  signal(SIGABRT, on_fatal);
   signal(SIGPIPE, SIG_IGN);
 
   const ustr station = from_utf8(o.station);

@@ -150,7 +150,12 @@ def test_zmq_to_acars_json_end_to_end(engine_lib, cpu_libs, tmp_path):
                             '--chunk', '12000', '--wait-ms', '1500', str(f)], capture_output=True, text=True,
                            timeout=120)
         assert r.returncode == 0, r.stderr
-        time.sleep(2.0)
+        # every message queued in the SUB socket is taken before SIGTERM (the
+        # reference stops reading on a signal too); the tail hop is flushed
+        t0 = time.time()
+        while sum(l.startswith('{') for l in lines) < len(want) - 4 and time.time() - t0 < 90:
+            time.sleep(0.2)
+        time.sleep(1.0)
     finally:
         dec.send_signal(signal.SIGTERM)
         rc = dec.wait(timeout=120)
