@@ -235,14 +235,16 @@ __global__ __launch_bounds__(256) void frame_msk_kernel(DevState S, int nch) {
 }
 
 // ---------------------------------------------------------------- Viterbi
-// BLK = interleaver block (N x 64 soft bits), N = BLK / 64; DL2 = dl2 length + 1
+// BLK = interleaver block (N x 64 soft bits), N = BLK / 64; DL2 = dl2 length + 1.
+// One wave per job, ~5.8 KB of LDS and no per-step barrier
+// (viterbi_decode_regs), so Viterbi waves fit beside a demod or coarse
+// workgroup on the same CU and run on their own stream (engine.hip).
 template <int BLK, int DL2>
 __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, int trace) {
   constexpr int NL = BLK / 64, HALF = BLK / 2;
+  constexpr int NW = (62 + BLK + 24) / 2 / 64 + 1;  // 64-bit words of decoded bits
   __shared__ uint8_t sbuf[62 + BLK + 24 + 2];
-  __shared__ unsigned long long hist[HCAP];
-  __shared__ uint8_t obits[HALF + 64];
-  __shared__ uint8_t dl[HALF];
+  __shared__ uint64_t obits[NW];
   __shared__ uint8_t info[320];
   // grid-stride over the jobs of this pass (the job count stays on the device,
   // so the host launches without waiting for the framing kernel)
@@ -264,47 +266,61 @@ __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, in
     for (int j = 0; j < NL; ++j) sbuf[ov + j * 64 + lane] = blk[row * NL + j];
   }
   if (lane < 24) sbuf[ov + BLK + lane] = 128;
-  for (int k = lane; k < HALF + 64; k += 64) obits[k] = 0;
   __syncthreads();
   // keep the last 62 deinterleaved soft values for the next block
   if (lane < 62) S.overlap[(size_t)c * 64 + lane] = sbuf[ov + BLK - 62 + lane];
 
   const int sets = nsoft / 2;
-  viterbi_decode_wave(sbuf, nsoft, hist, obits, lane);
+  uint64_t obw;
+  viterbi_decode_regs(sbuf, nsoft, obw, lane);
+  if (lane < NW) obits[lane] = obw;
+  __syncthreads();
+  auto obit = [&](int k) { return (int)((obits[k >> 6] >> (k & 63)) & 1ULL); };
   // Decode_Continuous: keep decoded bits [25, 25 + BLK/2) clipped to size/2
   const int nbits = (sets - 25) < HALF ? (sets - 25) : HALF;
   if (trace) {
     uint8_t *dbg = S.blocks_dbg + (size_t)c * 2500;
     if (lane == 0) *reinterpret_cast<int *>(dbg) = nbits;
-    for (int k = lane; k < nbits; k += 64) dbg[4 + k] = obits[25 + k];
+    for (int k = lane; k < nbits; k += 64) dbg[4 + k] = (uint8_t)obit(25 + k);
   }
   // DelayLine dl2 (aerol.h:464-471): out[q] = old[(p+q+1)%L], new[(p+q)%L] = in[q]
-  // (nbits < DL2: one wrap at most)
+  // (nbits < DL2: one wrap at most).  Each lane takes the eight bits of its
+  // output bytes: all old values are read (and used) before any new one is
+  // stored, as a neighbour's first read is this lane's last write.
   static_assert(HALF < DL2, "delay line longer than a block");
   uint8_t *dlg = S.dl2 + (size_t)c * DL2;
   const int p0 = S.is[IS_DL2_PTR * C + c];
-  for (int k = lane; k < nbits; k += 64) {
-    int r = p0 + k + 1;
-    r = r >= DL2 ? r - DL2 : r;
-    r = r >= DL2 ? r - DL2 : r;
-    dl[k] = dlg[r];
+  const int nbytes = nbits / 8;
+  constexpr int BPL = (HALF / 8 + 63) / 64;  // output bytes per lane
+  int bytev[BPL];
+#pragma unroll
+  for (int u = 0; u < BPL; ++u) {
+    const int bb = lane + 64 * u;
+    int v = 0;
+    if (bb < nbytes) {
+      // scrambler + LSB-first packing (aerol.cpp:1506-1520)
+      for (int i = 0; i < 8; ++i) {
+        int r = p0 + 8 * bb + i + 1;
+        r = r >= DL2 ? r - DL2 : r;
+        r = r >= DL2 ? r - DL2 : r;
+        v |= ((dlg[r] ^ T.scr[scr_pos + 8 * bb + i]) & 1) << i;
+      }
+    }
+    bytev[u] = v;
   }
-  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < BPL; ++u) {
+    const int bb = lane + 64 * u;
+    if (bb < 312) info[bb] = (uint8_t)(bb < nbytes ? bytev[u] : 0);
+  }
+  for (int bb = lane + 64 * BPL; bb < 312; bb += 64) info[bb] = 0;
+  __syncthreads();  // every old delay-line value read before the writes below
   for (int k = lane; k < nbits; k += 64) {
     int w = p0 + k;
     w = w >= DL2 ? w - DL2 : w;
-    dlg[w] = obits[25 + k];
+    dlg[w] = (uint8_t)obit(25 + k);
   }
   if (lane == 0) S.is[IS_DL2_PTR * C + c] = (p0 + nbits) % DL2;
-  // scrambler + LSB-first packing (aerol.cpp:1506-1520)
-  const int nbytes = nbits / 8;
-  for (int b = lane; b < nbytes; b += 64) {
-    int v = 0;
-    for (int i = 0; i < 8; ++i) v |= ((dl[8 * b + i] ^ T.scr[scr_pos + 8 * b + i]) & 1) << i;
-    info[b] = (uint8_t)v;
-  }
-  for (int b = nbytes + lane; b < 312; b += 64) info[b] = 0;
-  __syncthreads();
   // per-SU CRC (aerol.cpp:1531-1543); a 600/1200 frame spans 2-3 blocks and
   // its SUs are checked on the host once the frame's infofield is complete
   const int nsu = nbytes / 12;

@@ -117,16 +117,20 @@ enum { PI_MARG_P, PI_DT_P, PI_PM_P, PI_MS_P, PI_N };
 enum { PL_SOFTP, PL_PTN, PL_N };
 
 constexpr int DEMOD_BLOCK = 256;  // channels (= lanes) per workgroup
+// coarse-ring entries staged per channel before one 32-byte write; eight
+// (not sixteen) leave 11.8 KB of the CU's LDS free for two Viterbi waves
+// (aerol.hip) beside the demod workgroup
+constexpr int RING_GROUP = 8;
 
 template <bool TRACE>
 __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, DevTables T, int nch, int flush) {
-  // LDS (≈156 KB, one 256-channel block per CU): the imaginary RRC partial
+  // LDS (≈148 KB, one 256-channel block per CU): the imaginary RRC partial
   // sums, RRC taps (symmetric, 28 distinct values), the coarse-ring staging
-  // area (entries of 16 consecutive samples leave as one 64-byte write per
-  // channel instead of sixteen 4-byte ones) and the carrier-step state.
+  // area (entries of 8 consecutive samples leave as one 32-byte write per
+  // channel instead of eight 4-byte ones) and the carrier-step state.
   __shared__ double s_qim[NTAPS][DEMOD_BLOCK];
   __shared__ double s_taps[32];
-  __shared__ uint32_t s_ring[16][DEMOD_BLOCK];
+  __shared__ uint32_t s_ring[RING_GROUP][DEMOD_BLOCK];
   __shared__ double s_pd[PD_N][DEMOD_BLOCK];
   __shared__ long long s_pl[PL_N][DEMOD_BLOCK];
   __shared__ int s_pi[PI_N][DEMOD_BLOCK];
@@ -337,18 +341,18 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       // coarse-ring fill of the next sample (:351-356), staged in LDS
       if (i + 1 < ia) {
         const int m = rb + i + 1;  // ring slot before masking
-        const int k = m & 15;
+        const int k = m & (RING_GROUP - 1);
         {
           s_ring[k][pair] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)pcm_next << 16);
-          if (k == 15) {
-            uint32_t *dst = S.cring + (size_t)c * NFFT + ((m - 15) & (NFFT - 1));
-            if (i + 1 - 15 >= 1) {  // the whole group was staged by this launch
+          if (k == RING_GROUP - 1) {
+            uint32_t *dst = S.cring + (size_t)c * NFFT + ((m - (RING_GROUP - 1)) & (NFFT - 1));
+            if (i + 1 - (RING_GROUP - 1) >= 1) {  // the whole group was staged by this launch
 #pragma unroll
-              for (int q4 = 0; q4 < 4; ++q4)
+              for (int q4 = 0; q4 < RING_GROUP / 4; ++q4)
                 reinterpret_cast<uint4 *>(dst)[q4] = make_uint4(s_ring[4 * q4][pair], s_ring[4 * q4 + 1][pair],
                                                                 s_ring[4 * q4 + 2][pair], s_ring[4 * q4 + 3][pair]);
             } else {
-              for (int j = 15 - i; j < 16; ++j) dst[j] = s_ring[j][pair];
+              for (int j = (RING_GROUP - 1) - i; j < RING_GROUP; ++j) dst[j] = s_ring[j][pair];
             }
           }
         }
@@ -477,9 +481,9 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
     }
   }
   // staged entries of an unfinished 16-sample group
-  if (ifl - 1 >= 1 && ((rb + ifl - 1) & 15) != 15) {
-    const int last = ifl - 1;                  // relative sample of the last staged entry
-    const int g0 = last - ((rb + last) & 15);  // relative sample of its group's slot 0
+  if (ifl - 1 >= 1 && ((rb + ifl - 1) & (RING_GROUP - 1)) != RING_GROUP - 1) {
+    const int last = ifl - 1;                                // relative sample of the last staged entry
+    const int g0 = last - ((rb + last) & (RING_GROUP - 1));  // relative sample of its group's slot 0
     uint32_t *dst = S.cring + (size_t)c * NFFT + ((rb + g0) & (NFFT - 1));
     for (int j = (g0 >= 1 ? 0 : 1 - g0); j <= last - g0; ++j) dst[j] = s_ring[j][pair];
   }

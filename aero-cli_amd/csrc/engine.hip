@@ -238,6 +238,8 @@ struct Group {
   struct JobSlot {
     uint8_t *d_out = nullptr;   // [C][JOB_OUT] (device)
     int *d_n = nullptr;         // job count (device)
+    int *d_jobs = nullptr;      // [C] int4 job list of this pass (device)
+    hipEvent_t ev_vit = nullptr;  // this pass's Viterbi done (side stream)
     uint8_t *h_out = nullptr;   // pinned copy of the first `copied` records
     int *h_n = nullptr;         // pinned copy of the count
     int copied = 0;
@@ -261,6 +263,11 @@ struct Group {
   // compute stream's scatter then reads; a buffer is refilled only after the
   // scatter that read it has run
   hipStream_t st_in = nullptr;
+  // Viterbi + frame hand-off run on their own stream: pass k's decoding
+  // overlaps pass k+1's demodulation (the Viterbi waves are small enough to
+  // share the CUs with the demod / coarse workgroups)
+  hipStream_t st_vit = nullptr;
+  hipEvent_t ev_framed = nullptr;
   hipEvent_t ev_in = nullptr;
   int16_t *d_stage[2] = {};
   size_t stage_cap[2] = {};
@@ -348,16 +355,16 @@ size_t layout(DevState &S, DevTables &T, int mode, int C, int flags, char *base)
 
 std::string tname(const Group *e, const char *name) { return std::string(e->tag) + name; }
 
-void ev_begin(Group *e, const char *name, hipEvent_t &a, hipEvent_t &b) {
+void ev_begin(Group *e, const char *name, hipEvent_t &a, hipEvent_t &b, hipStream_t st = nullptr) {
   if (!(e->flags & AERO_F_TIMING)) return;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  hipEventRecord(a, e->st);
+  hipEventRecord(a, st ? st : e->st);
   e->pending_ev.push_back({tname(e, name), {a, b}});
 }
-void ev_end(Group *e, hipEvent_t b) {
+void ev_end(Group *e, hipEvent_t b, hipStream_t st = nullptr) {
   if (!(e->flags & AERO_F_TIMING)) return;
-  hipEventRecord(b, e->st);
+  hipEventRecord(b, st ? st : e->st);
 }
 void ev_collect(Group *e) {
   for (auto &pe : e->pending_ev) {
@@ -650,19 +657,29 @@ int run_group(Group *e, int flush) {
     DevState S2 = e->S;
     S2.njobs = sl.d_n;
     S2.jobout = sl.d_out;
+    S2.jobs = sl.d_jobs;
     HIPCHK(hipMemsetAsync(sl.d_n, 0, sizeof(int), e->st));
+    {
+      // a channel refills its other interleaver buffer >= 5 passes after a
+      // job took one; the Viterbi of two passes ago has read its buffer
+      const auto &old = e->slot[(si + Group::NSLOT - 2) % Group::NSLOT];
+      if (old.ev_vit) HIPCHK(hipStreamWaitEvent(e->st, old.ev_vit, 0));
+    }
     ev_begin(e, "frame", a, b);
     launch_frame(e->st, e->mode, S2, e->nch);
     ev_end(e, b);
-    ev_begin(e, "viterbi", a, b);
-    launch_viterbi(e->st, e->mode, S2, e->T, e->nch, (e->flags & AERO_F_TRACE_BLOCKS) ? 1 : 0);
-    ev_end(e, b);
+    HIPCHK(hipEventRecord(e->ev_framed, e->st));
+    HIPCHK(hipStreamWaitEvent(e->st_vit, e->ev_framed, 0));
+    ev_begin(e, "viterbi", a, b, e->st_vit);
+    launch_viterbi(e->st_vit, e->mode, S2, e->T, e->nch, (e->flags & AERO_F_TRACE_BLOCKS) ? 1 : 0);
+    ev_end(e, b, e->st_vit);
+    HIPCHK(hipEventRecord(sl.ev_vit, e->st_vit));
     HIPCHK(hipGetLastError());
     // async hand-off: the count plus the records the job count is likely to need
     sl.copied = std::min(e->nch, e->max_jobs_seen + e->max_jobs_seen / 4 + 256);
-    HIPCHK(hipMemcpyAsync(sl.h_n, sl.d_n, sizeof(int), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(hipMemcpyAsync(sl.h_out, sl.d_out, (size_t)sl.copied * JOB_OUT, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(hipEventRecord(sl.ev, e->st));
+    HIPCHK(hipMemcpyAsync(sl.h_n, sl.d_n, sizeof(int), hipMemcpyDeviceToHost, e->st_vit));
+    HIPCHK(hipMemcpyAsync(sl.h_out, sl.d_out, (size_t)sl.copied * JOB_OUT, hipMemcpyDeviceToHost, e->st_vit));
+    HIPCHK(hipEventRecord(sl.ev, e->st_vit));
     sl.pending = true;
     e->pending_slots.push_back(si);
     if (trace) {  // parity traces: synchronous, pass by pass
@@ -677,6 +694,7 @@ int run_group(Group *e, int flush) {
 int drain_group(Group *e) {
   HIPCHK(hipSetDevice(e->device));
   HIPCHK(hipStreamSynchronize(e->st));
+  HIPCHK(hipStreamSynchronize(e->st_vit));
   if (int rc = poll_slots(e, true)) return rc;
   if (e->flags & (AERO_F_TRACE_PT | AERO_F_TRACE_SOFT | AERO_F_TRACE_HOPS))
     if (int rc = collect_traces(e)) return rc;
@@ -744,8 +762,12 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
     if (hipMalloc(&sl.d_n, 64) != hipSuccess) return AERO_E_NOMEM;
     if (hipHostMalloc(&sl.h_out, (size_t)JOB_OUT * e->C) != hipSuccess) return AERO_E_NOMEM;
     if (hipHostMalloc(&sl.h_n, 64) != hipSuccess) return AERO_E_NOMEM;
+    if (hipMalloc(&sl.d_jobs, (size_t)16 * e->C) != hipSuccess) return AERO_E_NOMEM;
     HIPCHK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&sl.ev_vit, hipEventDisableTiming));
   }
+  HIPCHK(hipStreamCreateWithFlags(&e->st_vit, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&e->ev_framed, hipEventDisableTiming));
   for (int k = 0; k < Group::NPIN; k++) {
     if (hipHostMalloc(&e->pin_avail[k], sizeof(long long) * e->C) != hipSuccess) return AERO_E_NOMEM;
     HIPCHK(hipEventCreateWithFlags(&e->pin_ev[k], hipEventDisableTiming));
@@ -815,10 +837,13 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
 void group_destroy(Group *e) {
   if (!e) return;
   if (e->st) hipStreamSynchronize(e->st);
+  if (e->st_vit) hipStreamSynchronize(e->st_vit);
   ev_collect(e);
   for (auto &sl : e->slot) {
     if (sl.d_out) (void)hipFree(sl.d_out);
     if (sl.d_n) (void)hipFree(sl.d_n);
+    if (sl.d_jobs) (void)hipFree(sl.d_jobs);
+    if (sl.ev_vit) (void)hipEventDestroy(sl.ev_vit);
     if (sl.h_out) (void)hipHostFree(sl.h_out);
     if (sl.h_n) (void)hipHostFree(sl.h_n);
     if (sl.ev) (void)hipEventDestroy(sl.ev);
@@ -845,6 +870,8 @@ void group_destroy(Group *e) {
   if (e->st_in) (void)hipStreamDestroy(e->st_in);
   if (e->d_scratch) (void)hipFree(e->d_scratch);
   if (e->pool) (void)hipFree(e->pool);
+  if (e->ev_framed) (void)hipEventDestroy(e->ev_framed);
+  if (e->st_vit) (void)hipStreamDestroy(e->st_vit);
   if (e->st) (void)hipStreamDestroy(e->st);
 }
 

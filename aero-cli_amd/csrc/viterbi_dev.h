@@ -100,3 +100,125 @@ __device__ __forceinline__ void viterbi_decode_wave(const uint8_t *sbuf, int nso
 }
 
 }  // namespace aero
+
+namespace aero {
+
+// Same decoder as viterbi_decode_wave (same metrics, ties, renormalisation,
+// 140-column history, 35-column traceback depth, restricted tail), laid out
+// for co-residence with the demodulator and the coarse FFT: the history
+// lives in registers (lane l holds columns l, l + 64, l + 128) instead of
+// LDS, so a trellis step needs no LDS store and no barrier, and the
+// traceback runs on the scalar unit (the path state is wave-uniform): two
+// v_readlane per column instead of a dependent LDS read per column in lane 0.
+// Decoded bit b lands in bit (b & 63) of obw in lane b >> 6.
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nsoft, uint64_t &obw, int lane) {
+  const int sets = nsoft / 2;
+  const int s = lane;
+  const int tab_lo = conv_table(s), tab_hi = conv_table(s | 64);
+  uint64_t h0 = 0, h1 = 0, h2 = 0;  // history columns lane, lane + 64, lane + 128
+  obw = 0;
+  int m = 0;
+  for (int i = 0; i < 6 && i < sets; ++i) {
+    const int a = sbuf[2 * i], b = sbuf[2 * i + 1];
+    const int prev = shfl_idx(m, s >> 1);
+    if (s < (2 << i)) m = (soft_dist(conv_table(s), a, b) + prev) & 0xFFFF;
+  }
+  int index = 0, len = 0, renorm = 0, outpos = 0;
+  auto search = [&](int skip) -> int {
+    int key = (s % skip == 0) ? ((m << 6) | s) : 0x7FFFFFFF;
+    for (int off = 32; off > 0; off >>= 1) {
+      const int o = __shfl_xor(key, off, 64);
+      key = o < key ? o : key;
+    }
+    return __builtin_amdgcn_readfirstlane(key) & 63;
+  };
+  auto traceback = [&](int bestpath, int mintb) {
+    const int nout = len - mintb;
+    int idx = index;
+    int j = 0;
+    // columns walked newest to oldest, one 64-column register block at a time
+    while (j < len) {
+      idx = idx == 0 ? HCAP - 1 : idx - 1;
+      // steps inside this block: idx, idx - 1, ... down to the block start
+      int run = (idx & 63) + 1;
+      if (run > len - j) run = len - j;
+      auto walk = [&](const uint64_t hw) {
+        for (int k = 0; k < run; ++k, ++j) {
+          const int col = idx - k;
+          const uint64_t hv = readlane64(hw, col & 63);
+          const int hb = (int)((hv >> bestpath) & 1ULL);
+          bestpath = (bestpath | (hb << 6)) >> 1;
+          if (j >= mintb) {
+            const int b = outpos + (nout - 1 - (j - mintb));
+            if (lane == (b >> 6)) obw |= (uint64_t)hb << (b & 63);
+          }
+        }
+      };
+      // uniform branch per block (a selected copy would go through scratch)
+      const int w = __builtin_amdgcn_readfirstlane(idx >> 6);
+      if (w == 0)
+        walk(h0);
+      else if (w == 1)
+        walk(h1);
+      else
+        walk(h2);
+      idx -= run - 1;
+    }
+    outpos += nout;
+    len -= nout;
+  };
+  auto process = [&](int skip) {
+    index++;
+    if (index == HCAP) index = 0;
+    renorm++;
+    len++;
+    if (renorm == RENORM) {
+      renorm = 0;
+      const int best = search(skip);
+      const int mind = __builtin_amdgcn_readlane(m, best);
+      m = (m - mind) & 0xFFFF;
+      if (len == HCAP) traceback(best, MINTB);
+    } else if (len == HCAP) {
+      traceback(search(skip), MINTB);
+    }
+  };
+  int a = 0, b = 0;
+  if (6 < sets) {
+    a = sbuf[12];
+    b = sbuf[13];
+  }
+  for (int i = 6; i < sets; ++i) {
+    // this step's symbols were read one step ahead (LDS latency off the chain)
+    const int ca = a, cb = b;
+    if (i + 1 < sets) {
+      a = sbuf[2 * i + 2];
+      b = sbuf[2 * i + 3];
+    }
+    const bool tail = i >= sets - 6;
+    const int skip = tail ? (1 << (7 - (sets - i))) : 1;
+    const int m0 = shfl_idx(m, s >> 1), m1 = shfl_idx(m, (s >> 1) | 32);
+    const int e0 = (m0 + soft_dist(tab_lo, ca, cb)) & 0xFFFF;
+    const int e1 = (m1 + soft_dist(tab_hi, ca, cb)) & 0xFFFF;
+    const bool act = (s % skip) == 0;
+    const int h = (e0 <= e1) ? 0 : 1;
+    if (act) m = h ? e1 : e0;
+    const uint64_t mask = __ballot(act && h);
+    {
+      const int w = __builtin_amdgcn_readfirstlane(index >> 6);
+      const bool mine = lane == (index & 63);
+      h0 = (mine && w == 0) ? mask : h0;
+      h1 = (mine && w == 1) ? mask : h1;
+      h2 = (mine && w == 2) ? mask : h2;
+    }
+    process(skip);
+  }
+  traceback(0, 0);
+}
+
+}  // namespace aero
