@@ -240,6 +240,8 @@ struct Group {
     int *d_n = nullptr;         // job count (device)
     int *d_jobs = nullptr;      // [C] int4 job list of this pass (device)
     hipEvent_t ev_vit = nullptr;  // this pass's Viterbi done (side stream)
+    hipEvent_t ev_framed = nullptr;  // this pass's framing done (main stream)
+    bool trace_blocks = false;
     uint8_t *h_out = nullptr;   // pinned copy of the first `copied` records
     int *h_n = nullptr;         // pinned copy of the count
     int copied = 0;
@@ -267,7 +269,8 @@ struct Group {
   // overlaps pass k+1's demodulation (the Viterbi waves are small enough to
   // share the CUs with the demod / coarse workgroups)
   hipStream_t st_vit = nullptr;
-  hipEvent_t ev_framed = nullptr;
+  hipEvent_t ev_cut = nullptr;  // main stream past the next pass's coarse hop
+  int vit_pending = -1;          // slot whose Viterbi launch is deferred
   hipEvent_t ev_in = nullptr;
   int16_t *d_stage[2] = {};
   size_t stage_cap[2] = {};
@@ -604,6 +607,39 @@ int collect_traces(Group *e) {
   return AERO_OK;
 }
 
+// The Viterbi of a pass (side stream) is launched once the main stream has
+// moved past the next pass's coarse hop: the coarse workgroups fill every
+// register of their CUs, the demod workgroups leave room for two Viterbi
+// waves per SIMD, so deferring by one launch lets the decode of pass k run
+// beside the demodulation of pass k+1 instead of between coarse workgroups.
+int issue_viterbi(Group *e) {
+  const int si = e->vit_pending;
+  if (si < 0) return AERO_OK;
+  e->vit_pending = -1;
+  auto &sl = e->slot[si];
+  DevState S2 = e->S;
+  S2.njobs = sl.d_n;
+  S2.jobout = sl.d_out;
+  S2.jobs = sl.d_jobs;
+  hipEvent_t a, b;
+  HIPCHK(hipEventRecord(e->ev_cut, e->st));
+  HIPCHK(hipStreamWaitEvent(e->st_vit, sl.ev_framed, 0));
+  HIPCHK(hipStreamWaitEvent(e->st_vit, e->ev_cut, 0));
+  ev_begin(e, "viterbi", a, b, e->st_vit);
+  launch_viterbi(e->st_vit, e->mode, S2, e->T, e->nch, sl.trace_blocks ? 1 : 0);
+  ev_end(e, b, e->st_vit);
+  HIPCHK(hipEventRecord(sl.ev_vit, e->st_vit));
+  HIPCHK(hipGetLastError());
+  // async hand-off: the count plus the records the job count is likely to need
+  sl.copied = std::min(e->nch, e->max_jobs_seen + e->max_jobs_seen / 4 + 256);
+  HIPCHK(hipMemcpyAsync(sl.h_n, sl.d_n, sizeof(int), hipMemcpyDeviceToHost, e->st_vit));
+  HIPCHK(hipMemcpyAsync(sl.h_out, sl.d_out, (size_t)sl.copied * JOB_OUT, hipMemcpyDeviceToHost, e->st_vit));
+  HIPCHK(hipEventRecord(sl.ev, e->st_vit));
+  sl.pending = true;
+  e->pending_slots.push_back(si);
+  return AERO_OK;
+}
+
 int run_group(Group *e, int flush) {
   if (e->nch == 0) return AERO_OK;
   HIPCHK(hipSetDevice(e->device));
@@ -640,6 +676,7 @@ int run_group(Group *e, int flush) {
       launch_coarse(e->st, e->mode, e->S, e->T, e->nch);
       ev_end(e, b);
     }
+    if (int rc = issue_viterbi(e)) return rc;  // the previous pass's decode, beside this demod
     if (!progress) continue;  // no new soft bits: framing has nothing to do
     ev_begin(e, "demod", a, b);
     if (e->mode == MODE_OQPSK)
@@ -668,20 +705,11 @@ int run_group(Group *e, int flush) {
     ev_begin(e, "frame", a, b);
     launch_frame(e->st, e->mode, S2, e->nch);
     ev_end(e, b);
-    HIPCHK(hipEventRecord(e->ev_framed, e->st));
-    HIPCHK(hipStreamWaitEvent(e->st_vit, e->ev_framed, 0));
-    ev_begin(e, "viterbi", a, b, e->st_vit);
-    launch_viterbi(e->st_vit, e->mode, S2, e->T, e->nch, (e->flags & AERO_F_TRACE_BLOCKS) ? 1 : 0);
-    ev_end(e, b, e->st_vit);
-    HIPCHK(hipEventRecord(sl.ev_vit, e->st_vit));
-    HIPCHK(hipGetLastError());
-    // async hand-off: the count plus the records the job count is likely to need
-    sl.copied = std::min(e->nch, e->max_jobs_seen + e->max_jobs_seen / 4 + 256);
-    HIPCHK(hipMemcpyAsync(sl.h_n, sl.d_n, sizeof(int), hipMemcpyDeviceToHost, e->st_vit));
-    HIPCHK(hipMemcpyAsync(sl.h_out, sl.d_out, (size_t)sl.copied * JOB_OUT, hipMemcpyDeviceToHost, e->st_vit));
-    HIPCHK(hipEventRecord(sl.ev, e->st_vit));
-    sl.pending = true;
-    e->pending_slots.push_back(si);
+    HIPCHK(hipEventRecord(sl.ev_framed, e->st));
+    sl.trace_blocks = (e->flags & AERO_F_TRACE_BLOCKS) != 0;
+    e->vit_pending = si;
+    if (trace || flush)  // parity traces run pass by pass; a flush has no next pass
+      if (int rc = issue_viterbi(e)) return rc;
     if (trace) {  // parity traces: synchronous, pass by pass
       if (int rc = poll_slots(e, true)) return rc;
       if (int rc = collect_traces(e)) return rc;
@@ -693,6 +721,7 @@ int run_group(Group *e, int flush) {
 // waits for the group's GPU work and hands every completed slot over
 int drain_group(Group *e) {
   HIPCHK(hipSetDevice(e->device));
+  if (int rc = issue_viterbi(e)) return rc;
   HIPCHK(hipStreamSynchronize(e->st));
   HIPCHK(hipStreamSynchronize(e->st_vit));
   if (int rc = poll_slots(e, true)) return rc;
@@ -765,9 +794,10 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
     if (hipMalloc(&sl.d_jobs, (size_t)16 * e->C) != hipSuccess) return AERO_E_NOMEM;
     HIPCHK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_vit, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&sl.ev_framed, hipEventDisableTiming));
   }
   HIPCHK(hipStreamCreateWithFlags(&e->st_vit, hipStreamNonBlocking));
-  HIPCHK(hipEventCreateWithFlags(&e->ev_framed, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&e->ev_cut, hipEventDisableTiming));
   for (int k = 0; k < Group::NPIN; k++) {
     if (hipHostMalloc(&e->pin_avail[k], sizeof(long long) * e->C) != hipSuccess) return AERO_E_NOMEM;
     HIPCHK(hipEventCreateWithFlags(&e->pin_ev[k], hipEventDisableTiming));
@@ -844,6 +874,7 @@ void group_destroy(Group *e) {
     if (sl.d_n) (void)hipFree(sl.d_n);
     if (sl.d_jobs) (void)hipFree(sl.d_jobs);
     if (sl.ev_vit) (void)hipEventDestroy(sl.ev_vit);
+    if (sl.ev_framed) (void)hipEventDestroy(sl.ev_framed);
     if (sl.h_out) (void)hipHostFree(sl.h_out);
     if (sl.h_n) (void)hipHostFree(sl.h_n);
     if (sl.ev) (void)hipEventDestroy(sl.ev);
@@ -870,7 +901,7 @@ void group_destroy(Group *e) {
   if (e->st_in) (void)hipStreamDestroy(e->st_in);
   if (e->d_scratch) (void)hipFree(e->d_scratch);
   if (e->pool) (void)hipFree(e->pool);
-  if (e->ev_framed) (void)hipEventDestroy(e->ev_framed);
+  if (e->ev_cut) (void)hipEventDestroy(e->ev_cut);
   if (e->st_vit) (void)hipStreamDestroy(e->st_vit);
   if (e->st) (void)hipStreamDestroy(e->st);
 }
