@@ -336,3 +336,81 @@ PUB_CONFIGS = {
                          dict(frequency=CENTER + 70000, data_rate=1200, gain=100.0, filter_bandwidth=4000)],
                    tones=[(-38000.0, 0.3), (31000.0, 0.2), (72000.0, 0.2)]),
 }
+
+
+# ------------------------------------------------------------------ C5
+# SURVEY.md §8(d) C5 stand-in for the absent sdr_54W_all.ini: a 1.536 Msps
+# receiver, 3 main VFOs (VFOsub[3], publish/publisher.h:50) of 192 kHz, and
+# 64 [vfos]: 6 x 10500 bps on the first main, 29 x 600 / 1200 on each of the
+# other two.  Each VFO carries a synthetic Aero signal of its bit rate, put
+# in as the upper sideband aero-publish's USB demodulator recovers
+# (publish/vfo.cpp:188-258).
+C5_RATE = 1536000
+C5_MAIN_OFFSETS = (-300000, 0, 300000)
+
+
+def c5_config(n_mains=3, per_main=(6, 29, 29)):
+    mains = [dict(frequency=CENTER + off, out_rate=192000) for off in C5_MAIN_OFFSETS[:n_mains]]
+    vfos = []
+    for m, n in enumerate(per_main[:n_mains]):
+        base = CENTER + C5_MAIN_OFFSETS[m]
+        if m == 0:  # 10500 bps: audio band [f, f + 24 kHz], 26 kHz apart
+            for k in range(n):
+                vfos.append(dict(frequency=base - 78000 + 26000 * k, data_rate=10500, gain=100.0))
+        else:  # 600 / 1200 alternating, 5 kHz apart
+            for k in range(n):
+                vfos.append(dict(frequency=base - 75000 + 5000 * k, data_rate=600 if (k + m) % 2 else 1200,
+                                 gain=100.0, filter_bandwidth=3000 if (k % 3 == 0) else 0))
+    return dict(sample_rate=C5_RATE, center_frequency=CENTER, mains=mains, vfos=vfos)
+
+
+def c5_ini(cfg):
+    """SDRReceiver-style INI (the keys publish/publisher.cpp:55-227 reads) for cfg."""
+    lines = ['[General]', 'sample_rate=%d' % cfg['sample_rate'], 'center_frequency=%d' % cfg['center_frequency'],
+             'tuner_gain=30', 'mix_offset=0', 'zmq_address=tcp://*:6004', 'correct_dc_bias=0', '',
+             '[main_vfos]', 'size=%d' % len(cfg['mains'])]
+    for i, m in enumerate(cfg['mains'], 1):
+        lines += ['%d\\frequency=%d' % (i, m['frequency']), '%d\\out_rate=%d' % (i, m['out_rate'])]
+    lines += ['', '[vfos]', 'size=%d' % len(cfg['vfos'])]
+    for i, v in enumerate(cfg['vfos'], 1):
+        lines += ['%d\\frequency=%d' % (i, v['frequency']), '%d\\data_rate=%d' % (i, v['data_rate']),
+                  '%d\\gain=%g' % (i, v['gain']), '%d\\topic=VFO%02d' % (i, i)]
+        if v.get('filter_bandwidth'):
+            lines.append('%d\\filter_bandwidth=%d' % (i, v['filter_bandwidth']))
+    return '\n'.join(lines) + '\n'
+
+
+def c5_audio(v, seconds, seed):
+    """The audio a VFO's decoder should see: synthetic Aero PCM of its rate."""
+    if v['data_rate'] == 10500:
+        return synth(seconds=seconds, seed=seed, carrier=12000.0 + 37.5 + (seed % 7), ebn0=30.0), 48000
+    br = v['data_rate']
+    return synth_msk(seconds=seconds, bitrate=br, baud=600, seed=seed, carrier=300.0 + 2.0 * (seed % 16),
+                     ebn0=30.0), (12000 if br == 600 else 24000)
+
+
+def c5_wideband(cfg, seconds, seed=0xC500, noise=0.02):
+    """CF32 wideband at cfg's rate: every VFO's audio as an analytic
+    (upper-sideband) signal at its frequency, built per main VFO at 192 kHz
+    and then raised to the receiver rate, plus a complex noise floor."""
+    from scipy import signal
+    fs = cfg['sample_rate']
+    n = int(fs * seconds)
+    rng = np.random.default_rng(seed)
+    out = (rng.normal(0, noise, n) + 1j * rng.normal(0, noise, n)).astype(np.complex128)
+    for m, mv in enumerate(cfg['mains']):
+        mrate = mv['out_rate']
+        nm = int(mrate * seconds)
+        acc = np.zeros(nm, dtype=np.complex128)
+        tm = np.arange(nm) / mrate
+        for k, v in enumerate(cfg['vfos']):
+            if abs(v['frequency'] - mv['frequency']) >= mrate // 2:
+                continue
+            pcm, arate = c5_audio(v, seconds, seed + 17 * k + 1)
+            x = signal.hilbert(pcm.astype(np.float64) / 32768.0)
+            x = signal.resample_poly(x, mrate // arate, 1)[:nm]
+            acc[:len(x)] += 0.25 * x * np.exp(2j * np.pi * (v['frequency'] - mv['frequency']) * tm[:len(x)])
+        up = signal.resample_poly(acc, fs // mrate, 1)[:n]
+        t = np.arange(len(up)) / fs
+        out[:len(up)] += up * np.exp(2j * np.pi * (mv['frequency'] - cfg['center_frequency']) * t)
+    return out.astype(np.complex64)
