@@ -14,6 +14,7 @@ int burst_group_create(int device, int flags, int max_channels, BurstGroup **out
 void burst_group_destroy(BurstGroup *g);
 int burst_open(BurstGroup *g, bool disable_reassembly, int *local);
 int burst_push(BurstGroup *g, int c, const int16_t *pcm, size_t n, bool dev, bool msg_start);
+int burst_push_batch(BurstGroup *g, const int16_t *src, size_t n, size_t ld, int nch, bool dev);
 int burst_run(BurstGroup *g, int flush);
 int burst_sync(BurstGroup *g);
 int burst_pop_soft(BurstGroup *g, int c, int16_t *dst, size_t cap, size_t *n);
@@ -22,5 +23,8 @@ int burst_pop_tests(BurstGroup *g, int c, uint8_t *dst, size_t cap, size_t *n);
 int burst_pop_packets(BurstGroup *g, int c, uint8_t *dst, size_t cap, size_t *n);
 std::vector<aero_acars_item> &burst_items(BurstGroup *g, int c);
 uint64_t burst_processed(const BurstGroup *g);
+uint64_t burst_stat(const BurstGroup *g, int which);  // 0: R/T tests run, 1: R/T packets decoded
+void burst_timing(BurstGroup *g, const char *name, double *ms, long *launches);  // adds to *ms / *launches
+void burst_timing_reset(BurstGroup *g);
 
 }  // namespace aero

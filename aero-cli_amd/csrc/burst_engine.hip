@@ -17,6 +17,8 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <map>
+#include <string>
 #include <vector>
 
 #include "../../include/aero_engine.h"
@@ -55,6 +57,30 @@ __global__ void b_scatter_kernel(int16_t *ring, int C, long long capm, const int
                                  long long start) {
   for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x)
     ring[((start + k) & capm) * C + c] = src[k];
+}
+
+// lockstep batch of one message per channel: src time-major [n][ld], channel
+// j < nch at its own pushed count (the device copy, stream-ordered)
+__global__ void b_batch_scatter_kernel(int16_t *ring, int C, long long capm, const int16_t *src, long long n,
+                                       long long ld, int nch, const long long *avail) {
+  const long long total = n * nch;
+  for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < total;
+       k += (long long)gridDim.x * blockDim.x) {
+    const long long t = k / nch;
+    const int j = (int)(k - t * nch);
+    ring[((avail[j] + t) & capm) * C + j] = src[t * ld + j];
+  }
+}
+
+// the batch's message starts and pushed counts (after the scatter read them)
+__global__ void b_batch_counts_kernel(long long *ls, long long *chunks, int C, int nch, long long n) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nch) return;
+  const long long start = ls[(size_t)BL_AVAIL * C + j];
+  const long long k = ls[(size_t)BL_CHUNK_N * C + j];
+  chunks[(size_t)j * CHUNK_RING + (k & (CHUNK_RING - 1))] = start;
+  ls[(size_t)BL_CHUNK_N * C + j] = k + 1;
+  ls[(size_t)BL_AVAIL * C + j] = start + n;
 }
 
 template <class T>
@@ -121,6 +147,10 @@ struct BurstGroup {
   int16_t *d_scratch = nullptr;
   size_t scratch_cap = 0;
   uint64_t processed = 0;
+  uint64_t st_tests = 0, st_packets = 0;  // aero_stat "rt_tests" / "rt_packets"
+  // AERO_F_TIMING: HIP-event milliseconds and launches per kernel name
+  std::map<std::string, std::pair<double, long>> timing;
+  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending_ev;
   long long last_work = -1;
   std::vector<long long> hb_base;  // first sample the Hilbert stage still needs (host mirror)
   std::vector<int> since_run;      // messages pushed since the last run (message-start ring)
@@ -186,17 +216,47 @@ int h2d(const V *dst, const std::vector<V> &src) {
   return AERO_OK;
 }
 
+// times one launch (AERO_F_TIMING); collected after run_once's stream sync
+template <class F>
+void timed(BurstGroup *g, const char *name, F &&launch) {
+  if (!(g->flags & AERO_F_TIMING)) {
+    launch();
+    return;
+  }
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a, g->st);
+  launch();
+  hipEventRecord(b, g->st);
+  g->pending_ev.push_back({name, {a, b}});
+}
+
+void collect_timing(BurstGroup *g) {
+  for (auto &pe : g->pending_ev) {
+    float ms = 0;
+    hipEventSynchronize(pe.second.second);
+    hipEventElapsedTime(&ms, pe.second.first, pe.second.second);
+    auto &t = g->timing[pe.first];
+    t.first += ms;
+    t.second++;
+    hipEventDestroy(pe.second.first);
+    hipEventDestroy(pe.second.second);
+  }
+  g->pending_ev.clear();
+}
+
 int run_once(BurstGroup *g, bool trace, bool &progress) {
   const int nch = g->nch;
   progress = false;
-  launch_hilbert(g->st, g->S, g->T, nch);
+  timed(g, "burst_hilbert", [&] { launch_hilbert(g->st, g->S, g->T, nch); });
   for (int r = 0; r < DEMOD_ROUNDS; r++) {
-    launch_demod_burst(g->st, g->S, g->T, nch, (int)B_PCM_CAP, trace ? 1 : 0);
-    launch_trident(g->st, g->S, g->T, nch);
+    timed(g, "burst_demod", [&] { launch_demod_burst(g->st, g->S, g->T, nch, (int)B_PCM_CAP, trace ? 1 : 0); });
+    timed(g, "burst_trident", [&] { launch_trident(g->st, g->S, g->T, nch); });
   }
   BCHK(hipMemsetAsync(g->S.njobs, 0, sizeof(int), g->st));
-  launch_frame_burst(g->st, g->S, nch);
-  launch_rt_viterbi(g->st, g->S, nch * RT_TESTS_PER_PASS);
+  timed(g, "burst_frame", [&] { launch_frame_burst(g->st, g->S, nch); });
+  timed(g, "burst_viterbi", [&] { launch_rt_viterbi(g->st, g->S, nch * RT_TESTS_PER_PASS); });
   BCHK(hipGetLastError());
   int njobs = 0;
   BCHK(hipMemcpyAsync(&njobs, g->S.njobs, sizeof(int), hipMemcpyDeviceToHost, g->st));
@@ -241,11 +301,13 @@ int run_once(BurstGroup *g, bool trace, bool &progress) {
         if (!info.empty()) info.pop_back();  // infofield.chop(1)
       }
     }
+    g->st_tests++;
     if (g->flags & AERO_F_TRACE_FRAMES) {
       const uint32_t t2[2] = {(uint32_t)bp, (uint32_t)result};
       g->tests_hold[c].insert(g->tests_hold[c].end(), (const uint8_t *)t2, (const uint8_t *)t2 + 8);
     }
     if (result == OK_R || result == OK_T) {
+      g->st_packets++;
       g->ok_burst[c] = burst;
       if (g->flags & AERO_F_TRACE_FRAMES) {
         const uint32_t p2[2] = {(uint32_t)(result == OK_R ? 'R' : 'T'), (uint32_t)info.size()};
@@ -468,6 +530,51 @@ int burst_push(BurstGroup *g, int c, const int16_t *pcm, size_t n, bool dev, boo
   return AERO_OK;
 }
 
+// aero_push_pcm_batch for burst channels [0, nch): one message of n samples
+// per channel (the reference's message boundaries are what the caller's
+// batch boundaries are), src a device pointer or host memory
+int burst_push_batch(BurstGroup *g, const int16_t *src, size_t n, size_t ld, int nch, bool dev) {
+  if (!n) return AERO_OK;
+  if (nch > g->nch) return AERO_E_INVALID;
+  BCHK(hipSetDevice(g->device));
+  const int C = g->C;
+  if ((long long)n > B_PCM_CAP / 2) return AERO_E_FULL;
+  bool need_run = false;
+  for (int c = 0; c < nch; c++)
+    need_run |= g->avail[c] + (long long)n - g->hb_base[c] > B_PCM_CAP - 2 || g->since_run[c] >= CHUNK_RING - 1;
+  if (need_run)
+    if (int rc = burst_run(g, 0)) return rc;
+  const int16_t *d = src;
+  const size_t need = (n - 1) * ld + nch;
+  if (!dev) {
+    if (need > g->scratch_cap) {
+      BCHK(hipStreamSynchronize(g->st));
+      if (g->d_scratch) (void)hipFree(g->d_scratch);
+      g->d_scratch = nullptr;
+      g->scratch_cap = 0;
+      BCHK(hipMalloc(&g->d_scratch, need * sizeof(int16_t)));
+      g->scratch_cap = need;
+    }
+    BCHK(hipMemcpyAsync(g->d_scratch, src, need * sizeof(int16_t), hipMemcpyHostToDevice, g->st));
+    d = g->d_scratch;
+  }
+  const long long total = (long long)n * nch;
+  const int grid = (int)std::min<long long>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(b_batch_scatter_kernel, dim3(grid), dim3(256), 0, g->st, g->S.pcm, C, B_PCM_CAP - 1, d,
+                     (long long)n, (long long)ld, nch, (const long long *)(g->S.ls + (size_t)BL_AVAIL * C));
+  hipLaunchKernelGGL(b_batch_counts_kernel, dim3((nch + 255) / 256), dim3(256), 0, g->st, g->S.ls, g->S.chunks, C,
+                     nch, (long long)n);
+  BCHK(hipGetLastError());
+  for (int c = 0; c < nch; c++) {
+    g->chunk_n[c]++;
+    g->since_run[c]++;
+    g->avail[c] += (long long)n;
+  }
+  BCHK(hipStreamSynchronize(g->st));  // the caller's buffer is free again
+  g->processed += (uint64_t)n * nch;
+  return AERO_OK;
+}
+
 template <class T>
 static int pop_v(std::vector<T> &v, T *dst, size_t cap, size_t *n) {
   const size_t k = std::min(cap, v.size());
@@ -494,6 +601,20 @@ int burst_pop_packets(BurstGroup *g, int c, uint8_t *dst, size_t cap, size_t *n)
 }
 std::vector<aero_acars_item> &burst_items(BurstGroup *g, int c) { return g->host[c]->items; }
 uint64_t burst_processed(const BurstGroup *g) { return g ? g->processed : 0; }
+uint64_t burst_stat(const BurstGroup *g, int which) { return !g ? 0 : (which ? g->st_packets : g->st_tests); }
+void burst_timing(BurstGroup *g, const char *name, double *ms, long *launches) {
+  if (!g) return;
+  collect_timing(g);
+  auto it = g->timing.find(name);
+  if (it == g->timing.end()) return;
+  *ms += it->second.first;
+  *launches += it->second.second;
+}
+void burst_timing_reset(BurstGroup *g) {
+  if (!g) return;
+  collect_timing(g);
+  g->timing.clear();
+}
 int burst_sync(BurstGroup *g) {
   if (!g) return AERO_OK;
   BCHK(hipStreamSynchronize(g->st));

@@ -1231,9 +1231,13 @@ int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld,
   if (!e || !pcm || nch <= 0 || nch > (int)e->chmap.size() || ld < (size_t)nch) return AERO_E_INVALID;
   // channels [0, nch) must be one kind, opened in order (local == engine index)
   const int mode = e->chmap[0].first;
-  if (mode == MODE_BURST) return AERO_E_INVALID;  // burst channels take one message per call
   for (int j = 0; j < nch; j++)
     if (e->chmap[j].first != mode || e->chmap[j].second != j) return AERO_E_INVALID;
+  if (mode == MODE_BURST) {  // one message of n <= 16384 samples per channel
+    if (dev && check_dev_ptr(pcm)) return AERO_E_INVALID;
+    HIPCHK(hipSetDevice(e->device));
+    return burst_push_batch(e->burst, pcm, n, ld, nch, dev != 0);
+  }
   Group *g = e->groups[mode].get();
   HIPCHK(hipSetDevice(e->device));
   size_t off = 0;
@@ -1371,6 +1375,7 @@ int aero_timing(aero_engine *e, const char *name, double *ms, long *launches) {
       tl += it->second.launches;
     }
   }
+  burst_timing(e->burst, name, &tms, &tl);
   if (ms) *ms = tms;
   if (launches) *launches = tl;
   return AERO_OK;
@@ -1378,6 +1383,7 @@ int aero_timing(aero_engine *e, const char *name, double *ms, long *launches) {
 
 void aero_timing_reset(aero_engine *e) {
   if (!e) return;
+  burst_timing_reset(e->burst);
   for (auto &g : e->groups)
     if (g) {
       ev_collect(g.get());
@@ -1390,6 +1396,10 @@ int aero_stat(aero_engine *e, const char *name, uint64_t *value) {
   host_wait(e);  // counters of frames the host workers are still handling
   uint64_t v = 0;
   const std::string n(name);
+  if (n == "rt_tests" || n == "rt_packets") {
+    *value = burst_stat(e->burst, n == "rt_packets");
+    return AERO_OK;
+  }
   for (auto &g : e->groups) {
     if (!g) continue;
     if (n == "viterbi_jobs")

@@ -38,6 +38,12 @@ MODES = {
     'msk600': dict(bitrate=600, hop=2048, fs=12000, bytes=2.05, kernel='demod_msk_kernel<1>', timing='msk600_demod',
                    metric='Msamples/s demod+Viterbi, 600bps MSK (C3); ACARS frames bit-exact vs ref',
                    cpu_seconds=2400.0, config='C3', flops=1050.0),
+    # burst OQPSK (C4): 2 B int16 in + 16 B AGC ring r/w (48000-deep) + soft bits out;
+    # a step is one 12000-sample message per channel (burst output follows message boundaries)
+    'burst10500': dict(bitrate=10500, hop=12000, fs=48000, bytes=18.22, kernel='demod_burst_kernel',
+                       timing='burst_demod', burst=True, preroll=4,
+                       metric='Msamples/s demod+Viterbi, 10500bps burst OQPSK (C4); R/T packets bit-exact vs ref',
+                       cpu_seconds=240.0, config='C4', flops=1300.0),
     # 2 B int16 in + 0.025 B soft bits out (fb stays 600 at 24 kHz, decode/decode.cpp:142-150)
     'msk1200': dict(bitrate=1200, hop=2048, fs=24000, bytes=2.025, kernel='demod_msk_kernel<2>',
                     timing='msk1200_demod', metric='Msamples/s demod+Viterbi, 1200bps MSK; ACARS frames bit-exact vs ref',
@@ -60,7 +66,7 @@ CALIBRATION = {'oqpsk10500': {'port_msps_per_core': 0.967, 'reference_msps_per_c
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--mode', default='oqpsk10500', choices=sorted(MODES),
+    ap.add_argument('--mode', default='oqpsk10500', choices=sorted(MODES) + ['c5'],
                     help='channel kind (default: the BASELINE.json headline, C2 10500-bps OQPSK)')
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5,
@@ -81,6 +87,10 @@ def parse():
 
 def synth_one(M, seconds, seed, k=0, lead_in=0):
     import aero_testlib as tl
+    if M.get('burst'):
+        # C4: R/T bursts every 1-3 s on a carrier near 12 kHz (the burst demod has no hunter)
+        return tl.synth_burst(seconds=seconds, seed=seed, carrier=12000.0 + 0.5 * (k % 64), ebn0=14.0,
+                              phase0=0.1 * k, lead_in=lead_in or 24000)
     if M['bitrate'] == 10500:
         # seed 0xAE20+k, carrier 12000 + 37.5 + 0.5 k Hz, Eb/N0 12 dB
         return tl.synth(seconds=seconds, seed=seed, carrier=12037.5 + 0.5 * (k % 64), ebn0=12.0, phase0=0.1 * k,
@@ -148,7 +158,7 @@ def _cpu_one(arg):
     M, seconds, seed = arg
     import aero_testlib as tl
     pcm = synth_one(M, seconds, seed, lead_in=1000)
-    o = tl.Oracle(bitrate=M['bitrate'])
+    o = tl.Oracle(bitrate=M['bitrate'], burst=bool(M.get('burst')))
     t = time.perf_counter()
     o.push_chunked(pcm, M['fs'] // 4)
     return len(pcm), time.perf_counter() - t
@@ -187,6 +197,154 @@ def pmc_traffic(path, mode, channels):
     return d.get('hbm_bytes_per_launch'), os.path.relpath(path, ROOT)
 
 
+C5_SECONDS = 6.0  # synthetic wideband held in HBM, read after read in a loop
+
+
+def _c5_cpu_one(arg):
+    cfg, v, audio, spb = arg
+    import aero_testlib as tl
+    import aero_engine as ae
+    o = tl.Oracle(bitrate=ae.vfo_bitrate(cfg['vfos'][v]['data_rate']))
+    t = time.perf_counter()
+    o.push_chunked(audio, spb)
+    return len(audio), time.perf_counter() - t
+
+
+def c5_cpu_baseline(cfg, x, procs):
+    """aero-publish + one aero-decode per VFO, as the reference deploys C5:
+    the oracle publisher on one core over the whole sample, then the 64 oracle
+    decoders on `procs` processes; wideband Msamples/s and channel
+    Msamples/s of the bounded sample."""
+    import multiprocessing as mp
+    import aero_testlib as tl
+    ref = tl.OraclePublisher(cfg['sample_rate'], cfg['center_frequency'], cfg['mains'], cfg['vfos'])
+    nb = len(x) // ref.block_len
+    t = time.perf_counter()
+    ref.process(x[:nb * ref.block_len])
+    t_pub = time.perf_counter() - t
+    jobs = [(cfg, v, ref.usb(v), ref.info(v)['samples_per_block']) for v in range(len(cfg['vfos']))]
+    t = time.perf_counter()
+    with mp.get_context('fork').Pool(procs) as p:
+        res = p.map(_c5_cpu_one, jobs)
+    t_dec = time.perf_counter() - t
+    ch_samples = sum(r[0] for r in res)
+    wall = t_pub + t_dec  # the publisher feeds the decoders: sequential lower bound on one host
+    return {'value': round(ch_samples / wall / 1e6, 4), 'unit': 'Msamples/s', 'cores': procs, 'kind': 'port',
+            'sample': '%.1f s of the C5 wideband (%d reads): oracle publisher on 1 core (%.2f s) then 64 oracle '
+                      'decoders on %d processes (%.2f s)' % (nb * ref.block_len / cfg['sample_rate'], nb, t_pub,
+                                                              procs, t_dec),
+            'wideband_msps': round(nb * ref.block_len / wall / 1e6, 4), 'cpu_model': cpu_model()}
+
+
+def run_c5(a, rank, world, local):
+    """C5: one 1.536 Msps receiver (3 main VFOs, 64 [vfos], BASELINE
+    configs[4]); the wideband CF32 sits in HBM on rank 0, every read is
+    broadcast to all ranks (RCCL over xGMI, the path's one exchange step,
+    shard.broadcast_reads), and each rank channelises and decodes the VFOs
+    shard.shard_vfos gives it.  A step is one 0.25 s read."""
+    import aero_testlib as tl
+    import shard
+    cfg = tl.c5_config()
+    owner = shard.shard_vfos(cfg['vfos'], world)
+    mine = [owner[v] == rank for v in range(len(cfg['vfos']))]
+    x = tl.c5_wideband(cfg, C5_SECONDS) if rank == 0 else None
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = c5_cpu_baseline(cfg, x[:int(cfg['sample_rate'] * 4.0)], a.cpu_procs or host_cores())
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    import aero_engine as ae
+    ch = ae.Channeliser(cfg['sample_rate'], cfg['center_frequency'], cfg['mains'], cfg['vfos'], max_blocks=1,
+                        device=local, skip=[not m for m in mine])
+    B = ch.block_len
+    nread = int(cfg['sample_rate'] * C5_SECONDS) // B
+    wb = torch.empty((nread, B * 2), dtype=torch.float32, device='cuda')
+    if rank == 0:
+        wb.copy_(torch.from_numpy(x[:nread * B].view(np.float32).reshape(nread, B * 2)))
+    rd = torch.empty((B * 2,), dtype=torch.float32, device='cuda')
+    eng = ae.Engine(max_channels=max(1, sum(mine)), device=local, flags=ae.F_TIMING)
+    chans = [eng.open_channel(ae.vfo_bitrate(v['data_rate'])) if m else -1 for v, m in zip(cfg['vfos'], mine)]
+    per_read = sum(ch.vfo_info(v)['samples_per_block'] for v in range(len(cfg['vfos'])) if mine[v])
+
+    def step(s):
+        if rank == 0:
+            rd.copy_(wb[s % nread])
+        shard.broadcast_reads(rd)
+        torch.cuda.synchronize()
+        ch.push_device(rd.data_ptr(), 1)
+        ch.run()
+        ch.feed(eng, chans)
+        eng.run()
+        return eng.drain_items()
+
+    pre = 16 + a.warmup  # 4 s of audio: every hunter has locked
+    for s in range(pre):
+        step(s)
+    eng.sync()
+    ch.sync()
+    torch.cuda.synchronize()
+    eng.timing_reset()
+    s0 = eng.samples_processed()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    items = 0
+    for s in range(a.steps):
+        items += step(pre + s)
+    eng.sync()
+    ch.sync()
+    items += eng.drain_items()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    samples = eng.samples_processed() - s0
+    t = torch.tensor([elapsed, float(samples), float(items)], dtype=torch.float64, device='cuda')
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed, samples, items = float(tmax[0]), float(t[1]), int(t[2])
+    if rank == 0:
+        value = samples / elapsed / 1e6
+        wideband = a.steps * B / elapsed / 1e6
+        audio_s = a.steps * 0.25
+        # algorithmic bytes of a step: the CF32 read (8 B per wideband sample,
+        # SURVEY §8(d) C5) plus every channel's demod bytes per audio sample
+        vb = {600: 2.05, 1200: 2.025}
+        ch_bytes = sum(ch.vfo_info(v)['samples_per_block'] * vb.get(cfg['vfos'][v]['data_rate'], 18.22)
+                       for v in range(len(cfg['vfos'])))
+        step_bytes = 8.0 * B * world + ch_bytes
+        achieved = step_bytes * a.steps / elapsed / 1e9
+        out = {
+            'metric': 'Msamples/s demod+Viterbi, C5 64-VFO channeliser + mixed 600/1200/10500 (channel samples)',
+            'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
+            'preroll_reads': 16, 'ms_per_step': round(elapsed / a.steps * 1e3, 3), 'higher_is_better': True,
+            'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32 channeliser / f64 demod', 'data': 'synthetic',
+            'config': {'workload': 'C5: 1.536 Msps receiver, 3 main VFOs, 64 [vfos] (6 x 10500, 29 x 600/1200 '
+                                   'alternating), one 0.25 s read per step, reads broadcast to %d rank(s)' % world,
+                       'vfos': len(cfg['vfos']), 'vfos_per_rank': per_read and sum(mine),
+                       'parallelism': 'vfo-sharded x%d + read broadcast' % world},
+            'wideband_msps': round(wideband, 3), 'realtime_factor': round(audio_s / elapsed, 2),
+            'roofline': {'bound': 'hbm', 'kernel': 'whole step', 'achieved': round(achieved, 3),
+                         'peak': HBM_PEAK_GBS * world, 'unit': 'GB/s',
+                         'frac': round(achieved / (HBM_PEAK_GBS * world), 7), 'traffic': None,
+                         'bytes_per_step': round(step_bytes)},
+            'acars_items': items,
+        }
+        if cpu is not None:
+            out['cpu_baseline'] = cpu
+        print(json.dumps(out), flush=True)
+    eng.close()
+    ch.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     if a.gpus > 1 and 'RANK' not in os.environ:
@@ -194,11 +352,14 @@ def main():
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
+    if a.mode == 'c5':
+        return run_c5(a, rank, world, local)
     import shard
     M = MODES[a.mode]
     HOP, FS = M['hop'], M['fs']
     C, P = a.channels, a.pool
-    pre = PREROLL_HOPS + a.warmup  # untimed hops: lock-in pre-roll + warmup
+    preroll = M.get('preroll', PREROLL_HOPS)  # burst channels have no hunter to lock
+    pre = preroll + a.warmup  # untimed hops: lock-in pre-roll + warmup
     steps_total = pre + a.steps
     span = steps_total * HOP
     offsets = shard.channel_offsets(C, P, rank)
@@ -221,9 +382,11 @@ def main():
         views = [pool[:, int(o) + s * HOP:int(o) + (s + 1) * HOP] for o in offsets]
         return torch.stack(views).permute(2, 0, 1).reshape(HOP, C).contiguous()
 
+    burst = bool(M.get('burst'))
     eng = ae.Engine(max_channels=C, device=local, flags=ae.F_TIMING)
     for _ in range(C):
-        eng.open_channel(M['bitrate'], FS)
+        eng.open_channel(M['bitrate'], FS, burst=burst)
+    stat_names = ('rt_tests', 'rt_packets') if burst else ('viterbi_jobs', 'frames', 'su_crc_ok')
     # pre-roll (hunter scan, AFC and lock) + warmup, untimed
     for s in range(pre):
         x = step_input(s)
@@ -237,7 +400,7 @@ def main():
     torch.cuda.synchronize()
     eng.timing_reset()
     s0 = eng.samples_processed()
-    st0 = {k: eng.stat(k) for k in ('viterbi_jobs', 'frames', 'su_crc_ok')}
+    st0 = {k: eng.stat(k) for k in stat_names}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -266,7 +429,10 @@ def main():
         elapsed, samples = float(tmax[0]), float(t[1])
         stats = {k: int(t[2 + i]) for i, k in enumerate(keys)}
     tag = M['timing'][:-len('demod')]
-    kt = {k: eng.timing(tag + k) for k in ('demod', 'coarse', 'frame', 'viterbi')}
+    if burst:  # the burst path's kernels: Hilbert fast FIR, demod, trident FFT check, framing, R/T Viterbi
+        kt = {k: eng.timing('burst_' + k) for k in ('hilbert', 'demod', 'trident', 'frame', 'viterbi')}
+    else:
+        kt = {k: eng.timing(tag + k) for k in ('demod', 'coarse', 'frame', 'viterbi')}
     ht = {k: eng.timing(k) for k in ('host_push', 'host_run', 'host_wait_njobs', 'host_wait_jobs', 'host_frames')}
     if rank == 0:
         value = samples / elapsed / 1e6
@@ -279,13 +445,16 @@ def main():
         out = {
             'metric': M['metric'],
             'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world, 'steps': a.steps,
-            'warmup': a.warmup, 'preroll_hops': PREROLL_HOPS, 'ms_per_step': round(elapsed / a.steps * 1e3, 3),
+            'warmup': a.warmup, 'preroll_hops': preroll, 'ms_per_step': round(elapsed / a.steps * 1e3, 3),
             'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
-            'config': {'workload': '%s x %d: independent single-VFO %d-bps continuous %s P-channels '
+            'config': {'workload': ('%s x %d: independent single-VFO %d-bps burst OQPSK R/T channels per GPU, '
+                                    '%d Hz int16, one %d-sample message per channel per step' % (
+                                        M['config'], C, M['bitrate'], FS, HOP)) if burst else (
+                                   '%s x %d: independent single-VFO %d-bps continuous %s P-channels '
                                    'per GPU, %d Hz int16, one %d-sample hop per step' % (
                                        M['config'], C, M['bitrate'], 'OQPSK' if M['bitrate'] == 10500 else 'MSK',
-                                       FS, HOP),
+                                       FS, HOP)),
                        'channels_per_gpu': C, 'total_channels': C * world, 'hop_samples': HOP,
                        'parallelism': 'channel-sharded x%d' % world},
             'roofline': {'bound': 'hbm', 'kernel': M['kernel'], 'achieved': round(achieved, 2),
@@ -305,7 +474,7 @@ def main():
             out['cpu_baseline'] = cpu
             out['vs_cpu'] = round(value / cpu['value'], 1)
         print(json.dumps(out), flush=True)
-        if stats['viterbi_jobs'] <= 0 or stats['acars_items'] <= 0:
+        if stats[stat_names[0]] <= 0 or stats['acars_items'] <= 0:
             # the metric names demod + Viterbi: a timed region without decoded frames measured something else
             print('bench: timed region decoded no Viterbi jobs / ACARS items (%s)' % stats, file=sys.stderr)
             sys.exit(3)

@@ -88,7 +88,9 @@ int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t
 /* Lockstep batch push for channels [0, nch): pcm is time-major, n samples
  * per channel, sample t of channel c at pcm[t*ld + c].  dev != 0: pcm is a
  * HIP device pointer (inputs already resident in HBM).  Channels [0, nch)
- * must be of one kind (bit rate). */
+ * must be of one kind (bit rate, burst or not).  For burst channels the
+ * batch is one message per channel (at most 16384 samples; burst output
+ * depends on message boundaries, decode/burstoqpskdemodulator.cpp:264). */
 int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld, int nch, int dev);
 
 /* aero_push_pcm with pcm a HIP device pointer (e.g. channeliser audio already
@@ -144,9 +146,11 @@ int aero_pop_rt_packets(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t
 int aero_timing(aero_engine *e, const char *name, double *ms, long *launches);
 void aero_timing_reset(aero_engine *e);
 
-/* Continuous-channel counters since creation: "viterbi_jobs" (blocks the
- * GPU Viterbi decoded and handed back), "frames" (frames delivered to the
- * SU/ACARS host), "su_crc_ok" (SUs whose CRC-16 checked).  Joins the
+/* Counters since creation.  Continuous channels: "viterbi_jobs" (blocks
+ * the GPU Viterbi decoded and handed back), "frames" (frames delivered to
+ * the SU/ACARS host), "su_crc_ok" (SUs whose CRC-16 checked); burst
+ * channels: "rt_tests" (RTChannelDeleaveFECScram decodes run),
+ * "rt_packets" (R/T packets that passed their CRCs).  Joins the
  * asynchronous host frame work first.  AERO_E_INVALID for another name. */
 int aero_stat(aero_engine *e, const char *name, uint64_t *value);
 
