@@ -101,9 +101,9 @@ def build_oracle():
 
 HOST = os.path.join(HERE, 'host')
 BIN = os.path.join(HERE, 'bin')
-HOST_COMMON = ['qstr.cpp', 'output.cpp', 'forwarder.cpp', 'zmq_dl.cpp']
+HOST_COMMON = ['qstr.cpp', 'output.cpp', 'forwarder.cpp', 'zmq_dl.cpp', 'ini.cpp']
 # the host binaries: drop-in aero-decode / aero-publish over the engine's C ABI
-HOST_BINS = {'aero-decode': ['aero_decode.cpp']}
+HOST_BINS = {'aero-decode': ['aero_decode.cpp'], 'aero-publish': ['aero_publish.cpp']}
 TOOL_BINS = {'zmq_pcm_pub': os.path.join(ROOT, 'tools', 'zmq_pcm_pub.cpp')}
 
 

@@ -46,6 +46,24 @@ namespace aero {
 #define DM_DIVC(a, c) ((a) / (c))
 #endif
 
+// AERO_X_STAMPS (diagnostic build only): s_memtime cycle totals per loop
+// section of wave 0 of workgroup 0, with scheduling barriers at the stamps
+#ifdef AERO_X_STAMPS
+__device__ unsigned long long g_stamps[8];
+#define XSTAMP(k)                                         \
+  do {                                                    \
+    __builtin_amdgcn_sched_barrier(0);                    \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    xstamp_[k] += t_ - xtime_;                                     \
+    xtime_ = t_;                                          \
+    __builtin_amdgcn_sched_barrier(0);                    \
+  } while (0)
+#else
+#define XSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 __constant__ double c_taps[NTAPS];
 __constant__ DelayDesc c_dly[4];  // delays(1), delayt41(T/4), delayt42(T/4), delayt8(T/8)
 __constant__ double c_sr_b[3];    // st resonator (oqpskdemodulator.cpp:218-223)
@@ -224,9 +242,13 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
   // different channels changes.
   int i = 0;
   double ev_pr = 0.0, ev_pi = 0.0;
+#ifdef AERO_X_STAMPS
+  unsigned long long xstamp_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, xtime_ = __builtin_amdgcn_s_memtime();
+#endif
   while (i < ie) {
     bool pend = false;
     do {
+      XSTAMP(0);  // loop control
       const int16_t xs = pcm_next;
       const double agc_old = agc_next;
       // table lookups of this sample first, then the prefetch for the next
@@ -287,12 +309,14 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
         s2i *= g;
       }
       // clipping (:408-410)
+      XSTAMP(1);  // loads, FIR update, AGC
       const double ab = DM_HYPOT(s2r, s2i);
       if (ab > 2.84) {
         const double k = 2.84 / ab;
         s2r = k * s2r;
         s2i = k * s2i;
       }
+      XSTAMP(2);  // hypot + clip
       // symbol timer (:413-426)
       const double st_diff = delay_tap<2, 1, 0>(d1, c_dly[0], ab * ab) - (ab * ab);
       const double st_d1out = delay_tap<4, 3, 2>(d41, c_dly[1], st_diff);
@@ -313,6 +337,7 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
         s2l_im = s2i;
         s2l_init = 1;
       }
+      XSTAMP(3);  // timer: delays, resonator, atan2, NCO nudges
       // sample instant (:430) IfHavePassedPoint (DSP.cpp:222-238)
       double tl = so_last - PT, tw = so_ptr - PT;
       if (tl < 0.0) tl += WTSIZE;
@@ -362,7 +387,9 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
         nco_next(m2_ptr, m2_step);
         ++i;
       }
+      XSTAMP(4);  // sample instant, NCOs, coarse-ring staging
     } while (!pend && i < ie);
+    XSTAMP(0);
     if (pend) {
       // channel-row pointers from a laundered index: recomputed here, not
       // kept live across the sample loop
@@ -479,7 +506,14 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       nco_next(m2_ptr, m2_step);
       ++i;
     }
+    XSTAMP(5);  // carrier event step
   }
+#ifdef AERO_X_STAMPS
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    for (int k = 0; k < 6; ++k) g_stamps[k] += xstamp_[k];
+    g_stamps[6] += (unsigned long long)i;  // samples
+  }
+#endif
   // staged entries of an unfinished 16-sample group
   if (ifl - 1 >= 1 && ((rb + ifl - 1) & (RING_GROUP - 1)) != RING_GROUP - 1) {
     const int last = ifl - 1;                                // relative sample of the last staged entry
@@ -549,6 +583,17 @@ void launch_demod(hipStream_t st, const DevState &S, const DevTables &T, int nch
     hipLaunchKernelGGL(demod_oqpsk_kernel<true>, grid, block, 0, st, S, T, nch, flush);
   else
     hipLaunchKernelGGL(demod_oqpsk_kernel<false>, grid, block, 0, st, S, T, nch, flush);
+}
+
+// diagnostic build: cycle totals per section (7 values), then reset
+void demod_read_stamps(unsigned long long *out) {
+#ifdef AERO_X_STAMPS
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 7);
+  unsigned long long z[8] = {0};
+  hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z);
+#else
+  for (int k = 0; k < 7; ++k) out[k] = 0;
+#endif
 }
 
 void upload_demod_constants(const double *taps, const DelayDesc *dly, const double *sr_b, const double *sr_a,

@@ -44,6 +44,7 @@ void upload_demod_constants(const double *, const DelayDesc *, const double *, c
                             const double *);
 void launch_demod_msk(hipStream_t, int, const DevState &, const DevTables &, int, int);
 void upload_msk_constants(const double *, const double *, const double *);
+void demod_read_stamps(unsigned long long *);
 void launch_coarse(hipStream_t, int, const DevState &, const DevTables &, int);
 void launch_frame(hipStream_t, int, const DevState &, int);
 void launch_viterbi(hipStream_t, int, const DevState &, const DevTables &, int, int);
@@ -1514,3 +1515,9 @@ int aero_engine_feed_dev(aero_engine *e, int nitems, const int *ch, const int16_
       if (int rc = feed_group(e->groups[m].get(), per[m], ready, producer)) return rc;
   return AERO_OK;
 }
+
+// diagnostic builds (AERO_X_STAMPS): the demod's per-section cycle totals
+// (loop control, loads+FIR+AGC, hypot+clip, timer, instant+NCO+ring, event
+// step, samples) of wave 0; zeros in the product build
+extern "C" void aero_x_demod_stamps(unsigned long long *out7) { demod_read_stamps(out7); }
+

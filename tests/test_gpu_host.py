@@ -195,3 +195,54 @@ def test_no_signal_exit(engine_lib, tmp_path):
     assert 'Scanned entire VFO bandwidth and could not find a signal.' in text
     assert 'Exiting because of no signal' in text
     assert rc == 0
+
+
+def test_publish_to_decode_pipeline(engine_lib, cpu_libs, tmp_path):
+    """aero-publish (GPU channeliser, CF32 file source, the generated C5 INI,
+    64 VFOs) -> ZeroMQ -> two aero-decode processes (a 10500 and a 600 bps
+    topic) -> jsondump lines equal to the oracle publisher's audio through
+    the oracle decoder (publish/vfo.cpp -> decode/decode.cpp, config C5)."""
+    import build
+    build.build_host()
+    cfg = tl.c5_config()
+    x = tl.c5_wideband(cfg, 8.0)
+    ref = tl.OraclePublisher(cfg['sample_rate'], cfg['center_frequency'], cfg['mains'], cfg['vfos'])
+    nb = len(x) // ref.block_len
+    ref.process(x[:nb * ref.block_len])
+    wb = tmp_path / 'wideband.cf32'
+    x[:nb * ref.block_len].astype(np.complex64).tofile(str(wb))
+    port = free_port()
+    ini = tmp_path / 'c5.ini'
+    ini.write_text(tl.c5_ini(cfg).replace('tcp://*:6004', 'tcp://127.0.0.1:%d' % port))
+    picks = [0, 7]  # VFO01 (10500 bps), VFO08 (600 bps)
+    wants = []
+    for v in picks:
+        import aero_engine as ae
+        o = tl.Oracle(bitrate=ae.vfo_bitrate(cfg['vfos'][v]['data_rate']))
+        o.push_chunked(ref.usb(v), ref.info(v)['samples_per_block'])
+        wants.append(o.item_lines('A'))
+    assert len(wants[0]) >= 5
+    decs = []
+    for v in picks:
+        br = str(cfg['vfos'][v]['data_rate'])
+        decs.append(_start_decoder(['-p', 'tcp://127.0.0.1:%d' % port, '-t', 'VFO%02d' % (v + 1), '-b', br,
+                                    '--format', 'jsondump', '-s', STATION, '-v'], {}))
+    try:
+        r = subprocess.run([os.path.join(BIN, 'aero-publish'), '-d',
+                            'driver=file,path=%s,start_delay_ms=1500' % wb, str(ini)],
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-3000:]
+        t0 = time.time()
+        while any(sum(l.startswith('{') for l in d[1]) < len(w) - 4 for d, w in zip(decs, wants)) \
+                and time.time() - t0 < 90:
+            time.sleep(0.2)
+        time.sleep(1.0)
+    finally:
+        for p, _, _ in decs:
+            p.send_signal(signal.SIGTERM)
+        rcs = [p.wait(timeout=120) for p, _, _ in decs]
+    for (p, lines, th), want, rc in zip(decs, wants, rcs):
+        th.join(timeout=10)
+        assert rc == 0, '\n'.join(lines[-10:])
+        console = [l for l in lines if l.startswith('{')]
+        assert console == expected(want, 3)

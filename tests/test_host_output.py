@@ -100,3 +100,52 @@ def test_cli_surface(host_lib):
         assert r.returncode == 0 and 'Some forwarders configuration may be malformed' in r.stderr, bad
     r = _decode('-p', 'tcp://127.0.0.1:1', '-t', 'VFO01', '-b', '600', '-v')
     assert 'No station ID provided, using generated default' in r.stderr and '-AERO-INMARSAT' in r.stderr
+
+
+def _publish(*args):
+    exe = os.path.join(BIN, 'aero-publish')
+    return subprocess.run([exe] + list(args), capture_output=True, text=True, timeout=60)
+
+
+def test_publish_cli_surface(host_lib, tmp_path):
+    """aero-publish's command line and settings checks (publish/main.cpp:17-49,
+    publish/publisher.cpp:55-80), all before the GPU is touched."""
+    r = _publish('--help')
+    assert r.returncode == 0 and '--enable-dcc' in r.stdout and 'settings' in r.stdout
+    r = _publish('x.ini')
+    assert r.returncode == 1 and 'Required device option missing' in r.stderr
+    r = _publish('-d', 'driver=file,path=/dev/null')
+    assert r.returncode == 1 and 'Required settings path missing' in r.stderr
+    r = _publish('-d', 'driver=file,path=/dev/null', str(tmp_path / 'missing.ini'))
+    assert r.returncode == 0 and "doesn't exist or isn't a file" in r.stderr
+    ini = tmp_path / 'bad_rate.ini'
+    ini.write_text('[General]\nsample_rate=250000\n')
+    r = _publish('-d', 'driver=file,path=/dev/null', str(ini))
+    assert r.returncode == 0 and 'Provided sample rate is not supported: 250000' in r.stderr
+    ini.write_text('sample_rate=abc\n')
+    r = _publish('-d', 'driver=file,path=/dev/null', str(ini))
+    assert r.returncode == 0 and "either doesn't exist or isn't an integer" in r.stderr
+    import aero_testlib as tl
+    ini.write_text(tl.c5_ini(tl.c5_config()))
+    r = _publish('-d', 'driver=rtlsdr', str(ini))
+    assert r.returncode == 0 and '[ERROR] failed to find device: driver=rtlsdr' in r.stderr
+
+
+def test_publish_reads_the_ini_like_qsettings(host_lib, tmp_path):
+    """The host's QSettings restatement (host/ini.cpp) on the generated C5
+    INI: every main VFO and [vfos] entry as Publisher::loadSettings reads it
+    (publish/publisher.cpp:115-222), dumped with -v before the device opens."""
+    import re
+    import aero_testlib as tl
+    cfg = tl.c5_config()
+    ini = tmp_path / 'c5.ini'
+    ini.write_text(tl.c5_ini(cfg))
+    r = _publish('-v', '-d', 'driver=none', str(ini))
+    mains = re.findall(r'main (\d+) frequency (-?\d+) out_rate (\d+)', r.stderr)
+    vfos = re.findall(r'vfo (\d+) topic (\S+) frequency (-?\d+) data_rate (\d+) out_rate (\d+) '
+                      r'filter_bandwidth (\d+) gain ([0-9.e+-]+)', r.stderr)
+    assert [(int(f), int(o)) for _, f, o in mains] == [(m['frequency'], m['out_rate']) for m in cfg['mains']]
+    assert len(vfos) == 64
+    for (i, topic, f, dr, orate, fb, g), w in zip(vfos, cfg['vfos']):
+        assert topic == 'VFO%02d' % (int(i) + 1) and int(f) == w['frequency'] and int(dr) == w['data_rate']
+        assert int(orate) == 0 and int(fb) == w.get('filter_bandwidth', 0) and float(g) == w['gain']
