@@ -29,7 +29,8 @@ FP = ['-ffp-contract=off', '-fno-fast-math']
 HIP_FLAGS = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH, '-munsafe-fp-atomics'] + FP
 CXX_FLAGS = ['-O2', '-std=c++17', '-fPIC', '-Wall'] + FP
 
-HIP_SRCS = ['demod_oqpsk.hip', 'demod_msk.hip', 'coarse.hip', 'aerol.hip', 'engine.hip', 'chan.hip', 'burst.hip', 'burst_engine.hip']
+HIP_SRCS = ['demod_oqpsk.hip', 'demod_msk.hip', 'coarse.hip', 'aerol.hip', 'engine.hip', 'chan.hip', 'burst.hip', 'burst_msk.hip',
+            'burst_engine.hip']
 CXX_SRCS = ['tables_host.cpp', 'acars_host.cpp']
 
 

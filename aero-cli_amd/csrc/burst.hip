@@ -32,6 +32,7 @@
 #include "engine_common.h"
 #include "fft_dit.h"
 #include "viterbi_dev.h"
+#include "burst_dev.h"
 
 namespace aero {
 
@@ -42,77 +43,6 @@ constexpr uint32_t BUW = 0xE15AE893u;
 
 __constant__ double c_bsr_b[3];  // st_iir_resonator (burstoqpskdemodulator.cpp:220-227)
 __constant__ double c_bsr_a[3];
-
-__device__ __forceinline__ int b_cis_index(double WTptr) {  // WaveTable::WTCISValue (DSP.cpp:81-88)
-  int tint = (int)WTptr;
-  if (tint >= WTSIZE) tint = 0;
-  if (tint < 0) tint = WTSIZE - 1;
-  return tint;
-}
-
-__device__ __forceinline__ void b_nco_next(double &ptr, double &step) {  // WTnextFrame (DSP.cpp:71-79)
-  if (step < 0) step = 0;
-  ptr += step;
-  while (((int)ptr) >= WTSIZE) ptr -= WTSIZE;
-}
-
-__device__ __forceinline__ void b_set_freq(double &freq, double &step, double f) {  // SetFreq (DSP.cpp:163-168)
-  freq = f;
-  if (freq < 0) freq = 0;
-  step = (freq) * ((double)WTSIZE) / 48000.0;
-}
-
-__device__ __forceinline__ void b_set_phase_deg(double &ptr, double phase_deg) {  // SetPhaseDeg (DSP.cpp:177-187)
-  phase_deg = fmod(phase_deg, 360.0);
-  while (phase_deg < 0) phase_deg += 360.0;
-  ptr = (phase_deg / 360.0) * ((double)WTSIZE);
-}
-
-__device__ __forceinline__ void b_advance(double &ptr, double frac) {  // AdvanceFractionOfWave (DSP.h:59-65)
-  ptr += frac * WTSIZE;
-  while (ptr >= WTSIZE) ptr -= WTSIZE;
-  while (ptr < 0) ptr += WTSIZE;
-}
-
-__device__ __forceinline__ int b_qround(double d) {  // qRound (Qt 5.9 qglobal.h:525)
-  return d >= 0.0 ? int(d + 0.5) : int(d - double(int(d - 1)) + 0.5) + int(d - 1);
-}
-
-// std::exp(complex(0 * y, y)) as glibc's cexp returns it: (cos y, sin y), or
-// (1, y) when |y| <= DBL_MIN
-__device__ __forceinline__ void b_cexp_i(double y, double &c, double &s) {
-  if (fabs(y) > 2.2250738585072014e-308) {
-    aero_sincos(y, s, c);
-  } else {
-    s = y;
-    c = 1.0;
-  }
-}
-
-// Delay<T>::update (DSP.h:365-384) on a time-major ring with per-pointer weights
-struct DlyRef {
-  const double *w, *omw;
-  const int *io;
-  int size;
-};
-__device__ __forceinline__ double dly_update(double *ring, int C, int &p, const DlyRef &d, double sig) {
-  ring[(size_t)p * C] = sig;
-  const int io = d.io[p], in = io + 1 == d.size ? 0 : io + 1;
-  const double older = ring[(size_t)io * C], newer = ring[(size_t)in * C];
-  const double w = d.w[p], om = d.omw[p];
-  p = p + 1 == d.size ? 0 : p + 1;
-  return (w * newer + om * older);
-}
-__device__ __forceinline__ double2 dly_update2(double2 *ring, int C, int &p, const DlyRef &d, double2 sig) {
-  ring[(size_t)p * C] = sig;
-  const int io = d.io[p], in = io + 1 == d.size ? 0 : io + 1;
-  const double2 older = ring[(size_t)io * C], newer = ring[(size_t)in * C];
-  const double w = d.w[p], om = d.omw[p];
-  p = p + 1 == d.size ? 0 : p + 1;
-  return make_double2(w * newer.x + om * older.x, w * newer.y + om * older.y);
-}
-
-__device__ __forceinline__ DlyRef dref(const BurstTables &T, int k) { return {T.dw[k], T.domw[k], T.dio[k], T.dsize[k]}; }
 
 }  // namespace
 
@@ -243,11 +173,11 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   int tri_ptr = is[BI_TRI_PTR * C], msema_p = is[BI_MSEMA_P * C];
   int startstop = is[BI_STARTSTOP * C], cntr = is[BI_CNTR * C], insertpre = is[BI_INSERTPRE * C];
   int yui = is[BI_YUI * C];
+  int hop_n = S.hop_n[c];
   long long sp = ls[BL_SP * C], scommit = ls[BL_SCOMMIT * C];
   const long long scons = ls[BL_SCONS * C];
   long long chunk_h = ls[BL_CHUNK_H * C];
   const long long chunk_n = ls[BL_CHUNK_N * C];
-  int hop_n = is[BI_HOP_N * C];
 #pragma unroll 1
   for (int j = 0; j < NTAPS; ++j) {
     s_qre[j][col] = S.fir[(size_t)j * C + c];
@@ -647,7 +577,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   is[BI_INSERTPRE * C] = insertpre;
   is[BI_YUI * C] = yui;
   is[BI_PEND * C] = pend;
-  is[BI_HOP_N * C] = hop_n;
+  S.hop_n[c] = hop_n;
   ls[BL_NSAMP * C] = n;
   ls[BL_SP * C] = sp;
   ls[BL_SCOMMIT * C] = scommit;
@@ -902,8 +832,11 @@ __global__ __launch_bounds__(256) void frame_burst_kernel(BurstState S, int nch)
   is[BI_SKIP_GROUP * C] = skip;
 }
 
-// one wave per R/T test: del[j*64 + i] = block[((i*27) % 64) * cols + j],
-// Decode_soft over blockptr soft values, decoded bits MSB-first
+// one wave per R/T test: del[j*64 + i] = block[((i*27) % 64) * cols + j]
+// (OQPSK, AeroLInterleaver::deinterleave_ba, decode/aerol.cpp:594-613), or
+// for MSK jobs (w = 1) a 64 x 5 section then 64 x 3 sections
+// (deinterleaveMSK_ba, decode/aerol.cpp:651-686); Decode_soft over blockptr
+// soft values, decoded bits MSB-first
 __global__ __launch_bounds__(64) void rt_viterbi_kernel(BurstState S) {
   __shared__ uint8_t sbuf[RT_BLOCK];
   __shared__ unsigned long long hist[HCAP];
@@ -915,9 +848,21 @@ __global__ __launch_bounds__(64) void rt_viterbi_kernel(BurstState S) {
     const int4 jd = reinterpret_cast<const int4 *>(S.jobs)[job];
     const int c = jd.x, bp = jd.y, cols = bp / 64;
     const uint8_t *blk = S.rtblock + (size_t)c * RT_BLOCK;
-    for (int k = lane; k < bp; k += 64) {
-      const int j = k / 64, i = k % 64;
-      sbuf[k] = blk[((i * 27) % 64) * cols + j];
+    if (!jd.w) {
+      for (int k = lane; k < bp; k += 64) {
+        const int j = k / 64, i = k % 64;
+        sbuf[k] = blk[((i * 27) % 64) * cols + j];
+      }
+    } else {
+      for (int k = lane; k < bp; k += 64) {
+        const int j = k / 64, i = k % 64;
+        if (k < 320) {
+          sbuf[k] = blk[((i * 27) % 64) * 5 + j];
+        } else {
+          const int sec = (k - 320) / 192, jj = ((k - 320) % 192) / 64;
+          sbuf[k] = blk[64 * (5 + 3 * sec) + ((i * 27) % 64) * 3 + jj];
+        }
+      }
     }
     for (int k = lane; k < RT_BLOCK / 2 + 64; k += 64) obits[k] = 0;
     __syncthreads();

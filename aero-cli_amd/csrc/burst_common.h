@@ -1,10 +1,13 @@
 /*
- * burst_common.h — layout shared by the burst-mode 10500-bps OQPSK kernels
- * (burst.hip) and the engine host (engine.hip).  Geometry from
- * BurstOqpskDemodulator's constructor and setSettings
- * (decode/burstoqpskdemodulator.cpp:5-232) at Fs 48000, fb 10500
- * (SamplesPerSymbol = 9.142857), and AeroL's burst R/T block
- * (decode/aerol.h:755-836).
+ * burst_common.h — layout shared by the burst-mode kernels (burst.hip:
+ * 10500-bps OQPSK, burst_msk.hip: 600/1200-bps MSK) and their host
+ * (burst_engine.hip).  OQPSK geometry from BurstOqpskDemodulator's constructor
+ * and setSettings (decode/burstoqpskdemodulator.cpp:5-232) at Fs 48000,
+ * fb 10500 (SamplesPerSymbol = 9.142857); MSK geometry from
+ * BurstMskDemodulator::setSettings (decode/burstmskdemodulator.cpp:119-297) at
+ * Fs 48000, fb 1200 (SamplesPerSymbol = 40, the fb >= 1200 branch, which
+ * aero-decode uses for both MSK bit rates, decode/decode.cpp:123-132); AeroL's
+ * R/T block (decode/aerol.h:614-836).
  */
 #pragma once
 #include <stdint.h>
@@ -66,9 +69,52 @@ enum BIS : int {
   // AeroL burst framing
   BI_RI, BI_MUW, BI_FCNTR, BI_GSL, BI_UWI, BI_UWR, BI_UWI_INV, BI_UWR_INV, BI_DATACD, BI_BLOCKPTR, BI_BURST_ID,
   BI_SKIP_GROUP,
-  BI_HOP_N,
   BI_COUNT
 };
+
+// ---- burst MSK (burst_msk.hip)
+constexpr int M_NT = 80;           // matched filter taps, 2 * SPS (:142-149)
+constexpr int M_D1 = 11581;        // d1.setLength(289 * SPS + 20) + 1
+constexpr int M_D2 = 7681;         // d2.setLength((72 + 120) * SPS) + 1
+constexpr int M_TRI = 8000;        // tridentbuffer_sz = qRound(200 * SPS)
+constexpr int M_TRI_BASE = 5040;   // qRound(126 * SPS): start tone window
+constexpr int M_TRI_TOP = 2960;    // qRound(74 * SPS): 0-1 preamble window
+constexpr int M_MA = 5040;         // bt_ma1 (complex) and mav1: 126 * SPS
+constexpr int M_MADIFF = 5041;     // bt_ma_diff.setdelay(126 * SPS): ceil + 1 slots
+constexpr int M_BTD = 41;          // bt_d1.setdelay(SPS) (complex)
+constexpr int M_A1 = 21, M_D8 = 21;  // a1 / delayt8 .setdelay(SPS / 2)
+constexpr int M_DSM = 41;          // delayedsmpl.setLength(SPS)
+constexpr int M_PD1 = 5041, M_PD2 = 2521, M_PD3 = 5041;  // PeakDetector(2520, 0.1)
+constexpr int M_PD_MAXCD = 5040;
+constexpr int M_AGC2 = 5120;       // AGC(SPS * 128 / Fs, Fs)
+constexpr int M_MSEMA = 75;
+constexpr int M_STARTSTOP = 20000; // SPS * 500
+constexpr int M_SOFT_GROUP = 12;   // RxDataBits emitted at >= 12 entries (:689-692)
+
+enum BMDS : int {
+  BM_M2_PTR, BM_M2_STEP, BM_M2_FREQ,
+  BM_SO_PTR, BM_SO_LAST, BM_SO_STEP, BM_SH_PTR, BM_SH_STEP,
+  BM_AGC_SUM, BM_AGC2_SUM, BM_MA1_RE, BM_MA1_IM, BM_MAV1_SUM,
+  BM_PD_LASTDY, BM_VOL_GAIN,
+  BM_SR_X1, BM_SR_X2, BM_SR_Y1, BM_SR_Y2,
+  BM_AVE_RE, BM_AVE_IM, BM_ROT_RE, BM_ROT_IM, BM_STR_RE, BM_STR_IM, BM_ROTF,
+  BM_MSE, BM_MSEMA_SUM, BM_DIFF_LAST,
+  BM_RESUME_VAL,
+  BM_TRI_MINVAL, BM_TRI_BRE, BM_TRI_BIM,
+  BM_COUNT
+};
+enum BMIS : int {
+  BMI_AGC_P, BMI_AGC2_P, BMI_D1_P, BMI_D2_P, BMI_MA1_P, BMI_MAV1_P, BMI_MADIFF_P, BMI_BTD_P, BMI_A1_P, BMI_D8_P,
+  BMI_DSM_P, BMI_PD1_P, BMI_PD2_P, BMI_PD3_P, BMI_PD_CNTDOWN, BMI_PD_MAXPOSCD,
+  BMI_TRI_PTR, BMI_MSEMA_P, BMI_STARTSTOP, BMI_CNTR,
+  BMI_PEND,  // 0 running, 1 trident check requested, 2 trident spectra ready
+  BMI_TRI_MINBIN, BMI_TRI_TOPLO, BMI_TRI_TOPHI,
+  // AeroL MSK burst framing
+  BMI_MUW, BMI_FCNTR, BMI_UW, BMI_UW_INV, BMI_BLOCKPTR, BMI_BURST_ID, BMI_SKIP_GROUP, BMI_TOTAL,
+  BMI_COUNT
+};
+constexpr int BURST_DS_COUNT = BD_COUNT > BM_COUNT ? BD_COUNT : BM_COUNT;
+constexpr int BURST_IS_COUNT = BI_COUNT > BMI_COUNT ? BI_COUNT : BMI_COUNT;
 
 // 64-bit counters
 enum BLS : int {
@@ -85,10 +131,11 @@ enum BLS : int {
 
 struct BurstState {
   int C;
+  int *hop_n;       // [C] trident records written this pass
   double *ds;
   int *is;
   long long *ls;
-  double *fir;      // [2 * 55][C] transposed RRC partial sums
+  double *fir;      // [2 * 55][C] transposed RRC partial sums (MSK: [2 * 80][C] matched filter)
   double2 *ana;     // [ANA_LEN][C] analytic signal
   int16_t *pcm;     // [pcm_cap][C]
   long long pcm_cap;
@@ -98,7 +145,8 @@ struct BurstState {
   double *d2;                   // [B_D2][C]
   double2 *ma1;                 // [B_MA][C]
   double *mav1;                 // [B_MA][C]
-  double *dl[BDL_COUNT];        // Delay rings [size][C] (BDL_BT holds double2)
+  double *dl[BDL_COUNT];        // Delay rings [size][C] (BDL_BT holds double2); MSK: bt_d1 (double2),
+                                // bt_ma_diff, a1, delayt8, delayedsmpl (double2) in slots 0-4
   double *pd1, *pd2, *pd3;      // [len][C]
   double *tri;                  // [C][B_TRI]
   double *msema;                // [C][B_MSEMA]

@@ -1,0 +1,112 @@
+/*
+ * burst_dev.h — device helpers shared by the burst kernels (burst.hip,
+ * burst_msk.hip): WaveTable operations (decode/DSP.cpp:35-262, DSP.h:59-65),
+ * qRound, glibc cexp of a pure imaginary argument and Delay<T>::update
+ * (DSP.h:365-384) on time-major rings.
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "aero_math.h"
+#include "burst_common.h"
+#include "engine_common.h"
+
+namespace aero {
+namespace {
+
+__device__ __forceinline__ int b_cis_index(double WTptr) {  // WaveTable::WTCISValue (DSP.cpp:81-88)
+  int tint = (int)WTptr;
+  if (tint >= WTSIZE) tint = 0;
+  if (tint < 0) tint = WTSIZE - 1;
+  return tint;
+}
+
+__device__ __forceinline__ void b_nco_next(double &ptr, double &step) {  // WTnextFrame (DSP.cpp:71-79)
+  if (step < 0) step = 0;
+  ptr += step;
+  while (((int)ptr) >= WTSIZE) ptr -= WTSIZE;
+}
+
+__device__ __forceinline__ void b_set_freq(double &freq, double &step, double f) {  // SetFreq (DSP.cpp:163-168)
+  freq = f;
+  if (freq < 0) freq = 0;
+  step = (freq) * ((double)WTSIZE) / 48000.0;
+}
+
+__device__ __forceinline__ void b_set_phase_deg(double &ptr, double phase_deg) {  // SetPhaseDeg (DSP.cpp:177-187)
+  phase_deg = fmod(phase_deg, 360.0);
+  while (phase_deg < 0) phase_deg += 360.0;
+  ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+}
+
+__device__ __forceinline__ void b_advance(double &ptr, double frac) {  // AdvanceFractionOfWave (DSP.h:59-65)
+  ptr += frac * WTSIZE;
+  while (ptr >= WTSIZE) ptr -= WTSIZE;
+  while (ptr < 0) ptr += WTSIZE;
+}
+
+__device__ __forceinline__ int b_qround(double d) {  // qRound (Qt 5.9 qglobal.h:525)
+  return d >= 0.0 ? int(d + 0.5) : int(d - double(int(d - 1)) + 0.5) + int(d - 1);
+}
+
+// std::exp(complex(0 * y, y)) as glibc's cexp returns it: (cos y, sin y), or
+// (1, y) when |y| <= DBL_MIN
+__device__ __forceinline__ void b_cexp_i(double y, double &c, double &s) {
+  if (fabs(y) > 2.2250738585072014e-308) {
+    aero_sincos(y, s, c);
+  } else {
+    s = y;
+    c = 1.0;
+  }
+}
+
+// Delay<T>::update (DSP.h:365-384) on a time-major ring with per-pointer weights
+struct DlyRef {
+  const double *w, *omw;
+  const int *io;
+  int size;
+};
+__device__ __forceinline__ double dly_update(double *ring, int C, int &p, const DlyRef &d, double sig) {
+  ring[(size_t)p * C] = sig;
+  const int io = d.io[p], in = io + 1 == d.size ? 0 : io + 1;
+  const double older = ring[(size_t)io * C], newer = ring[(size_t)in * C];
+  const double w = d.w[p], om = d.omw[p];
+  p = p + 1 == d.size ? 0 : p + 1;
+  return (w * newer + om * older);
+}
+__device__ __forceinline__ double2 dly_update2(double2 *ring, int C, int &p, const DlyRef &d, double2 sig) {
+  ring[(size_t)p * C] = sig;
+  const int io = d.io[p], in = io + 1 == d.size ? 0 : io + 1;
+  const double2 older = ring[(size_t)io * C], newer = ring[(size_t)in * C];
+  const double w = d.w[p], om = d.omw[p];
+  p = p + 1 == d.size ? 0 : p + 1;
+  return make_double2(w * newer.x + om * older.x, w * newer.y + om * older.y);
+}
+
+__device__ __forceinline__ DlyRef dref(const BurstTables &T, int k) { return {T.dw[k], T.domw[k], T.dio[k], T.dsize[k]}; }
+
+
+// Delay<T>::update with an integer delay D on a ring of D + 1 slots: the
+// weighting is exactly 0, and the reference's sum is kept literally
+// (0 * newer + 1 * older) so signed zeros come out the same
+__device__ __forceinline__ double dly_int(double *ring, int C, int &p, int size, int D, double sig) {
+  ring[(size_t)p * C] = sig;
+  int io = p - D;
+  if (io < 0) io += size;
+  const int in = io + 1 == size ? 0 : io + 1;
+  const double older = ring[(size_t)io * C], newer = ring[(size_t)in * C];
+  p = p + 1 == size ? 0 : p + 1;
+  return (0.0 * newer + (1.0 - 0.0) * older);
+}
+__device__ __forceinline__ double2 dly_int2(double2 *ring, int C, int &p, int size, int D, double2 sig) {
+  ring[(size_t)p * C] = sig;
+  int io = p - D;
+  if (io < 0) io += size;
+  const int in = io + 1 == size ? 0 : io + 1;
+  const double2 older = ring[(size_t)io * C], newer = ring[(size_t)in * C];
+  p = p + 1 == size ? 0 : p + 1;
+  return make_double2(0.0 * newer.x + (1.0 - 0.0) * older.x, 0.0 * newer.y + (1.0 - 0.0) * older.y);
+}
+
+}  // namespace
+}  // namespace aero

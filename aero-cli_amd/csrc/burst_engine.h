@@ -10,9 +10,10 @@
 namespace aero {
 
 struct BurstGroup;
-int burst_group_create(int device, int flags, int max_channels, BurstGroup **out);
+enum BurstKind { BURST_OQPSK = 0, BURST_MSK = 1 };  // 10500 OQPSK / 600-1200 MSK (both bit rates in one group)
+int burst_group_create(int device, int flags, int max_channels, int kind, BurstGroup **out);
 void burst_group_destroy(BurstGroup *g);
-int burst_open(BurstGroup *g, bool disable_reassembly, int *local);
+int burst_open(BurstGroup *g, int bitrate, bool disable_reassembly, int *local);
 int burst_push(BurstGroup *g, int c, const int16_t *pcm, size_t n, bool dev, bool msg_start);
 int burst_push_batch(BurstGroup *g, const int16_t *src, size_t n, size_t ld, int nch, bool dev);
 int burst_run(BurstGroup *g, int flush);

@@ -1,14 +1,16 @@
 /*
- * burst_engine.hip — host side of the burst-mode 10500-bps OQPSK group
- * (aero-decode --burst, decode/decode.cpp:131-136, 175): device layout and
- * initial state (BurstOqpskDemodulator ctor + setSettings,
- * decode/burstoqpskdemodulator.cpp:5-232; AeroL::setSettings(10500, burst),
- * decode/aerol.cpp:960-1039), one message per push (the lastmse gate makes
- * burst output depend on message boundaries, burstoqpskdemodulator.cpp:264,
- * 685), the pass loop over the kernels of burst.hip, and the R/T test results:
- * descrambling, CRC checks and packet handling of
- * RTChannelDeleaveFECScram::test (decode/aerol.h:755-836) and the R/T branch
- * of AeroL::Decode (decode/aerol.cpp:1240-1460).
+ * burst_engine.hip — host side of the burst-mode groups (aero-decode --burst,
+ * decode/decode.cpp:123-140, 171-212): one group of 10500-bps OQPSK channels
+ * and one of 600/1200-bps MSK channels.  Device layout and initial state
+ * (BurstOqpskDemodulator ctor + setSettings, decode/burstoqpskdemodulator.cpp:5-232;
+ * BurstMskDemodulator ctor + setSettings, decode/burstmskdemodulator.cpp:9-297;
+ * AeroL::setSettings(fb, burst), decode/aerol.cpp:960-1039), one message per
+ * push (the OQPSK lastmse gate makes its output depend on message boundaries,
+ * burstoqpskdemodulator.cpp:264, 685), the pass loop over the kernels of
+ * burst.hip / burst_msk.hip, and the R/T test results: descrambling, CRC
+ * checks and packet handling of RTChannelDeleaveFECScram::update / updateMSK
+ * (decode/aerol.h:614-836) and the R/T branch of AeroL::Decode
+ * (decode/aerol.cpp:1240-1460).
  */
 #include <hip/hip_runtime.h>
 
@@ -37,6 +39,10 @@ void launch_demod_burst(hipStream_t st, const BurstState &S, const BurstTables &
 void launch_trident(hipStream_t st, const BurstState &S, const BurstTables &T, int nch);
 void launch_frame_burst(hipStream_t st, const BurstState &S, int nch);
 void launch_rt_viterbi(hipStream_t st, const BurstState &S, int max_jobs);
+void burst_msk_upload_constants(const double *sr_b, const double *sr_a, const double *taps);
+void launch_demod_bmsk(hipStream_t st, const BurstState &S, const BurstTables &T, int nch, int max_n, int trace);
+void launch_trident_bmsk(hipStream_t st, const BurstState &S, const BurstTables &T, int nch);
+void launch_frame_bmsk(hipStream_t st, const BurstState &S, int nch);
 
 namespace {
 
@@ -130,7 +136,8 @@ std::vector<uint8_t> pack_bits(const std::vector<int> &bits) {
 }  // namespace
 
 struct BurstGroup {
-  int device = 0, flags = 0, C = 0, nch = 0;
+  int device = 0, flags = 0, C = 0, nch = 0, kind = BURST_OQPSK;
+  std::vector<int> tsu, tblocks;  // MSK: updateMSK's targetSUSize / targetBlocks per channel
   hipStream_t st = nullptr;
   BurstState S{};
   BurstTables T{};
@@ -158,30 +165,37 @@ struct BurstGroup {
 
 namespace {
 
-size_t burst_layout(BurstState &S, BurstTables &T, int C, char *base, double2 **hk_out) {
+size_t burst_layout(int kind, BurstState &S, BurstTables &T, int C, char *base, double2 **hk_out) {
+  const bool msk = kind == BURST_MSK;
   char *p = base;
   S.C = C;
-  S.ds = carve<double>(p, (size_t)BD_COUNT * C);
-  S.is = carve<int>(p, (size_t)BI_COUNT * C);
+  S.hop_n = carve<int>(p, (size_t)C);
+  S.ds = carve<double>(p, (size_t)BURST_DS_COUNT * C);
+  S.is = carve<int>(p, (size_t)BURST_IS_COUNT * C);
   S.ls = carve<long long>(p, (size_t)BL_COUNT * C);
-  S.fir = carve<double>(p, (size_t)2 * NTAPS * C);
+  S.fir = carve<double>(p, (size_t)2 * (msk ? M_NT : NTAPS) * C);
   S.ana = carve<double2>(p, (size_t)ANA_LEN * C);
   S.pcm = carve<int16_t>(p, (size_t)B_PCM_CAP * C);
   S.pcm_cap = B_PCM_CAP;
   S.hb_rem = carve<double2>(p, (size_t)HB_REM * C);
   S.agc = carve<double>(p, (size_t)B_AGC * C);
-  S.agc2 = carve<double>(p, (size_t)B_AGC2 * C);
-  S.d1 = carve<double2>(p, (size_t)B_D1 * C);
-  S.d2 = carve<double>(p, (size_t)B_D2 * C);
-  S.ma1 = carve<double2>(p, (size_t)B_MA * C);
-  S.mav1 = carve<double>(p, (size_t)B_MA * C);
-  for (int k = 0; k < BDL_COUNT; k++)  // sizes <= 1172 (bt_ma_diff); BDL_BT holds double2
-    S.dl[k] = carve<double>(p, (size_t)(k == BDL_BT ? 2 : 1) * 1172 * C);
-  S.pd1 = carve<double>(p, (size_t)B_PD1 * C);
-  S.pd2 = carve<double>(p, (size_t)B_PD2 * C);
-  S.pd3 = carve<double>(p, (size_t)B_PD3 * C);
-  S.tri = carve<double>(p, (size_t)B_TRI * C);
-  S.msema = carve<double>(p, (size_t)B_MSEMA * C);
+  S.agc2 = carve<double>(p, (size_t)(msk ? M_AGC2 : B_AGC2) * C);
+  S.d1 = carve<double2>(p, (size_t)(msk ? M_D1 : B_D1) * C);
+  S.d2 = carve<double>(p, (size_t)(msk ? M_D2 : B_D2) * C);
+  S.ma1 = carve<double2>(p, (size_t)(msk ? M_MA : B_MA) * C);
+  S.mav1 = carve<double>(p, (size_t)(msk ? M_MA : B_MA) * C);
+  if (msk) {  // bt_d1 (complex), bt_ma_diff, a1, delayt8, delayedsmpl (complex)
+    const int sz[5] = {2 * M_BTD, M_MADIFF, M_A1, M_D8, 2 * M_DSM};
+    for (int k = 0; k < 5; k++) S.dl[k] = carve<double>(p, (size_t)sz[k] * C);
+  } else {
+    for (int k = 0; k < BDL_COUNT; k++)  // sizes <= 1172 (bt_ma_diff); BDL_BT holds double2
+      S.dl[k] = carve<double>(p, (size_t)(k == BDL_BT ? 2 : 1) * 1172 * C);
+  }
+  S.pd1 = carve<double>(p, (size_t)(msk ? M_PD1 : B_PD1) * C);
+  S.pd2 = carve<double>(p, (size_t)(msk ? M_PD2 : B_PD2) * C);
+  S.pd3 = carve<double>(p, (size_t)(msk ? M_PD3 : B_PD3) * C);
+  S.tri = carve<double>(p, (size_t)(msk ? M_TRI : B_TRI) * C);
+  S.msema = carve<double>(p, (size_t)(msk ? M_MSEMA : B_MSEMA) * C);
   S.chunks = carve<long long>(p, (size_t)CHUNK_RING * C);
   S.soft = carve<int16_t>(p, (size_t)B_SOFT_RING * C);
   S.hop_cap = B_HOP_CAP;
@@ -190,7 +204,7 @@ size_t burst_layout(BurstState &S, BurstTables &T, int C, char *base, double2 **
   S.jobs = carve<int>(p, (size_t)4 * RT_TESTS_PER_PASS * C);
   S.njobs = carve<int>(p, 16);
   S.jobout = carve<uint8_t>(p, (size_t)RT_JOB_OUT * RT_TESTS_PER_PASS * C);
-  S.tri_abs = carve<double>(p, (size_t)TRI_N * C);
+  S.tri_abs = carve<double>(p, (size_t)(msk ? 1 : TRI_N) * C);
   T.cis = carve<double2>(p, WTSIZE);
   T.tw8 = carve<double2>(p, 8192);
   T.twi8 = carve<double2>(p, 8192);
@@ -201,7 +215,7 @@ size_t burst_layout(BurstState &S, BurstTables &T, int C, char *base, double2 **
   T.hk_time = carve<double2>(p, HB_N);
   T.da = carve<double2>(p, TRI_N);
   T.db = carve<double2>(p, TRI_N);
-  T.taps = carve<double>(p, 64);
+  T.taps = carve<double>(p, 128);
   for (int k = 0; k < BDL_COUNT; k++) {
     T.dw[k] = carve<double>(p, 1172);
     T.domw[k] = carve<double>(p, 1172);
@@ -249,13 +263,22 @@ void collect_timing(BurstGroup *g) {
 int run_once(BurstGroup *g, bool trace, bool &progress) {
   const int nch = g->nch;
   progress = false;
+  const bool msk = g->kind == BURST_MSK;
   timed(g, "burst_hilbert", [&] { launch_hilbert(g->st, g->S, g->T, nch); });
   for (int r = 0; r < DEMOD_ROUNDS; r++) {
-    timed(g, "burst_demod", [&] { launch_demod_burst(g->st, g->S, g->T, nch, (int)B_PCM_CAP, trace ? 1 : 0); });
-    timed(g, "burst_trident", [&] { launch_trident(g->st, g->S, g->T, nch); });
+    if (msk) {
+      timed(g, "burst_demod", [&] { launch_demod_bmsk(g->st, g->S, g->T, nch, (int)B_PCM_CAP, trace ? 1 : 0); });
+      timed(g, "burst_trident", [&] { launch_trident_bmsk(g->st, g->S, g->T, nch); });
+    } else {
+      timed(g, "burst_demod", [&] { launch_demod_burst(g->st, g->S, g->T, nch, (int)B_PCM_CAP, trace ? 1 : 0); });
+      timed(g, "burst_trident", [&] { launch_trident(g->st, g->S, g->T, nch); });
+    }
   }
   BCHK(hipMemsetAsync(g->S.njobs, 0, sizeof(int), g->st));
-  timed(g, "burst_frame", [&] { launch_frame_burst(g->st, g->S, nch); });
+  if (msk)
+    timed(g, "burst_frame", [&] { launch_frame_bmsk(g->st, g->S, nch); });
+  else
+    timed(g, "burst_frame", [&] { launch_frame_burst(g->st, g->S, nch); });
   timed(g, "burst_viterbi", [&] { launch_rt_viterbi(g->st, g->S, nch * RT_TESTS_PER_PASS); });
   BCHK(hipGetLastError());
   int njobs = 0;
@@ -276,10 +299,43 @@ int run_once(BurstGroup *g, bool trace, bool &progress) {
     if (c < 0 || c >= nch || burst == g->ok_burst[c]) continue;  // packet already decoded: the block is FULL
     deconvol.assign(nbits, 0);
     for (int b = 0; b < nbits; b++) deconvol[b] = ((rec[16 + b / 8] >> (7 - (b % 8))) & 1) ^ g->scr[b];
-    enum { OK_R = 3, OK_T = 5, Bad = 0, Test_Failed = 32 };
+    enum { OK_R = 3, OK_T = 5, Bad = 0, Test_Failed = 32, Nothing = 8 };
     int result, nsus = 0;
     std::vector<uint8_t> info;
-    if (bp == 64 * 5) {
+    if (msk) {
+      // RTChannelDeleaveFECScram::updateMSK (decode/aerol.h:614-753): only
+      // blocks 5, 11, 50 and the target block are tests
+      const int blocks = bp / 64;
+      int &tsu = g->tsu[c], &tb = g->tblocks[c];
+      if (!(blocks == 5 || blocks == tb || blocks == 11 || blocks == 50)) continue;
+      if (bp == 64 * 5) {
+        tsu = 0;
+        tb = 0;
+        if (crc_bits_check(deconvol.data(), 8 * 19)) {
+          info = pack_bits(deconvol);
+          result = OK_R;
+        } else {
+          result = Nothing;
+        }
+      } else if (!crc_bits_check(deconvol.data(), 8 * 6)) {
+        result = Bad;
+      } else if (blocks == 11) {  // peek at the SU after the first for the SU count
+        const int *isu = deconvol.data() + (8 * 6) + (8 * 12) * 1;
+        int bin = 2;
+        bin += ((isu[0] * 1) + (isu[1] * 2) + (isu[2] * 4) + (isu[3] * 8) + (isu[4] * 16) + (isu[5] * 32));
+        tsu = bin;
+        if (tsu >= 16) tsu = tsu / 2 + 1;
+        tb = ((tsu + 1) * 3) + 2;
+        result = Nothing;
+      } else if (blocks == tb) {  // `ok <= targetSUSize` always holds
+        info = pack_bits(deconvol);
+        if (!info.empty()) info.pop_back();  // infofield.chop(1)
+        nsus = tsu;
+        result = OK_T;
+      } else {
+        result = Nothing;
+      }
+    } else if (bp == 64 * 5) {
       if (!crc_bits_check(deconvol.data(), 8 * 19)) {
         result = Test_Failed;
       } else {
@@ -337,7 +393,7 @@ int run_once(BurstGroup *g, bool trace, bool &progress) {
   }
   if (g->flags & AERO_F_TRACE_HOPS) {  // trident records of this pass, then the counters restart
     std::vector<int> hn(nch);
-    BCHK(hipMemcpy(hn.data(), g->S.is + (size_t)BI_HOP_N * g->C, sizeof(int) * nch, hipMemcpyDeviceToHost));
+    BCHK(hipMemcpy(hn.data(), g->S.hop_n, sizeof(int) * nch, hipMemcpyDeviceToHost));
     std::vector<double> hops;
     for (int c = 0; c < nch; c++) {
       if (hn[c] <= 0) continue;
@@ -349,7 +405,7 @@ int run_once(BurstGroup *g, bool trace, bool &progress) {
       g->hop_hold[c].insert(g->hop_hold[c].end(), hops.begin() + (size_t)c * B_HOP_CAP * 6,
                             hops.begin() + ((size_t)c * B_HOP_CAP + hn[c]) * 6);
     }
-    BCHK(hipMemset(g->S.is + (size_t)BI_HOP_N * g->C, 0, sizeof(int) * nch));
+    BCHK(hipMemset(g->S.hop_n, 0, sizeof(int) * nch));
   }
   // more passes while any channel has samples or committed soft bits left
   long long work = 0;
@@ -364,29 +420,34 @@ int run_once(BurstGroup *g, bool trace, bool &progress) {
 
 }  // namespace
 
-int burst_group_create(int device, int flags, int max_channels, BurstGroup **out) {
+int burst_group_create(int device, int flags, int max_channels, int kind, BurstGroup **out) {
   // every early return below releases what was already allocated
   std::unique_ptr<BurstGroup, void (*)(BurstGroup *)> g(new BurstGroup(), burst_group_destroy);
   g->device = device;
   g->flags = flags;
+  g->kind = kind;
+  const bool msk = kind == BURST_MSK;
   g->C = (max_channels + 63) & ~63;
   BurstState S{};
   BurstTables T{};
-  const size_t bytes = burst_layout(S, T, g->C, nullptr, nullptr) + 4096;
+  const size_t bytes = burst_layout(kind, S, T, g->C, nullptr, nullptr) + 4096;
   if (hipMalloc(&g->pool, bytes) != hipSuccess) return AERO_E_NOMEM;
   BCHK(hipMemset(g->pool, 0, bytes));
   double2 *hk = nullptr;
-  burst_layout(g->S, g->T, g->C, reinterpret_cast<char *>(g->pool), &hk);
+  burst_layout(kind, g->S, g->T, g->C, reinterpret_cast<char *>(g->pool), &hk);
   BCHK(hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking));
   // tables (host glibc, g++-compiled: tables_host.cpp)
   std::vector<double> cis(2 * WTSIZE), tw8(2 * 8192), twi8(2 * 8192), tw16(2 * 16384), twi16(2 * 16384);
   host_cis(cis.data());
   host_twiddles(8192, tw8.data(), twi8.data());
   host_twiddles(16384, tw16.data(), twi16.data());
-  std::vector<double> hk_time(2 * HB_N), da(2 * TRI_N), db(2 * TRI_N), taps(64, 0.0);
+  std::vector<double> hk_time(2 * HB_N), da(2 * TRI_N), db(2 * TRI_N), taps(128, 0.0);
   host_hilbert_kernel(hk_time.data());
   host_fftr_split(TRI_N, da.data(), db.data());
-  if (host_rrc(1.0, 55, 48000, 10500 / 2.0, taps.data()) != NTAPS) return AERO_E_INVALID;
+  if (msk)
+    host_msk_taps(40, taps.data());  // matched filter, SamplesPerSymbol 40 (burstmskdemodulator.cpp:142-149)
+  else if (host_rrc(1.0, 55, 48000, 10500 / 2.0, taps.data()) != NTAPS)
+    return AERO_E_INVALID;
   if (int rc = h2d((const double *)g->T.cis, cis)) return rc;
   if (int rc = h2d((const double *)g->T.tw8, tw8)) return rc;
   if (int rc = h2d((const double *)g->T.twi8, twi8)) return rc;
@@ -395,11 +456,12 @@ int burst_group_create(int device, int flags, int max_channels, BurstGroup **out
   if (int rc = h2d((const double *)g->T.da, da)) return rc;
   if (int rc = h2d((const double *)g->T.db, db)) return rc;
   if (int rc = h2d(g->T.taps, taps)) return rc;
-  // Delay<> instances (burstoqpskdemodulator.cpp:186-196, 213-216)
+  // Delay<> instances (burstoqpskdemodulator.cpp:186-196, 213-216); the MSK
+  // group's delays are whole samples (burst_dev.h dly_int)
   const double fds[BDL_COUNT] = {1.0, (2.0 * 48000.0 / 10500.0) / 4.0, (2.0 * 48000.0 / 10500.0) / 4.0,
                                  (2.0 * 48000.0 / 10500.0) / 8.0, (2.0 * 48000.0 / 10500.0) / 2.0,
                                  1.0 * (2.0 * 48000.0 / 10500.0), (2.0 * 48000.0 / 10500.0) * 128};
-  for (int k = 0; k < BDL_COUNT; k++) {
+  for (int k = 0; k < BDL_COUNT && !msk; k++) {
     std::vector<double> w(1172), omw(1172);
     std::vector<int> io(1172);
     const int size = host_delay_table(fds[k], w.data(), omw.data(), io.data(), 1172);
@@ -409,9 +471,15 @@ int burst_group_create(int device, int flags, int max_channels, BurstGroup **out
     if (int rc = h2d(g->T.domw[k], omw)) return rc;
     if (int rc = h2d(g->T.dio[k], io)) return rc;
   }
-  const double sr_b[3] = {0.0048847995518126464, 0, -0.0048847995518126464};
-  const double sr_a[3] = {1, -0.3882746897971619, 0.99023040089637471};
-  burst_upload_constants(sr_b, sr_a);
+  if (msk) {  // 600 Hz resonator at 48 kHz, 4 Hz bandwidth (burstmskdemodulator.cpp:214-227)
+    const double sr_b[3] = {2.617308727964618e-04, 0, -2.617308727964618e-04};
+    const double sr_a[3] = {1, -1.993312819378528, 0.999476538254407};
+    burst_msk_upload_constants(sr_b, sr_a, taps.data());
+  } else {
+    const double sr_b[3] = {0.0048847995518126464, 0, -0.0048847995518126464};
+    const double sr_a[3] = {1, -0.3882746897971619, 0.99023040089637471};
+    burst_upload_constants(sr_b, sr_a);
+  }
   launch_hk_spectrum(g->st, g->T, hk);
   BCHK(hipGetLastError());
   BCHK(hipStreamSynchronize(g->st));
@@ -430,28 +498,49 @@ void burst_group_destroy(BurstGroup *g) {
   delete g;
 }
 
-int burst_open(BurstGroup *g, bool disable_reassembly, int *local) {
+int burst_open(BurstGroup *g, int bitrate, bool disable_reassembly, int *local) {
   if (g->nch >= g->C) return AERO_E_FULL;
   const int c = g->nch;
   const int C = g->C;
-  // BurstOqpskDemodulator ctor + setSettings (burstoqpskdemodulator.cpp:5-232) and AeroL burst state
-  std::vector<double> ds(BD_COUNT, 0.0);
-  std::vector<int> is(BI_COUNT, 0);
-  ds[BD_M2_FREQ] = 8000;  // freq_center (burstoqpskdemodulator.h:33)
-  ds[BD_M2_STEP] = (8000.0) * ((double)WTSIZE) / ((float)48000);
-  ds[BD_SO_FREQ] = 10500;
-  ds[BD_SO_STEP] = (10500.0) * ((double)WTSIZE) / ((float)48000);
-  ds[BD_Q_STEP] = (10500.0 / 4.0) * ((double)WTSIZE) / ((float)48000);
-  ds[BD_VOL_GAIN] = 1;
-  ds[BD_AVE_RE] = ds[BD_ROT_RE] = ds[BD_STR_RE] = 1;
-  ds[BD_MSE] = 100;
-  ds[BD_LASTMSE] = 100;
-  is[BI_PD_CNTDOWN] = B_PD_MAXCD;
-  is[BI_PD_MAXPOSCD] = -1;
-  is[BI_STARTSTOP] = -1;
-  is[BI_FCNTR] = 1000000000;
-  for (int f = 0; f < BD_COUNT; f++) BCHK(hipMemcpy(g->S.ds + (size_t)f * C + c, &ds[f], 8, hipMemcpyHostToDevice));
-  for (int f = 0; f < BI_COUNT; f++) BCHK(hipMemcpy(g->S.is + (size_t)f * C + c, &is[f], 4, hipMemcpyHostToDevice));
+  std::vector<double> ds(BURST_DS_COUNT, 0.0);
+  std::vector<int> is(BURST_IS_COUNT, 0);
+  if (g->kind == BURST_MSK) {
+    if (bitrate != 600 && bitrate != 1200) return AERO_E_INVALID;
+    // BurstMskDemodulator ctor + setSettings (burstmskdemodulator.cpp:9-297):
+    // mixer2 at freq_center 1000, st_osc / st_osc_half at fb / 2; AeroL MSK
+    // burst window ifb * 3 bits (aerol.cpp:1031-1038)
+    ds[BM_M2_FREQ] = 1000;
+    ds[BM_M2_STEP] = (1000.0) * ((double)WTSIZE) / ((float)48000);
+    ds[BM_SO_STEP] = ds[BM_SH_STEP] = (1200 / 2.0) * ((double)WTSIZE) / ((float)48000);
+    ds[BM_AVE_RE] = ds[BM_ROT_RE] = ds[BM_STR_RE] = 1;
+    ds[BM_MSE] = 10.0;
+    ds[BM_DIFF_LAST] = -1;  // DiffDecode lastsoftstate (DSP.h)
+    is[BMI_PD_CNTDOWN] = M_PD_MAXCD;
+    is[BMI_PD_MAXPOSCD] = -1;
+    is[BMI_STARTSTOP] = -1;
+    is[BMI_FCNTR] = 1000000000;
+    is[BMI_TOTAL] = bitrate * 3;
+  } else {
+    if (bitrate != 10500) return AERO_E_INVALID;
+    // BurstOqpskDemodulator ctor + setSettings (burstoqpskdemodulator.cpp:5-232) and AeroL burst state
+    ds[BD_M2_FREQ] = 8000;  // freq_center (burstoqpskdemodulator.h:33)
+    ds[BD_M2_STEP] = (8000.0) * ((double)WTSIZE) / ((float)48000);
+    ds[BD_SO_FREQ] = 10500;
+    ds[BD_SO_STEP] = (10500.0) * ((double)WTSIZE) / ((float)48000);
+    ds[BD_Q_STEP] = (10500.0 / 4.0) * ((double)WTSIZE) / ((float)48000);
+    ds[BD_VOL_GAIN] = 1;
+    ds[BD_AVE_RE] = ds[BD_ROT_RE] = ds[BD_STR_RE] = 1;
+    ds[BD_MSE] = 100;
+    ds[BD_LASTMSE] = 100;
+    is[BI_PD_CNTDOWN] = B_PD_MAXCD;
+    is[BI_PD_MAXPOSCD] = -1;
+    is[BI_STARTSTOP] = -1;
+    is[BI_FCNTR] = 1000000000;
+  }
+  for (int f = 0; f < BURST_DS_COUNT; f++)
+    BCHK(hipMemcpy(g->S.ds + (size_t)f * C + c, &ds[f], 8, hipMemcpyHostToDevice));
+  for (int f = 0; f < BURST_IS_COUNT; f++)
+    BCHK(hipMemcpy(g->S.is + (size_t)f * C + c, &is[f], 4, hipMemcpyHostToDevice));
   g->nch++;
   g->avail.push_back(0);
   g->chunk_n.push_back(0);
@@ -465,6 +554,8 @@ int burst_open(BurstGroup *g, bool disable_reassembly, int *local) {
   g->packets_hold.emplace_back();
   g->hb_base.push_back(0);
   g->since_run.push_back(0);
+  g->tsu.push_back(0);
+  g->tblocks.push_back(0);
   *local = c;
   return AERO_OK;
 }

@@ -293,12 +293,13 @@ struct Group {
   std::vector<uint8_t> h_jobs_task, h_dbg_task;  // buffers owned by the running host task
 };
 
-constexpr int MODE_BURST = MODE_COUNT;  // chmap kind of burst-mode channels (burst_engine.hip)
+// chmap kinds of burst-mode channels (burst_engine.hip): MODE_BURST + BurstKind
+constexpr int MODE_BURST = MODE_COUNT;
 
 struct aero_engine {
   int device = 0, flags = 0, max_channels = 0;
   std::unique_ptr<Group> groups[MODE_COUNT];
-  BurstGroup *burst = nullptr;
+  BurstGroup *burst[2] = {nullptr, nullptr};  // BURST_OQPSK, BURST_MSK
   std::vector<std::pair<int, int>> chmap;  // engine channel -> (mode, local index)
   std::unique_ptr<HostPool> hpool;
   std::map<std::string, TimingSlot> timing;  // engine-level host sections
@@ -731,15 +732,19 @@ int drain_group(Group *e) {
   return AERO_OK;
 }
 
-// engine channel -> burst-group index, or -1
-int route_burst(aero_engine *e, int ch) {
-  if (!e || ch < 0 || ch >= (int)e->chmap.size() || e->chmap[ch].first != MODE_BURST) return -1;
+// engine channel -> burst-group index (its group in *bg), or -1
+int route_burst(aero_engine *e, int ch, BurstGroup **bg = nullptr) {
+  if (!e || ch < 0 || ch >= (int)e->chmap.size()) return -1;
+  const int k = e->chmap[ch].first - MODE_BURST;
+  if (k < 0 || k > 1) return -1;
+  if (bg) *bg = e->burst[k];
   return e->chmap[ch].second;
 }
 
 int run_impl(aero_engine *e, int flush) {
-  if (e->burst)
-    if (int rc = burst_run(e->burst, flush)) return rc;
+  for (BurstGroup *b : e->burst)
+    if (b)
+      if (int rc = burst_run(b, flush)) return rc;
   for (auto &g : e->groups)
     if (g) {
       int rc = run_group(g.get(), flush);
@@ -915,7 +920,7 @@ namespace {
 
 // engine channel -> (group, local index); nullptr if out of range
 Group *route(aero_engine *e, int ch, int &local) {
-  if (!e || ch < 0 || ch >= (int)e->chmap.size() || e->chmap[ch].first == MODE_BURST) return nullptr;
+  if (!e || ch < 0 || ch >= (int)e->chmap.size() || e->chmap[ch].first >= MODE_BURST) return nullptr;
   local = e->chmap[ch].second;
   return e->groups[e->chmap[ch].first].get();
 }
@@ -1120,21 +1125,32 @@ void aero_engine_destroy(aero_engine *e) {
     if (g) (void)drain_group(g.get());
   host_wait(e);
   for (auto &g : e->groups) g.reset();
-  if (e->burst) burst_group_destroy(e->burst);
+  for (BurstGroup *b : e->burst)
+    if (b) burst_group_destroy(b);
   delete e;
 }
 
 int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) {
   if (!e || !cfg || !ch_out) return AERO_E_INVALID;
-  if (cfg->burst) {  // aero-decode --burst: 10500 bps OQPSK (burst MSK is not built)
-    if (cfg->bitrate != 10500 || cfg->fs != 48000) return AERO_E_INVALID;
+  if (cfg->burst) {
+    // aero-decode --burst: 10500 bps OQPSK at 48 kHz; 600 / 1200 bps MSK run
+    // one fb = 1200 demodulator configured for 48 kHz whatever rate the audio
+    // is labelled with (decode/decode.cpp:123-132; a mismatch is only logged,
+    // burstmskdemodulator.cpp:708-714)
+    int kind;
+    if (cfg->bitrate == 10500 && cfg->fs == 48000)
+      kind = BURST_OQPSK;
+    else if ((cfg->bitrate == 600 || cfg->bitrate == 1200) && cfg->fs > 0)
+      kind = BURST_MSK;
+    else
+      return AERO_E_INVALID;
     HIPCHK(hipSetDevice(e->device));
-    if (!e->burst)
-      if (int rc = burst_group_create(e->device, e->flags, e->max_channels, &e->burst)) return rc;
+    if (!e->burst[kind])
+      if (int rc = burst_group_create(e->device, e->flags, e->max_channels, kind, &e->burst[kind])) return rc;
     int local;
-    if (int rc = burst_open(e->burst, cfg->disable_reassembly != 0, &local)) return rc;
+    if (int rc = burst_open(e->burst[kind], (int)cfg->bitrate, cfg->disable_reassembly != 0, &local)) return rc;
     *ch_out = (int)e->chmap.size();
-    e->chmap.push_back({MODE_BURST, local});
+    e->chmap.push_back({MODE_BURST + kind, local});
     return AERO_OK;
   }
   int mode;
@@ -1175,20 +1191,21 @@ int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) 
 
 // burst: one message = one BurstOqpskDemodulator::writeDataSlot call; pieces
 // of a long message keep its single message start
-int push_burst(aero_engine *e, int b, const int16_t *pcm, size_t n, bool dev) {
+int push_burst(aero_engine *e, BurstGroup *bg, int b, const int16_t *pcm, size_t n, bool dev) {
   HIPCHK(hipSetDevice(e->device));
   size_t off = 0;
   while (off < n) {
     const size_t piece = std::min<size_t>(n - off, 16384);
-    if (int rc = burst_push(e->burst, b, pcm + off, piece, dev, off == 0)) return rc;
+    if (int rc = burst_push(bg, b, pcm + off, piece, dev, off == 0)) return rc;
     off += piece;
   }
   return AERO_OK;
 }
 
 int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t fs) {
-  const int b = route_burst(e, ch);
-  if (b >= 0) return (pcm || !n) ? push_burst(e, b, pcm, n, false) : AERO_E_INVALID;  // rate only logged (:626-628)
+  BurstGroup *bg;
+  const int b = route_burst(e, ch, &bg);
+  if (b >= 0) return (pcm || !n) ? push_burst(e, bg, b, pcm, n, false) : AERO_E_INVALID;  // rate only logged (:626-628)
   int c;
   Group *g = route(e, ch, c);
   if (!g || (!pcm && n)) return AERO_E_INVALID;
@@ -1210,8 +1227,9 @@ int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t
 }
 
 int aero_push_pcm_dev(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t fs) {
-  const int b = route_burst(e, ch);
-  if (b >= 0) return (pcm || !n) ? push_burst(e, b, pcm, n, true) : AERO_E_INVALID;
+  BurstGroup *bg;
+  const int b = route_burst(e, ch, &bg);
+  if (b >= 0) return (pcm || !n) ? push_burst(e, bg, b, pcm, n, true) : AERO_E_INVALID;
   int c;
   Group *g = route(e, ch, c);
   if (!g || (!pcm && n)) return AERO_E_INVALID;
@@ -1234,10 +1252,10 @@ int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld,
   const int mode = e->chmap[0].first;
   for (int j = 0; j < nch; j++)
     if (e->chmap[j].first != mode || e->chmap[j].second != j) return AERO_E_INVALID;
-  if (mode == MODE_BURST) {  // one message of n <= 16384 samples per channel
+  if (mode >= MODE_BURST) {  // one message of n <= 16384 samples per channel
     if (dev && check_dev_ptr(pcm)) return AERO_E_INVALID;
     HIPCHK(hipSetDevice(e->device));
-    return burst_push_batch(e->burst, pcm, n, ld, nch, dev != 0);
+    return burst_push_batch(e->burst[mode - MODE_BURST], pcm, n, ld, nch, dev != 0);
   }
   Group *g = e->groups[mode].get();
   HIPCHK(hipSetDevice(e->device));
@@ -1262,8 +1280,9 @@ int aero_flush(aero_engine *e) {
 }
 
 int aero_pop_softbits(aero_engine *e, int ch, int16_t *dst, size_t cap, size_t *n) {
-  const int b = route_burst(e, ch);
-  if (b >= 0) return burst_pop_soft(e->burst, b, dst, cap, n);
+  BurstGroup *bg;
+  const int b = route_burst(e, ch, &bg);
+  if (b >= 0) return burst_pop_soft(bg, b, dst, cap, n);
   int c;
   Group *g = route(e, ch, c);
   if (!g) return AERO_E_INVALID;
@@ -1271,8 +1290,9 @@ int aero_pop_softbits(aero_engine *e, int ch, int16_t *dst, size_t cap, size_t *
 }
 
 int aero_pop_items(aero_engine *e, int ch, aero_acars_item *dst, size_t cap, size_t *n) {
-  const int b = route_burst(e, ch);
-  if (b >= 0) return pop_vec(burst_items(e->burst, b), dst, cap, n);
+  BurstGroup *bg;
+  const int b = route_burst(e, ch, &bg);
+  if (b >= 0) return pop_vec(burst_items(bg, b), dst, cap, n);
   int c;
   Group *g = route(e, ch, c);
   if (!g) return AERO_E_INVALID;
@@ -1287,8 +1307,9 @@ int aero_pop_items_all(aero_engine *e, aero_acars_item *dst, int *ch, size_t cap
   host_wait(e);
   size_t k = 0;
   for (int gc = 0; gc < (int)e->chmap.size() && k < cap; gc++) {
-    auto &v = e->chmap[gc].first == MODE_BURST ? burst_items(e->burst, e->chmap[gc].second)
-                                               : e->groups[e->chmap[gc].first]->host[e->chmap[gc].second]->items;
+    auto &v = e->chmap[gc].first >= MODE_BURST
+                  ? burst_items(e->burst[e->chmap[gc].first - MODE_BURST], e->chmap[gc].second)
+                  : e->groups[e->chmap[gc].first]->host[e->chmap[gc].second]->items;
     const size_t m = std::min(cap - k, v.size());
     for (size_t i = 0; i < m; i++) {  // msg bytes past msg_len are left unspecified
       memcpy(&dst[k + i], &v[i], offsetof(aero_acars_item, msg) + v[i].msg_len);
@@ -1302,8 +1323,9 @@ int aero_pop_items_all(aero_engine *e, aero_acars_item *dst, int *ch, size_t cap
 }
 
 int aero_pop_hops(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n) {
-  const int b = route_burst(e, ch);
-  if (b >= 0) return burst_pop_hops(e->burst, b, dst, cap_records, n);
+  BurstGroup *bg;
+  const int b = route_burst(e, ch, &bg);
+  if (b >= 0) return burst_pop_hops(bg, b, dst, cap_records, n);
   int c;
   Group *g = route(e, ch, c);
   if (!g) return AERO_E_INVALID;
@@ -1352,15 +1374,17 @@ int aero_pop_frames(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n)
 }
 
 int aero_pop_rt_tests(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
-  const int b = route_burst(e, ch);
+  BurstGroup *bg;
+  const int b = route_burst(e, ch, &bg);
   if (b < 0) return AERO_E_INVALID;
-  return burst_pop_tests(e->burst, b, dst, cap, n);
+  return burst_pop_tests(bg, b, dst, cap, n);
 }
 
 int aero_pop_rt_packets(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
-  const int b = route_burst(e, ch);
+  BurstGroup *bg;
+  const int b = route_burst(e, ch, &bg);
   if (b < 0) return AERO_E_INVALID;
-  return burst_pop_packets(e->burst, b, dst, cap, n);
+  return burst_pop_packets(bg, b, dst, cap, n);
 }
 
 int aero_timing(aero_engine *e, const char *name, double *ms, long *launches) {
@@ -1376,7 +1400,7 @@ int aero_timing(aero_engine *e, const char *name, double *ms, long *launches) {
       tl += it->second.launches;
     }
   }
-  burst_timing(e->burst, name, &tms, &tl);
+  for (BurstGroup *b : e->burst) burst_timing(b, name, &tms, &tl);
   if (ms) *ms = tms;
   if (launches) *launches = tl;
   return AERO_OK;
@@ -1384,7 +1408,7 @@ int aero_timing(aero_engine *e, const char *name, double *ms, long *launches) {
 
 void aero_timing_reset(aero_engine *e) {
   if (!e) return;
-  burst_timing_reset(e->burst);
+  for (BurstGroup *b : e->burst) burst_timing_reset(b);
   for (auto &g : e->groups)
     if (g) {
       ev_collect(g.get());
@@ -1398,7 +1422,7 @@ int aero_stat(aero_engine *e, const char *name, uint64_t *value) {
   uint64_t v = 0;
   const std::string n(name);
   if (n == "rt_tests" || n == "rt_packets") {
-    *value = burst_stat(e->burst, n == "rt_packets");
+    *value = burst_stat(e->burst[0], n == "rt_packets") + burst_stat(e->burst[1], n == "rt_packets");
     return AERO_OK;
   }
   for (auto &g : e->groups) {
@@ -1454,15 +1478,16 @@ uint64_t aero_samples_processed(aero_engine *e) {
   if (e) {
     for (auto &g : e->groups)
       if (g) s += g->processed;
-    s += burst_processed(e->burst);
+    for (BurstGroup *b : e->burst) s += burst_processed(b);
   }
   return s;
 }
 
 int aero_sync(aero_engine *e) {
   if (!e) return AERO_E_INVALID;
-  if (e->burst)
-    if (int rc = burst_sync(e->burst)) return rc;
+  for (BurstGroup *b : e->burst)
+    if (b)
+      if (int rc = burst_sync(b)) return rc;
   for (auto &g : e->groups)
     if (g) {
       int rc = drain_group(g.get());
@@ -1498,10 +1523,11 @@ int aero_engine_feed_dev(aero_engine *e, int nitems, const int *ch, const int16_
   std::vector<std::pair<int, std::pair<const int16_t *, size_t>>> per[MODE_COUNT];
   for (int i = 0; i < nitems; i++) {
     if (!n[i]) continue;
-    const int b = route_burst(e, ch[i]);
+    BurstGroup *bg;
+    const int b = route_burst(e, ch[i], &bg);
     if (b >= 0) {  // burst channels keep one message per call (synchronous copy)
       HIPCHK(hipEventSynchronize(ready));
-      if (int rc = push_burst(e, b, src[i], n[i], true)) return rc;
+      if (int rc = push_burst(e, bg, b, src[i], n[i], true)) return rc;
       continue;
     }
     int c;

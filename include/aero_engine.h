@@ -48,9 +48,13 @@ typedef struct {
 
 typedef struct {
   int bitrate;            /* 10500 (OQPSK), 600 or 1200 (MSK); decode/decode.h:42 */
-  int burst;              /* 1: aero-decode --burst (10500 bps OQPSK only)    */
+  int burst;              /* 1: aero-decode --burst: 10500 bps OQPSK, or
+                             600 / 1200 bps MSK (one fb = 1200 demodulator at
+                             48 kHz, decode/decode.cpp:123-132)               */
   uint32_t fs;            /* 48000 / 12000 / 24000 for 10500 / 600 / 1200 bps
-                             (decode/decode.cpp:145, 152-159)                 */
+                             (decode/decode.cpp:145, 152-159); burst MSK takes
+                             any rate, the audio is demodulated as 48 kHz
+                             (burstmskdemodulator.cpp:708-714 only logs it)   */
   int disable_reassembly; /* 1: items are ACARSfragmentsignal (decode.cpp:233) */
 } aero_channel_cfg;
 
@@ -88,9 +92,10 @@ int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t
 /* Lockstep batch push for channels [0, nch): pcm is time-major, n samples
  * per channel, sample t of channel c at pcm[t*ld + c].  dev != 0: pcm is a
  * HIP device pointer (inputs already resident in HBM).  Channels [0, nch)
- * must be of one kind (bit rate, burst or not).  For burst channels the
- * batch is one message per channel (at most 16384 samples; burst output
- * depends on message boundaries, decode/burstoqpskdemodulator.cpp:264). */
+ * must be of one kind (continuous bit rate, burst OQPSK or burst MSK).  For
+ * burst channels the batch is one message per channel (at most 16384
+ * samples; burst OQPSK output depends on message boundaries,
+ * decode/burstoqpskdemodulator.cpp:264). */
 int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld, int nch, int dev);
 
 /* aero_push_pcm with pcm a HIP device pointer (e.g. channeliser audio already

@@ -1210,6 +1210,17 @@ struct RTChannel {
     blockptr = (int)block.size();
     return lastpacketstate = OK_T;
   }
+  void trace(int at, int r) {
+    if (tests_out) {
+      const uint32_t rec[2] = {(uint32_t)at, (uint32_t)r};
+      tests_out->insert(tests_out->end(), (const uint8_t *)rec, (const uint8_t *)rec + 8);
+    }
+    if (packets_out && (r == OK_R || r == OK_T)) {
+      const uint32_t rec[2] = {(uint32_t)(r == OK_R ? 'R' : 'T'), (uint32_t)infofield.size()};
+      packets_out->insert(packets_out->end(), (const uint8_t *)rec, (const uint8_t *)rec + 8);
+      packets_out->insert(packets_out->end(), infofield.begin(), infofield.end());
+    }
+  }
   int update(int bit) {
     if (blockptr >= (int)block.size()) return FULL;
     block[blockptr] = bit;
@@ -1217,15 +1228,80 @@ struct RTChannel {
     if (((blockptr - (64 * 5)) % (64 * 3)) == 0) {
       const int at = blockptr;
       const int r = test();
-      if (tests_out) {
-        const uint32_t rec[2] = {(uint32_t)at, (uint32_t)r};
-        tests_out->insert(tests_out->end(), (const uint8_t *)rec, (const uint8_t *)rec + 8);
+      trace(at, r);
+      return r;
+    }
+    return Nothing;
+  }
+
+  // MSK bursts: RTChannelDeleaveFECScram::updateMSK (decode/aerol.h:614-753)
+  // with AeroLInterleaver::deinterleaveMSK_ba (decode/aerol.cpp:651-686):
+  // the first 5 columns interleave as one 64 x 5 section, every later 3 as
+  // 64 x 3; tests only at blocks 5, 11, 50 and the T packet's target block
+  // (from the SU count peeked at block 11).  `ok <= targetSUSize` always
+  // holds, so a T packet whose header CRC is good at the target block is OK.
+  int targetSUSize = 0, targetBlocks = 0;
+  void decode_msk() {
+    const int blocks = blockptr / 64;
+    std::vector<uint8_t> del(blockptr);
+    int k = 0;
+    for (int j = 0; j < 5; j++)
+      for (int i = 0; i < 64; i++) del[k++] = (uint8_t)block[((i * 27) % 64) * 5 + j];
+    int procblocks = 5;
+    while (k < blocks * 64) {
+      for (int j = 0; j < 3; j++)
+        for (int i = 0; i < 64; i++) del[k++] = (uint8_t)block[64 * procblocks + ((i * 27) % 64) * 3 + j];
+      procblocks += 3;
+    }
+    std::vector<uint8_t> decoded(blockptr / 2 + 1, 0);
+    viterbi().decode_soft(del.data(), blockptr, decoded.data());
+    const int dbits = blockptr / 2;
+    deconvol.assign(dbits, 0);
+    for (int b = 0; b < dbits; b++) deconvol[b] = (decoded[b / 8] >> (7 - (b % 8))) & 1;
+    for (int b = 0; b < dbits; b++) deconvol[b] ^= (*pre_state)[b];
+  }
+  int test_msk() {
+    const int blocks = blockptr / 64;
+    decode_msk();
+    if (blockptr == 64 * 5) {
+      targetSUSize = 0;
+      targetBlocks = 0;
+      if (crc_bits_check(deconvol.data(), 8 * 19)) {
+        packintobytes();
+        blockptr = (int)block.size();
+        return lastpacketstate = OK_R;
       }
-      if (packets_out && (r == OK_R || r == OK_T)) {
-        const uint32_t rec[2] = {(uint32_t)(r == OK_R ? 'R' : 'T'), (uint32_t)infofield.size()};
-        packets_out->insert(packets_out->end(), (const uint8_t *)rec, (const uint8_t *)rec + 8);
-        packets_out->insert(packets_out->end(), infofield.begin(), infofield.end());
-      }
+      return Nothing;
+    }
+    if (!crc_bits_check(deconvol.data(), 8 * 6)) return lastpacketstate = Bad;
+    if (blocks == 11) {
+      const int *isu = deconvol.data() + (8 * 6) + (8 * 12) * 1;
+      int bin = 2;
+      bin += ((isu[0] * 1) + (isu[1] * 2) + (isu[2] * 4) + (isu[3] * 8) + (isu[4] * 16) + (isu[5] * 32));
+      targetSUSize = bin;
+      if (targetSUSize >= 16) targetSUSize = (int)std::floor(targetSUSize / 2) + 1;
+      targetBlocks = ((targetSUSize + 1) * 3) + 2;
+      return Nothing;
+    }
+    if (blocks == targetBlocks) {
+      packintobytes();
+      infofield.pop_back();  // chop(1)
+      numberofsus = targetSUSize;
+      blockptr = (int)block.size();
+      return lastpacketstate = OK_T;
+    }
+    return Nothing;
+  }
+  int updateMSK(int bit) {
+    if (blockptr >= (int)block.size()) return FULL;
+    block[blockptr] = bit;
+    blockptr++;
+    const int blocks = blockptr / 64;
+    if ((((blockptr - (64 * 5)) % (64 * 3)) == 0) &&
+        (blocks == 5 || blocks == targetBlocks || blocks == 11 || blocks == 50)) {
+      const int at = blockptr;
+      const int r = test_msk();
+      trace(at, r);
       return r;
     }
     return Nothing;
@@ -1269,6 +1345,7 @@ struct AeroL {
   explicit AeroL(int bitrate = 10500) {
     uw_imag.setPreamble(3780831379ULL, 32);
     uw_real.setPreamble(3780831379ULL, 32);
+    msk_uw.setPreamble(3780831379ULL, 32);
     perm.resize(64);
     for (int i = 0; i < 64; i++) perm[i] = (i * 27) % 64;
     if (bitrate == 10500) {
@@ -1286,12 +1363,15 @@ struct AeroL {
     pre_state = scrambler_table();
     rt.pre_state = &pre_state;
   }
-  void setBurst() {  // 10500 burst: UW tolerance 4, a burst lasts at most 1 s of bits
+  void setBurst() {  // AeroL::setSettings(fb, true) (aerol.cpp:965-970, 1031-1038)
     burstmode = true;
     uw_imag.tollerence = 4;
     uw_real.tollerence = 4;
-    TotalNumberOfBits = 10500;
+    msk_uw.tollerence = 4;
+    // OQPSK: 1 s of bits; MSK: 3 s (ifb * 3)
+    TotalNumberOfBits = useingOQPSK ? 10500 : (leaverN == 6 ? 600 : 1200) * 3;
   }
+  UWDetector msk_uw;  // mskBurstDetector (aerol.cpp:939-940)
 
   // R / T packet results (decode/aerol.cpp:1240-1460; only what emits items)
   void rt_result(int result) {
@@ -1478,7 +1558,23 @@ struct AeroL {
       }
       if (muw < 100000) muw++;
       int gotsync;
-      if (!useingOQPSK) {
+      if (!useingOQPSK && burstmode) {
+        // MSK burst: phase-invariant UW (tolerance 4) accepted only within
+        // 250 bits of the start-of-packet marker (aerol.cpp:1155-1178)
+        const bool inverted = msk_uw.inverted;
+        gotsync = msk_uw.Update(bit);
+        if (muw > 250 && gotsync) {
+          if (inverted != msk_uw.inverted) msk_uw.inverted = inverted;
+          gotsync = false;
+        }
+        if (msk_uw.inverted) {
+          bit = 1 - bit;
+          if (soft_bit > 128)
+            soft_bit = 255 - soft_bit;
+          else if (soft_bit < 128)
+            soft_bit = 255 - soft_bit;
+        }
+      } else if (!useingOQPSK) {
         // continuous MSK: PreambleDetector::Update, exact match, buffer
         // cleared on a hit (aerol.cpp:716-725, :1178-1180); no inversion
         pd_reg = (pd_reg << 1) | bit;
@@ -1553,7 +1649,7 @@ struct AeroL {
         framecounter2 = (frameinfo >> 0) & 0x000F;
       }
       if (cntr >= 16 && burstmode) {
-        rt_result(rt.update(soft_bit));
+        rt_result(useingOQPSK ? rt.update(soft_bit) : rt.updateMSK(soft_bit));
       } else if (cntr >= 16) {
         if (cntr == 16) blockcnt = -1;
         int idx = (cntr - BitsInHeader) % (int)block.size();
@@ -2561,6 +2657,270 @@ struct BurstOqpsk {
   }
 };
 
+// BurstMskDemodulator (decode/burstmskdemodulator.cpp:9-704) as Decoder
+// configures it for -b 600 / 1200 --burst (decode/decode.cpp:123-132: Fs 48000,
+// fb 1200, lockingbw 10500, the Settings defaults freq_center 1000,
+// signalthreshold 0.6; AFC on; the hunter is disabled, decode.cpp:203, and
+// DCDstatSlot is unconnected, so dcd stays false).  Both bit rates run the
+// same fb = 1200 demodulator (SamplesPerSymbol 40, the fb >= 1200 branch of
+// setSettings, :176-232); only AeroL's framing differs.  The spectrum display,
+// MSKEbNoMeasure and scatter buffers are output-dead and not run; mixer_center
+// only holds the frequency CenterFreqChangedSlot copies into mixer2.
+struct BurstMsk {
+  const double Fs = 48000, fb = 1200, lockingbw = 10500, signalthreshold = 0.6;
+  const double SamplesPerSymbol = 40;  // int(Fs / fb)
+  const cpx imag = cpx(0, 1);
+  const double ee = 0.025;
+  const int startProcessing = 120, endRotation = (120 + 37) * 40, startstopstart = 40 * 500;
+  const int tridentbuffer_sz = 8000;  // qRound(200 * SPS)
+  double mse = 10.0, vol_gain = 0, rotator_freq = 0;
+  WaveTable mixer2, st_osc, st_osc_half;
+  AGC agc, agc2;
+  HilbertFir hfir;
+  DelayC bt_d1;
+  Delay bt_ma_diff, a1, delayt8;
+  TMovingAverageC bt_ma1;
+  MovingAverage mav1{5040}, msema{75};
+  PeakDetector pdet;
+  DelayThingT<cpx> d1, delayedsmpl;
+  DelayThingT<double> d2;
+  std::vector<double> tridentbuffer;
+  int tridentbuffer_ptr = 0;
+  FFTr fftr{4096 * 4 * 2};
+  FIR fir_re, fir_im;
+  IIR st_iir_resonator;
+  cpx symboltone_averotator = 1, rotator = 1, symboltone_rotator = 1;
+  int startstop = -1, cntr = 0;
+  DiffDecode diffdecode;
+  std::vector<short> RxDataBits;
+  AeroL aerol;
+  long long nsamples = 0;
+  std::vector<uint8_t> soft_out;
+  std::vector<int16_t> soft16;
+  std::vector<double> hops, pts;  // hops: per trident check (sample, detected, mixer2 Hz, vol_gain, minval, minvalbin)
+  bool trace_pt = false;
+
+  explicit BurstMsk(int bitrate) : aerol(bitrate) {
+    trig();
+    aerol.setBurst();
+    // setSettings (burstmskdemodulator.cpp:119-297), fb >= 1200 branch
+    mixer2.SetFreq(1000, 48000);
+    st_osc.SetFreq(fb / 2.0, (int)Fs);
+    st_osc_half.SetFreq(fb / 2.0, (int)Fs);
+    std::vector<double> mf(2 * 40);
+    for (int i = 0; i < 2 * 40; i++) mf[i] = sin(M_PI * i / (2.0 * SamplesPerSymbol)) / (2.0 * SamplesPerSymbol);
+    fir_re.init(mf);
+    fir_im.init(mf);
+    agc.init(1, Fs);
+    agc2.init(SamplesPerSymbol * 128.0 / Fs, Fs);
+    a1.setdelay(40 / 2);
+    bt_d1.setdelay(1.0 * SamplesPerSymbol);
+    bt_ma1.setLength(qRound(126.0 * SamplesPerSymbol));
+    mav1 = MovingAverage((int)(SamplesPerSymbol * 126));
+    bt_ma_diff.setdelay(SamplesPerSymbol * 126);
+    pdet.setSettings((int)(SamplesPerSymbol * 126.0 / 2.0), 0.1);
+    tridentbuffer.assign(tridentbuffer_sz, 0.0);
+    d1.setLength(((int)289 * 40) + 20);
+    d2.setLength(qRound(72 + 120.0) * 40);
+    st_iir_resonator.a[0] = 1;
+    st_iir_resonator.a[1] = -1.993312819378528;
+    st_iir_resonator.a[2] = 0.999476538254407;
+    st_iir_resonator.b[0] = 2.617308727964618e-04;
+    st_iir_resonator.b[1] = 0;
+    st_iir_resonator.b[2] = -2.617308727964618e-04;
+    st_iir_resonator.init();
+    delayt8.setdelay((SamplesPerSymbol) / 2.0);
+    delayedsmpl.setLength(40);
+  }
+
+  void emit_bits() {
+    for (short v : RxDataBits) {
+      soft16.push_back(v);
+      if (v >= 0) soft_out.push_back((uint8_t)v);
+    }
+    aerol.decode(RxDataBits.data(), (int)RxDataBits.size());
+    RxDataBits.clear();
+  }
+
+  void trident_check() {  // burstmskdemodulator.cpp:398-523
+    const int size_base = 126, size_top = 74;
+    std::vector<double> in(32768, 0.0);
+    std::vector<cpx> out_base, out_top;
+    const int LB = qRound(size_base * SamplesPerSymbol), LT = qRound(size_top * SamplesPerSymbol);
+    for (int k = 0; k < LB; k++) in[k] = tridentbuffer[k];
+    fftr.transform(in, out_base);
+    std::fill(in.begin(), in.end(), 0.0);
+    for (int k = 0; k < LT; k++) in[k] = tridentbuffer[LB + k];
+    fftr.transform(in, out_top);
+    const double hzperbin = Fs / ((double)out_base.size());
+    const int peakspacingbins = qRound((0.5 * fb) / hzperbin);
+    int minvalbin = 0;
+    double minval = 0;
+    for (int i = 0; i < (int)out_base.size() / 2; i++) {
+      if (std::abs(out_base[i]) > minval) {
+        minval = std::abs(out_base[i]);
+        minvalbin = i;
+      }
+    }
+    double maxtop = 0, maxtophigh = 0;
+    int maxtoppos = 0, maxtopposhigh = 0;
+    for (int i = 0; i < (int)out_top.size() / 2; i++) {
+      if (i > 50) {
+        if ((i < minvalbin - (peakspacingbins / 2)) && std::abs(out_top[i]) > maxtop) {
+          maxtop = std::abs(out_top[i]);
+          maxtoppos = i;
+        }
+        if ((i > minvalbin + (peakspacingbins / 2)) && std::abs(out_top[i]) > maxtophigh) {
+          maxtophigh = std::abs(out_top[i]);
+          maxtopposhigh = i;
+        }
+      }
+    }
+    const int distfrompeak = std::abs(maxtoppos - minvalbin);
+    const bool det = minval > 500.0 && std::abs(distfrompeak - peakspacingbins) < std::abs(peakspacingbins / 20) &&
+                     !(cntr > 0 && cntr < (500 * SamplesPerSymbol));  // && !dcd
+    if (det) {
+      vol_gain = 1.4142 * (500.0 / (minval / 3));
+      const double carrierphase = std::arg(out_base[minvalbin]) - (M_PI / 4.0);
+      mixer2.SetPhaseDeg((180.0 / M_PI) * carrierphase);
+      mixer2.SetFreq(((maxtopposhigh + maxtoppos) / 2) * hzperbin);
+      {  // CenterFreqChangedSlot (:299-317), afc on; mixer_center then mixer2 = its frequency
+        double freq_center = ((maxtopposhigh + maxtoppos) / 2) * hzperbin;
+        if (freq_center < (0.75 * fb)) freq_center = 0.75 * fb;
+        if (freq_center > (Fs / 2.0 - 0.75 * fb)) freq_center = Fs / 2.0 - 0.75 * fb;
+        WaveTable mixer_center;
+        mixer_center.SetFreq(freq_center, (int)Fs);
+        mixer2.SetFreq(mixer_center.GetFreqHz());
+        if ((mixer2.GetFreqHz() - mixer_center.GetFreqHz()) > (lockingbw / 2.0))
+          mixer2.SetFreq(mixer_center.GetFreqHz() + (lockingbw / 2.0));
+        if ((mixer2.GetFreqHz() - mixer_center.GetFreqHz()) < (-lockingbw / 2.0))
+          mixer2.SetFreq(mixer_center.GetFreqHz() - (lockingbw / 2.0));
+      }
+      startstop = startstopstart;
+      cntr = 0;
+      RxDataBits.clear();
+      RxDataBits.push_back(-1);  // start of burst
+      mse = 0;
+      msema = MovingAverage(75);
+      symboltone_averotator = 1;
+      symboltone_rotator = 1;
+      rotator = 1;
+      rotator_freq = 0;
+      st_iir_resonator.init();
+      st_osc.SetPhaseDeg(0);
+      st_osc_half.SetPhaseDeg(0);
+    }
+    hops.push_back((double)nsamples);
+    hops.push_back(det ? 1.0 : 0.0);
+    hops.push_back(mixer2.GetFreqHz());
+    hops.push_back(vol_gain);
+    hops.push_back(minval);
+    hops.push_back((double)minvalbin + 65536.0 * (double)maxtoppos);
+  }
+
+  void writeData(const short *ptr, int n) {  // burstmskdemodulator.cpp:328-704
+    for (int i = 0; i < n; i++, ptr++, nsamples++) {
+      cpx cval = hfir.update(cpx(((double)(*ptr)) / 32768.0, 0));
+      agc.Update(std::abs(cval));
+      cval *= agc.AGCVal;
+      cpx cval_d = d1.update_dont_touch(cval);
+      double val_to_demod = d2.update_dont_touch(std::real(cval_d));
+      double fastarm = std::abs(bt_ma1.UpdateSigned(cval * std::conj(bt_d1.update(cval))));
+      fastarm = mav1.UpdateSigned(fastarm);
+      fastarm -= bt_ma_diff.update(fastarm);
+      if (fastarm < 0) fastarm = 0;
+      double bt_sig = fastarm * fastarm;
+      if (bt_sig > 500) bt_sig = 500;
+      if (pdet.update(bt_sig)) tridentbuffer_ptr = 0;
+      if (tridentbuffer_ptr < tridentbuffer_sz) {
+        tridentbuffer[tridentbuffer_ptr] = std::real(cval_d);
+        tridentbuffer_ptr++;
+      } else if (tridentbuffer_ptr == tridentbuffer_sz) {
+        tridentbuffer_ptr++;
+        trident_check();
+      }
+      if (startstop > 0) {
+        if (cntr >= (startProcessing * SamplesPerSymbol)) startstop--;
+        if (cntr < 1000000) cntr++;
+        if (mse < signalthreshold) startstop = startstopstart;
+      }
+      if (startstop == 0) {
+        startstop--;
+        cntr = 0;
+        mse = 1;
+      }
+      if (!(startstop > 0 || mse < signalthreshold)) continue;
+      cval = mixer2.WTCISValue() * (val_to_demod)*vol_gain;
+      cpx sig2 = cpx(fir_re.FIRUpdateAndProcess(cval.real()), fir_im.FIRUpdateAndProcess(cval.imag()));
+      if (cntr > (startProcessing * SamplesPerSymbol) && cntr < endRotation) {
+        cpx symboltone_pt = sig2 * symboltone_rotator * imag;
+        double er = std::tanh(symboltone_pt.imag()) * (symboltone_pt.real());
+        symboltone_rotator = symboltone_rotator * std::exp(imag * er * 0.5);
+        symboltone_averotator = symboltone_averotator * 0.999 + 0.001 * symboltone_rotator;
+        symboltone_pt = cpx((symboltone_pt.real()), a1.update(symboltone_pt.real()));
+        double progress = (double)cntr - (SamplesPerSymbol * (startProcessing));
+        double goal = endRotation - (SamplesPerSymbol * startProcessing);
+        progress = progress / goal;
+        double st_err = std::arg((st_osc_half.WTCISValue()) * std::conj(symboltone_pt));
+        st_err *= 0.5 * (1.0 - progress * progress);
+        st_osc_half.AdvanceFractionOfWave(-(1.0 / (2.0 * M_PI)) * st_err * 0.05);
+        st_osc.SetPhaseDeg((360.0 * st_osc_half.WTptr / ((double)WTSIZE)) + (360.0 * (1.0 - ee)));
+      }
+      sig2 *= symboltone_averotator;
+      rotator = rotator * std::exp(imag * rotator_freq);
+      sig2 *= rotator;
+      sig2 *= agc2.Update(std::abs(sig2));
+      double abval = std::abs(sig2);
+      if (abval > 2.84) sig2 = (2.84 / abval) * sig2;
+      cpx pt_d = delayedsmpl.update_dont_touch(sig2);
+      cpx pt_msk = cpx(sig2.real(), pt_d.imag());
+      double st_eta = std::abs(pt_msk);
+      st_eta = st_iir_resonator.update(st_eta);
+      cpx st_m1 = cpx(st_eta, -delayt8.update(st_eta));
+      cpx st_out = st_osc.WTCISValue() * st_m1;
+      double st_angle_error = std::arg(st_out);
+      if (cntr > endRotation) st_osc.AdvanceFractionOfWave(-st_angle_error * 0.002 / 360.0);
+      if (st_osc.IfHavePassedPoint(ee)) {
+        double ct_xt = tanh(sig2.imag()) * sig2.real();
+        double ct_xt_d = tanh(pt_d.real()) * pt_d.imag();
+        double ct_ec = ct_xt_d - ct_xt;
+        if (ct_ec > M_PI) ct_ec = M_PI;
+        if (ct_ec < -M_PI) ct_ec = -M_PI;
+        if (ct_ec > M_PI_2) ct_ec = M_PI_2;
+        if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
+        if (cntr > (startProcessing * SamplesPerSymbol)) {
+          rotator = rotator * std::exp(imag * ct_ec * 0.25);
+          if (cntr > endRotation) rotator_freq = rotator_freq + ct_ec * 0.0001;
+        }
+        if (trace_pt) {
+          pts.push_back(pt_msk.real());
+          pts.push_back(pt_msk.imag());
+        }
+        if (cntr > (startProcessing * SamplesPerSymbol)) {
+          double tda = (fabs((pt_msk * 0.75).real()) - 1.0);
+          double tdb = (fabs((pt_msk * 0.75).imag()) - 1.0);
+          mse = msema.Update((tda * tda) + (tdb * tdb));
+        }
+        double imagin = diffdecode.UpdateSoft(pt_msk.imag());
+        int ibit = qRound((imagin) * 127.0 + 128.0);
+        if (ibit > 255) ibit = 255;
+        if (ibit < 0) ibit = 0;
+        RxDataBits.push_back((short)(uint8_t)ibit);
+        double real = diffdecode.UpdateSoft(pt_msk.real());
+        real = -real;
+        ibit = qRound((real) * 127.0 + 128.0);
+        if (ibit > 255) ibit = 255;
+        if (ibit < 0) ibit = 0;
+        RxDataBits.push_back((short)(uint8_t)ibit);
+        if (RxDataBits.size() >= 12) emit_bits();
+      }
+      st_osc.WTnextFrame();
+      st_osc_half.WTnextFrame();
+      mixer2.WTnextFrame();
+    }
+  }
+};
+
 template <class T>
 size_t copy_out(const std::vector<T> &v, T *dst, size_t cap) {
   size_t n = std::min(cap, v.size());
@@ -2574,12 +2934,15 @@ struct oracle_chan {
   std::unique_ptr<Oqpsk> oq;
   std::unique_ptr<Msk> msk;
   std::unique_ptr<BurstOqpsk> bq;
+  std::unique_ptr<BurstMsk> bm;
   std::vector<uint8_t> blocks, frames, rt_tests, rt_packets;
   std::string items;
-  AeroL &aerol() { return oq ? oq->aerol : (msk ? msk->aerol : bq->aerol); }
-  const std::vector<uint8_t> &soft() const { return oq ? oq->soft_out : (msk ? msk->soft_out : bq->soft_out); }
-  const std::vector<double> &hops() const { return oq ? oq->hops : (msk ? msk->hops : bq->hops); }
-  const std::vector<double> &pts() const { return oq ? oq->pts : (msk ? msk->pts : bq->pts); }
+  AeroL &aerol() { return oq ? oq->aerol : (msk ? msk->aerol : (bq ? bq->aerol : bm->aerol)); }
+  const std::vector<uint8_t> &soft() const {
+    return oq ? oq->soft_out : (msk ? msk->soft_out : (bq ? bq->soft_out : bm->soft_out));
+  }
+  const std::vector<double> &hops() const { return oq ? oq->hops : (msk ? msk->hops : (bq ? bq->hops : bm->hops)); }
+  const std::vector<double> &pts() const { return oq ? oq->pts : (msk ? msk->pts : (bq ? bq->pts : bm->pts)); }
 };
 
 extern "C" {
@@ -2590,13 +2953,14 @@ oracle_chan *oracle_create(int bitrate, int flags) {
   const bool tp = (flags & ORACLE_TRACE_PT) != 0;
   if (flags & ORACLE_BURST) {
     if (bitrate != 10500) {
-      delete c;
-      return nullptr;
+      c->bm.reset(new BurstMsk(bitrate));
+      c->bm->trace_pt = tp;
+    } else {
+      c->bq.reset(new BurstOqpsk());
+      c->bq->trace_pt = tp;
     }
-    c->bq.reset(new BurstOqpsk());
-    c->bq->trace_pt = tp;
-    c->bq->aerol.rt.tests_out = &c->rt_tests;
-    c->bq->aerol.rt.packets_out = &c->rt_packets;
+    c->aerol().rt.tests_out = &c->rt_tests;
+    c->aerol().rt.packets_out = &c->rt_packets;
   } else if (bitrate == 10500) {
     c->oq.reset(new Oqpsk());
     c->oq->trace_pt = tp;
@@ -2616,13 +2980,15 @@ int oracle_push(oracle_chan *c, const int16_t *pcm, size_t n) {
     c->oq->writeData(pcm, (int)n);
   else if (c->msk)
     c->msk->writeData(pcm, (int)n);
-  else
+  else if (c->bq)
     c->bq->writeData(pcm, (int)n);
+  else
+    c->bm->writeData(pcm, (int)n);
   return 0;
 }
 size_t oracle_softbits16(const oracle_chan *c, int16_t *dst, size_t cap) {
   static const std::vector<int16_t> none;
-  return copy_out(c->bq ? c->bq->soft16 : none, dst, cap);
+  return copy_out(c->bq ? c->bq->soft16 : (c->bm ? c->bm->soft16 : none), dst, cap);
 }
 size_t oracle_rt_tests(const oracle_chan *c, uint8_t *dst, size_t cap) { return copy_out(c->rt_tests, dst, cap); }
 size_t oracle_rt_packets(const oracle_chan *c, uint8_t *dst, size_t cap) { return copy_out(c->rt_packets, dst, cap); }

@@ -26,7 +26,7 @@ typedef struct oracle_chan oracle_chan;
 
 /* flags */
 #define ORACLE_TRACE_PT 1 /* record every rotated pt_qpsk (re,im) */
-#define ORACLE_BURST 2    /* burst mode (aero-decode --burst; 10500 only) */
+#define ORACLE_BURST 2    /* burst mode (aero-decode --burst): 10500 OQPSK, 600/1200 MSK */
 
 oracle_chan *oracle_create(int bitrate, int flags);
 void oracle_destroy(oracle_chan *c);

@@ -106,6 +106,35 @@ def synth_burst(seconds=10.0, seed=0xAE50, carrier=12000.0, ebn0=14.0, amplitude
     return pcm, pk
 
 
+def synth_burst_msk(seconds=10.0, bitrate=1200, seed=0xAE70, carrier=2500.0, ebn0=14.0, amplitude=0.25, phase0=0.3,
+                    lead_in=24000, p1=126, p2=74, alt_sign=1, return_packets=False):
+    """int16 48 kHz PCM of 1200-baud burst MSK R/T packets for `aero-decode
+    -b <bitrate> --burst` (p1 carrier / p2 alternating preamble bit periods)
+    + the transmitted packets [(kind 'R'/'T', bytes)]."""
+    global _synth
+    if _synth is None:
+        _synth = ctypes.CDLL(SYNTH_SO)
+    _synth.aero_synth_burst_msk.restype = ctypes.c_size_t
+    n = int(48000 * seconds)
+    pcm = np.zeros(n, dtype=np.int16)
+    cap = int(seconds + 4) * 400
+    buf = np.zeros(cap, dtype=np.uint8)
+    npk = ctypes.c_size_t()
+    cfg = SynthCfg(48000.0, carrier, phase0, amplitude, ebn0, seed, 0.6, lead_in)
+    used = _synth.aero_synth_burst_msk(ctypes.byref(cfg), ctypes.c_int(bitrate), ctypes.c_int(p1), ctypes.c_int(p2),
+                                       ctypes.c_int(alt_sign), pcm.ctypes.data_as(ctypes.c_void_p),
+                                       ctypes.c_size_t(n), buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(cap),
+                                       ctypes.byref(npk))
+    if not return_packets:
+        return pcm
+    pk, i = [], 0
+    while i < used:
+        kind, ln = np.frombuffer(buf[i:i + 8].tobytes(), np.uint32)
+        pk.append((chr(kind), bytes(buf[i + 8:i + 8 + ln])))
+        i += 8 + int(ln)
+    return pcm, pk
+
+
 class Oracle:
     """One reference channel (a whole `aero-decode -b <bitrate>` instance)."""
     _lib = None

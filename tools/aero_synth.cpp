@@ -457,6 +457,7 @@ struct BurstTx {
   // queued packets (bytes incl. CRCs) + kind
   std::vector<std::pair<char, std::vector<uint8_t>>> pending;
 
+  int t_maxtext = 40;  // T-packet text length bound (MSK bursts: the SU count must fit the burst window)
   void refill() {
     unsigned aes = tx.aes_pool[tx.rng.below(8)];
     uint8_t ges = (uint8_t)(0x80 + tx.rng.below(8));
@@ -500,7 +501,7 @@ struct BurstTx {
       }
     } else {
       // T packet: header + 0x71 ISU + SSUs (ISUData, decode/aerol.cpp:158-227)
-      std::vector<uint8_t> ud = acars_ud(aes, 40);
+      std::vector<uint8_t> ud = acars_ud(aes, t_maxtext);
       tx.queue.clear();
       // reuse the P-channel ISU/SSU builder on this message's user data
       const int rest = (int)ud.size() - 2;
@@ -530,15 +531,18 @@ struct BurstTx {
     }
   }
 
-  // channel bits of the next burst's packet part (after the UW)
-  std::vector<int> next_packet(char &kind, std::vector<uint8_t> &bytes) {
+  // channel bits of the next burst's packet part (after the UW).  MSK bursts
+  // (decode/aerol.h:614-753) carry a T packet of S SUs in 320 + 192 S bits,
+  // interleaved as a 64 x 5 section and then 64 x 3 sections
+  // (AeroLInterleaver::deinterleaveMSK_ba, decode/aerol.cpp:651-686).
+  std::vector<int> next_packet(char &kind, std::vector<uint8_t> &bytes, bool msk = false) {
     if (pending.empty()) refill();
     kind = pending.front().first;
     bytes = pending.front().second;
     pending.erase(pending.begin());
     const int nbytes = (int)bytes.size();
     const int S = kind == 'T' ? (nbytes - 6) / 12 : 1;
-    const int blockptr = kind == 'R' ? 320 : 320 + 192 * (S - 1);
+    const int blockptr = kind == 'R' ? 320 : 320 + 192 * (msk ? S : S - 1);
     const int dbits = blockptr / 2;
     std::vector<int> in(dbits, 0);
     for (int h = 0; h < 8 * nbytes && h < dbits - 6; h++) in[h] = ((bytes[h / 8] >> (h % 8)) & 1) ^ tx.scr[h];
@@ -552,8 +556,17 @@ struct BurstTx {
     }
     const int cols = blockptr / 64;
     std::vector<int> blk(blockptr);
-    for (int j = 0; j < cols; j++)
-      for (int i = 0; i < 64; i++) blk[tx.perm[i] * cols + j] = coded[j * 64 + i];
+    if (!msk) {
+      for (int j = 0; j < cols; j++)
+        for (int i = 0; i < 64; i++) blk[tx.perm[i] * cols + j] = coded[j * 64 + i];
+    } else {
+      int k = 0;
+      for (int j = 0; j < 5; j++)
+        for (int i = 0; i < 64; i++) blk[tx.perm[i] * 5 + j] = coded[k++];
+      for (int pb = 5; k < blockptr; pb += 3)
+        for (int j = 0; j < 3; j++)
+          for (int i = 0; i < 64; i++) blk[64 * pb + tx.perm[i] * 3 + j] = coded[k++];
+    }
     return blk;
   }
 };
@@ -638,6 +651,106 @@ extern "C" size_t aero_synth_burst(const aero_synth_cfg *cfg, int16_t *pcm, size
     }
     const double ph = w * (double)n + cfg->phase0;
     double x = A * (I * cos(ph) + Q * sin(ph));
+    if (sigma > 0) x += sigma * nrng.gauss();
+    double v = floor(x * 32768.0 + 0.5);
+    if (v > 32767) v = 32767;
+    if (v < -32768) v = -32768;
+    pcm[n] = (int16_t)v;
+  }
+  return used;
+}
+
+/* 600/1200-bps burst MSK (R / T channels, aero-decode -b 600|1200 --burst).
+ * aero-decode demodulates both rates with one fb = 1200 BurstMskDemodulator at
+ * 48 kHz (decode/decode.cpp:123-132), so bursts are 1200-baud MSK: P1 bit
+ * periods of unmodulated carrier (the trident check's "start tone",
+ * decode/burstmskdemodulator.cpp:437-446), P2 of alternating frequency (the
+ * 0-1 preamble whose lines sit fb/2 either side, :448-473), the UW, the packet
+ * and a few random bits.  Data bits are differentially encoded onto
+ * alternating half-sine arms exactly as aero_synth_msk does, generated as the
+ * equivalent continuous-phase signal (+-90 degrees per bit period) so the
+ * preamble and the data join without a phase step.  bitrate selects the
+ * AeroL window (1800 / 3600 bits, decode/aerol.cpp:1031-1038) and so the
+ * largest T packet; packets[] as aero_synth_burst. */
+extern "C" size_t aero_synth_burst_msk(const aero_synth_cfg *cfg, int bitrate, int p1, int p2, int alt_sign,
+                                       int16_t *pcm, size_t nsamples, uint8_t *packets, size_t packets_cap,
+                                       size_t *npackets) {
+  BurstTx bt(*cfg);
+  bt.t_maxtext = bitrate == 600 ? 12 : 40;
+  const double Fs = cfg->fs, T = Fs / 1200.0;
+  const size_t nbits = (size_t)(nsamples / T) + 4;
+  // phase (in quarter turns) at every bit boundary; NaN-free: silent bits flagged
+  std::vector<int> quarter(nbits + 1, 0);
+  std::vector<char> on(nbits, 0);
+  size_t k = (size_t)(cfg->lead_in / T), np = 0, used = 0;
+  int q = 0;
+  while (true) {
+    char kind;
+    std::vector<uint8_t> bytes;
+    std::vector<int> pk = bt.next_packet(kind, bytes, true);
+    std::vector<int> data;
+    const uint32_t uw = 0xE15AE893u;
+    for (int j = 0; j < 32; j++) data.push_back((uw >> (31 - j)) & 1);
+    data.insert(data.end(), pk.begin(), pk.end());
+    for (int s = 0; s < 16; s++) data.push_back(bt.tx.rng.below(2));
+    const size_t len = (size_t)p1 + (size_t)p2 + data.size();
+    if (k + len + 2 >= nbits) break;
+    size_t at = k;
+    quarter[at] = q;
+    for (int s = 0; s < p1; s++, at++) {  // carrier
+      on[at] = 1;
+      quarter[at + 1] = q;
+    }
+    for (int s = 0; s < p2; s++, at++) {  // alternating frequency
+      on[at] = 1;
+      q += ((s & 1) ? -alt_sign : alt_sign);
+      quarter[at + 1] = q;
+    }
+    // data: arms a[n] (I on even n, Q on odd n), a 1 is a sign change on the
+    // arm read first and no change on the other (aero_synth_msk); baseband
+    // I - iQ turns by +90 deg * a[n] * a[n-1] over an even bit, -90 deg * ...
+    // over an odd one
+    int last = 1;
+    for (size_t b = 0; b < data.size(); b++, at++) {
+      const bool flip = (b % 2 == 0) ? !data[b] : data[b];
+      const int a = flip ? -last : last;
+      const int dq = ((b % 2 == 0) ? 1 : -1) * a * last;
+      last = a;
+      on[at] = 1;
+      q += dq;
+      quarter[at + 1] = q;
+    }
+    if (packets && used + 8 + bytes.size() <= packets_cap) {
+      uint32_t h[2] = {(uint32_t)kind, (uint32_t)bytes.size()};
+      memcpy(packets + used, h, 8);
+      memcpy(packets + used + 8, bytes.data(), bytes.size());
+      used += 8 + bytes.size();
+    }
+    np++;
+    k = at + (size_t)((1.0 + 2.0 * bt.tx.rng.uniform()) * 1200.0);  // next burst 1-3 s later
+    if (k >= nbits) break;
+    for (size_t z = at + 1; z <= k && z <= nbits; z++) quarter[z] = q;
+  }
+  if (npackets) *npackets = np;
+  const double A = cfg->amplitude;
+  const double P = A * A / 2.0;
+  double sigma = 0;
+  if (cfg->ebn0_db < 99) {
+    const double Eb = P / 1200.0;
+    const double N0 = Eb / pow(10.0, cfg->ebn0_db / 10.0);
+    sigma = sqrt(N0 / 2.0 * Fs);
+  }
+  Rng nrng(cfg->seed ^ 0xA5A5A5A55A5A5A5AULL);
+  const double w = 2.0 * M_PI * cfg->carrier_hz / Fs;
+  for (size_t n = 0; n < nsamples; n++) {
+    const double t = (double)n / T;
+    const size_t b = (size_t)t;
+    double x = 0;
+    if (b < nbits && on[b]) {
+      const double u = t - (double)b;
+      const double ph = (M_PI / 2.0) * ((double)quarter[b] * (1.0 - u) + (double)quarter[b + 1] * u);
+      x = A * cos(w * (double)n + cfg->phase0 + ph);
+    }
     if (sigma > 0) x += sigma * nrng.gauss();
     double v = floor(x * 32768.0 + 0.5);
     if (v > 32767) v = 32767;
