@@ -160,6 +160,10 @@ struct BurstGroup {
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending_ev;
   long long last_work = -1;
   std::vector<long long> hb_base;  // first sample the Hilbert stage still needs (host mirror)
+  // initial state of channels [init_lo, nch), uploaded field by field before the next push or run
+  int init_lo = 0;
+  std::vector<double> init_ds;  // [field][channel - init_lo]
+  std::vector<int> init_is;
   std::vector<int> since_run;      // messages pushed since the last run (message-start ring)
 };
 
@@ -537,10 +541,11 @@ int burst_open(BurstGroup *g, int bitrate, bool disable_reassembly, int *local) 
     is[BI_STARTSTOP] = -1;
     is[BI_FCNTR] = 1000000000;
   }
-  for (int f = 0; f < BURST_DS_COUNT; f++)
-    BCHK(hipMemcpy(g->S.ds + (size_t)f * C + c, &ds[f], 8, hipMemcpyHostToDevice));
-  for (int f = 0; f < BURST_IS_COUNT; f++)
-    BCHK(hipMemcpy(g->S.is + (size_t)f * C + c, &is[f], 4, hipMemcpyHostToDevice));
+  // the device copy waits for the next push or run (flush_init): one copy per
+  // field for every channel opened since, not one per field per channel
+  (void)C;
+  g->init_ds.insert(g->init_ds.end(), ds.begin(), ds.end());
+  g->init_is.insert(g->init_is.end(), is.begin(), is.end());
   g->nch++;
   g->avail.push_back(0);
   g->chunk_n.push_back(0);
@@ -560,10 +565,31 @@ int burst_open(BurstGroup *g, int bitrate, bool disable_reassembly, int *local) 
   return AERO_OK;
 }
 
+// initial device state of the channels opened since the last push or run
+static int flush_init(BurstGroup *g) {
+  const int n = g->nch - g->init_lo;
+  if (n <= 0) return AERO_OK;
+  std::vector<double> col(n);
+  std::vector<int> icol(n);
+  for (int f = 0; f < BURST_DS_COUNT; f++) {
+    for (int k = 0; k < n; k++) col[k] = g->init_ds[(size_t)k * BURST_DS_COUNT + f];
+    BCHK(hipMemcpy(g->S.ds + (size_t)f * g->C + g->init_lo, col.data(), 8 * n, hipMemcpyHostToDevice));
+  }
+  for (int f = 0; f < BURST_IS_COUNT; f++) {
+    for (int k = 0; k < n; k++) icol[k] = g->init_is[(size_t)k * BURST_IS_COUNT + f];
+    BCHK(hipMemcpy(g->S.is + (size_t)f * g->C + g->init_lo, icol.data(), 4 * n, hipMemcpyHostToDevice));
+  }
+  g->init_lo = g->nch;
+  g->init_ds.clear();
+  g->init_is.clear();
+  return AERO_OK;
+}
+
 int burst_run(BurstGroup *g, int flush) {
   (void)flush;  // every pushed sample is processed (burst output depends on message boundaries only)
   if (!g || !g->nch) return AERO_OK;
   BCHK(hipSetDevice(g->device));
+  if (int rc = flush_init(g)) return rc;
   const bool trace = (g->flags & (AERO_F_TRACE_HOPS | AERO_F_TRACE_SOFT)) != 0;
   g->last_work = -1;
   for (int guard = 0; guard < 100000; guard++) {
@@ -582,6 +608,7 @@ int burst_run(BurstGroup *g, int flush) {
 int burst_push(BurstGroup *g, int c, const int16_t *pcm, size_t n, bool dev, bool msg_start) {
   if (!n) return AERO_OK;
   BCHK(hipSetDevice(g->device));
+  if (int rc = flush_init(g)) return rc;
   const int C = g->C;
   if ((long long)n > B_PCM_CAP / 2) return AERO_E_FULL;  // one message is at most 16384 samples here
   // never outrun the PCM ring (the Hilbert stage reads from hb_base on) or
@@ -628,6 +655,7 @@ int burst_push_batch(BurstGroup *g, const int16_t *src, size_t n, size_t ld, int
   if (!n) return AERO_OK;
   if (nch > g->nch) return AERO_E_INVALID;
   BCHK(hipSetDevice(g->device));
+  if (int rc = flush_init(g)) return rc;
   const int C = g->C;
   if ((long long)n > B_PCM_CAP / 2) return AERO_E_FULL;
   bool need_run = false;

@@ -44,6 +44,13 @@ MODES = {
                        timing='burst_demod', burst=True, preroll=4,
                        metric='Msamples/s demod+Viterbi, 10500bps burst OQPSK (C4); R/T packets bit-exact vs ref',
                        cpu_seconds=240.0, config='C4', flops=1300.0),
+    # burst MSK (aero-decode -b 1200 --burst: one fb = 1200 demodulator at 48 kHz), the C4
+    # accounting: 2 B int16 in + 16 B AGC ring r/w (48000-deep) + soft bits out; a step is one
+    # 12000-sample message per channel
+    'burstmsk1200': dict(bitrate=1200, hop=12000, fs=48000, bytes=18.05, kernel='demod_bmsk_kernel',
+                         timing='burst_demod', burst=True, preroll=4,
+                         metric='Msamples/s demod+Viterbi, 1200bps burst MSK; R/T packets bit-exact vs ref',
+                         cpu_seconds=240.0, config='f1 (burst MSK 1200)', flops=900.0),
     # 2 B int16 in + 0.025 B soft bits out (fb stays 600 at 24 kHz, decode/decode.cpp:142-150)
     'msk1200': dict(bitrate=1200, hop=2048, fs=24000, bytes=2.025, kernel='demod_msk_kernel<2>',
                     timing='msk1200_demod', metric='Msamples/s demod+Viterbi, 1200bps MSK; ACARS frames bit-exact vs ref',
@@ -66,7 +73,7 @@ CALIBRATION = {'oqpsk10500': {'port_msps_per_core': 0.967, 'reference_msps_per_c
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--mode', default='oqpsk10500', choices=sorted(MODES) + ['c5'],
+    ap.add_argument('--mode', default='oqpsk10500', choices=sorted(MODES) + ['c1', 'c5'],
                     help='channel kind (default: the BASELINE.json headline, C2 10500-bps OQPSK)')
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5,
@@ -87,6 +94,10 @@ def parse():
 
 def synth_one(M, seconds, seed, k=0, lead_in=0):
     import aero_testlib as tl
+    if M.get('burst') and M['bitrate'] != 10500:
+        # 1200-baud MSK R/T bursts every 1-3 s near 2.5 kHz
+        return tl.synth_burst_msk(seconds=seconds, bitrate=M['bitrate'], seed=seed, carrier=2500.0 + 3.0 * (k % 64),
+                                  ebn0=14.0, phase0=0.1 * k, lead_in=lead_in or 24000)
     if M.get('burst'):
         # C4: R/T bursts every 1-3 s on a carrier near 12 kHz (the burst demod has no hunter)
         return tl.synth_burst(seconds=seconds, seed=seed, carrier=12000.0 + 0.5 * (k % 64), ebn0=14.0,
@@ -345,6 +356,90 @@ def run_c5(a, rank, world, local):
         dist.destroy_process_group()
 
 
+C1_SECONDS = 60.0  # one VFO of synthetic 10500-bps audio, published as fast as ZeroMQ takes it
+
+
+def run_c1(a):
+    """C1 end to end: the drop-in binaries on one VFO, ZeroMQ
+    loopback PUB (tools/zmq_pcm_pub, aero-publish's wire format) -> SUB
+    bin/aero-decode -> ACARS JSON lines, timed from the publisher's first
+    message to the last expected item; beside it the oracle decoding the same
+    audio on one core (the reference runs one process per VFO).  A single VFO
+    is one lane of one wave on the GPU: this measures the binary path and its
+    per-sample latency, not GPU throughput (that is the C2 line)."""
+    import signal
+    import socket
+    import subprocess
+    import tempfile
+    import threading
+    import aero_testlib as tl
+    M = MODES['oqpsk10500']
+    pcm = tl.synth(seconds=C1_SECONDS, seed=0xC100, carrier=12037.5, ebn0=12.0)
+    o = tl.Oracle()
+    t = time.perf_counter()
+    o.push_chunked(pcm, 12000)
+    t_cpu = time.perf_counter() - t
+    want = len(o.item_lines('A'))
+    bindir = os.path.join(ROOT, 'aero-cli_amd', 'bin')
+    pub = os.path.join(ROOT, 'tools', 'zmq_pcm_pub')
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    tmp = tempfile.mkdtemp(prefix='aero_c1_')
+    f = os.path.join(tmp, 'vfo.pcm')
+    pcm.astype('<i2').tofile(f)
+    dec = subprocess.Popen([os.path.join(bindir, 'aero-decode'), '-p', 'tcp://127.0.0.1:%d' % port, '-t', 'VFO01',
+                            '-b', '10500', '--format', 'jsondump', '-s', 'BENCH', '-v'],
+                           stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    lines, stamps = [], []
+
+    def pump():
+        for raw in dec.stderr:
+            lines.append(raw.decode('utf-8', 'replace'))
+            stamps.append(time.perf_counter())
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    t_wait = time.perf_counter()
+    while not any('Listening for samples' in l for l in lines):
+        if dec.poll() is not None or time.perf_counter() - t_wait > 180:
+            sys.exit('bench c1: aero-decode did not start:\n' + ''.join(lines[-20:]))
+        time.sleep(0.05)
+    wait_ms = 1000
+    t_pub = time.perf_counter()
+    pp = subprocess.Popen([pub, '--bind', 'tcp://127.0.0.1:%d' % port, '--topic', 'VFO01', '--rate', '48000',
+                           '--chunk', '12000', '--wait-ms', str(wait_ms), f], stderr=subprocess.PIPE)
+    t0 = t_pub + wait_ms / 1000.0  # the publisher sends its first message after the slow-joiner wait
+    deadline = time.perf_counter() + 600
+    while sum(l.startswith('{') for l in lines) < want and time.perf_counter() < deadline and dec.poll() is None:
+        time.sleep(0.01)
+    got = [s for l, s in zip(lines, stamps) if l.startswith('{')]
+    t_end = got[-1] if got else time.perf_counter()
+    dec.send_signal(signal.SIGTERM)
+    dec.wait(timeout=120)
+    pp.wait(timeout=60)
+    th.join(timeout=10)
+    os.remove(f)
+    os.rmdir(tmp)
+    if len(got) < want:
+        sys.exit('bench c1: %d of %d ACARS items arrived' % (len(got), want))
+    elapsed = t_end - t0
+    out = {'metric': 'Msamples/s end-to-end ZeroMQ PUB -> aero-decode -> ACARS JSON, single 10500-bps VFO (C1)',
+           'value': round(len(pcm) / elapsed / 1e6, 4), 'unit': 'Msamples/s', 'n_gpus': 1, 'steps': 1, 'warmup': 0,
+           'ms_per_step': round(elapsed * 1e3, 1), 'higher_is_better': True, 'scaling': 'none', 'vs_baseline': None,
+           'dtype': 'f64', 'data': 'synthetic',
+           'config': {'workload': 'C1: one VFO, %.0f s of synthetic 48 kHz int16 10500-bps P-channel in 12000-sample '
+                                  'ZeroMQ messages, published without pacing' % C1_SECONDS,
+                      'binary': 'aero-cli_amd/bin/aero-decode --format jsondump', 'items': len(got)},
+           'realtime_factor': round(C1_SECONDS / elapsed, 2),
+           'timing_note': 'first message (publisher start + %d ms slow-joiner wait) to the last ACARS JSON line; '
+                          'the audio after the last frame is counted as processed' % wait_ms,
+           'roofline': None,
+           'cpu_baseline': {'value': round(len(pcm) / t_cpu / 1e6, 4), 'unit': 'Msamples/s', 'cores': 1,
+                            'kind': 'port', 'sample': 'the same %.0f s through oracle/liboracle.so in one process'
+                                                      % C1_SECONDS, 'cpu_model': cpu_model()}}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     a = parse()
     if a.gpus > 1 and 'RANK' not in os.environ:
@@ -354,6 +449,10 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', 0))
     if a.mode == 'c5':
         return run_c5(a, rank, world, local)
+    if a.mode == 'c1':
+        if rank == 0:
+            run_c1(a)
+        return None
     import shard
     M = MODES[a.mode]
     HOP, FS = M['hop'], M['fs']
@@ -448,9 +547,10 @@ def main():
             'warmup': a.warmup, 'preroll_hops': preroll, 'ms_per_step': round(elapsed / a.steps * 1e3, 3),
             'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
-            'config': {'workload': ('%s x %d: independent single-VFO %d-bps burst OQPSK R/T channels per GPU, '
+            'config': {'workload': ('%s x %d: independent single-VFO %d-bps burst %s R/T channels per GPU, '
                                     '%d Hz int16, one %d-sample message per channel per step' % (
-                                        M['config'], C, M['bitrate'], FS, HOP)) if burst else (
+                                        M['config'], C, M['bitrate'], 'OQPSK' if M['bitrate'] == 10500 else 'MSK',
+                                        FS, HOP)) if burst else (
                                    '%s x %d: independent single-VFO %d-bps continuous %s P-channels '
                                    'per GPU, %d Hz int16, one %d-sample hop per step' % (
                                        M['config'], C, M['bitrate'], 'OQPSK' if M['bitrate'] == 10500 else 'MSK',
