@@ -200,48 +200,54 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         lastmse = mse;
         chunk_h++;
       }
+      // every ring slot (and Delay weight) this sample reads, loaded before
+      // any of its stores so the round trips overlap; none is the slot
+      // written this sample (burst_dev.h dly_pre)
+      const int d1r = d1_p + 1 == B_D1 ? 0 : d1_p + 1, d2r = d2_p + 1 == B_D2 ? 0 : d2_p + 1;
+      const int p1r = pd1_p + 1 == B_PD1 ? 0 : pd1_p + 1, p2r = pd2_p + 1 == B_PD2 ? 0 : pd2_p + 1;
+      double2 *btr = reinterpret_cast<double2 *>(S.dl[BDL_BT]) + c;
       const double2 a = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
+      const double agc_old = S.agc[(size_t)agc_p * C + c];
+      const double2 cvd = S.d1[(size_t)d1r * C + c];  // d1.update_dont_touch(cval)
+      vtd = S.d2[(size_t)d2r * C + c];                 // d2.update_dont_touch(real(cval_d))
+      const DlyPre2 btp = dly_pre2(btr, C, dlp[BDL_BT], dBT);
+      const double2 ma_old = S.ma1[(size_t)ma1_p * C + c];
+      const double mv_old = S.mav1[(size_t)mav1_p * C + c];
+      const DlyPre mdp = dly_pre(S.dl[BDL_MADIFF] + c, C, dlp[BDL_MADIFF], dMD);
+      const double pd1_old = S.pd1[(size_t)p1r * C + c], pd2_old = S.pd2[(size_t)p2r * C + c];
       double cr = a.x, ci = a.y;
       {  // agc.Update(|cval|); cval *= AGCVal (:316-317)
         const double av = aero_hypot(cr, ci);
-        double *ring = S.agc + (size_t)agc_p * C + c;
-        agc_sum = agc_sum - *ring;
+        agc_sum = agc_sum - agc_old;
         agc_sum = agc_sum + fabs(av);
-        *ring = fabs(av);
+        S.agc[(size_t)agc_p * C + c] = fabs(av);
         agc_p = agc_p + 1 == B_AGC ? 0 : agc_p + 1;
         double g = 1.414213562 / fmax(agc_sum / ((double)B_AGC), 0.000001);
         g = fmax(g, 0.000001);
         cr *= g;
         ci *= g;
       }
-      double2 cvd;  // d1.update_dont_touch(cval)
       S.d1[(size_t)d1_p * C + c] = make_double2(cr, ci);
-      d1_p = d1_p + 1 == B_D1 ? 0 : d1_p + 1;
-      cvd = S.d1[(size_t)d1_p * C + c];
-      S.d2[(size_t)d2_p * C + c] = cvd.x;  // d2.update_dont_touch(real(cval_d))
-      d2_p = d2_p + 1 == B_D2 ? 0 : d2_p + 1;
-      vtd = S.d2[(size_t)d2_p * C + c];
+      d1_p = d1r;
+      S.d2[(size_t)d2_p * C + c] = cvd.x;
+      d2_p = d2r;
       double fastarm;
       {  // burst-timing statistic (:326-339)
-        const double2 bd = dly_update2(reinterpret_cast<double2 *>(S.dl[BDL_BT]) + c, C, dlp[BDL_BT], dBT,
-                                       make_double2(cr, ci));
+        const double2 bd = dly_commit2(btr, C, dlp[BDL_BT], btp, make_double2(cr, ci));
         const double pr = cr * bd.x - ci * (-bd.y), pi = cr * (-bd.y) + ci * bd.x;  // cval * conj(bd)
-        double2 *mr = S.ma1 + (size_t)ma1_p * C + c;
-        const double2 old = *mr;
-        ma1r = ma1r - old.x;
-        ma1i = ma1i - old.y;
+        ma1r = ma1r - ma_old.x;
+        ma1i = ma1i - ma_old.y;
         ma1r = ma1r + pr;
         ma1i = ma1i + pi;
-        *mr = make_double2(pr, pi);
+        S.ma1[(size_t)ma1_p * C + c] = make_double2(pr, pi);
         ma1_p = ma1_p + 1 == B_MA ? 0 : ma1_p + 1;
         fastarm = aero_hypot(ma1r / ((double)B_MA), ma1i / ((double)B_MA));
-        double *mv = S.mav1 + (size_t)mav1_p * C + c;
-        mav1_sum = mav1_sum - *mv;
+        mav1_sum = mav1_sum - mv_old;
         mav1_sum = mav1_sum + (fastarm);
-        *mv = fastarm;
+        S.mav1[(size_t)mav1_p * C + c] = fastarm;
         mav1_p = mav1_p + 1 == B_MA ? 0 : mav1_p + 1;
         fastarm = mav1_sum / ((double)B_MA);
-        fastarm -= dly_update(S.dl[BDL_MADIFF] + c, C, dlp[BDL_MADIFF], dMD, fastarm);
+        fastarm -= dly_commit(S.dl[BDL_MADIFF] + c, C, dlp[BDL_MADIFF], mdp, fastarm);
         if (fastarm < 0) fastarm = 0;
       }
       double bt = fastarm * fastarm;
@@ -251,13 +257,12 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         double *r3 = S.pd3 + (size_t)pd3_p * C + c;
         *r3 = val;
         pd3_p = pd3_p + 1 == B_PD3 ? 0 : pd3_p + 1;
-        double *r1 = S.pd1 + (size_t)pd1_p * C + c;
-        *r1 = val;
-        pd1_p = pd1_p + 1 == B_PD1 ? 0 : pd1_p + 1;
-        const double dy = val - S.pd1[(size_t)pd1_p * C + c];
+        S.pd1[(size_t)pd1_p * C + c] = val;
+        pd1_p = p1r;
+        const double dy = val - pd1_old;
         S.pd2[(size_t)pd2_p * C + c] = val;
-        pd2_p = pd2_p + 1 == B_PD2 ? 0 : pd2_p + 1;
-        val = S.pd2[(size_t)pd2_p * C + c];  // d2.update(val)
+        pd2_p = p2r;
+        val = pd2_old;  // d2.update(val)
         if ((!pd_cntdown) && (val > 0.2) && ((pd_lastdy >= 0 && dy < 0))) {
           pd_cntdown = B_PD_MAXCD;
           // d3.findmaxpos: first maximum, scanning from the oldest slot
@@ -331,7 +336,14 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       resume = false;
       pend = 0;
     }
-    // ---- part B (:450-702)
+    // ---- part B (:450-702); its ring and weight reads first (a1's whatever
+    // the symbol-tone window says: a read changes nothing)
+    const double agc2_old = S.agc2[(size_t)agc2_p * C + c];
+    const DlyPre pS = dly_pre(S.dl[BDL_S] + c, C, dlp[BDL_S], dS);
+    const DlyPre p41 = dly_pre(S.dl[BDL_41] + c, C, dlp[BDL_41], d41);
+    const DlyPre p42 = dly_pre(S.dl[BDL_42] + c, C, dlp[BDL_42], d42);
+    const DlyPre p8 = dly_pre(S.dl[BDL_8] + c, C, dlp[BDL_8], d8);
+    const DlyPre pA1 = dly_pre(S.dl[BDL_A1] + c, C, dlp[BDL_A1], dA1);
     double s2r, s2i;
     {
       const double2 m2 = T.cis[b_cis_index(m2_ptr)];
@@ -371,7 +383,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       str_i = ni;
       ave_r = ave_r * 0.95 + 0.05 * str_r;
       ave_i = ave_i * 0.95 + 0.05 * str_i;
-      const double spi2 = dly_update(S.dl[BDL_A1] + c, C, dlp[BDL_A1], dA1, spr);
+      const double spi2 = dly_commit(S.dl[BDL_A1] + c, C, dlp[BDL_A1], pA1, spr);
       const double2 qv = T.cis[b_cis_index(q_ptr)];
       const double er_r = qv.x * spr - qv.y * (-spi2), er_i = qv.x * (-spi2) + qv.y * spr;
       double st_err = aero_atan2(er_i, er_r);
@@ -391,10 +403,9 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     }
     {  // agc2 (AGC(SPS*64/Fs)) and clip (:478-481)
       const double sa = aero_hypot(s2r, s2i);
-      double *ring = S.agc2 + (size_t)agc2_p * C + c;
-      agc2_sum = agc2_sum - *ring;
+      agc2_sum = agc2_sum - agc2_old;
       agc2_sum = agc2_sum + fabs(sa);
-      *ring = fabs(sa);
+      S.agc2[(size_t)agc2_p * C + c] = fabs(sa);
       agc2_p = agc2_p + 1 == B_AGC2 ? 0 : agc2_p + 1;
       double g = 1.414213562 / fmax(agc2_sum / ((double)B_AGC2), 0.000001);
       g = fmax(g, 0.000001);
@@ -408,9 +419,9 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       s2i = k * s2i;
     }
     {  // symbol timing (:482-496)
-      const double st_diff = dly_update(S.dl[BDL_S] + c, C, dlp[BDL_S], dS, abval * abval) - (abval * abval);
-      const double st_d1out = dly_update(S.dl[BDL_41] + c, C, dlp[BDL_41], d41, st_diff);
-      const double st_d2out = dly_update(S.dl[BDL_42] + c, C, dlp[BDL_42], d42, st_d1out);
+      const double st_diff = dly_commit(S.dl[BDL_S] + c, C, dlp[BDL_S], pS, abval * abval) - (abval * abval);
+      const double st_d1out = dly_commit(S.dl[BDL_41] + c, C, dlp[BDL_41], p41, st_diff);
+      const double st_d2out = dly_commit(S.dl[BDL_42] + c, C, dlp[BDL_42], p42, st_d1out);
       double st_eta = (st_d2out - st_diff) * st_d1out;
       {  // st_iir_resonator.update(st_eta)
         double y = 0;
@@ -425,7 +436,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         sry1 = y;
         if (cntr > SPS * (128 + 128)) st_eta = y;
       }
-      const double m1r = st_eta, m1i = -dly_update(S.dl[BDL_8] + c, C, dlp[BDL_8], d8, st_eta);
+      const double m1r = st_eta, m1i = -dly_commit(S.dl[BDL_8] + c, C, dlp[BDL_8], p8, st_eta);
       const double2 so = T.cis[b_cis_index(so_ptr)];
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
       const double st_angle_error = aero_atan2(oim, ore);

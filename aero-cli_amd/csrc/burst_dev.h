@@ -86,6 +86,42 @@ __device__ __forceinline__ double2 dly_update2(double2 *ring, int C, int &p, con
 __device__ __forceinline__ DlyRef dref(const BurstTables &T, int k) { return {T.dw[k], T.domw[k], T.dio[k], T.dsize[k]}; }
 
 
+// Delay<T>::update split in two so a sample's ring reads can all be issued
+// before its stores: dly_pre reads the slots the update at write pointer p
+// will read (older = p + 1, newer = p + 2 mod size, which the host checks
+// against the reference's pointer arithmetic, burst_engine.hip) and the
+// pointer's weights; dly_commit writes sig and returns the weighted sum.  On a
+// 2-slot ring "newer" is the slot written now: its value is sig.
+struct DlyPre {
+  double w, om, older, newer;
+  int next;
+  bool newer_is_sig;
+};
+__device__ __forceinline__ DlyPre dly_pre(const double *ring, int C, int p, const DlyRef &d) {
+  const int io = p + 1 == d.size ? 0 : p + 1, in = io + 1 == d.size ? 0 : io + 1;
+  return {d.w[p], d.omw[p], ring[(size_t)io * C], ring[(size_t)in * C], io, in == p};
+}
+__device__ __forceinline__ double dly_commit(double *ring, int C, int &p, const DlyPre &r, double sig) {
+  ring[(size_t)p * C] = sig;
+  p = r.next;
+  const double newer = r.newer_is_sig ? sig : r.newer;
+  return (r.w * newer + r.om * r.older);
+}
+struct DlyPre2 {
+  double w, om;
+  double2 older, newer;
+  int next;
+};
+__device__ __forceinline__ DlyPre2 dly_pre2(const double2 *ring, int C, int p, const DlyRef &d) {
+  const int io = p + 1 == d.size ? 0 : p + 1, in = io + 1 == d.size ? 0 : io + 1;
+  return {d.w[p], d.omw[p], ring[(size_t)io * C], ring[(size_t)in * C], io};
+}
+__device__ __forceinline__ double2 dly_commit2(double2 *ring, int C, int &p, const DlyPre2 &r, double2 sig) {
+  ring[(size_t)p * C] = sig;
+  p = r.next;
+  return make_double2(r.w * r.newer.x + r.om * r.older.x, r.w * r.newer.y + r.om * r.older.y);
+}
+
 // Delay<T>::update with an integer delay D on a ring of D + 1 slots: the
 // weighting is exactly 0, and the reference's sum is kept literally
 // (0 * newer + 1 * older) so signed zeros come out the same

@@ -470,6 +470,11 @@ int burst_group_create(int device, int flags, int max_channels, int kind, BurstG
     std::vector<int> io(1172);
     const int size = host_delay_table(fds[k], w.data(), omw.data(), io.data(), 1172);
     if (size <= 0) return AERO_E_INVALID;
+    // burst_dev.h dly_pre reads slots p + 1 and p + 2: the reference's older
+    // slot must be p + 1 for every write pointer p
+    for (int q = 0; q < size; q++)
+      if (io[q] != (q + 1) % size) return AERO_E_INVALID;
+    if (k == BDL_BT && size <= 2) return AERO_E_INVALID;  // dly_pre2 has no newer-is-sig case
     g->T.dsize[k] = size;
     if (int rc = h2d(g->T.dw[k], w)) return rc;
     if (int rc = h2d(g->T.domw[k], omw)) return rc;

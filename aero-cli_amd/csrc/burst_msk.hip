@@ -127,47 +127,61 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
     double vtd;  // val_to_demod
     if (!resume) {
       if (sp - scons > B_SOFT_RING - 64) break;  // soft ring full: framing frees it next
+      // every ring slot this sample reads, loaded before any of its stores so
+      // the round trips overlap (the compiler cannot hoist a load above a
+      // store to another ring it cannot prove distinct); no slot read here is
+      // the one written this sample (rings hold > 2 slots)
+      const int d1r = d1_p + 1 == M_D1 ? 0 : d1_p + 1, d2r = d2_p + 1 == M_D2 ? 0 : d2_p + 1;
+      const int bto = btd_p + 1 == M_BTD ? 0 : btd_p + 1, btn = bto + 1 == M_BTD ? 0 : bto + 1;
+      const int mdo = madiff_p + 1 == M_MADIFF ? 0 : madiff_p + 1, mdn = mdo + 1 == M_MADIFF ? 0 : mdo + 1;
+      const int p1r = pd1_p + 1 == M_PD1 ? 0 : pd1_p + 1, p2r = pd2_p + 1 == M_PD2 ? 0 : pd2_p + 1;
       const double2 a = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
+      const double agc_old = S.agc[(size_t)agc_p * C + c];
+      const double2 cvd = S.d1[(size_t)d1r * C + c];  // d1.update_dont_touch(cval)
+      vtd = S.d2[(size_t)d2r * C + c];                 // d2.update_dont_touch(real(cval_d))
+      const double2 bt_old = btd[(size_t)bto * C], bt_new = btd[(size_t)btn * C];
+      const double2 ma_old = S.ma1[(size_t)ma1_p * C + c];
+      const double mv_old = S.mav1[(size_t)mav1_p * C + c];
+      const double md_old = madiff[(size_t)mdo * C], md_new = madiff[(size_t)mdn * C];
+      const double pd1_old = S.pd1[(size_t)p1r * C + c], pd2_old = S.pd2[(size_t)p2r * C + c];
       double cr = a.x, ci = a.y;
       {  // agc->Update(abs(cval)); cval *= agc->AGCVal (:366-368)
         const double av = aero_hypot(cr, ci);
-        double *ring = S.agc + (size_t)agc_p * C + c;
-        agc_sum = agc_sum - *ring;
+        agc_sum = agc_sum - agc_old;
         agc_sum = agc_sum + fabs(av);
-        *ring = fabs(av);
+        S.agc[(size_t)agc_p * C + c] = fabs(av);
         agc_p = agc_p + 1 == B_AGC ? 0 : agc_p + 1;
         double g = 1.414213562 / fmax(agc_sum / ((double)B_AGC), 0.000001);
         g = fmax(g, 0.000001);
         cr *= g;
         ci *= g;
       }
-      double2 cvd;  // d1.update_dont_touch(cval)
       S.d1[(size_t)d1_p * C + c] = make_double2(cr, ci);
-      d1_p = d1_p + 1 == M_D1 ? 0 : d1_p + 1;
-      cvd = S.d1[(size_t)d1_p * C + c];
-      S.d2[(size_t)d2_p * C + c] = cvd.x;  // d2.update_dont_touch(real(cval_d))
-      d2_p = d2_p + 1 == M_D2 ? 0 : d2_p + 1;
-      vtd = S.d2[(size_t)d2_p * C + c];
+      d1_p = d1r;
+      S.d2[(size_t)d2_p * C + c] = cvd.x;
+      d2_p = d2r;
       double fastarm;
-      {  // burst-timing statistic (:376-385)
-        const double2 bd = dly_int2(btd, C, btd_p, M_BTD, 40, make_double2(cr, ci));
+      {  // burst-timing statistic (:376-385); bt_d1 = Delay(SPS): weights 0 / 1 (dly_int2)
+        btd[(size_t)btd_p * C] = make_double2(cr, ci);
+        btd_p = bto;
+        const double2 bd = make_double2(0.0 * bt_new.x + (1.0 - 0.0) * bt_old.x,
+                                        0.0 * bt_new.y + (1.0 - 0.0) * bt_old.y);
         const double pr = cr * bd.x - ci * (-bd.y), pi = cr * (-bd.y) + ci * bd.x;  // cval * conj(bd)
-        double2 *mr = S.ma1 + (size_t)ma1_p * C + c;
-        const double2 old = *mr;
-        ma1r = ma1r - old.x;
-        ma1i = ma1i - old.y;
+        ma1r = ma1r - ma_old.x;
+        ma1i = ma1i - ma_old.y;
         ma1r = ma1r + pr;
         ma1i = ma1i + pi;
-        *mr = make_double2(pr, pi);
+        S.ma1[(size_t)ma1_p * C + c] = make_double2(pr, pi);
         ma1_p = ma1_p + 1 == M_MA ? 0 : ma1_p + 1;
         fastarm = aero_hypot(ma1r / ((double)M_MA), ma1i / ((double)M_MA));
-        double *mv = S.mav1 + (size_t)mav1_p * C + c;
-        mav1_sum = mav1_sum - *mv;
+        mav1_sum = mav1_sum - mv_old;
         mav1_sum = mav1_sum + (fastarm);
-        *mv = fastarm;
+        S.mav1[(size_t)mav1_p * C + c] = fastarm;
         mav1_p = mav1_p + 1 == M_MA ? 0 : mav1_p + 1;
         fastarm = mav1_sum / ((double)M_MA);
-        fastarm -= dly_int(madiff, C, madiff_p, M_MADIFF, 5040, fastarm);
+        madiff[(size_t)madiff_p * C] = fastarm;  // bt_ma_diff.update(fastarm), whole-sample delay
+        madiff_p = mdo;
+        fastarm -= (0.0 * md_new + (1.0 - 0.0) * md_old);
         if (fastarm < 0) fastarm = 0;
       }
       double bt = fastarm * fastarm;
@@ -177,13 +191,12 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         double *r3 = S.pd3 + (size_t)pd3_p * C + c;
         *r3 = val;
         pd3_p = pd3_p + 1 == M_PD3 ? 0 : pd3_p + 1;
-        double *r1 = S.pd1 + (size_t)pd1_p * C + c;
-        *r1 = val;
-        pd1_p = pd1_p + 1 == M_PD1 ? 0 : pd1_p + 1;
-        const double dy = val - S.pd1[(size_t)pd1_p * C + c];
+        S.pd1[(size_t)pd1_p * C + c] = val;
+        pd1_p = p1r;
+        const double dy = val - pd1_old;
         S.pd2[(size_t)pd2_p * C + c] = val;
-        pd2_p = pd2_p + 1 == M_PD2 ? 0 : pd2_p + 1;
-        val = S.pd2[(size_t)pd2_p * C + c];  // d2.update(val)
+        pd2_p = p2r;
+        val = pd2_old;  // d2.update(val)
         if ((!pd_cntdown) && (val > 0.1) && ((pd_lastdy >= 0 && dy < 0))) {
           pd_cntdown = M_PD_MAXCD;
           // d3.findmaxpos: first maximum, scanning from the oldest slot
@@ -286,6 +299,19 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       mse = 1;
     }
     if (startstop > 0 || mse < 0.6) {  // the demodulator proper (:547-700)
+      // this part's ring reads first, as in the front end
+      const bool tone = cntr > (M_START * MSPS) && cntr < M_ENDROT;
+      const int dsr = dsm_p + 1 == M_DSM ? 0 : dsm_p + 1;
+      const int d8o = d8_p + 1 == M_D8 ? 0 : d8_p + 1, d8n = d8o + 1 == M_D8 ? 0 : d8o + 1;
+      const int a1o = a1_p + 1 == M_A1 ? 0 : a1_p + 1, a1n = a1o + 1 == M_A1 ? 0 : a1o + 1;
+      const double agc2_old = S.agc2[(size_t)agc2_p * C + c];
+      const double2 pd_slot = dsm[(size_t)dsr * C];
+      const double d8_old = d8[(size_t)d8o * C], d8_new = d8[(size_t)d8n * C];
+      double a1_old = 0.0, a1_new = 0.0;
+      if (tone) {
+        a1_old = a1[(size_t)a1o * C];
+        a1_new = a1[(size_t)a1n * C];
+      }
       double s2r, s2i;
       {
         const double2 m2 = T.cis[b_cis_index(m2_ptr)];
@@ -302,7 +328,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         s_qre[0][col] = 0.0 + c_mtaps[0] * cr;
         s_qim[0][col] = 0.0 + c_mtaps[0] * ci;
       }
-      if (cntr > (M_START * MSPS) && cntr < M_ENDROT) {  // symbol-tone x4 PLL (:555-578)
+      if (tone) {  // symbol-tone x4 PLL (:555-578)
         const double t1r = s2r * str_r - s2i * str_i, t1i = s2r * str_i + s2i * str_r;
         const double spr = t1r * 0.0 - t1i * 1.0, spi = t1r * 1.0 + t1i * 0.0;  // * imag
         const double er = aero_tanh(spi) * (spr);
@@ -313,7 +339,9 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         str_i = ni;
         ave_r = ave_r * 0.999 + 0.001 * str_r;
         ave_i = ave_i * 0.999 + 0.001 * str_i;
-        const double spi2 = dly_int(a1, C, a1_p, M_A1, 20, spr);
+        a1[(size_t)a1_p * C] = spr;  // a1.update(spr), whole-sample delay (dly_int)
+        a1_p = a1o;
+        const double spi2 = (0.0 * a1_new + (1.0 - 0.0) * a1_old);
         double progress = (double)cntr - (MSPS * (M_START));
         const double goal = M_ENDROT - (MSPS * M_START);
         progress = progress / goal;
@@ -336,10 +364,9 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       }
       {  // agc2 and clip (:592-598)
         const double sa = aero_hypot(s2r, s2i);
-        double *ring = S.agc2 + (size_t)agc2_p * C + c;
-        agc2_sum = agc2_sum - *ring;
+        agc2_sum = agc2_sum - agc2_old;
         agc2_sum = agc2_sum + fabs(sa);
-        *ring = fabs(sa);
+        S.agc2[(size_t)agc2_p * C + c] = fabs(sa);
         agc2_p = agc2_p + 1 == M_AGC2 ? 0 : agc2_p + 1;
         double g = 1.414213562 / fmax(agc2_sum / ((double)M_AGC2), 0.000001);
         g = fmax(g, 0.000001);
@@ -355,10 +382,9 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       double pdr, pdi;  // pt_d = delayedsmpl.update_dont_touch(sig2)
       {
         dsm[(size_t)dsm_p * C] = make_double2(s2r, s2i);
-        dsm_p = dsm_p + 1 == M_DSM ? 0 : dsm_p + 1;
-        const double2 o = dsm[(size_t)dsm_p * C];
-        pdr = o.x;
-        pdi = o.y;
+        dsm_p = dsr;
+        pdr = pd_slot.x;
+        pdi = pd_slot.y;
       }
       double st_eta = aero_hypot(s2r, pdi);  // abs(pt_msk), pt_msk = (sig2.re, pt_d.im)
       {  // st_iir_resonator.update (DSP.cpp:635-685)
@@ -375,7 +401,9 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         sry1 = y;
         st_eta = y;
       }
-      const double m1r = st_eta, m1i = -dly_int(d8, C, d8_p, M_D8, 20, st_eta);
+      d8[(size_t)d8_p * C] = st_eta;  // delayt8.update(st_eta), whole-sample delay (dly_int)
+      d8_p = d8o;
+      const double m1r = st_eta, m1i = -(0.0 * d8_new + (1.0 - 0.0) * d8_old);
       const double2 so = T.cis[b_cis_index(so_ptr)];
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
       const double st_angle_error = aero_atan2(oim, ore);
