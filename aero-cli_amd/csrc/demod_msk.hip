@@ -143,7 +143,14 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
     bool pend = false;
     do {
       const long long n = n0 + i;
+      // this sample's ring reads before any of its stores, so their round
+      // trips overlap (the rings are distinct, the compiler cannot prove it);
+      // no slot read is the slot written this sample
       const int16_t xs = S.pcm[(size_t)(n & capm) * C + c];
+      const double agc_old = S.agc[(size_t)(n % AGC) * C + c];
+      const double2 dsm_old = S.dsm[(size_t)((n + 1) % DSM) * C + c];
+      const double d8_older = S.d8[(size_t)((n + 1) % D8) * C + c];
+      const double d8_newer = S.d8[(size_t)((n + 2) % D8) * C + c];
       const double dval = ((double)xs) / 32768.0;
       const double2 cm = T.cis[cis_index(m2_ptr)];
       const double cv = cm.x * dval, cvi = cm.y * dval;  // mixer2.WTCISValue() * dval
@@ -160,11 +167,9 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       s_qim[0][lane] = 0.0 + s_taps[0] * cvi;
       const double dab = sqrt(s2r * s2r + s2i * s2i);
       {  // AGC::Update (DSP.cpp:371-380)
-        const int ap = (int)(n % AGC);
-        double *slot = S.agc + (size_t)ap * C + c;
-        agc_sum = agc_sum - *slot;
+        agc_sum = agc_sum - agc_old;
         agc_sum = agc_sum + fabs(dab);
-        *slot = fabs(dab);
+        S.agc[(size_t)(n % AGC) * C + c] = fabs(dab);
         double g = 1.414213562 / fmax(agc_sum / ((double)AGC), 0.000001);
         g = fmax(g, 0.000001);
         s2r *= g;
@@ -180,9 +185,8 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       double pdr, pdi;
       {
         S.dsm[(size_t)(n % DSM) * C + c] = make_double2(s2r, s2i);
-        const double2 o = S.dsm[(size_t)((n + 1) % DSM) * C + c];
-        pdr = o.x;
-        pdi = o.y;
+        pdr = dsm_old.x;
+        pdi = dsm_old.y;
       }
       // st_eta = resonator(|pt_msk|), pt_msk = (sig2.re, pt_d.im)
       double st_eta;
@@ -204,9 +208,7 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       double d8v;
       {
         S.d8[(size_t)(n % D8) * C + c] = st_eta;
-        const double older = S.d8[(size_t)((n + 1) % D8) * C + c];
-        const double newer = S.d8[(size_t)((n + 2) % D8) * C + c];
-        d8v = (d8w * newer + d8omw * older);
+        d8v = (d8w * d8_newer + d8omw * d8_older);
       }
       const double m1r = st_eta, m1i = -d8v;
       const double2 so = T.cis[cis_index(so_ptr)];
