@@ -43,6 +43,7 @@ constexpr uint32_t BUW = 0xE15AE893u;
 
 __constant__ double c_bsr_b[3];  // st_iir_resonator (burstoqpskdemodulator.cpp:220-227)
 __constant__ double c_bsr_a[3];
+__constant__ double c_btaps[NTAPS];  // RRC (burstoqpskdemodulator.cpp:199-201)
 
 }  // namespace
 
@@ -128,15 +129,17 @@ __global__ __launch_bounds__(512) void hilbert_kernel(BurstState S, BurstTables 
 }
 
 // ----------------------------------------------------------------- demod
-constexpr int BD_BLOCK = 128;  // channels per workgroup: both RRC halves in LDS (110 KB)
+// One wave per workgroup.  The transposed RRC partial sums of taps
+// [BD_LDS_TAPS, 55) live in registers, the rest (real and imaginary) in LDS:
+// 40 x 2 x 8 B x 64 = 40 KB per wave, so four waves (one per SIMD) share a
+// CU and 65536 channels run in one round instead of two.
+constexpr int BD_BLOCK = 64;
+constexpr int BD_LDS_TAPS = 40, BD_REG_TAPS = NTAPS - BD_LDS_TAPS;
 
 __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, BurstTables T, int nch, int max_n,
                                                                int trace) {
-  __shared__ double s_qre[NTAPS][BD_BLOCK];
-  __shared__ double s_qim[NTAPS][BD_BLOCK];
-  __shared__ double s_taps[NTAPS];
-  if (threadIdx.x < NTAPS) s_taps[threadIdx.x] = T.taps[threadIdx.x];
-  __syncthreads();
+  __shared__ double s_qre[BD_LDS_TAPS][BD_BLOCK];
+  __shared__ double s_qim[BD_LDS_TAPS][BD_BLOCK];
   const int c = blockIdx.x * BD_BLOCK + threadIdx.x, col = threadIdx.x;
   if (c >= nch) return;
   const int C = S.C;
@@ -179,9 +182,15 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   long long chunk_h = ls[BL_CHUNK_H * C];
   const long long chunk_n = ls[BL_CHUNK_N * C];
 #pragma unroll 1
-  for (int j = 0; j < NTAPS; ++j) {
+  for (int j = 0; j < BD_LDS_TAPS; ++j) {
     s_qre[j][col] = S.fir[(size_t)j * C + c];
     s_qim[j][col] = S.fir[(size_t)(NTAPS + j) * C + c];
+  }
+  double hre[BD_REG_TAPS], him[BD_REG_TAPS];  // partial sums of taps BD_LDS_TAPS..54
+#pragma unroll
+  for (int j = 0; j < BD_REG_TAPS; ++j) {
+    hre[j] = S.fir[(size_t)(BD_LDS_TAPS + j) * C + c];
+    him[j] = S.fir[(size_t)(NTAPS + BD_LDS_TAPS + j) * C + c];
   }
   int16_t *soft = S.soft + (size_t)c * B_SOFT_RING;
   const long long *chunks = S.chunks + (size_t)c * CHUNK_RING;
@@ -350,14 +359,21 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       const double sc = vol_gain * vtd;
       const double ddr = m2.x * sc, ddi = m2.y * sc;
       // RRC, transposed form (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
-      s2r = s_qre[NTAPS - 1][col];
-      s2i = s_qim[NTAPS - 1][col];
-      for (int j = NTAPS - 1; j >= 1; --j) {
-        s_qre[j][col] = s_qre[j - 1][col] + s_taps[j] * ddr;
-        s_qim[j][col] = s_qim[j - 1][col] + s_taps[j] * ddi;
+      s2r = hre[BD_REG_TAPS - 1];
+      s2i = him[BD_REG_TAPS - 1];
+#pragma unroll
+      for (int j = NTAPS - 1; j > BD_LDS_TAPS; --j) {  // register part, descending: q[j - 1] read before rewritten
+        hre[j - BD_LDS_TAPS] = hre[j - 1 - BD_LDS_TAPS] + c_btaps[j] * ddr;
+        him[j - BD_LDS_TAPS] = him[j - 1 - BD_LDS_TAPS] + c_btaps[j] * ddi;
       }
-      s_qre[0][col] = 0.0 + s_taps[0] * ddr;
-      s_qim[0][col] = 0.0 + s_taps[0] * ddi;
+      hre[0] = s_qre[BD_LDS_TAPS - 1][col] + c_btaps[BD_LDS_TAPS] * ddr;
+      him[0] = s_qim[BD_LDS_TAPS - 1][col] + c_btaps[BD_LDS_TAPS] * ddi;
+      for (int j = BD_LDS_TAPS - 1; j >= 1; --j) {
+        s_qre[j][col] = s_qre[j - 1][col] + c_btaps[j] * ddr;
+        s_qim[j][col] = s_qim[j - 1][col] + c_btaps[j] * ddi;
+      }
+      s_qre[0][col] = 0.0 + c_btaps[0] * ddr;
+      s_qim[0][col] = 0.0 + c_btaps[0] * ddi;
     }
     if (startstop > 0) {
       startstop--;
@@ -530,9 +546,14 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   }
   // state back
 #pragma unroll 1
-  for (int j = 0; j < NTAPS; ++j) {
+  for (int j = 0; j < BD_LDS_TAPS; ++j) {
     S.fir[(size_t)j * C + c] = s_qre[j][col];
     S.fir[(size_t)(NTAPS + j) * C + c] = s_qim[j][col];
+  }
+#pragma unroll
+  for (int j = 0; j < BD_REG_TAPS; ++j) {
+    S.fir[(size_t)(BD_LDS_TAPS + j) * C + c] = hre[j];
+    S.fir[(size_t)(NTAPS + BD_LDS_TAPS + j) * C + c] = him[j];
   }
   ds[BD_M2_PTR * C] = m2_ptr;
   ds[BD_M2_STEP * C] = m2_step;
@@ -891,7 +912,8 @@ __global__ __launch_bounds__(64) void rt_viterbi_kernel(BurstState S) {
 }
 
 // ------------------------------------------------------------ launchers
-void burst_upload_constants(const double *sr_b, const double *sr_a) {
+void burst_upload_constants(const double *sr_b, const double *sr_a, const double *taps) {
+  hipMemcpyToSymbol(HIP_SYMBOL(c_btaps), taps, sizeof(double) * NTAPS);
   hipMemcpyToSymbol(HIP_SYMBOL(c_bsr_b), sr_b, sizeof(double) * 3);
   hipMemcpyToSymbol(HIP_SYMBOL(c_bsr_a), sr_a, sizeof(double) * 3);
 }

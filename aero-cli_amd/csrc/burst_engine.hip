@@ -32,7 +32,7 @@
 
 namespace aero {
 
-void burst_upload_constants(const double *sr_b, const double *sr_a);
+void burst_upload_constants(const double *sr_b, const double *sr_a, const double *taps);
 void launch_hk_spectrum(hipStream_t st, const BurstTables &T, double2 *hk);
 void launch_hilbert(hipStream_t st, const BurstState &S, const BurstTables &T, int nch);
 void launch_demod_burst(hipStream_t st, const BurstState &S, const BurstTables &T, int nch, int max_n, int trace);
@@ -487,7 +487,7 @@ int burst_group_create(int device, int flags, int max_channels, int kind, BurstG
   } else {
     const double sr_b[3] = {0.0048847995518126464, 0, -0.0048847995518126464};
     const double sr_a[3] = {1, -0.3882746897971619, 0.99023040089637471};
-    burst_upload_constants(sr_b, sr_a);
+    burst_upload_constants(sr_b, sr_a, taps.data());
   }
   launch_hk_spectrum(g->st, g->T, hk);
   BCHK(hipGetLastError());
