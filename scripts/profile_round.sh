@@ -3,7 +3,8 @@
 # own command, rocprofv3 kernel stats of that command, PMC HBM traffic of the
 # demod kernel at the bench config (FETCH_SIZE and WRITE_SIZE in separate
 # passes, MI355X_MICROARCH.md §HBM), then the burst (C4) and C5 lines with
-# their kernel stats.  Usage: bash scripts/profile_round.sh TAG
+# their kernel stats, C3 (msk600), burst MSK (f1) and the C1 end-to-end line.
+# Usage: bash scripts/profile_round.sh TAG
 set -eo pipefail
 TAG=$1
 R=$GRAFT_REPO_ROOT
@@ -24,4 +25,9 @@ find /tmp/profb_$TAG -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats_bur
 timeout -k 10 400 python3 $R/bench.py --mode c5 --steps 20 > $OUT/bench_c5.log 2>&1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/profc_$TAG -o prof -- python3 $R/bench.py --mode c5 --steps 20 --no-cpu-baseline > $OUT/bench_c5_prof.log 2>&1
 find /tmp/profc_$TAG -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats_c5.csv \;
+timeout -k 10 400 python3 $R/bench.py --mode msk600 --steps 20 > $OUT/bench_msk600.log 2>&1
+timeout -k 10 600 python3 $R/bench.py --mode burstmsk1200 --steps 6 > $OUT/bench_burstmsk.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/profm_$TAG -o prof -- python3 $R/bench.py --mode burstmsk1200 --steps 4 --no-cpu-baseline > $OUT/bench_burstmsk_prof.log 2>&1
+find /tmp/profm_$TAG -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats_burstmsk.csv \;
+timeout -k 10 400 python3 $R/bench.py --mode c1 > $OUT/bench_c1.log 2>&1
 ls -la $OUT
