@@ -237,8 +237,8 @@ __global__ __launch_bounds__(256) void frame_msk_kernel(DevState S, int nch) {
 // ---------------------------------------------------------------- Viterbi
 // BLK = interleaver block (N x 64 soft bits), N = BLK / 64; DL2 = dl2 length + 1.
 // One wave per job, ~5.8 KB of LDS and no per-step barrier
-// (viterbi_decode_regs), so Viterbi waves fit beside a demod or coarse
-// workgroup on the same CU and run on their own stream (engine.hip).
+// (viterbi_decode_regs), launched between a coarse hop and a demod launch
+// (engine.hip issue_viterbi).
 template <int BLK, int DL2>
 __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, int trace) {
   constexpr int NL = BLK / 64, HALF = BLK / 2;

@@ -135,9 +135,7 @@ enum { PI_MARG_P, PI_DT_P, PI_PM_P, PI_MS_P, PI_N };
 enum { PL_SOFTP, PL_PTN, PL_N };
 
 constexpr int DEMOD_BLOCK = 256;  // channels (= lanes) per workgroup
-// coarse-ring entries staged per channel before one 32-byte write; eight
-// (not sixteen) leave 11.8 KB of the CU's LDS free for two Viterbi waves
-// (aerol.hip) beside the demod workgroup
+// coarse-ring entries staged per channel before one 32-byte write
 constexpr int RING_GROUP = 8;
 
 template <bool TRACE>

@@ -20,6 +20,7 @@
 #include <cstring>
 #include <atomic>
 #include <chrono>
+#include <climits>
 #include <deque>
 #include <condition_variable>
 #include <functional>
@@ -240,7 +241,7 @@ struct Group {
     uint8_t *d_out = nullptr;   // [C][JOB_OUT] (device)
     int *d_n = nullptr;         // job count (device)
     int *d_jobs = nullptr;      // [C] int4 job list of this pass (device)
-    hipEvent_t ev_vit = nullptr;  // this pass's Viterbi done (side stream)
+    hipEvent_t ev_vit = nullptr;  // this pass's Viterbi done (main stream)
     hipEvent_t ev_framed = nullptr;  // this pass's framing done (main stream)
     bool trace_blocks = false;
     uint8_t *h_out = nullptr;   // pinned copy of the first `copied` records
@@ -261,22 +262,19 @@ struct Group {
   int16_t *pin_pcm = nullptr;
   size_t pin_pcm_cap = 0;
   hipEvent_t pin_pcm_ev = nullptr;
-  // device-pointer pushes: the caller's buffer is copied (side stream, the
-  // host waits for that copy only) into one of two staging buffers, which the
-  // compute stream's scatter then reads; a buffer is refilled only after the
-  // scatter that read it has run
+  // device-pointer pushes: the caller's rows are copied straight into the PCM
+  // ring on a high-priority side stream (the host waits for that copy only, so
+  // it can run beside a coarse or demod launch); the copy first waits for the
+  // demod launch that consumed the ring rows it overwrites: `consumed` holds
+  // (least nsamp over the channels after a demod launch, event after it)
   hipStream_t st_in = nullptr;
-  // Viterbi + frame hand-off run on their own stream: pass k's decoding
-  // overlaps pass k+1's demodulation (the Viterbi waves are small enough to
-  // share the CUs with the demod / coarse workgroups)
+  std::deque<std::pair<long long, hipEvent_t>> consumed;
+  std::vector<hipEvent_t> ev_free;
+  // the job records' copy back to the host runs on its own stream, beside
+  // the next pass's kernels
   hipStream_t st_vit = nullptr;
-  hipEvent_t ev_cut = nullptr;  // main stream past the next pass's coarse hop
   int vit_pending = -1;          // slot whose Viterbi launch is deferred
   hipEvent_t ev_in = nullptr;
-  int16_t *d_stage[2] = {};
-  size_t stage_cap[2] = {};
-  hipEvent_t ev_stage_used[2] = {};
-  int next_stage = 0;
   // aero_chan_feed job tables (pinned -> device, reused once their event completed)
   GatherJob *pin_gjobs[NPIN] = {}, *d_gjobs[NPIN] = {};
   hipEvent_t gjob_ev[NPIN] = {};
@@ -609,11 +607,12 @@ int collect_traces(Group *e) {
   return AERO_OK;
 }
 
-// The Viterbi of a pass (side stream) is launched once the main stream has
-// moved past the next pass's coarse hop: the coarse workgroups fill every
-// register of their CUs, the demod workgroups leave room for two Viterbi
-// waves per SIMD, so deferring by one launch lets the decode of pass k run
-// beside the demodulation of pass k+1 instead of between coarse workgroups.
+// The Viterbi of a pass runs on the main stream, between the next pass's
+// coarse hop and demod launch, with the whole GPU to itself.  (Measured, see
+// beside the demod its waves take issue and LDS cycles from the
+// latency-bound demod waves, which then lose as much time as the Viterbi
+// takes; beside the coarse FFT there is no room.)  Its job records go back to
+// the host on a side stream.
 int issue_viterbi(Group *e) {
   const int si = e->vit_pending;
   if (si < 0) return AERO_OK;
@@ -624,13 +623,11 @@ int issue_viterbi(Group *e) {
   S2.jobout = sl.d_out;
   S2.jobs = sl.d_jobs;
   hipEvent_t a, b;
-  HIPCHK(hipEventRecord(e->ev_cut, e->st));
-  HIPCHK(hipStreamWaitEvent(e->st_vit, sl.ev_framed, 0));
-  HIPCHK(hipStreamWaitEvent(e->st_vit, e->ev_cut, 0));
-  ev_begin(e, "viterbi", a, b, e->st_vit);
-  launch_viterbi(e->st_vit, e->mode, S2, e->T, e->nch, sl.trace_blocks ? 1 : 0);
-  ev_end(e, b, e->st_vit);
-  HIPCHK(hipEventRecord(sl.ev_vit, e->st_vit));
+  ev_begin(e, "viterbi", a, b);
+  launch_viterbi(e->st, e->mode, S2, e->T, e->nch, sl.trace_blocks ? 1 : 0);
+  ev_end(e, b);
+  HIPCHK(hipEventRecord(sl.ev_vit, e->st));
+  HIPCHK(hipStreamWaitEvent(e->st_vit, sl.ev_vit, 0));
   HIPCHK(hipGetLastError());
   // async hand-off: the count plus the records the job count is likely to need
   sl.copied = std::min(e->nch, e->max_jobs_seen + e->max_jobs_seen / 4 + 256);
@@ -639,6 +636,27 @@ int issue_viterbi(Group *e) {
   HIPCHK(hipEventRecord(sl.ev, e->st_vit));
   sl.pending = true;
   e->pending_slots.push_back(si);
+  return AERO_OK;
+}
+
+// after a demod launch: the ring rows of samples below every channel's new
+// nsamp are free once the main stream has passed this point
+int note_consumed(Group *e) {
+  long long mn = LLONG_MAX;
+  for (int c = 0; c < e->nch; c++) mn = std::min(mn, e->nsamp[c]);
+  hipEvent_t ev;
+  if (e->ev_free.empty()) {
+    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  } else {
+    ev = e->ev_free.back();
+    e->ev_free.pop_back();
+  }
+  HIPCHK(hipEventRecord(ev, e->st));
+  e->consumed.push_back({mn, ev});
+  while (e->consumed.size() > 32) {  // older ones: a push that needs them waits for the stream instead
+    e->ev_free.push_back(e->consumed.front().second);
+    e->consumed.pop_front();
+  }
   return AERO_OK;
 }
 
@@ -678,7 +696,7 @@ int run_group(Group *e, int flush) {
       launch_coarse(e->st, e->mode, e->S, e->T, e->nch);
       ev_end(e, b);
     }
-    if (int rc = issue_viterbi(e)) return rc;  // the previous pass's decode, beside this demod
+    if (int rc = issue_viterbi(e)) return rc;  // the previous pass's decode, before this demod
     if (!progress) continue;  // no new soft bits: framing has nothing to do
     ev_begin(e, "demod", a, b);
     if (e->mode == MODE_OQPSK)
@@ -686,6 +704,7 @@ int run_group(Group *e, int flush) {
     else
       launch_demod_msk(e->st, e->mode, e->S, e->T, e->nch, flush);
     ev_end(e, b);
+    if (int rc = note_consumed(e)) return rc;
     // framing + Viterbi into the next job slot (at most one job per channel per pass)
     const int si = e->next_slot;
     e->next_slot = (si + 1) % Group::NSLOT;
@@ -803,16 +822,18 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
     HIPCHK(hipEventCreateWithFlags(&sl.ev_framed, hipEventDisableTiming));
   }
   HIPCHK(hipStreamCreateWithFlags(&e->st_vit, hipStreamNonBlocking));
-  HIPCHK(hipEventCreateWithFlags(&e->ev_cut, hipEventDisableTiming));
   for (int k = 0; k < Group::NPIN; k++) {
     if (hipHostMalloc(&e->pin_avail[k], sizeof(long long) * e->C) != hipSuccess) return AERO_E_NOMEM;
     HIPCHK(hipEventCreateWithFlags(&e->pin_ev[k], hipEventDisableTiming));
   }
   HIPCHK(hipEventCreateWithFlags(&e->pin_pcm_ev, hipEventDisableTiming));
   if (hipHostMalloc(&e->pin_stat, 64) != hipSuccess) return AERO_E_NOMEM;
-  HIPCHK(hipStreamCreateWithFlags(&e->st_in, hipStreamNonBlocking));
+  {
+    int lo = 0, hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPCHK(hipStreamCreateWithPriority(&e->st_in, hipStreamNonBlocking, hi));
+  }
   HIPCHK(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
-  for (auto &ev : e->ev_stage_used) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   const int nfft = e->g.nfft;
   std::vector<double> cis(2 * WTSIZE), tw(2 * nfft), twi(2 * nfft), taps(128, 0.0);
   std::vector<uint8_t> scr(5000);
@@ -899,15 +920,12 @@ void group_destroy(Group *e) {
   if (e->pin_pcm) (void)hipHostFree(e->pin_pcm);
   if (e->pin_pcm_ev) (void)hipEventDestroy(e->pin_pcm_ev);
   if (e->st_in) hipStreamSynchronize(e->st_in);
-  for (int b = 0; b < 2; b++) {
-    if (e->d_stage[b]) (void)hipFree(e->d_stage[b]);
-    if (e->ev_stage_used[b]) (void)hipEventDestroy(e->ev_stage_used[b]);
-  }
   if (e->ev_in) (void)hipEventDestroy(e->ev_in);
+  for (auto &pr : e->consumed) (void)hipEventDestroy(pr.second);
+  for (auto ev : e->ev_free) (void)hipEventDestroy(ev);
   if (e->st_in) (void)hipStreamDestroy(e->st_in);
   if (e->d_scratch) (void)hipFree(e->d_scratch);
   if (e->pool) (void)hipFree(e->pool);
-  if (e->ev_cut) (void)hipEventDestroy(e->ev_cut);
   if (e->st_vit) (void)hipStreamDestroy(e->st_vit);
   if (e->st) (void)hipStreamDestroy(e->st);
 }
@@ -982,34 +1000,49 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
     HIPCHK(hipEventRecord(e->pin_pcm_ev, e->st));
     dsrc = e->d_scratch;
   } else {
-    const size_t need = ((n - 1) * ld + nch) * sizeof(int16_t);
-    const int b = e->next_stage;
-    e->next_stage ^= 1;
-    if (need > e->stage_cap[b]) {
-      HIPCHK(hipStreamSynchronize(e->st));
-      if (e->d_stage[b]) (void)hipFree(e->d_stage[b]);
-      e->d_stage[b] = nullptr;
-      e->stage_cap[b] = 0;
-      HIPCHK(hipMalloc(&e->d_stage[b], need));
-      e->stage_cap[b] = need;
+    const long long start = e->avail[c0];
+    for (int j = 1; j < nch; j++)
+      if (e->avail[c0 + j] != start) return AERO_E_INVALID;  // batch pushes are lockstep
+    // rows of samples [start, start + n) overwrite those of samples below
+    // start + n - PCM_CAP: wait for the demod launch that consumed them
+    const long long need = start + (long long)n - PCM_CAP;
+    if (need > 0) {
+      hipEvent_t w = nullptr;
+      while (!e->consumed.empty() && e->consumed.front().first < need) {
+        e->ev_free.push_back(e->consumed.front().second);
+        e->consumed.pop_front();
+      }
+      if (!e->consumed.empty()) w = e->consumed.front().second;
+      if (w) {
+        HIPCHK(hipStreamWaitEvent(e->st_in, w, 0));
+      } else {
+        HIPCHK(hipEventRecord(e->ev_in, e->st));  // not tracked: after all enqueued work
+        HIPCHK(hipStreamWaitEvent(e->st_in, e->ev_in, 0));
+      }
     }
-    HIPCHK(hipStreamWaitEvent(e->st_in, e->ev_stage_used[b], 0));
-    HIPCHK(hipMemcpyAsync(e->d_stage[b], src, need, hipMemcpyDeviceToDevice, e->st_in));
+    const long long r0 = start & (PCM_CAP - 1);
+    const size_t n1 = (size_t)std::min<long long>((long long)n, PCM_CAP - r0);
+    HIPCHK(hipMemcpy2DAsync(e->S.pcm + r0 * e->C + c0, sizeof(int16_t) * e->C, src, sizeof(int16_t) * ld,
+                            sizeof(int16_t) * nch, n1, hipMemcpyDeviceToDevice, e->st_in));
+    if (n1 < n)
+      HIPCHK(hipMemcpy2DAsync(e->S.pcm + c0, sizeof(int16_t) * e->C, src + n1 * ld, sizeof(int16_t) * ld,
+                              sizeof(int16_t) * nch, n - n1, hipMemcpyDeviceToDevice, e->st_in));
     HIPCHK(hipEventRecord(e->ev_in, e->st_in));
     HIPCHK(hipEventSynchronize(e->ev_in));  // the caller's buffer is free again
-    dsrc = e->d_stage[b];
     HIPCHK(hipStreamWaitEvent(e->st, e->ev_in, 0));
+    for (int j = 0; j < nch; j++) e->avail[c0 + j] += (long long)n;
   }
-  const long long start = e->avail[c0];
-  for (int j = 1; j < nch; j++)
-    if (e->avail[c0 + j] != start) return AERO_E_INVALID;  // batch pushes are lockstep
-  const long long total = (long long)n * nch;
-  const int grid = (int)std::min<long long>((total + 255) / 256, 65536);
-  hipLaunchKernelGGL(pcm_scatter_kernel, dim3(grid), dim3(256), 0, e->st, e->S.pcm, e->C, (long long)PCM_CAP - 1,
-                     dsrc, (long long)n, (long long)ld, nch, c0, start);
-  HIPCHK(hipGetLastError());
-  if (dev) HIPCHK(hipEventRecord(e->ev_stage_used[e->next_stage ^ 1], e->st));
-  for (int j = 0; j < nch; j++) e->avail[c0 + j] += (long long)n;
+  if (!dev) {
+    const long long start = e->avail[c0];
+    for (int j = 1; j < nch; j++)
+      if (e->avail[c0 + j] != start) return AERO_E_INVALID;  // batch pushes are lockstep
+    const long long total = (long long)n * nch;
+    const int grid = (int)std::min<long long>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(pcm_scatter_kernel, dim3(grid), dim3(256), 0, e->st, e->S.pcm, e->C, (long long)PCM_CAP - 1,
+                       dsrc, (long long)n, (long long)ld, nch, c0, start);
+    HIPCHK(hipGetLastError());
+    for (int j = 0; j < nch; j++) e->avail[c0 + j] += (long long)n;
+  }
   // device copy of the counters, from pinned staging (stream-ordered before the next demod)
   const int k = e->next_pin;
   e->next_pin = (k + 1) % Group::NPIN;

@@ -104,12 +104,12 @@ __device__ __forceinline__ void viterbi_decode_wave(const uint8_t *sbuf, int nso
 namespace aero {
 
 // Same decoder as viterbi_decode_wave (same metrics, ties, renormalisation,
-// 140-column history, 35-column traceback depth, restricted tail), laid out
-// for co-residence with the demodulator and the coarse FFT: the history
-// lives in registers (lane l holds columns l, l + 64, l + 128) instead of
-// LDS, so a trellis step needs no LDS store and no barrier, and the
-// traceback runs on the scalar unit (the path state is wave-uniform): two
-// v_readlane per column instead of a dependent LDS read per column in lane 0.
+// 140-column history, 35-column traceback depth, restricted tail) with the
+// history in registers (lane l holds columns l, l + 64, l + 128) instead of
+// LDS, so a trellis step needs no LDS store and no barrier (two bpermutes,
+// ~10 VALU and two v_writelane per step before the tail), and the traceback
+// runs on the scalar unit (the path state is wave-uniform): two v_readlane
+// per column instead of a dependent LDS read per column in lane 0.
 // Decoded bit b lands in bit (b & 63) of obw in lane b >> 6.
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
@@ -193,7 +193,54 @@ __device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nso
     a = sbuf[12];
     b = sbuf[13];
   }
-  for (int i = 6; i < sets; ++i) {
+  // Steps before the restricted tail (every state active), with the column
+  // register fixed per run of steps: soft_dist(tab_lo, a, b) = base + sa*a +
+  // sb*b for a, b in [0, 255], and the s | 64 edge carries the complementary
+  // code bits (both polynomials have bit 6 set: tab_hi == tab_lo ^ 3), so its
+  // metric is 510 minus that.  The decision mask is the compare itself and
+  // lands in column `index` through two v_writelane.
+  const int tail0 = sets - 6 > 6 ? sets - 6 : 6;
+  {
+    const int sa = (tab_lo & 1) ? -1 : 1, sb = (tab_lo & 2) ? -1 : 1;
+    const int nbase = -(((tab_lo & 1) ? 255 : 0) + ((tab_lo & 2) ? 255 : 0));
+    const int src0 = (s >> 1) << 2, src1 = ((s >> 1) | 32) << 2;
+    int i = 6;
+    auto steps = [&](uint64_t &hw, int run) {
+      for (int k = 0; k < run; ++k, ++i) {
+        const int ca = a, cb = b;
+        if (i + 1 < sets) {
+          a = sbuf[2 * i + 2];
+          b = sbuf[2 * i + 3];
+        }
+        const int m0 = __builtin_amdgcn_ds_bpermute(src0, m), m1 = __builtin_amdgcn_ds_bpermute(src1, m);
+        const int nd = nbase - __mul24(sa, ca) - __mul24(sb, cb);  // -soft_dist(tab_lo, ca, cb)
+        const int e0 = (m0 - nd) & 0xFFFF;
+        const int e1 = (m1 + 510 + nd) & 0xFFFF;
+        const uint64_t mask = __ballot(e0 > e1);
+        m = e0 < e1 ? e0 : e1;
+        const int col = __builtin_amdgcn_readfirstlane(index & 63);
+        uint32_t lo = (uint32_t)hw, hi = (uint32_t)(hw >> 32);
+        asm("v_writelane_b32 %0, %1, m0" : "+v"(lo) : "s"((uint32_t)mask), "{m0}"(col));
+        asm("v_writelane_b32 %0, %1, m0" : "+v"(hi) : "s"((uint32_t)(mask >> 32)), "{m0}"(col));
+        hw = ((uint64_t)hi << 32) | lo;
+        process(1);
+      }
+    };
+    while (i < tail0) {
+      // steps until the column index leaves its register (64, 128, wrap at 140)
+      const int idx = __builtin_amdgcn_readfirstlane(index);
+      const int w = idx >> 6;
+      int run = (w == 2 ? HCAP : 64 * (w + 1)) - idx;
+      if (run > tail0 - i) run = tail0 - i;
+      if (w == 0)
+        steps(h0, run);
+      else if (w == 1)
+        steps(h1, run);
+      else
+        steps(h2, run);
+    }
+  }
+  for (int i = tail0; i < sets; ++i) {
     // this step's symbols were read one step ahead (LDS latency off the chain)
     const int ca = a, cb = b;
     if (i + 1 < sets) {
