@@ -481,6 +481,7 @@ int process_slot(Group *e, int si) {
   // queue order and no two workers share state
   auto work = [e, njobs, nch, blocks, msk](int t, int T) {
     const uint8_t *jobs = e->h_jobs_task.data();
+    uint64_t frames = 0, su_ok = 0;  // this worker's counts, added once (no shared atomics per job)
     for (int j = 0; j < njobs; j++) {
       const uint8_t *o = jobs + (size_t)j * JOB_OUT;
       int meta[4];
@@ -518,8 +519,8 @@ int process_slot(Group *e, int si) {
         flen = meta[0];
       }
       if (flen >= 0) {
-        e->st_frames++;
-        e->st_su_ok += (uint64_t)__builtin_popcount(mask);
+        frames++;
+        su_ok += (uint64_t)__builtin_popcount(mask);
         e->host[c]->frame(info, flen, mask, meta[2]);
         if (e->flags & AERO_F_TRACE_FRAMES) {
           uint8_t rec[320] = {0};
@@ -531,6 +532,8 @@ int process_slot(Group *e, int si) {
         }
       }
     }
+    e->st_frames += frames;
+    e->st_su_ok += su_ok;
   };
   e->hpool->submit(work, std::max(1, std::min(njobs / 64, nch)));
   return AERO_OK;
@@ -743,6 +746,9 @@ int run_group(Group *e, int flush) {
 int drain_group(Group *e) {
   HIPCHK(hipSetDevice(e->device));
   if (int rc = issue_viterbi(e)) return rc;
+  // slot by slot as their records come back: the host work of each overlaps
+  // the GPU's remaining passes
+  if (int rc = poll_slots(e, true)) return rc;
   HIPCHK(hipStreamSynchronize(e->st));
   HIPCHK(hipStreamSynchronize(e->st_vit));
   if (int rc = poll_slots(e, true)) return rc;

@@ -509,12 +509,15 @@ def main():
         eng.push_batch_device(x.data_ptr(), HOP, C, C)
         eng.run()
         items += eng.drain_items()  # ACARS items leave every step, as a serving host would take them
+    t_tail = time.perf_counter()
     eng.sync()
     items += eng.drain_items()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    t_end = time.perf_counter()
+    elapsed = t_end - t0
+    tail_ms = (t_end - t_tail) * 1e3  # final drain: the last passes' decode, copy-back and host items
     samples = eng.samples_processed() - s0
     stats = {k: eng.stat(k) - v for k, v in st0.items()}
     stats['acars_items'] = items
@@ -569,6 +572,7 @@ def main():
             'kernel_ms_per_step': {k: round(v[0] / max(a.steps, 1), 3) for k, v in kt.items()},
             'timed_region': stats,
             'host_ms_per_step': {k: round(v[0] / max(a.steps, 1), 3) for k, v in ht.items()},
+            'drain_ms': round(tail_ms, 3),
         }
         if cpu is not None:
             out['cpu_baseline'] = cpu
