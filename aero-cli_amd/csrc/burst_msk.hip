@@ -53,7 +53,7 @@ constexpr int M_START = 120, M_ENDROT = (120 + 37) * 40;
 
 __constant__ double c_msr_b[3];  // st_iir_resonator, 600 Hz at 48 kHz (burstmskdemodulator.cpp:214-227)
 __constant__ double c_msr_a[3];
-__constant__ double c_mtaps[M_NT];  // matched filter (:142-149); LDS holds only the partial sums (2 WGs / CU)
+__constant__ double c_mtaps[M_NT];  // matched filter (:142-149); LDS and registers hold only the partial sums
 
 __device__ __forceinline__ double m_diff_soft(double &last, double soft) {  // DiffDecode::UpdateSoft (DSP.cpp:523-548)
   double retval;
@@ -71,12 +71,16 @@ __device__ __forceinline__ double m_diff_soft(double &last, double soft) {  // D
 }  // namespace
 
 // ----------------------------------------------------------------- demod
-constexpr int BM_BLOCK = 64;  // channels per workgroup: both matched-filter partial sums in LDS (80 KB)
+// channels per workgroup (one wave).  The matched filter's transposed partial
+// sums of taps [BM_LDS_TAPS, 80) live in registers, the rest (real and
+// imaginary) in LDS: 40 KB per wave, four waves per CU.
+constexpr int BM_BLOCK = 64;
+constexpr int BM_LDS_TAPS = 40, BM_REG_TAPS = M_NT - BM_LDS_TAPS;
 
 __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, BurstTables T, int nch, int max_n,
                                                               int trace) {
-  __shared__ double s_qre[M_NT][BM_BLOCK];
-  __shared__ double s_qim[M_NT][BM_BLOCK];
+  __shared__ double s_qre[BM_LDS_TAPS][BM_BLOCK];
+  __shared__ double s_qim[BM_LDS_TAPS][BM_BLOCK];
   const int c = blockIdx.x * BM_BLOCK + threadIdx.x, col = threadIdx.x;
   if (c >= nch) return;
   const int C = S.C;
@@ -111,9 +115,15 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
   long long sp = ls[BL_SP * C], scommit = ls[BL_SCOMMIT * C];
   const long long scons = ls[BL_SCONS * C];
 #pragma unroll 1
-  for (int j = 0; j < M_NT; ++j) {
+  for (int j = 0; j < BM_LDS_TAPS; ++j) {
     s_qre[j][col] = S.fir[(size_t)j * C + c];
     s_qim[j][col] = S.fir[(size_t)(M_NT + j) * C + c];
+  }
+  double hre[BM_REG_TAPS], him[BM_REG_TAPS];  // partial sums of taps BM_LDS_TAPS..79
+#pragma unroll
+  for (int j = 0; j < BM_REG_TAPS; ++j) {
+    hre[j] = S.fir[(size_t)(BM_LDS_TAPS + j) * C + c];
+    him[j] = S.fir[(size_t)(M_NT + BM_LDS_TAPS + j) * C + c];
   }
   int16_t *soft = S.soft + (size_t)c * B_SOFT_RING;
   double2 *btd = reinterpret_cast<double2 *>(S.dl[0]) + c;
@@ -319,9 +329,16 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         cr = cr * vol_gain;
         ci = ci * vol_gain;
         // matched filter, transposed form (FIR::FIRUpdateAndProcess reads the 80 samples before the newest)
-        s2r = s_qre[M_NT - 1][col];
-        s2i = s_qim[M_NT - 1][col];
-        for (int j = M_NT - 1; j >= 1; --j) {
+        s2r = hre[BM_REG_TAPS - 1];
+        s2i = him[BM_REG_TAPS - 1];
+#pragma unroll
+        for (int j = M_NT - 1; j > BM_LDS_TAPS; --j) {  // register part, descending: q[j - 1] read before rewritten
+          hre[j - BM_LDS_TAPS] = hre[j - 1 - BM_LDS_TAPS] + c_mtaps[j] * cr;
+          him[j - BM_LDS_TAPS] = him[j - 1 - BM_LDS_TAPS] + c_mtaps[j] * ci;
+        }
+        hre[0] = s_qre[BM_LDS_TAPS - 1][col] + c_mtaps[BM_LDS_TAPS] * cr;
+        him[0] = s_qim[BM_LDS_TAPS - 1][col] + c_mtaps[BM_LDS_TAPS] * ci;
+        for (int j = BM_LDS_TAPS - 1; j >= 1; --j) {
           s_qre[j][col] = s_qre[j - 1][col] + c_mtaps[j] * cr;
           s_qim[j][col] = s_qim[j - 1][col] + c_mtaps[j] * ci;
         }
@@ -469,9 +486,14 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
   }
   // state back
 #pragma unroll 1
-  for (int j = 0; j < M_NT; ++j) {
+  for (int j = 0; j < BM_LDS_TAPS; ++j) {
     S.fir[(size_t)j * C + c] = s_qre[j][col];
     S.fir[(size_t)(M_NT + j) * C + c] = s_qim[j][col];
+  }
+#pragma unroll
+  for (int j = 0; j < BM_REG_TAPS; ++j) {
+    S.fir[(size_t)(BM_LDS_TAPS + j) * C + c] = hre[j];
+    S.fir[(size_t)(M_NT + BM_LDS_TAPS + j) * C + c] = him[j];
   }
   ds[BM_M2_PTR * C] = m2_ptr;
   ds[BM_M2_STEP * C] = m2_step;
