@@ -319,7 +319,11 @@ AERO_HD double approx_rcp(double b) {
  * 2^-65 relative without any IEEE division, returned only when that bound
  * proves the rounding; otherwise (≈2^-10 of arguments, and every special or
  * extreme-exponent argument) the double-double path decides.  Same results
- * as aero_atan2_dd by construction (tests/test_math_host.py compares them). */
+ * as aero_atan2_dd by construction (tests/test_math_host.py compares them).
+ * The quadrant (pi/2 - r when |y| > |x|, pi - r when x < 0) is folded into
+ * one table row, C + s atan(k/64) in double-double, so the result is
+ * B + s (u + corr) with a single two_sum, and the series runs in fused
+ * Horner form (both only tighten the bound the rounding test assumes). */
 AERO_HD double aero_atan2(double y, double x) {
   const double ay = __builtin_fabs(y), ax = __builtin_fabs(x);
   if (!(ax >= 0x1p-500 && ax <= 0x1p500 && ay >= 0x1p-500 && ay <= 0x1p500)) return aero_atan2_dd(y, x);
@@ -333,27 +337,28 @@ AERO_HD double aero_atan2(double y, double x) {
   // u = (t - c) / (1 + t c), |u| <= 2^-7
   const dd num = two_sum(th - c, tl);  // th - c exact (Sterbenz)
   const double ph = th * c, pl = fma(th, c, -ph);
-  const dd den0 = two_sum(1.0, ph);
+  const dd den0 = quick_two_sum(1.0, ph);  // ph = t c <= 1
   const double dh = den0.hi, dl = den0.lo + (pl + tl * c);
   const double rd = approx_rcp(dh);
   const double uh = num.hi * rd;
   const double ul = ((fma(-uh, dh, num.hi) + num.lo) - uh * dl) * rd;
   // atan(u) - u = u^3 (-1/3 + u^2/5 - ...) - u^2 ul
   const double v = uh * uh;
-  double p = -1.0 / 15;
-  p = 1.0 / 13 + v * p;
-  p = -1.0 / 11 + v * p;
-  p = 1.0 / 9 + v * p;
-  p = -1.0 / 7 + v * p;
-  p = 1.0 / 5 + v * p;
-  p = -AERO_INV3_HI + v * p;
-  const double corr = (v * uh) * p - v * ul;
-  // atan(t) = A + u + corr
-  dd r = two_sum(aero_atan_tab[k][0], uh);
-  r.lo += aero_atan_tab[k][1] + (ul + corr);
+  double p = fma(v, -1.0 / 15, 1.0 / 13);
+  p = fma(v, p, -1.0 / 11);
+  p = fma(v, p, 1.0 / 9);
+  p = fma(v, p, -1.0 / 7);
+  p = fma(v, p, 1.0 / 5);
+  p = fma(v, p, -AERO_INV3_HI);
+  const double corr = fma(v * uh, p, -v * ul);
+  // atan2 = C + s (A + u + corr): (C, s) = (0, 1), (pi/2, -1), (pi, -1),
+  // (pi/2, 1) for q = swap | 2 (x < 0); the row holds C + s A
+  const int q = (swap ? 1 : 0) | (__builtin_signbit(x) ? 2 : 0);
+  const double sg = (q == 1 || q == 2) ? -1.0 : 1.0;
+  const int row = q * 65 + k;
+  dd r = two_sum(aero_atan2_quad_tab[row][0], sg * uh);
+  r.lo += aero_atan2_quad_tab[row][1] + sg * (ul + corr);
   r = quick_two_sum(r.hi, r.lo);
-  if (swap) r = dd_add(dd{AERO_PI_2_HI, AERO_PI_2_LO}, dd_neg(r));
-  if (__builtin_signbit(x)) r = dd_add(dd{AERO_PI_HI, AERO_PI_LO}, dd_neg(r));
   const double e = 0x1p-63 * __builtin_fabs(r.hi);
   const double out = r.hi + r.lo;
   if (out != r.hi + (r.lo + e) || out != r.hi + (r.lo - e)) return aero_atan2_dd(y, x);

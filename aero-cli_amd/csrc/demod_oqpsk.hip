@@ -29,14 +29,20 @@ namespace aero {
 // Timing experiments only (never in the product build): AERO_X_OCML swaps
 // the bit-exact libm for the device ocml one, AERO_X_DIVMUL turns divisions
 // by constants into multiplications, to price those parts of the loop.
-#ifdef AERO_X_OCML
+#if defined(AERO_X_OCML) || defined(AERO_X_OCML_HYPOT)
 #define DM_HYPOT ::hypot
+#else
+#define DM_HYPOT aero_hypot
+#endif
+#if defined(AERO_X_OCML) || defined(AERO_X_OCML_ATAN2)
 #define DM_ATAN2 ::atan2
+#else
+#define DM_ATAN2 aero_atan2
+#endif
+#if defined(AERO_X_OCML) || defined(AERO_X_OCML_EVENT)
 #define DM_TANH ::tanh
 #define DM_SINCOS(x, s, c) ::sincos(x, &(s), &(c))
 #else
-#define DM_HYPOT aero_hypot
-#define DM_ATAN2 aero_atan2
 #define DM_TANH aero_tanh
 #define DM_SINCOS(x, s, c) aero_sincos(x, s, c)
 #endif
