@@ -147,20 +147,14 @@ constexpr int RING_GROUP = 8;
 template <bool TRACE>
 __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, DevTables T, int nch, int flush) {
   // LDS (≈148 KB, one 256-channel block per CU): the imaginary RRC partial
-  // sums, RRC taps (symmetric, 28 distinct values), the coarse-ring staging
-  // area (entries of 8 consecutive samples leave as one 32-byte write per
-  // channel instead of eight 4-byte ones) and the carrier-step state.
+  // sums, the coarse-ring staging area (entries of 8 consecutive samples
+  // leave as one 32-byte write per channel instead of eight 4-byte ones) and
+  // the carrier-step state.  The RRC taps are scalar constant-memory loads.
   __shared__ double s_qim[NTAPS][DEMOD_BLOCK];
-  __shared__ double s_taps[32];
   __shared__ uint32_t s_ring[RING_GROUP][DEMOD_BLOCK];
   __shared__ double s_pd[PD_N][DEMOD_BLOCK];
   __shared__ long long s_pl[PL_N][DEMOD_BLOCK];
   __shared__ int s_pi[PI_N][DEMOD_BLOCK];
-  {
-    const int l = threadIdx.x;
-    if (l < (NTAPS + 1) / 2) s_taps[l] = T.taps[l];  // h[j] == h[54 - j] bit for bit (host-checked)
-    __syncthreads();
-  }
   const int c = blockIdx.x * DEMOD_BLOCK + threadIdx.x;
   const int pair = threadIdx.x;  // this channel's LDS column
   if (c >= nch) return;
@@ -269,35 +263,29 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       // rrc (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
       double s2r = q[NTAPS - 1], s2i = s_qim[NTAPS - 1][pair];
       {
-        // taps from LDS through an opaque offset, in groups, so they are
-        // re-read every sample instead of pinning registers
-        int toff = 0;
-        asm volatile("" : "+v"(toff));
+        // R_j(n) = R_{j-1}(n-1) + h[j] x(n) with h[j] == h[54 - j] bit for bit
+        // (host-checked): the slots of a tap pair share one product, so the
+        // taps run outside-in (slots 54 - k and k for k = 0..26, then the
+        // centre), with the old value of slot k kept for slot k + 1.  Taps are
+        // uniform scalar loads from constant memory; groups of eight keep few
+        // LDS reads in flight.
+        double prev_re = 0.0, prev_im = 0.0;  // slot k - 1 before this sample
 #pragma unroll
-        for (int j = NTAPS - 1; j >= 1; --j) {
-          const int tj = j < NTAPS - 1 - j ? j : NTAPS - 1 - j;
-          q[j] = q[j - 1] + s_taps[tj + toff] * cv;
-          if ((j & 7) == 0) asm volatile("" : "+v"(toff));
+        for (int k = 0; k < (NTAPS - 1) / 2; ++k) {
+          const double t = c_taps[k];
+          const double pr = t * cv, pim = t * cvi;
+          const double old_re = q[k], old_im = s_qim[k][pair];
+          q[NTAPS - 1 - k] = q[NTAPS - 2 - k] + pr;
+          s_qim[NTAPS - 1 - k][pair] = s_qim[NTAPS - 2 - k][pair] + pim;
+          q[k] = prev_re + pr;
+          s_qim[k][pair] = prev_im + pim;
+          prev_re = old_re;
+          prev_im = old_im;
+          if ((k & 7) == 7) asm volatile("" : : : "memory");
         }
-        q[0] = 0.0 + s_taps[toff] * cv;
-#ifdef AERO_PIN_FIR
-        // (experiment) pin the update here instead of letting the compiler
-        // sink it to the loop latch: fewer live registers, but measured
-        // slower, the sunk FIR fills the latency gaps of the serial chain
-#pragma unroll
-        for (int j = 0; j < NTAPS; ++j) asm volatile("" : "+v"(q[j]));
-#endif
-      }
-      {
-        // imaginary partial sums: descending taps, so slot j-1 is read
-        // before it is rewritten; groups of 8 keep few reads in flight
-#pragma unroll
-        for (int j = NTAPS - 1; j >= 1; --j) {
-          const int tj = j < NTAPS - 1 - j ? j : NTAPS - 1 - j;
-          s_qim[j][pair] = s_qim[j - 1][pair] + s_taps[tj] * cvi;
-          if ((j & 7) == 0) asm volatile("" : : : "memory");
-        }
-        s_qim[0][pair] = 0.0 + s_taps[0] * cvi;
+        const double tc = c_taps[(NTAPS - 1) / 2];
+        q[(NTAPS - 1) / 2] = prev_re + tc * cv;
+        s_qim[(NTAPS - 1) / 2][pair] = prev_im + tc * cvi;
       }
       // AGC (DSP.cpp:371-380) on |sig2| (oqpskdemodulator.cpp:399-405)
       const double dab = sqrt(s2r * s2r + s2i * s2i);
