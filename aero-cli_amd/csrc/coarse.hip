@@ -153,6 +153,26 @@ __device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<in
   return gotasignal;
 }
 
+// AERO_X_STAMPS (diagnostic build only): s_memtime cycle totals per section
+// of wave 0 of every workgroup that ran a hop (prologue+ring, FFT 1,
+// boxcar+iFFT+square, FFT 3, hypot, log10 smoothing, fold+control), and the
+// number of such workgroups
+#ifdef AERO_X_STAMPS
+__device__ unsigned long long g_cstamps[8];
+#define CSTAMP(k)                                                  \
+  do {                                                             \
+    __builtin_amdgcn_sched_barrier(0);                             \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
+    cst_[k] += t_ - ctime_;                                        \
+    ctime_ = t_;                                                   \
+    __builtin_amdgcn_sched_barrier(0);                             \
+  } while (0)
+#else
+#define CSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 template <int M>
 __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 13 ? 4 : 1) void coarse_kernel(DevState S, DevTables T, int nch) {
   using K = CoarseK<M>;
@@ -173,6 +193,9 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   const long long nk = (long long)K::HOPN * (hops_done + 1) - 1;
   const long long avail = S.ls[LS_AVAIL * C + c];
   if (nsamp != nk || avail <= nk) return;
+#ifdef AERO_X_STAMPS
+  unsigned long long cst_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ctime_ = __builtin_amdgcn_s_memtime();
+#endif
   const long long zero_before = S.ls[LS_ZERO_BEFORE * C + c];
   if (filled <= nk && t == 0) {
     // ring entry of the hop sample not written yet (the demod segment ended
@@ -210,8 +233,10 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
       x[i] = make_double2(cs.x * dval, cs.y * dval);
     }
   }
+  CSTAMP(0);
   // forward FFT
   fft_dit<L, false, true>(x, t, lds, T.tw, s_tw);
+  CSTAMP(1);
   // boxcar: zero bins startbin..stopbin (coarsefreqestimate.cpp:143-146)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -233,7 +258,9 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     x[i] = make_double2(r, im);
   }
   exchange<L, 3, 0, true>(x, t, lds);
+  CSTAMP(2);
   fft_dit<L, false, true>(x, t, lds, T.tw, s_tw);
+  CSTAMP(3);
   // fftshift + smoothing y = 0.9 y + 10 log10(max(|X|,1)) over the bins the fold reads:
   // |X| per bin to LDS first (keeps the log10 out of the register-heavy FFT scope)
   // the y history (HBM) is read three iterations ahead of its update, the
@@ -251,6 +278,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   }
   double yp2 = yload(t + 2 * FT);
   __syncthreads();
+  CSTAMP(4);
 #pragma unroll 1
   for (int k = t; k < YLEN; k += FT) {
     const double yold = yp0;
@@ -262,6 +290,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     ylds[k] = ynew;
   }
   __syncthreads();
+  CSTAMP(5);
   // fold search (coarsefreqestimate.cpp:166-185): first strict maximum above 0
   double bv = 0.0;
   int bi = 0x7fffffff;
@@ -289,6 +318,13 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     red_i[t >> 6] = bi;
   }
   __syncthreads();
+  CSTAMP(6);
+#ifdef AERO_X_STAMPS
+  if (t == 0) {
+    for (int k = 0; k < 7; ++k) atomicAdd(&g_cstamps[k], cst_[k]);
+    atomicAdd(&g_cstamps[7], 1ull);
+  }
+#endif
   if (t != 0) return;
   for (int w = 1; w < FT / 64; ++w) {
     if (red_v[w] > bv || (red_v[w] == bv && red_i[w] < bi)) {
@@ -347,6 +383,16 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     hr[5] = gotasignal ? 1.0 : 0.0;
   }
   S.hop_n[c] = hn + 1;
+}
+
+void coarse_read_stamps(unsigned long long *out) {
+#ifdef AERO_X_STAMPS
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cstamps), sizeof(unsigned long long) * 8);
+  unsigned long long z[8] = {0};
+  hipMemcpyToSymbol(HIP_SYMBOL(g_cstamps), z, sizeof z);
+#else
+  for (int k = 0; k < 8; ++k) out[k] = 0;
+#endif
 }
 
 void launch_coarse(hipStream_t st, int mode, const DevState &S, const DevTables &T, int nch) {

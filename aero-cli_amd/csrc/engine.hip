@@ -46,6 +46,7 @@ void upload_demod_constants(const double *, const DelayDesc *, const double *, c
 void launch_demod_msk(hipStream_t, int, const DevState &, const DevTables &, int, int);
 void upload_msk_constants(const double *, const double *, const double *);
 void demod_read_stamps(unsigned long long *);
+void coarse_read_stamps(unsigned long long *);
 void launch_coarse(hipStream_t, int, const DevState &, const DevTables &, int);
 void launch_frame(hipStream_t, int, const DevState &, int);
 void launch_viterbi(hipStream_t, int, const DevState &, const DevTables &, int, int);
@@ -334,6 +335,7 @@ size_t layout(DevState &S, DevTables &T, int mode, int C, int flags, char *base)
   S.pcm = carve<int16_t>(p, (size_t)PCM_CAP * C);
   S.pcm_cap = PCM_CAP;
   S.cring = carve<uint32_t>(p, (size_t)g.nfft * C);
+  S.bring = carve<double2>(p, msk ? 1 : (size_t)g.nfft * C);
   S.y = carve<double>(p, (size_t)(g.y_hi - g.y_lo + 1) * C);
   S.soft = carve<uint8_t>(p, (size_t)SOFT_RING * C);
   S.pt_cap = (flags & AERO_F_TRACE_PT) ? PT_CAP : 0;
@@ -1585,4 +1587,7 @@ int aero_engine_feed_dev(aero_engine *e, int nitems, const int *ch, const int16_
 // (loop control, loads+FIR+AGC, hypot+clip, timer, instant+NCO+ring, event
 // step, samples) of wave 0; zeros in the product build
 extern "C" void aero_x_demod_stamps(unsigned long long *out7) { demod_read_stamps(out7); }
+// the coarse kernel's per-section cycle totals over every hop's wave 0
+// (7 sections + the hop count)
+extern "C" void aero_x_coarse_stamps(unsigned long long *out8) { coarse_read_stamps(out8); }
 

@@ -13,13 +13,23 @@
 
 namespace aero {
 
-// LDS padding of the transposes: one double per 32 (one 64-bank row of
+// LDS padding of the transposes (1 -> 2, 2 -> 3, 3 -> 0): one double per 32 (one 64-bank row of
 // dwords).  Contiguous 32-lane accesses (layouts 2, 3) stay conflict-free and
 // the stride-16 ones (layout 0) spread over all banks; it is additive over
 // bit-disjoint parts, which the base + immediate-offset addressing needs.
 // (p + p/16 left 2-way conflicts on layouts 2/3 and the bit-reversed reads:
 // SQ_LDS_BANK_CONFLICT ~= SQ_ACTIVE_INST_LDS on coarse_kernel.)
 __device__ __forceinline__ int pad(int p) { return p + (p >> 5); }
+// The 0 -> 1 transpose writes stride-16 positions (16-lane store groups hit
+// 8 of the 16 double-banks under pad()) and reads two 16-position runs 256
+// apart per 32-lane group (2-way under pad()); one double per 16 makes both
+// conflict-free.  Each exchange picks its own map: only its writer and its
+// reader share the layout.  Buffers hold N + N/16 doubles.
+__device__ __forceinline__ int pad16(int p) { return p + (p >> 4); }
+template <int PH_FROM, int PH_TO, bool BR>
+__device__ __forceinline__ int xpad(int p) {
+  return (PH_FROM == 0 && PH_TO == 1 && !BR) ? pad16(p) : pad(p);
+}
 
 // position of value i of thread t in register phase PH (4 FFT stages per
 // phase; the last phase holds the LOG2N - 12 remaining stage bits in i's low bits)
@@ -113,25 +123,31 @@ __device__ __forceinline__ void stage(double2 (&x)[16], int t, int lb, int n, co
 // BR: the destination reads bit-reversed positions (start of a new transform)
 template <int LOG2N, int PH_FROM, int PH_TO, bool BR>
 __device__ __forceinline__ void exchange(double2 (&x)[16], int t0, double *lds) {
+#ifdef AERO_X_NOEXCH  // timing experiment only (wrong results): no transposes
+  if (!BR) {
+    asm volatile("" : "+v"(x[0].x), "+v"(x[5].y), "+v"(x[15].x));
+    return;
+  }
+#endif
 #pragma unroll
   for (int part = 0; part < 2; ++part) {
     const int t = fresh(t0);
     // pad(A | B) = pad(A) + pad(B) for bit-disjoint A = epos(t, 0), B = epos(0, i)
     // (bit reversal permutes bits, so it keeps them disjoint): one base address
     // per thread, the per-value part is an immediate offset
-    double *wb = lds + pad(epos<LOG2N, PH_FROM>(t, 0));
+    double *wb = lds + xpad<PH_FROM, PH_TO, BR>(epos<LOG2N, PH_FROM>(t, 0));
     int rp = epos<LOG2N, PH_TO>(t, 0);
     if (BR) rp = bitrev<LOG2N>(rp);
-    const double *rb = lds + pad(rp);
+    const double *rb = lds + xpad<PH_FROM, PH_TO, BR>(rp);
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 16; ++i) wb[pad(epos<LOG2N, PH_FROM>(0, i))] = part ? x[i].y : x[i].x;
+    for (int i = 0; i < 16; ++i) wb[xpad<PH_FROM, PH_TO, BR>(epos<LOG2N, PH_FROM>(0, i))] = part ? x[i].y : x[i].x;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       int p = epos<LOG2N, PH_TO>(0, i);
       if (BR) p = bitrev<LOG2N>(p);
-      const double v = rb[pad(p)];
+      const double v = rb[xpad<PH_FROM, PH_TO, BR>(p)];
       if (part)
         x[i].y = v;
       else

@@ -1,0 +1,7 @@
+#!/bin/bash
+set -eo pipefail
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/r03d
+mkdir -p $OUT
+AERO_ENGINE_SO=$R/aero-cli_amd/libaero_engine_stamps.so timeout -k 10 300 python3 -u $R/scripts/coarse_stamps.py 65536 > $OUT/coarse_stamps.log 2>&1
+cat $OUT/coarse_stamps.log
