@@ -243,18 +243,20 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     const int p = epos<L, 3>(t, i);
     if (p >= K::START && p <= K::STOP) x[i] = make_double2(0.0, 0.0);
   }
-  // inverse FFT (JFFT scales by 1/N, FFTWrapper multiplies by N)
+  // inverse FFT.  JFFT scales by 1/N and FFTWrapper multiplies by N
+  // (jfft.cpp:206-212, fftwrapper.cpp:22-29): x * 2^-L * 2^L == x exactly for every
+  // x with |x| >= 2^-1008, and a nonzero value of this path is far above that
+  // (magnitudes >= ~2^-200: sums and products of pcm/32768, CIS and twiddle
+  // values), so both multiplies are the identity here and are skipped.
   exchange<L, 3, 0, true>(x, t, lds);
   fft_dit<L, true, true>(x, t, lds, T.twi, s_tw);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    x[i].x *= (1.0 / ((double)N));
-    x[i].y *= (1.0 / ((double)N));
-    x[i].x *= (double)N;
-    x[i].y *= (double)N;
     // square
+    // (x*y + y*x: the two products are the same IEEE product, so the sum is
+    // exactly 2 (x*y))
     const double r = x[i].x * x[i].x - x[i].y * x[i].y;
-    const double im = x[i].x * x[i].y + x[i].y * x[i].x;
+    const double im = 2.0 * (x[i].x * x[i].y);
     x[i] = make_double2(r, im);
   }
   exchange<L, 3, 0, true>(x, t, lds);

@@ -19,6 +19,8 @@ for c in FETCH_SIZE WRITE_SIZE; do
     -d /tmp/pmc_${TAG}_$c -o pmc -- python3 $R/bench.py --steps 4 --warmup 1 --no-cpu-baseline > $OUT/pmc_$c.log 2>&1
   find /tmp/pmc_${TAG}_$c -name '*counter_collection.csv' -exec cp {} $OUT/pmc_$c.csv \;
 done
+python3 $R/tools/pmc_json.py $OUT/pmc_FETCH_SIZE.csv $OUT/pmc_WRITE_SIZE.csv $OUT/pmc_oqpsk10500.json oqpsk10500 65536 \
+  "rocprofv3 --pmc, one pass per counter, bench.py --steps 4 --warmup 1 (65536 channels, after the 48-hop pre-roll; averages over every dispatch of the run), profiles/$TAG/pmc_{FETCH,WRITE}_SIZE.csv" > /dev/null
 timeout -k 10 600 python3 $R/bench.py --mode burst10500 --steps 10 > $OUT/bench_burst.log 2>&1
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/profb_$TAG -o prof -- python3 $R/bench.py --mode burst10500 --steps 6 --no-cpu-baseline > $OUT/bench_burst_prof.log 2>&1
 find /tmp/profb_$TAG -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats_burst.csv \;
