@@ -146,11 +146,17 @@ constexpr int RING_GROUP = 8;
 
 template <bool TRACE>
 __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, DevTables T, int nch, int flush) {
-  // LDS (≈148 KB, one 256-channel block per CU): the imaginary RRC partial
-  // sums, the coarse-ring staging area (entries of 8 consecutive samples
-  // leave as one 32-byte write per channel instead of eight 4-byte ones) and
-  // the carrier-step state.  The RRC taps are scalar constant-memory loads.
+  // LDS (38 KB per 256-channel block): the coarse-ring staging area (entries
+  // of 8 consecutive samples leave as one 32-byte write per channel instead
+  // of eight 4-byte ones) and the carrier-step state.  The RRC taps are
+  // scalar constant-memory loads.  (AERO_X_QIM_LDS, timing experiment only:
+  // the imaginary RRC partial sums in LDS instead of registers, +112 KB.)
+#ifdef AERO_X_QIM_LDS
   __shared__ double s_qim[NTAPS][DEMOD_BLOCK];
+#define QIM(j) s_qim[j][pair]
+#else
+#define QIM(j) qi[j]
+#endif
   __shared__ uint32_t s_ring[RING_GROUP][DEMOD_BLOCK];
   __shared__ double s_pd[PD_N][DEMOD_BLOCK];
   __shared__ long long s_pl[PL_N][DEMOD_BLOCK];
@@ -217,13 +223,18 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
     s_pl[PL_PTN][pair] = TRACE ? S.ls[LS_PT_N * C + c] : 0;
   }
 
-  // transposed RRC partial sums R_j(n-1), j = 0..54: real part in VGPRs,
-  // imaginary part in LDS
+  // transposed RRC partial sums R_j(n-1), j = 0..54, real and imaginary, in
+  // registers (110 doubles of the 512-register budget of the one wave per
+  // SIMD; as LDS the imaginary part cost two LDS round trips per tap and
+  // sample)
   double q[NTAPS];
+#ifndef AERO_X_QIM_LDS
+  double qi[NTAPS];
+#endif
 #pragma unroll
   for (int j = 0; j < NTAPS; ++j) q[j] = S.fir[(size_t)j * C + c];
 #pragma unroll
-  for (int j = 0; j < NTAPS; ++j) s_qim[j][pair] = S.fir[(size_t)(NTAPS + j) * C + c];
+  for (int j = 0; j < NTAPS; ++j) QIM(j) = S.fir[(size_t)(NTAPS + j) * C + c];
 
   const double PT = 0.4 * WTSIZE;  // IfHavePassedPoint(ee) with ee = 0.4 (oqpskdemodulator.cpp:225)
 
@@ -261,31 +272,32 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       // mix (oqpskdemodulator.cpp:390): cval = CIS * dval, componentwise
       const double cv = cm.x * dval, cvi = cm.y * dval;
       // rrc (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
-      double s2r = q[NTAPS - 1], s2i = s_qim[NTAPS - 1][pair];
+      double s2r = q[NTAPS - 1], s2i = QIM(NTAPS - 1);
       {
         // R_j(n) = R_{j-1}(n-1) + h[j] x(n) with h[j] == h[54 - j] bit for bit
         // (host-checked): the slots of a tap pair share one product, so the
         // taps run outside-in (slots 54 - k and k for k = 0..26, then the
         // centre), with the old value of slot k kept for slot k + 1.  Taps are
-        // uniform scalar loads from constant memory; groups of eight keep few
-        // LDS reads in flight.
+        // uniform scalar loads from constant memory.
         double prev_re = 0.0, prev_im = 0.0;  // slot k - 1 before this sample
 #pragma unroll
         for (int k = 0; k < (NTAPS - 1) / 2; ++k) {
           const double t = c_taps[k];
           const double pr = t * cv, pim = t * cvi;
-          const double old_re = q[k], old_im = s_qim[k][pair];
+          const double old_re = q[k], old_im = QIM(k);
           q[NTAPS - 1 - k] = q[NTAPS - 2 - k] + pr;
-          s_qim[NTAPS - 1 - k][pair] = s_qim[NTAPS - 2 - k][pair] + pim;
+          QIM(NTAPS - 1 - k) = QIM(NTAPS - 2 - k) + pim;
           q[k] = prev_re + pr;
-          s_qim[k][pair] = prev_im + pim;
+          QIM(k) = prev_im + pim;
           prev_re = old_re;
           prev_im = old_im;
+#ifdef AERO_X_QIM_LDS
           if ((k & 7) == 7) asm volatile("" : : : "memory");
+#endif
         }
         const double tc = c_taps[(NTAPS - 1) / 2];
         q[(NTAPS - 1) / 2] = prev_re + tc * cv;
-        s_qim[(NTAPS - 1) / 2][pair] = prev_im + tc * cvi;
+        QIM((NTAPS - 1) / 2) = prev_im + tc * cvi;
       }
       // AGC (DSP.cpp:371-380) on |sig2| (oqpskdemodulator.cpp:399-405)
       const double dab = sqrt(s2r * s2r + s2i * s2i);
@@ -523,7 +535,7 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
 #pragma unroll
     for (int j = 0; j < NTAPS; ++j) fir[(size_t)j * C] = q[j];
 #pragma unroll
-    for (int j = 0; j < NTAPS; ++j) fir[(size_t)(NTAPS + j) * C] = s_qim[j][pair];
+    for (int j = 0; j < NTAPS; ++j) fir[(size_t)(NTAPS + j) * C] = QIM(j);
   }
   double *ds = S.ds + cl;
   int *is = S.is + cl;
