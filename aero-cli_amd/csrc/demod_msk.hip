@@ -78,7 +78,11 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   constexpr int DTL = SPS / 2 + 1;       // dt.setLength(SPS / 2)
   constexpr int MARG = SPS;              // marg = MovingAverage(SPS)
   constexpr double FS = (double)K::FS;
-  __shared__ double s_qim[NT][WG];
+  // imaginary matched-filter partial sums: registers for 600 bps (40 taps,
+  // ~400 of the 512 registers with the real ones), LDS for 1200 bps (80 taps
+  // would not fit)
+  constexpr bool QREG = NT <= 40;
+  __shared__ double s_qim[QREG ? 1 : NT][WG];
   __shared__ double s_taps[NT];
   {
     const int l = threadIdx.x;
@@ -128,10 +132,17 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   long long ptn = S.ls[LS_PT_N * C + c];
 
   double q[NT];
+  double qi[QREG ? NT : 1];
+  auto QI = [&](int j) -> double & {
+    if constexpr (QREG)
+      return qi[j];
+    else
+      return s_qim[j][lane];
+  };
 #pragma unroll
   for (int j = 0; j < NT; ++j) q[j] = S.fir[(size_t)j * C + c];
 #pragma unroll
-  for (int j = 0; j < NT; ++j) s_qim[j][lane] = S.fir[(size_t)(NT + j) * C + c];
+  for (int j = 0; j < NT; ++j) QI(j) = S.fir[(size_t)(NT + j) * C + c];
 
   const double PT = 0.0125 * WTSIZE;  // IfHavePassedPoint(ee), ee = 0.0125 (mskdemodulator.cpp:203)
   const double d8w = c_msk_d8w[0], d8omw = c_msk_d8w[1];
@@ -155,16 +166,16 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       const double2 cm = T.cis[cis_index(m2_ptr)];
       const double cv = cm.x * dval, cvi = cm.y * dval;  // mixer2.WTCISValue() * dval
       // matched filter: FIRUpdateAndProcess reads the 2*SPS samples before the newest
-      double s2r = q[NT - 1], s2i = s_qim[NT - 1][lane];
+      double s2r = q[NT - 1], s2i = QI(NT - 1);
 #pragma unroll
       for (int j = NT - 1; j >= 1; --j) q[j] = q[j - 1] + s_taps[j] * cv;
       q[0] = 0.0 + s_taps[0] * cv;
 #pragma unroll
       for (int j = NT - 1; j >= 1; --j) {
-        s_qim[j][lane] = s_qim[j - 1][lane] + s_taps[j] * cvi;
-        if ((j & 7) == 0) asm volatile("" : : : "memory");
+        QI(j) = QI(j - 1) + s_taps[j] * cvi;
+        if (!QREG && (j & 7) == 0) asm volatile("" : : : "memory");
       }
-      s_qim[0][lane] = 0.0 + s_taps[0] * cvi;
+      QI(0) = 0.0 + s_taps[0] * cvi;
       const double dab = sqrt(s2r * s2r + s2i * s2i);
       {  // AGC::Update (DSP.cpp:371-380)
         agc_sum = agc_sum - agc_old;
@@ -346,7 +357,7 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
 #pragma unroll
     for (int j = 0; j < NT; ++j) fir[(size_t)j * C] = q[j];
 #pragma unroll
-    for (int j = 0; j < NT; ++j) fir[(size_t)(NT + j) * C] = s_qim[j][lane];
+    for (int j = 0; j < NT; ++j) fir[(size_t)(NT + j) * C] = QI(j);
   }
   double *ds = S.ds + cl;
   long long *ls = S.ls + cl;

@@ -1,7 +1,7 @@
 #!/bin/bash
 set -eo pipefail
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/r03k
+OUT=$R/gpurun_out/r03l
 mkdir -p $OUT
 AERO_ENGINE_SO=$R/aero-cli_amd/libaero_engine_stamps.so timeout -k 10 300 python3 -u $R/scripts/demod_stamps.py 65536 > $OUT/stamps.log 2>&1
 cat $OUT/stamps.log
