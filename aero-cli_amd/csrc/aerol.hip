@@ -239,6 +239,35 @@ __global__ __launch_bounds__(256) void frame_msk_kernel(DevState S, int nch) {
 // One wave per job, ~5.8 KB of LDS and no per-step barrier
 // (viterbi_decode_regs), launched between a coarse hop and a demod launch
 // (engine.hip issue_viterbi).
+#ifdef AERO_X_STAMPS
+// diagnostic build only: s_memtime cycle totals of the Viterbi kernel's
+// sections over every job (load + deinterleave, decode, post + record) and
+// the job count
+__device__ unsigned long long g_vstamps[4];
+#define VSTAMP(k)                                               \
+  do {                                                          \
+    __builtin_amdgcn_sched_barrier(0);                          \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    vst_[k] += t_ - vtime_;                                     \
+    vtime_ = t_;                                                \
+    __builtin_amdgcn_sched_barrier(0);                          \
+  } while (0)
+#else
+#define VSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
+void viterbi_read_stamps(unsigned long long *out) {
+#ifdef AERO_X_STAMPS
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vstamps), sizeof(unsigned long long) * 4);
+  unsigned long long z[4] = {0};
+  hipMemcpyToSymbol(HIP_SYMBOL(g_vstamps), z, sizeof z);
+#else
+  for (int k = 0; k < 4; ++k) out[k] = 0;
+#endif
+}
+
 template <int BLK, int DL2>
 __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, int trace) {
   constexpr int NL = BLK / 64, HALF = BLK / 2;
@@ -251,6 +280,9 @@ __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, in
   const int njobs = *S.njobs;
   for (int job = blockIdx.x; job < njobs; job += gridDim.x) {
   __syncthreads();  // LDS of the previous job fully consumed
+#ifdef AERO_X_STAMPS
+  unsigned long long vst_[4] = {0, 0, 0, 0}, vtime_ = __builtin_amdgcn_s_memtime();
+#endif
   const int lane = threadIdx.x;
   const int4 jd = reinterpret_cast<const int4 *>(S.jobs)[job];
   const int c = jd.x, buf = jd.y & 1, first = (jd.y >> 1) & 1, reset = (jd.y >> 2) & 1, clear = (jd.y >> 3) & 1;
@@ -272,9 +304,11 @@ __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, in
 
   const int sets = nsoft / 2;
   uint64_t obw;
+  VSTAMP(0);
   viterbi_decode_regs(sbuf, nsoft, obw, lane);
   if (lane < NW) obits[lane] = obw;
   __syncthreads();
+  VSTAMP(1);
   auto obit = [&](int k) { return (int)((obits[k >> 6] >> (k & 63)) & 1ULL); };
   // Decode_Continuous: keep decoded bits [25, 25 + BLK/2) clipped to size/2
   const int nbits = (sets - 25) < HALF ? (sets - 25) : HALF;
@@ -359,6 +393,13 @@ __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, in
     o[2] = formatid;
     o[3] = c | (reset << 30);
   }
+  VSTAMP(2);
+#ifdef AERO_X_STAMPS
+  if (lane == 0) {
+    for (int k = 0; k < 3; ++k) atomicAdd(&g_vstamps[k], vst_[k]);
+    atomicAdd(&g_vstamps[3], 1ull);
+  }
+#endif
   }  // job loop
 }
 

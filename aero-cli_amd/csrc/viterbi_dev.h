@@ -193,6 +193,13 @@ __device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nso
     a = sbuf[12];
     b = sbuf[13];
   }
+  // the soft pairs of the next 64 steps: lane l holds step i0 + l's pair
+  // (a | b << 8); a step takes its pair with one v_readlane, so no LDS read
+  // sits on the step's dependency chain
+  auto pairs = [&](int i0) -> uint32_t {
+    const int st = i0 + lane;
+    return st < sets ? (uint32_t)sbuf[2 * st] | ((uint32_t)sbuf[2 * st + 1] << 8) : 0u;
+  };
   // Steps before the restricted tail (every state active), with the column
   // register fixed per run of steps: soft_dist(tab_lo, a, b) = base + sa*a +
   // sb*b for a, b in [0, 255], and the s | 64 edge carries the complementary
@@ -205,13 +212,17 @@ __device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nso
     const int nbase = -(((tab_lo & 1) ? 255 : 0) + ((tab_lo & 2) ? 255 : 0));
     const int src0 = (s >> 1) << 2, src1 = ((s >> 1) | 32) << 2;
     int i = 6;
+    uint32_t pv = pairs(6);
+    int pk = 0;  // step i's pair is lane pk of pv
     auto steps = [&](uint64_t &hw, int run) {
       for (int k = 0; k < run; ++k, ++i) {
-        const int ca = a, cb = b;
-        if (i + 1 < sets) {
-          a = sbuf[2 * i + 2];
-          b = sbuf[2 * i + 3];
+        if (pk == 64) {
+          pv = pairs(i);
+          pk = 0;
         }
+        const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane((int)pv, pk);
+        ++pk;
+        const int ca = (int)(ab & 255u), cb = (int)(ab >> 8);
         const int m0 = __builtin_amdgcn_ds_bpermute(src0, m), m1 = __builtin_amdgcn_ds_bpermute(src1, m);
         const int nd = nbase - __mul24(sa, ca) - __mul24(sb, cb);  // -soft_dist(tab_lo, ca, cb)
         const int e0 = (m0 - nd) & 0xFFFF;
@@ -239,6 +250,10 @@ __device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nso
       else
         steps(h2, run);
     }
+  }
+  if (tail0 < sets) {
+    a = sbuf[2 * tail0];
+    b = sbuf[2 * tail0 + 1];
   }
   for (int i = tail0; i < sets; ++i) {
     // this step's symbols were read one step ahead (LDS latency off the chain)

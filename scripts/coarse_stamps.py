@@ -26,6 +26,9 @@ lib = ae.load_library()
 fn = lib.aero_x_coarse_stamps
 fn.argtypes = [ctypes.c_void_p]
 out = (ctypes.c_ulonglong * 8)()
+vfn = lib.aero_x_viterbi_stamps
+vfn.argtypes = [ctypes.c_void_p]
+vout = (ctypes.c_ulonglong * 4)()
 names = ['prologue+ring+cis', 'FFT 1', 'boxcar+iFFT+square', 'FFT 3', 'hypot', 'log10 smoothing', 'fold search']
 for s in range(steps):
     views = [pool[:, int(o) + s * 4096:int(o) + (s + 1) * 4096] for o in offs]
@@ -36,10 +39,16 @@ for s in range(steps):
     eng.sync()
     if s == 47:
         fn(out)  # reset after the lock-in pre-roll
+        vfn(vout)
 fn(out)
+vfn(vout)
 tot = sum(out[:7])
 n = out[7]
 print('channels %d, hops %d, s_memtime cycles per hop (wave 0) %.0f' % (C, n, tot / max(n, 1)))
 for k in range(7):
     print('  %-20s %9.0f  %5.1f %%' % (names[k], out[k] / max(n, 1), 100.0 * out[k] / max(tot, 1)))
 eng.close()
+vn = vout[3]
+print('viterbi jobs %d, s_memtime cycles per job %.0f' % (vn, sum(vout[:3]) / max(vn, 1)))
+for k, nm in enumerate(['load + deinterleave', 'decode', 'delay line, descramble, CRC, record']):
+    print('  %-38s %9.0f' % (nm, vout[k] / max(vn, 1)))
