@@ -149,14 +149,14 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
   // LDS (38 KB per 256-channel block): the coarse-ring staging area (entries
   // of 8 consecutive samples leave as one 32-byte write per channel instead
   // of eight 4-byte ones) and the carrier-step state.  The RRC taps are
-  // scalar constant-memory loads.  (AERO_X_QIM_LDS, timing experiment only:
-  // the imaginary RRC partial sums in LDS instead of registers, +112 KB.)
-#ifdef AERO_X_QIM_LDS
-  __shared__ double s_qim[NTAPS][DEMOD_BLOCK];
-#define QIM(j) s_qim[j][pair]
-#else
-#define QIM(j) qi[j]
+  // scalar constant-memory loads.
+// the first QIM_LDS imaginary partial sums live in LDS, the rest in
+// registers (0: all in registers; 55: all in LDS, the round-2 layout)
+#ifndef QIM_LDS
+#define QIM_LDS 0
 #endif
+  __shared__ double s_qim[QIM_LDS > 0 ? QIM_LDS : 1][DEMOD_BLOCK];
+#define QIM(j) (*((j) < QIM_LDS ? &s_qim[(j) < QIM_LDS ? (j) : 0][pair] : &qi[j]))
   __shared__ uint32_t s_ring[RING_GROUP][DEMOD_BLOCK];
   __shared__ double s_pd[PD_N][DEMOD_BLOCK];
   __shared__ long long s_pl[PL_N][DEMOD_BLOCK];
@@ -228,9 +228,7 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
   // SIMD; as LDS the imaginary part cost two LDS round trips per tap and
   // sample)
   double q[NTAPS];
-#ifndef AERO_X_QIM_LDS
   double qi[NTAPS];
-#endif
 #pragma unroll
   for (int j = 0; j < NTAPS; ++j) q[j] = S.fir[(size_t)j * C + c];
 #pragma unroll
@@ -291,9 +289,7 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
           QIM(k) = prev_im + pim;
           prev_re = old_re;
           prev_im = old_im;
-#ifdef AERO_X_QIM_LDS
-          if ((k & 7) == 7) asm volatile("" : : : "memory");
-#endif
+          if (QIM_LDS > 0 && (k & 7) == 7) asm volatile("" : : : "memory");
         }
         const double tc = c_taps[(NTAPS - 1) / 2];
         q[(NTAPS - 1) / 2] = prev_re + tc * cv;
