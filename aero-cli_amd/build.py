@@ -97,6 +97,10 @@ def build_mathhost():
 
 def build_oracle():
     _run(['make', '-s', '-C', ORACLE_DIR])
+    # the reference's own Qt-free sources (JFFT, Oscillator) as a second
+    # checker, only where the reference tree exists (not on the GPU box)
+    if os.path.isdir('/root/reference'):
+        _run(['make', '-s', '-C', ORACLE_DIR, 'ref'])
     return os.path.join(ORACLE_DIR, 'liboracle.so')
 
 
