@@ -77,6 +77,10 @@ class ChanVfo(ctypes.Structure):
 CHAN_F_HOST_OUT = 0x1
 
 
+class ChannelEvents(ctypes.Structure):
+    _fields_ = [('dcd_edges', ctypes.c_int64), ('hunter_steps', ctypes.c_int64), ('hunter_fc', ctypes.c_double * 8)]
+
+
 # every entry point declared in include/aero_engine.h and include/aero_chan.h (tests/test_abi.py checks the header)
 _SIGS = {
     'aero_engine_create': (ctypes.c_int, [ctypes.POINTER(EngineCfg), ctypes.POINTER(ctypes.c_void_p)]),
@@ -115,6 +119,7 @@ _SIGS = {
     'aero_stat': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]),
     'aero_channel_stat': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p,
                                          ctypes.POINTER(ctypes.c_int64)]),
+    'aero_channel_get_events': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ChannelEvents)]),
     'aero_sync': (ctypes.c_int, [ctypes.c_void_p]),
     'aero_device_math': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_size_t]),
@@ -269,6 +274,11 @@ class Engine:
         fs = fs or self._fs.get(ch, 48000)
         _check(self.lib.aero_push_pcm_dev(self.h, ch, ctypes.c_void_p(ptr), n, fs), 'aero_push_pcm_dev')
 
+    def push_batch_host(self, ptr, n, ld, nch):
+        """ptr: host pointer of int16 [n, ld]; pinned memory (e.g. a torch
+        pin_memory() tensor) is DMA'd straight into HBM."""
+        _check(self.lib.aero_push_pcm_batch(self.h, ctypes.c_void_p(ptr), n, ld, nch, 0), 'aero_push_pcm_batch')
+
     def push_batch_device(self, ptr, n, ld, nch):
         """ptr: HIP device pointer of int16 [n, ld] (e.g. torch tensor.data_ptr())."""
         _check(self.lib.aero_push_pcm_batch(self.h, ctypes.c_void_p(ptr), n, ld, nch, 1), 'aero_push_pcm_batch')
@@ -375,6 +385,15 @@ class Engine:
         v = ctypes.c_int64()
         _check(self.lib.aero_channel_stat(self.h, ch, name.encode(), ctypes.byref(v)), 'aero_channel_stat')
         return int(v.value)
+
+    def channel_events(self, ch):
+        """aero_channel_get_events: (dcd_edges, hunter_steps, [centre of each
+        of the last min(8, steps) steps, oldest first])."""
+        ev = ChannelEvents()
+        _check(self.lib.aero_channel_get_events(self.h, ch, ctypes.byref(ev)), 'aero_channel_get_events')
+        n = int(ev.hunter_steps)
+        fcs = [ev.hunter_fc[(k - 1) & 7] for k in range(max(1, n - 7), n + 1)]
+        return int(ev.dcd_edges), n, fcs
 
     def samples_processed(self):
         return int(self.lib.aero_samples_processed(self.h))

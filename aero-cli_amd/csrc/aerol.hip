@@ -118,6 +118,7 @@ __global__ __launch_bounds__(256) void frame_kernel(DevState S, int nch) {
     if (gotsync) {
       if (cntr + 1 != Total) isu_reset = 1;
       cntr = -1;
+      if (!datacd) is[IS_DCD_EDGES * C + c]++;  // SignalHunter::handleDcd: dcdChange(false, true)
       datacd = 1;
       scr_pos = 0;
     }
@@ -215,6 +216,10 @@ __global__ __launch_bounds__(256) void frame_msk_kernel(DevState S, int nch) {
       if (cntr + 1 != Total) isu_reset = 1;
       cntr = -1;
       scr_pos = 0;
+      if (!is[IS_DATACD * C + c]) {  // datacd = true (aerol.cpp:2010-2012), a change for SignalHunter::handleDcd
+        is[IS_DATACD * C + c] = 1;
+        is[IS_DCD_EDGES * C + c]++;
+      }
     }
     if (cntr + 1 == Total) {
       scr_pos = 0;

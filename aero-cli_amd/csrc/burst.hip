@@ -841,10 +841,12 @@ __global__ __launch_bounds__(256) void frame_burst_kernel(BurstState S, int nch)
     }
     if (gotsync) {
       cntr = -1;
+      if (!datacd) is[BI_DCD_EDGES * C]++;
       datacd = 1;
     }
     if (cntr + 1 == 10500) {  // end of the burst window: Decode returns
       cntr = 1000000000;
+      if (datacd) is[BI_DCD_EDGES * C]++;
       datacd = 0;
       if (!last) skip = 1;
     }

@@ -69,6 +69,7 @@ enum BIS : int {
   // AeroL burst framing
   BI_RI, BI_MUW, BI_FCNTR, BI_GSL, BI_UWI, BI_UWR, BI_UWI_INV, BI_UWR_INV, BI_DATACD, BI_BLOCKPTR, BI_BURST_ID,
   BI_SKIP_GROUP,
+  BI_DCD_EDGES,  // DataCarrierDetect changes (SignalHunter::handleDcd, decode/hunter.cpp:14-19)
   BI_COUNT
 };
 
@@ -111,6 +112,7 @@ enum BMIS : int {
   BMI_TRI_MINBIN, BMI_TRI_TOPLO, BMI_TRI_TOPHI,
   // AeroL MSK burst framing
   BMI_MUW, BMI_FCNTR, BMI_UW, BMI_UW_INV, BMI_BLOCKPTR, BMI_BURST_ID, BMI_SKIP_GROUP, BMI_TOTAL,
+  BMI_DATACD, BMI_DCD_EDGES,  // AeroL datacd (aerol.cpp:2010-2028) and its changes
   BMI_COUNT
 };
 constexpr int BURST_DS_COUNT = BD_COUNT > BM_COUNT ? BD_COUNT : BM_COUNT;

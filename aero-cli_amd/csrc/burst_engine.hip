@@ -725,6 +725,18 @@ int burst_pop_packets(BurstGroup *g, int c, uint8_t *dst, size_t cap, size_t *n)
 }
 std::vector<aero_acars_item> &burst_items(BurstGroup *g, int c) { return g->host[c]->items; }
 uint64_t burst_processed(const BurstGroup *g) { return g ? g->processed : 0; }
+int burst_dcd_edges(BurstGroup *g, int c, int64_t *edges) {
+  if (!g || c < 0 || c >= g->nch) return AERO_E_INVALID;
+  BCHK(hipSetDevice(g->device));
+  if (int rc = flush_init(g)) return rc;
+  BCHK(hipStreamSynchronize(g->st));
+  const int f = g->kind == BURST_MSK ? BMI_DCD_EDGES : BI_DCD_EDGES;
+  int v = 0;
+  BCHK(hipMemcpy(&v, g->S.is + (size_t)f * g->C + c, sizeof(int), hipMemcpyDeviceToHost));
+  *edges = v;
+  return AERO_OK;
+}
+
 uint64_t burst_stat(const BurstGroup *g, int which) { return !g ? 0 : (which ? g->st_packets : g->st_tests); }
 void burst_timing(BurstGroup *g, const char *name, double *ms, long *launches) {
   if (!g) return;

@@ -754,9 +754,19 @@ __global__ __launch_bounds__(256) void frame_bmsk_kernel(BurstState S, int nch) 
         emitted++;
       }
     }
-    if (gotsync) cntr = -1;
+    if (gotsync) {
+      cntr = -1;
+      if (!is[BMI_DATACD * C]) {  // datacd = true (aerol.cpp:2010-2012), a change for SignalHunter::handleDcd
+        is[BMI_DATACD * C] = 1;
+        is[BMI_DCD_EDGES * C]++;
+      }
+    }
     if (cntr + 1 == total) {  // end of the burst window: Decode returns
       cntr = 1000000000;
+      if (is[BMI_DATACD * C]) {  // datacd = false (aerol.cpp:2021-2028)
+        is[BMI_DATACD * C] = 0;
+        is[BMI_DCD_EDGES * C]++;
+      }
       if (!last) skip = 1;
     }
   }

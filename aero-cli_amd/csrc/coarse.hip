@@ -65,6 +65,8 @@ struct HopCtl {
   double m2f, m2s, mcf, mcs;
   int countdown2, countdown, ecd, yres_next;
   long long zb;
+  bool stepped;  // SignalHunter emitted newFreqCenter(step_fc) this hop
+  double step_fc;
 };
 
 // OqpskDemodulator::FreqOffsetEstimateSlot (decode/oqpskdemodulator.cpp:562-620),
@@ -107,6 +109,8 @@ __device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<in
         iter = 0;
         scans++;
       }
+      h.stepped = true;
+      h.step_fc = fc;
       // CenterFreqChangedSlot, fb != 8400, afc on
       if (fc < (0.5 * 10500.0)) fc = 0.5 * 10500.0;
       if (fc > (Fs / 2.0 - 0.5 * 10500.0)) fc = Fs / 2.0 - 0.5 * 10500.0;
@@ -141,6 +145,8 @@ __device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<in
         iter = 0;
         scans++;
       }
+      h.stepped = true;
+      h.step_fc = fc;
       if (fc < (0.75 * fb)) fc = 0.75 * fb;
       if (fc > (Fs / 2.0 - 0.75 * fb)) fc = Fs / 2.0 - 0.75 * fb;
       set_freq1(h.mcf, h.mcs, fc, Fs);
@@ -359,11 +365,18 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   h.ecd = ecd;
   h.yres_next = 0;
   h.zb = zero_before;
+  h.stepped = false;
+  h.step_fc = 0.0;
   unsigned iter = (unsigned)is[IS_HUNT_ITER * C + c];
   int scans = is[IS_HUNT_SCANS * C + c];
   const bool gotasignal = hop_control(h, std::integral_constant<int, M>(), est, mse, iter, scans, nk);
   is[IS_HUNT_ITER * C + c] = (int)iter;
   is[IS_HUNT_SCANS * C + c] = scans;
+  if (h.stepped) {
+    const int k = is[IS_HUNT_STEPS * C + c];
+    ds[(DS_HUNT_FC0 + (k & 7)) * C + c] = h.step_fc;
+    is[IS_HUNT_STEPS * C + c] = k + 1;
+  }
   ds[DS_M2_FREQ * C + c] = h.m2f;
   ds[DS_M2_STEP * C + c] = h.m2s;
   ds[DS_MC_FREQ * C + c] = h.mcf;

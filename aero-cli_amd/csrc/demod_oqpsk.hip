@@ -8,11 +8,10 @@
  * expression keeps the reference's operation order; std::complex products
  * are expanded as GCC does ((ac-bd), (ad+bc)); libm calls go to aero_math.h.
  *
- * One lane per channel.  The 55-tap RRC runs in transposed form: the real
- * partial sums live in VGPRs, the imaginary ones in LDS ([tap][lane], read
- * and rewritten in descending tap order so the slots never move); together
- * they would not fit beside the rest of the state in gfx950's 256
- * architected VGPRs.
+ * One lane per channel.  The 55-tap RRC runs in transposed form with all
+ * 110 partial sums (real and imaginary) in registers for the whole launch
+ * (one wave per SIMD, up to 512 VGPR+AGPR); the QIM_LDS build switch puts
+ * the imaginary ones back in LDS ([tap][lane]) for experiments only.
  *
  * Segment contract: a launch advances every channel from nsamp up to (but
  * excluding) its next coarse-estimate hop sample, or to the pushed end; it

@@ -648,8 +648,11 @@ int issue_viterbi(Group *e) {
 // after a demod launch: the ring rows of samples below every channel's new
 // nsamp are free once the main stream has passed this point
 int note_consumed(Group *e) {
+  // a caught-up channel (nsamp == avail: an idle or never-pushed one) holds
+  // no unconsumed rows, so only channels with samples still queued bound it
   long long mn = LLONG_MAX;
-  for (int c = 0; c < e->nch; c++) mn = std::min(mn, e->nsamp[c]);
+  for (int c = 0; c < e->nch; c++)
+    if (e->avail[c] > e->nsamp[c]) mn = std::min(mn, e->nsamp[c]);
   hipEvent_t ev;
   if (e->ev_free.empty()) {
     HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -742,7 +745,10 @@ int run_group(Group *e, int flush) {
       if (int rc = collect_traces(e)) return rc;
     }
   }
-  return AERO_OK;
+  // the deferral only reorders passes inside this call: the last pass's
+  // decode is launched before aero_run returns, so its items never wait for
+  // more audio (the reference emits them as soon as they are decoded)
+  return issue_viterbi(e);
 }
 
 // waits for the group's GPU work and hands every completed slot over
@@ -836,7 +842,7 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
     HIPCHK(hipEventCreateWithFlags(&e->pin_ev[k], hipEventDisableTiming));
   }
   HIPCHK(hipEventCreateWithFlags(&e->pin_pcm_ev, hipEventDisableTiming));
-  if (hipHostMalloc(&e->pin_stat, 64) != hipSuccess) return AERO_E_NOMEM;
+  if (hipHostMalloc(&e->pin_stat, 128) != hipSuccess) return AERO_E_NOMEM;
   {
     int lo = 0, hi = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -969,10 +975,27 @@ int check_dev_ptr(const void *p) {
 
 namespace {
 
+// host memory the HIP runtime has pinned (hipHostMalloc / hipHostRegister,
+// e.g. a torch pin_memory() tensor): the DMA engines read it directly
+bool is_pinned_host(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
 int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int c0, bool dev) {
   HOST_TIMER(e, "host_push");
   if (dev)
     if (int rc = check_dev_ptr(src)) return rc;
+  // pinned host input goes straight into the PCM ring rows (one 2-D DMA on
+  // the input stream, overlapping the kernels already queued), as a device
+  // source does; pageable input is staged
+  const bool pinned = !dev && nch >= 64 && is_pinned_host(src);
+  const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  if (pinned) dev = true;
   if (int rc = flush_pending_init(e)) return rc;
   // keep the ring from overrunning unprocessed samples
   for (int j = 0; j < nch; j++) {
@@ -1032,10 +1055,10 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
     const long long r0 = start & (PCM_CAP - 1);
     const size_t n1 = (size_t)std::min<long long>((long long)n, PCM_CAP - r0);
     HIPCHK(hipMemcpy2DAsync(e->S.pcm + r0 * e->C + c0, sizeof(int16_t) * e->C, src, sizeof(int16_t) * ld,
-                            sizeof(int16_t) * nch, n1, hipMemcpyDeviceToDevice, e->st_in));
+                            sizeof(int16_t) * nch, n1, kind, e->st_in));
     if (n1 < n)
       HIPCHK(hipMemcpy2DAsync(e->S.pcm + c0, sizeof(int16_t) * e->C, src + n1 * ld, sizeof(int16_t) * ld,
-                              sizeof(int16_t) * nch, n - n1, hipMemcpyDeviceToDevice, e->st_in));
+                              sizeof(int16_t) * nch, n - n1, kind, e->st_in));
     HIPCHK(hipEventRecord(e->ev_in, e->st_in));
     HIPCHK(hipEventSynchronize(e->ev_in));  // the caller's buffer is free again
     HIPCHK(hipStreamWaitEvent(e->st, e->ev_in, 0));
@@ -1463,6 +1486,8 @@ int aero_stat(aero_engine *e, const char *name, uint64_t *value) {
   host_wait(e);  // counters of frames the host workers are still handling
   uint64_t v = 0;
   const std::string n(name);
+  if (n != "rt_tests" && n != "rt_packets" && n != "viterbi_jobs" && n != "frames" && n != "su_crc_ok")
+    return AERO_E_INVALID;
   if (n == "rt_tests" || n == "rt_packets") {
     *value = burst_stat(e->burst[0], n == "rt_packets") + burst_stat(e->burst[1], n == "rt_packets");
     return AERO_OK;
@@ -1473,10 +1498,8 @@ int aero_stat(aero_engine *e, const char *name, uint64_t *value) {
       v += g->st_jobs.load();
     else if (n == "frames")
       v += g->st_frames.load();
-    else if (n == "su_crc_ok")
-      v += g->st_su_ok.load();
     else
-      return AERO_E_INVALID;
+      v += g->st_su_ok.load();
   }
   *value = v;
   return AERO_OK;
@@ -1512,6 +1535,33 @@ int aero_channel_stat(aero_engine *e, int ch, const char *name, int64_t *value) 
   } else {
     return AERO_E_INVALID;
   }
+  return AERO_OK;
+}
+
+int aero_channel_get_events(aero_engine *e, int ch, aero_channel_events *out) {
+  if (!e || !out) return AERO_E_INVALID;
+  memset(out, 0, sizeof *out);
+  BurstGroup *bg;
+  const int b = route_burst(e, ch, &bg);
+  HIPCHK(hipSetDevice(e->device));
+  if (b >= 0) return burst_dcd_edges(bg, b, &out->dcd_edges);
+  int c;
+  Group *g = route(e, ch, c);
+  if (!g) return AERO_E_INVALID;
+  if (int rc = flush_pending_init(g)) return rc;
+  // two ints and eight doubles into pinned staging, one wait
+  int *pi = reinterpret_cast<int *>(g->pin_stat);
+  double *pd = reinterpret_cast<double *>(g->pin_stat) + 1;
+  HIPCHK(hipMemcpyAsync(pi, g->S.is + (size_t)IS_DCD_EDGES * g->C + c, sizeof(int), hipMemcpyDeviceToHost, g->st));
+  HIPCHK(hipMemcpyAsync(pi + 1, g->S.is + (size_t)IS_HUNT_STEPS * g->C + c, sizeof(int), hipMemcpyDeviceToHost,
+                        g->st));
+  for (int k = 0; k < 8; k++)
+    HIPCHK(hipMemcpyAsync(pd + k, g->S.ds + (size_t)(DS_HUNT_FC0 + k) * g->C + c, sizeof(double),
+                          hipMemcpyDeviceToHost, g->st));
+  HIPCHK(hipStreamSynchronize(g->st));
+  out->dcd_edges = pi[0];
+  out->hunter_steps = pi[1];
+  for (int k = 0; k < 8; k++) out->hunter_fc[k] = pd[k];
   return AERO_OK;
 }
 

@@ -82,6 +82,9 @@ enum DS : int {
   DS_MSE,
   DS_PTD_RE, DS_PTD_IM, DS_S2L_RE, DS_S2L_IM,
   DS_DIFF_LAST,   // MSK DiffDecode::lastsoftstate (decode/DSP.cpp:517-520)
+  // SignalHunter::newFreqCenter values (decode/hunter.cpp:34-40) of the last
+  // eight steps: step k (1-based) at DS_HUNT_FC0 + ((k - 1) & 7)
+  DS_HUNT_FC0, DS_HUNT_FC_END = DS_HUNT_FC0 + 7,
   DS_COUNT
 };
 
@@ -99,6 +102,9 @@ enum IS : int {
   IS_SCR_POS, IS_BLKBUF, IS_HAS_OVERLAP, IS_DL2_PTR,
   IS_MSK_PD,      // MSK PreambleDetector shift register (aerol.cpp:716-725)
   IS_BLK_SINCE_CLEAR,  // blocks appended to the infofield since cntr == 0
+  // decoder status events (decode/decode.cpp:429-439): DataCarrierDetect
+  // changes as SignalHunter::handleDcd sees them, newFreqCenter emissions
+  IS_DCD_EDGES, IS_HUNT_STEPS,
   IS_COUNT
 };
 

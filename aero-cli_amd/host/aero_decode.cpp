@@ -13,7 +13,16 @@
  *  - on SIGINT / SIGTERM the samples already received are flushed through
  *    the engine and their items printed and forwarded before exit (the
  *    reference's synchronous chain has no tail to flush);
- *  - libacars enrichment (`parsed`) is absent (libacars is not in the image).
+ *  - libacars enrichment (`parsed`) is absent (libacars is not in the image);
+ *  - a continuous MSK channel runs at the rate aero-decode configures for its
+ *    bit rate (12000 / 24000 Hz); a message at another rate is dropped with a
+ *    CRIT line (MskDemodulator would re-apply its settings at that rate,
+ *    decode/mskdemodulator.cpp:472-480);
+ *  - the verbose DCD / frequency-centre lines (decode/decode.cpp:429-439)
+ *    are printed after each engine run, not as the demodulator emits them;
+ *  - extension: several -t options decode several topics in one process,
+ *    one engine channel per topic (-b / -s once, or once per topic); every
+ *    message queued on the socket is pushed before one aero_run.
  */
 #include <execinfo.h>
 #include <signal.h>
@@ -63,9 +72,17 @@ void on_signal(int sig) {
 }
 
 struct Options {
-  std::string bitrate, fwd, publisher, station, topic, format;
+  // QCommandLineParser keeps every occurrence of an option: the reference
+  // reads value(), the last one; repeated -t / -b / -s select the
+  // multi-topic mode (one process, one engine channel per topic)
+  std::vector<std::string> bitrate, fwd, publisher, station, topic, format;
   bool verbose = false, burst = false, disable_reassembly = false, no_signal_exit = false;
 };
+
+const std::string &last(const std::vector<std::string> &v) {
+  static const std::string none;
+  return v.empty() ? none : v.back();
+}
 
 const char *kUsage =
     "Usage: aero-decode [options]\n"
@@ -88,14 +105,17 @@ const char *kUsage =
     "  --format <format>            ACARS format type to display on console; valid:\n"
     "                               jaero, jsondump, text (default)\n"
     "  --no-signal-exit             Exit if no signal is found after a full scan of\n"
-    "                               a VFO\n";
+    "                               a VFO\n"
+    "\n"
+    "Several -t options decode several VFO topics in one process on one engine\n"
+    "(-b and -s then given once, or once per topic in the same order).\n";
 
 // QCommandLineParser (decode/main.cpp:17-51): -x value, -xvalue, --name value,
 // --name=value; an unknown option or a missing value ends the program with 1
 bool parse_args(int argc, char **argv, Options &o) {
   struct Opt {
     const char *s, *l;
-    std::string *val;
+    std::vector<std::string> *val;
     bool *flag;
   } opts[] = {{"b", "bit-rate", &o.bitrate, nullptr},     {"f", "fwd", &o.fwd, nullptr},
               {"p", "publisher", &o.publisher, nullptr},  {"s", "station-id", &o.station, nullptr},
@@ -148,9 +168,9 @@ bool parse_args(int argc, char **argv, Options &o) {
     if (hit->flag) {
       *hit->flag = true;
     } else if (has_inl) {
-      *hit->val = inl;
+      hit->val->push_back(inl);
     } else if (i + 1 < argc) {
-      *hit->val = argv[++i];
+      hit->val->push_back(argv[++i]);
     } else {
       fprintf(stderr, "Missing value after '%s'.\n", a.c_str());
       exit(1);
@@ -222,49 +242,90 @@ std::string hostname_upper() {
 
 }  // namespace
 
+// one subscribed VFO topic: its engine channel and what aero-decode keeps
+// per Decoder (decode/decode.cpp:72-115)
+struct Topic {
+  std::string name;
+  int bitrate = 0;
+  uint32_t fs = 0;
+  ustr station;
+  int ch = -1;
+  bool live = true;               // still decoding (--no-signal-exit stops a topic)
+  long long scans_seen = 0;       // SignalHunter full scans reported
+  long long dcd_seen = 0, steps_seen = 0;  // status events logged
+};
+
 int main(int argc, char **argv) {
   Options o;
   parse_args(argc, argv, o);
   g_verbose = o.verbose;
-  if (o.publisher.empty()) {
+  if (last(o.publisher).empty()) {
     AH_CRIT("Required publisher option is missing, example: -p tcp://127.0.0.1:6004");
     return 1;
   }
-  if (o.station.empty()) {
-    o.station = hostname_upper() + "-AERO-INMARSAT";
-    AH_WARN("No station ID provided, using generated default %s", o.station.c_str());
+  const std::string publisher = last(o.publisher);
+  const bool multi = o.topic.size() > 1;
+  if (o.station.empty() || last(o.station).empty()) {
+    o.station = {hostname_upper() + "-AERO-INMARSAT"};
+    AH_WARN("No station ID provided, using generated default %s", o.station[0].c_str());
   }
-  if (o.topic.empty()) {
+  if (last(o.topic).empty()) {
     AH_CRIT("Required topic option is missing, example: -t VFO51");
     return 1;
   }
-  if (o.format.empty()) o.format = "text";
-  const int bitrate = atoi(o.bitrate.c_str());  // QString::toInt: 0 when not a number
+  const std::string format = o.format.empty() ? std::string("text") : last(o.format);
+  // one topic: the reference's last-value semantics; several: -b / -s given
+  // once for all topics or once per topic
+  std::vector<Topic> topics;
+  if (multi) {
+    for (const auto *v : {&o.bitrate, &o.station})
+      if (v->size() > 1 && v->size() != o.topic.size()) {
+        AH_CRIT("With %zu topics, -b and -s are given once or once per topic", o.topic.size());
+        return 0;
+      }
+    for (size_t k = 0; k < o.topic.size(); k++) {
+      Topic t;
+      t.name = o.topic[k];
+      t.bitrate = atoi((o.bitrate.size() > 1 ? o.bitrate[k] : last(o.bitrate)).c_str());
+      t.station = from_utf8(o.station.size() > 1 ? o.station[k] : last(o.station));
+      topics.push_back(t);
+    }
+  } else {
+    Topic t;
+    t.name = last(o.topic);
+    t.bitrate = atoi(last(o.bitrate).c_str());  // QString::toInt: 0 when not a number
+    t.station = from_utf8(last(o.station));
+    topics.push_back(t);
+  }
 
   // Decoder::Decoder (decode/decode.cpp:72-115): a bad configuration logs and
   // leaves the decoder stopped; the application then completes with status 0
-  if (bitrate != 600 && bitrate != 1200 && bitrate != 10500) {
-    AH_CRIT("Unsupported bit rate: %d", bitrate);
-    return 0;
-  }
-  const OutputFormat fmt = parse_output_format(o.format);
+  for (auto &t : topics)
+    if (t.bitrate != 600 && t.bitrate != 1200 && t.bitrate != 10500) {
+      AH_CRIT("Unsupported bit rate: %d", t.bitrate);
+      return 0;
+    }
+  const OutputFormat fmt = parse_output_format(format);
   if (fmt == OutputFormat::None) {
-    AH_CRIT("Invalid output format provided: %s", o.format.c_str());
+    AH_CRIT("Invalid output format provided: %s", format.c_str());
     return 0;
   }
-  std::vector<std::unique_ptr<ForwardTarget>> targets;
-  if (!o.fwd.empty()) {
-    size_t s = 0;
-    for (;;) {
-      const size_t e = o.fwd.find(',', s);
-      auto t = ForwardTarget::from_raw(o.fwd.substr(s, e == std::string::npos ? std::string::npos : e - s));
-      if (!t) {
-        AH_CRIT("Some forwarders configuration may be malformed: %s", o.fwd.c_str());
-        return 0;
+  const std::string fwd_raw = last(o.fwd);
+  std::vector<std::vector<std::unique_ptr<ForwardTarget>>> targets(topics.size());
+  if (!fwd_raw.empty()) {
+    for (auto &tv : targets) {
+      size_t s = 0;
+      for (;;) {
+        const size_t e = fwd_raw.find(',', s);
+        auto t = ForwardTarget::from_raw(fwd_raw.substr(s, e == std::string::npos ? std::string::npos : e - s));
+        if (!t) {
+          AH_CRIT("Some forwarders configuration may be malformed: %s", fwd_raw.c_str());
+          return 0;
+        }
+        tv.push_back(std::move(t));
+        if (e == std::string::npos) break;
+        s = e + 1;
       }
-      targets.push_back(std::move(t));
-      if (e == std::string::npos) break;
-      s = e + 1;
     }
   }
   const Zmq *z = zmq_load();
@@ -279,23 +340,27 @@ int main(int argc, char **argv) {
     AH_CRIT("Failed to create ZeroMQ socket, error code = %d", z->errno_());
     return 0;
   }
-  // the engine: one channel, this topic's demodulator + AeroL + hunter
+  // the engine: one channel per topic (its demodulator + AeroL + hunter);
+  // every aero_run advances all of them in the same batched launches
   aero_engine *eng = nullptr;
   const char *dev = getenv("AERO_DEVICE");
-  aero_engine_cfg ecfg{dev ? atoi(dev) : 0, 1, 0};
+  aero_engine_cfg ecfg{dev ? atoi(dev) : 0, (int)topics.size(), 0};
   if (int rc = aero_engine_create(&ecfg, &eng)) {
     AH_CRIT("Failed to create the MI355X demodulation engine: %s", aero_strerror(rc));
     return 1;
   }
-  const uint32_t fs_cfg = bitrate == 600 ? 12000 : (bitrate == 1200 ? 24000 : 48000);
-  aero_channel_cfg ccfg{bitrate, o.burst ? 1 : 0, fs_cfg, o.disable_reassembly ? 1 : 0};
-  int ch = -1;
-  if (int rc = aero_channel_open(eng, &ccfg, &ch)) {
-    AH_CRIT("Unsupported channel configuration (bit rate %d%s): %s", bitrate, o.burst ? ", burst" : "",
-            aero_strerror(rc));
-    aero_engine_destroy(eng);
-    return 1;
+  for (auto &t : topics) {
+    t.fs = t.bitrate == 600 ? 12000 : (t.bitrate == 1200 ? 24000 : 48000);
+    aero_channel_cfg ccfg{t.bitrate, o.burst ? 1 : 0, t.fs, o.disable_reassembly ? 1 : 0};
+    if (int rc = aero_channel_open(eng, &ccfg, &t.ch)) {
+      AH_CRIT("Unsupported channel configuration (bit rate %d%s): %s", t.bitrate, o.burst ? ", burst" : "",
+              aero_strerror(rc));
+      aero_engine_destroy(eng);
+      return 1;
+    }
   }
+  std::vector<int> topic_of(topics.size());
+  for (size_t k = 0; k < topics.size(); k++) topic_of[topics[k].ch] = (int)k;
   g_running.store(1);
   struct sigaction sa;
   memset(&sa, 0, sizeof sa);
@@ -308,23 +373,26 @@ int main(int argc, char **argv) {
   signal(SIGABRT, on_fatal);
   signal(SIGPIPE, SIG_IGN);
 
-  const ustr station = from_utf8(o.station);
-  Forwarders fwd(std::move(targets), station, o.disable_reassembly);
-  std::vector<aero_acars_item> items(16);
+  std::vector<std::unique_ptr<Forwarders>> fwd;
+  for (size_t k = 0; k < topics.size(); k++)
+    fwd.emplace_back(new Forwarders(std::move(targets[k]), topics[k].station, o.disable_reassembly));
+  std::vector<aero_acars_item> items(64);
+  std::vector<int> item_ch(items.size());
   // handleACARS (decode/decode.cpp:441-455): console line, then the forwarders
   auto drain = [&]() {
     size_t n = 0;
     do {
-      if (aero_pop_items(eng, ch, items.data(), items.size(), &n)) break;
+      if (aero_pop_items_all(eng, items.data(), item_ch.data(), items.size(), &n)) break;
       for (size_t i = 0; i < n; i++) {
+        const int k = topic_of[item_ch[i]];
         const long long ms = now_ms();
         ustr out;
-        if (!to_output_format(fmt, station, o.disable_reassembly, items[i], ms, out)) {
+        if (!to_output_format(fmt, topics[k].station, o.disable_reassembly, items[i], ms, out)) {
           AH_CRIT("Failed to generate output format!");
           continue;
         }
         AH_INF("%s", to_utf8(out).c_str());
-        fwd.push(items[i], ms);
+        fwd[k]->push(items[i], ms);
       }
     } while (n == items.size());
   };
@@ -333,60 +401,115 @@ int main(int argc, char **argv) {
   const int buf_size = 192000;
   std::vector<char> samples(buf_size);
   int rc_exit = 0;
-  long long scans_seen = 0, last_check = 0;
-  AH_DBG("Connecting to ZMQ endpoint at %s", o.publisher.c_str());
-  if (z->connect(sub, o.publisher.c_str()) == -1) {
+  AH_DBG("Connecting to ZMQ endpoint at %s", publisher.c_str());
+  if (z->connect(sub, publisher.c_str()) == -1) {
     AH_CRIT("Failed to connect to publisher, error code: %d; is aero-publish or SDRReceiver running?", -1);
     g_running.store(0);
   } else {
-    AH_DBG("Subscribing to ZMQ topic %s", o.topic.c_str());
-    if (z->setsockopt(sub, ZMQ_SUBSCRIBE_, o.topic.c_str(), strlen(o.topic.c_str())) == -1) {
-      AH_CRIT("Failed to subscribe to %s; error code = %d", o.topic.c_str(), z->errno_());
-      g_running.store(0);
+    for (auto &t : topics) {
+      AH_DBG("Subscribing to ZMQ topic %s", t.name.c_str());
+      if (z->setsockopt(sub, ZMQ_SUBSCRIBE_, t.name.c_str(), strlen(t.name.c_str())) == -1) {
+        AH_CRIT("Failed to subscribe to %s; error code = %d", t.name.c_str(), z->errno_());
+        g_running.store(0);
+        break;
+      }
     }
   }
+  // in multi-topic mode a log line about one VFO names its topic
+  auto tag = [&](const Topic &t) { return multi ? " [" + t.name + "]" : std::string(); };
+  // Decoder::handleDcdChange / handleNewFreqCenter (decode/decode.cpp:429-439):
+  // verbose only, polled with the scan check (about once a second) and at exit
+  auto log_events = [&]() {
+    if (!g_verbose) return;
+    for (auto &t : topics) {
+      aero_channel_events ev;
+      if (aero_channel_get_events(eng, t.ch, &ev) != AERO_OK) continue;
+      for (long long k = t.dcd_seen + 1; k <= ev.dcd_edges; k++) {
+        if (k & 1)
+          AH_DBG("Data carrier detected: no signal => signal%s", tag(t).c_str());
+        else
+          AH_DBG("Data carrier lost: signal => no signal%s", tag(t).c_str());
+      }
+      t.dcd_seen = ev.dcd_edges;
+      for (long long k = std::max(t.steps_seen + 1, (long long)ev.hunter_steps - 7); k <= ev.hunter_steps; k++)
+        AH_DBG("Trying frequency center %.1f in search of signal%s", ev.hunter_fc[(k - 1) & 7], tag(t).c_str());
+      t.steps_seen = ev.hunter_steps;
+    }
+  };
   // SignalHunter::noSignalAfterScan -> handleNoSignalAfterFullScan
   // (decode/decode.cpp:418-427), polled about once a second
+  long long last_check = 0;
   auto check_scans = [&]() {
-    const long long t = std::chrono::duration_cast<std::chrono::milliseconds>(
-                            std::chrono::steady_clock::now().time_since_epoch()).count();
-    if (last_check && t - last_check < 1000) return;
-    last_check = t;
-    int64_t scans = 0;
-    if (aero_channel_stat(eng, ch, "hunter_scans", &scans) == AERO_OK && scans > scans_seen) {
-      scans_seen = scans;
-      AH_WARN("Scanned entire VFO bandwidth and could not find a signal.");
-      if (o.no_signal_exit) {
-        AH_WARN("Please confirm and verify that the specified topic is correct and that aero-publish is using "
-                "correct settings");
-        g_running.store(0);
-        AH_FATAL("Exiting because of no signal");  // the application then completes (status 0)
+    const long long now = std::chrono::duration_cast<std::chrono::milliseconds>(
+                              std::chrono::steady_clock::now().time_since_epoch())
+                              .count();
+    if (last_check && now - last_check < 1000) return;
+    last_check = now;
+    log_events();
+    bool any_live = false;
+    for (auto &t : topics) {
+      int64_t scans = 0;
+      if (t.live && aero_channel_stat(eng, t.ch, "hunter_scans", &scans) == AERO_OK && scans > t.scans_seen) {
+        t.scans_seen = scans;
+        AH_WARN("Scanned entire VFO bandwidth and could not find a signal.%s", tag(t).c_str());
+        if (o.no_signal_exit) {
+          AH_WARN("Please confirm and verify that the specified topic is correct and that aero-publish is using "
+                  "correct settings%s", tag(t).c_str());
+          t.live = false;  // a reference process per topic: this one exits
+        }
       }
+      any_live |= t.live;
+    }
+    if (!any_live) {
+      g_running.store(0);
+      AH_FATAL("Exiting because of no signal");  // the application then completes (status 0)
     }
   };
   if (g_running.load()) AH_DBG("Listening for samples...");
+  char tbuf[256];
   while (g_running.load()) {
     int n;
-    while ((n = z->recv(sub, nullptr, 0, ZMQ_DONTWAIT_)) < 0 && g_running.load()) {
+    while ((n = z->recv(sub, tbuf, sizeof tbuf, ZMQ_DONTWAIT_)) < 0 && g_running.load()) {
       usleep(10000);
       check_scans();
     }
     if (!g_running.load()) break;
-    unsigned char rate_buf[4];
-    n = z->recv(sub, rate_buf, sizeof rate_buf, ZMQ_DONTWAIT_);
-    if (n != (int)sizeof rate_buf) continue;
-    uint32_t rate;
-    memcpy(&rate, rate_buf, 4);
-    n = z->recv(sub, samples.data(), buf_size, ZMQ_DONTWAIT_);
-    if (!g_running.load()) break;
-    if (n < 0) continue;
-    const size_t bytes = (size_t)(n < buf_size ? n : buf_size);
-    // emit audioReceived -> dataReceived: len/2 int16 samples
-    int rc = aero_push_pcm(eng, ch, reinterpret_cast<const int16_t *>(samples.data()), bytes / 2, rate);
-    if (rc == AERO_E_RATE) {
-      AH_CRIT("Sample rate %u differs from the %u Hz this bit rate's demodulator runs at", rate, fs_cfg);
-      continue;
+    // every message already queued goes in before one aero_run (the engine
+    // re-blocks continuous channels into hop segments, burst channels keep
+    // each message's boundaries), at most 256 per run
+    int rc = AERO_OK;
+    for (int batch = 0; n >= 0 && g_running.load();) {
+      unsigned char rate_buf[4];
+      const int tlen = n < (int)sizeof tbuf ? n : (int)sizeof tbuf;
+      n = z->recv(sub, rate_buf, sizeof rate_buf, ZMQ_DONTWAIT_);
+      if (n == (int)sizeof rate_buf) {
+        uint32_t rate;
+        memcpy(&rate, rate_buf, 4);
+        n = z->recv(sub, samples.data(), buf_size, ZMQ_DONTWAIT_);
+        if (n >= 0) {
+          const size_t bytes = (size_t)(n < buf_size ? n : buf_size);
+          // ZMQ's prefix match: the message goes to every topic it matches
+          // (one reference process per topic would each receive it)
+          for (auto &t : topics) {
+            if (!t.live || (int)t.name.size() > tlen || memcmp(tbuf, t.name.data(), t.name.size())) continue;
+            // emit audioReceived -> dataReceived: len/2 int16 samples
+            rc = aero_push_pcm(eng, t.ch, reinterpret_cast<const int16_t *>(samples.data()), bytes / 2, rate);
+            if (rc == AERO_E_RATE) {
+              // MskDemodulator::dataReceived would re-apply its settings at
+              // this rate (mskdemodulator.cpp:472-480); this engine's MSK
+              // channels run at 12000 / 24000 Hz only, so the message is dropped
+              AH_CRIT("Sample rate %u differs from the %u Hz this bit rate's demodulator runs at; message "
+                      "dropped%s", rate, t.fs, tag(t).c_str());
+              rc = AERO_OK;
+            }
+            if (rc) break;
+          }
+        }
+      }
+      if (rc || ++batch >= 256) break;
+      n = z->recv(sub, tbuf, sizeof tbuf, ZMQ_DONTWAIT_);
     }
+    if (!g_running.load()) break;
     if (rc || (rc = aero_run(eng))) {
       AH_CRIT("engine error: %s", aero_strerror(rc));
       rc_exit = 1;
@@ -396,8 +519,11 @@ int main(int argc, char **argv) {
     check_scans();
   }
   // the tail of what was received
-  if (aero_flush(eng) == AERO_OK) drain();
-  fwd.stop();
+  if (aero_flush(eng) == AERO_OK) {
+    drain();
+    log_events();
+  }
+  for (auto &f : fwd) f->stop();
   aero_engine_destroy(eng);
   z->close(sub);
   z->ctx_term(ctx);

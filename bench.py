@@ -31,30 +31,42 @@ for p in (os.path.join(ROOT, 'aero-cli_amd'), os.path.join(ROOT, 'tests')):
 # bytes per input sample, synthetic carrier range, CPU-baseline signal seconds
 MODES = {
     # 2 B int16 in + 16 B AGC ring r/w (192000-deep, cannot stay on chip) + 0.22 B soft bits out
-    'oqpsk10500': dict(bitrate=10500, hop=4096, fs=48000, bytes=18.22, kernel='demod_oqpsk_kernel', timing='demod',
+    'oqpsk10500': dict(bitrate=10500, hop=4096, fs=48000, bytes=18.22, timing='demod',
                        metric='Msamples/s demod+Viterbi, 10500bps OQPSK, 1/2/4/8 GPU; ACARS frames bit-exact vs ref',
-                       cpu_seconds=240.0, config='C2', flops=1300.0),
+                       cpu_seconds=240.0, config='C2', flops=1300.0, nfft_log2=14,
+                       kernels={'demod': 'demod_oqpsk_kernel', 'coarse': 'coarse_kernel', 'frame': 'frame_kernel',
+                                'viterbi': 'viterbi_kernel'}),
     # 2 B int16 in + 0.05 B soft bits out
-    'msk600': dict(bitrate=600, hop=2048, fs=12000, bytes=2.05, kernel='demod_msk_kernel<1>', timing='msk600_demod',
+    'msk600': dict(bitrate=600, hop=2048, fs=12000, bytes=2.05, timing='msk600_demod',
                    metric='Msamples/s demod+Viterbi, 600bps MSK (C3); ACARS frames bit-exact vs ref',
-                   cpu_seconds=2400.0, config='C3', flops=1050.0),
+                   cpu_seconds=2400.0, config='C3', flops=1050.0, nfft_log2=13,
+                   kernels={'demod': 'demod_msk_kernel', 'coarse': 'coarse_kernel', 'frame': 'frame_msk_kernel',
+                            'viterbi': 'viterbi_kernel'}),
     # burst OQPSK (C4): 2 B int16 in + 16 B AGC ring r/w (48000-deep) + soft bits out;
     # a step is one 12000-sample message per channel (burst output follows message boundaries)
-    'burst10500': dict(bitrate=10500, hop=12000, fs=48000, bytes=18.22, kernel='demod_burst_kernel',
+    'burst10500': dict(bitrate=10500, hop=12000, fs=48000, bytes=18.22,
                        timing='burst_demod', burst=True, preroll=4,
                        metric='Msamples/s demod+Viterbi, 10500bps burst OQPSK (C4); R/T packets bit-exact vs ref',
-                       cpu_seconds=240.0, config='C4', flops=1300.0),
+                       cpu_seconds=240.0, config='C4', flops=1300.0,
+                       kernels={'hilbert': 'hilbert_kernel', 'demod': 'demod_burst_kernel',
+                                'trident': 'trident_kernel', 'frame': 'frame_burst_kernel',
+                                'viterbi': 'rt_viterbi_kernel'}),
     # burst MSK (aero-decode -b 1200 --burst: one fb = 1200 demodulator at 48 kHz), the C4
     # accounting: 2 B int16 in + 16 B AGC ring r/w (48000-deep) + soft bits out; a step is one
     # 12000-sample message per channel
-    'burstmsk1200': dict(bitrate=1200, hop=12000, fs=48000, bytes=18.05, kernel='demod_bmsk_kernel',
+    'burstmsk1200': dict(bitrate=1200, hop=12000, fs=48000, bytes=18.05,
                          timing='burst_demod', burst=True, preroll=4,
                          metric='Msamples/s demod+Viterbi, 1200bps burst MSK; R/T packets bit-exact vs ref',
-                         cpu_seconds=240.0, config='f1 (burst MSK 1200)', flops=900.0),
+                         cpu_seconds=240.0, config='f1 (burst MSK 1200)', flops=900.0,
+                         kernels={'hilbert': 'hilbert_kernel', 'demod': 'demod_bmsk_kernel',
+                                  'trident': 'trident_bmsk_kernel', 'frame': 'frame_bmsk_kernel',
+                                  'viterbi': 'rt_viterbi_kernel'}),
     # 2 B int16 in + 0.025 B soft bits out (fb stays 600 at 24 kHz, decode/decode.cpp:142-150)
-    'msk1200': dict(bitrate=1200, hop=2048, fs=24000, bytes=2.025, kernel='demod_msk_kernel<2>',
+    'msk1200': dict(bitrate=1200, hop=2048, fs=24000, bytes=2.025,
                     timing='msk1200_demod', metric='Msamples/s demod+Viterbi, 1200bps MSK; ACARS frames bit-exact vs ref',
-                    cpu_seconds=1200.0, config='C3 (1200 variant)', flops=1050.0),
+                    cpu_seconds=1200.0, config='C3 (1200 variant)', flops=1050.0, nfft_log2=13,
+                    kernels={'demod': 'demod_msk_kernel', 'coarse': 'coarse_kernel', 'frame': 'frame_msk_kernel',
+                             'viterbi': 'viterbi_kernel'}),
 }
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6    # MI355X vector FP64 (spec)
@@ -73,7 +85,7 @@ CALIBRATION = {'oqpsk10500': {'port_msps_per_core': 0.967, 'reference_msps_per_c
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--mode', default='oqpsk10500', choices=sorted(MODES) + ['c1', 'c5'],
+    ap.add_argument('--mode', default='oqpsk10500', choices=sorted(MODES) + ['c1', 'c5', 'c5bin'],
                     help='channel kind (default: the BASELINE.json headline, C2 10500-bps OQPSK)')
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5,
@@ -85,7 +97,11 @@ def parse():
     ap.add_argument('--cpu-procs', type=int, default=None,
                     help='CPU-baseline processes (default: the host cores this process may use, at most 16 = '
                          'the GPU box CPU share)')
+    ap.add_argument('--cpu-runs', type=int, default=3, help='CPU-baseline repetitions (the median is reported)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--h2d-steps', type=int, default=10,
+                    help='continuous modes: steps of the second, H2D-inclusive timed region (int16 blocks pushed '
+                         'from pinned host memory inside it); 0 skips it')
     ap.add_argument('--pmc', default=None,
                     help='rocprofv3 PMC summary for the roofline traffic field (default profiles/pmc_<mode>.json; '
                          'used only when it was captured at this mode and channel count)')
@@ -141,25 +157,58 @@ def cpu_model():
     return 'unknown'
 
 
-def cpu_baseline(mode, M, seconds, procs):
-    """The oracle (CPU port of the reference path) on host cores, one process
-    per channel as aero-decode is deployed (one VFO per process); bounded
-    sample: each process decodes `seconds` of its own synthetic stream.  The
-    1-core figure is samples per CPU-second of the same runs."""
+def cgroup_cpus():
+    """CPUs the cgroup quota grants this process (cpu.max), or None."""
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        return None if q == 'max' else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def _cpu_run(M, seconds, procs, seed0):
     import multiprocessing as mp
     ctx = mp.get_context('fork')
     with ctx.Pool(procs) as p:
-        res = p.map(_cpu_one, [(M, seconds, 0xBE00 + k) for k in range(procs)])
+        res = p.map(_cpu_one, [(M, seconds, seed0 + k) for k in range(procs)])
     total = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     cpu = sum(r[1] for r in res)
-    out = {'value': round(total / wall / 1e6, 4), 'unit': 'Msamples/s', 'cores': procs, 'kind': 'port',
+    return total / wall / 1e6, total / cpu / 1e6, cpu
+
+
+def cpu_baseline(mode, M, seconds, procs, runs=3):
+    """The oracle (CPU port of the reference path) on host cores, one process
+    per channel as aero-decode is deployed (one VFO per process); bounded
+    sample: each process decodes `seconds` of its own synthetic stream.
+    `value` is the median of `runs` runs at `procs` processes (the GPU box's
+    per-GPU CPU share); one more run at the visible CPU count (nproc) with
+    the same total work split across that many processes.  The 1-core figure
+    is samples per CPU-second of the same runs."""
+    rates, ones, cpus = [], [], []
+    for r in range(max(1, runs)):
+        v, one, cpu = _cpu_run(M, seconds, procs, 0xBE00 + 1000 * r)
+        rates.append(v)
+        ones.append(one)
+        cpus.append(cpu)
+    try:
+        nvis = len(os.sched_getaffinity(0))
+    except AttributeError:
+        nvis = os.cpu_count() or 1
+    med = sorted(rates)[len(rates) // 2]
+    out = {'value': round(med, 4), 'unit': 'Msamples/s', 'cores': procs, 'kind': 'port',
            'sample': '%d processes x %.0f s of synthetic %d-bps P-channel (%d Hz int16) through '
                      'oracle/liboracle.so (demod + coarse + hunter + AeroL + Viterbi + ACARS), '
-                     '%d-sample messages; %.1f s CPU total' % (procs, seconds, M['bitrate'], M['fs'], M['fs'] // 4,
-                                                            cpu),
-           'one_core_msps': round(total / cpu / 1e6, 4), 'cpu_model': cpu_model(),
-           'host_cpus_visible': os.cpu_count()}
+                     '%d-sample messages; median of %d runs (%.1f s CPU each)' % (
+                         procs, seconds, M['bitrate'], M['fs'], M['fs'] // 4, len(rates), sorted(cpus)[len(cpus) // 2]),
+           'runs_msps': [round(v, 4) for v in rates],
+           'one_core_msps': round(sorted(ones)[len(ones) // 2], 4), 'cpu_model': cpu_model(),
+           'host_cpus_visible': os.cpu_count(), 'affinity_cpus': nvis, 'cgroup_cpus': cgroup_cpus()}
+    if nvis != procs:
+        # the same total CPU work spread over nproc processes
+        v, one, cpu = _cpu_run(M, max(1.0, seconds * procs / nvis), min(nvis, 512), 0xBF00)
+        out['nproc'] = {'value': round(v, 4), 'processes': min(nvis, 512),
+                        'seconds_per_process': round(max(1.0, seconds * procs / nvis), 2)}
     if mode in CALIBRATION:
         out['calibration'] = dict(CALIBRATION[mode], host='survey container Intel Xeon, 8 vCPU, 1 thread')
     return out
@@ -195,9 +244,10 @@ def spawn_ranks(n):
     return rc
 
 
-def pmc_traffic(path, mode, channels):
-    """HBM bytes per dominant-kernel launch from a rocprofv3 PMC capture of
-    this same bench configuration (scripts/pmc_bench.sh); None otherwise."""
+def pmc_traffic(path, mode, channels, kernel):
+    """HBM bytes per launch of `kernel` (name prefix) from a rocprofv3 PMC
+    capture of this same bench configuration (tools/pmc_json.py over
+    scripts/profile_round.sh's FETCH_SIZE / WRITE_SIZE passes); None otherwise."""
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
@@ -205,7 +255,10 @@ def pmc_traffic(path, mode, channels):
     cfg = d.get('config', {})
     if cfg.get('mode') != mode or int(cfg.get('channels', -1)) != channels:
         return None, None
-    return d.get('hbm_bytes_per_launch'), os.path.relpath(path, ROOT)
+    for k, v in d.get('kernels', {}).items():
+        if k.startswith(kernel):
+            return v.get('hbm_bytes_per_launch'), os.path.relpath(path, ROOT)
+    return None, None
 
 
 C5_SECONDS = 6.0  # synthetic wideband held in HBM, read after read in a loop
@@ -440,6 +493,130 @@ def run_c1(a):
     print(json.dumps(out), flush=True)
 
 
+C5BIN_SECONDS = 12.0  # wideband CF32 file the publisher reads without pacing
+
+
+def run_c5bin(a):
+    """C5 through the drop-in binaries on one GPU: bin/aero-publish (GPU
+    channeliser, CF32 file source, the generated 64-VFO INI) -> ZeroMQ ->
+    ONE bin/aero-decode subscribed to all 64 topics (one engine channel per
+    topic, one aero_run per batch of queued messages).  Timed from the
+    publisher's first read to the last ACARS line; the item count is checked
+    against the oracle publisher + 64 oracle decoders on the same wideband,
+    which is also the CPU baseline (the reference's deployment: one
+    aero-publish, one aero-decode process per VFO)."""
+    import signal
+    import socket
+    import subprocess
+    import tempfile
+    import threading
+    import aero_testlib as tl
+    import aero_engine as ae
+    cfg = tl.c5_config()
+    x = tl.c5_wideband(cfg, C5BIN_SECONDS)
+    nv = len(cfg['vfos'])
+    # reference chain on the host: expected items, channel samples, CPU time
+    ref = tl.OraclePublisher(cfg['sample_rate'], cfg['center_frequency'], cfg['mains'], cfg['vfos'])
+    nb = len(x) // ref.block_len
+    t = time.perf_counter()
+    ref.process(x[:nb * ref.block_len])
+    t_pub = time.perf_counter() - t
+    import multiprocessing as mp
+    jobs = [(cfg, v, ref.usb(v), ref.info(v)['samples_per_block']) for v in range(nv)]
+    procs = a.cpu_procs or host_cores()
+    t = time.perf_counter()
+    with mp.get_context('fork').Pool(procs) as p:
+        res = p.map(_c5_items_one, jobs)
+    t_dec = time.perf_counter() - t
+    want = sum(r[1] for r in res)
+    ch_samples = sum(r[0] for r in res)
+    bindir = os.path.join(ROOT, 'aero-cli_amd', 'bin')
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    tmp = tempfile.mkdtemp(prefix='aero_c5bin_')
+    wb = os.path.join(tmp, 'wideband.cf32')
+    x[:nb * ref.block_len].astype(np.complex64).tofile(wb)
+    ini = os.path.join(tmp, 'c5.ini')
+    open(ini, 'w').write(tl.c5_ini(cfg).replace('tcp://*:6004', 'tcp://127.0.0.1:%d' % port))
+    args = [os.path.join(bindir, 'aero-decode'), '-p', 'tcp://127.0.0.1:%d' % port, '--format', 'jsondump', '-v']
+    for v in range(nv):
+        args += ['-t', 'VFO%02d' % (v + 1), '-b', str(cfg['vfos'][v]['data_rate']), '-s', 'BENCH']
+    dec = subprocess.Popen(args, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    lines, stamps = [], []
+
+    def pump(pipe, out, st):
+        for raw in pipe:
+            out.append(raw.decode('utf-8', 'replace'))
+            st.append(time.perf_counter())
+    th = threading.Thread(target=pump, args=(dec.stderr, lines, stamps), daemon=True)
+    th.start()
+    t_wait = time.perf_counter()
+    while not any('Listening for samples' in l for l in lines):
+        if dec.poll() is not None or time.perf_counter() - t_wait > 180:
+            sys.exit('bench c5bin: aero-decode did not start:\n' + ''.join(lines[-20:]))
+        time.sleep(0.05)
+    pub = subprocess.Popen([os.path.join(bindir, 'aero-publish'), '-v', '-d',
+                            'driver=file,path=%s,start_delay_ms=1500' % wb, ini], stdout=subprocess.DEVNULL,
+                           stderr=subprocess.PIPE)
+    plines, pstamps = [], []
+    tp = threading.Thread(target=pump, args=(pub.stderr, plines, pstamps), daemon=True)
+    tp.start()
+    pub.wait(timeout=300)
+    tp.join(timeout=10)
+    t0 = next((s for l, s in zip(plines, pstamps) if 'Starting concurrent reader' in l), None)
+    if pub.returncode != 0 or t0 is None:
+        dec.kill()
+        sys.exit('bench c5bin: aero-publish failed:\n' + ''.join(plines[-20:]))
+    # wait for the decoder to go quiet (every queued message decoded)
+    n_last, t_last = -1, time.perf_counter()
+    while time.perf_counter() - t_last < 3.0 and time.perf_counter() - t0 < 600:
+        n = sum(l.startswith('{') for l in lines)
+        if n != n_last:
+            n_last, t_last = n, time.perf_counter()
+        time.sleep(0.1)
+    got = [s for l, s in zip(lines, stamps) if l.startswith('{')]
+    t_end = got[-1] if got else time.perf_counter()
+    n_run = len(got)
+    dec.send_signal(signal.SIGTERM)
+    dec.wait(timeout=120)
+    th.join(timeout=10)
+    n_all = sum(l.startswith('{') for l in lines)  # with the flushed tail
+    os.remove(wb)
+    os.remove(ini)
+    os.rmdir(tmp)
+    if n_all != want:
+        sys.exit('bench c5bin: %d ACARS items, the oracle chain gives %d' % (n_all, want))
+    elapsed = t_end - t0
+    out = {'metric': 'Msamples/s end-to-end aero-publish -> ZeroMQ -> one 64-topic aero-decode -> ACARS JSON (C5)',
+           'value': round(ch_samples / elapsed / 1e6, 4), 'unit': 'Msamples/s', 'n_gpus': 1, 'steps': 1,
+           'warmup': 0, 'ms_per_step': round(elapsed * 1e3, 1), 'higher_is_better': True, 'scaling': 'none',
+           'vs_baseline': None, 'dtype': 'f32 channeliser / f64 demod', 'data': 'synthetic',
+           'config': {'workload': 'C5 through the binaries: %.0f s of 1.536 Msps CF32 (3 main VFOs, 64 [vfos]) read '
+                                  'without pacing by bin/aero-publish; one bin/aero-decode with 64 -t topics'
+                                  % C5BIN_SECONDS, 'vfos': nv, 'items': n_all, 'items_before_sigterm': n_run},
+           'wideband_msps': round(nb * ref.block_len / elapsed / 1e6, 3),
+           'realtime_factor': round(C5BIN_SECONDS / elapsed, 2),
+           'timing_note': "publisher's first read to the last ACARS JSON line before SIGTERM; audio after the "
+                          'last frame counts as processed',
+           'roofline': None,
+           'cpu_baseline': {'value': round(ch_samples / (t_pub + t_dec) / 1e6, 4), 'unit': 'Msamples/s',
+                            'cores': procs, 'kind': 'port',
+                            'sample': 'the same %.0f s: oracle publisher on 1 core (%.2f s) then 64 oracle decoders '
+                                      'on %d processes (%.2f s)' % (C5BIN_SECONDS, t_pub, procs, t_dec),
+                            'cpu_model': cpu_model()}}
+    print(json.dumps(out), flush=True)
+
+
+def _c5_items_one(arg):
+    cfg, v, audio, spb = arg
+    import aero_testlib as tl
+    import aero_engine as ae
+    o = tl.Oracle(bitrate=ae.vfo_bitrate(cfg['vfos'][v]['data_rate']))
+    o.push_chunked(audio, spb)
+    return len(audio), len(o.item_lines('A'))
+
+
 def main():
     a = parse()
     if a.gpus > 1 and 'RANK' not in os.environ:
@@ -453,20 +630,26 @@ def main():
         if rank == 0:
             run_c1(a)
         return None
+    if a.mode == 'c5bin':
+        if rank == 0:
+            run_c5bin(a)
+        return None
     import shard
     M = MODES[a.mode]
     HOP, FS = M['hop'], M['fs']
     C, P = a.channels, a.pool
     preroll = M.get('preroll', PREROLL_HOPS)  # burst channels have no hunter to lock
     pre = preroll + a.warmup  # untimed hops: lock-in pre-roll + warmup
-    steps_total = pre + a.steps
+    burst = bool(M.get('burst'))
+    h2d_steps = 0 if burst else max(0, a.h2d_steps)
+    steps_total = pre + a.steps + h2d_steps
     span = steps_total * HOP
     offsets = shard.channel_offsets(C, P, rank)
     pool_host = make_pool(M, P, span + int(offsets.max()) + 1, 0xAE20 + 1000 * rank)
     # CPU baseline first, in worker processes forked before this process touches the GPU
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(a.mode, M, a.cpu_seconds or M['cpu_seconds'], a.cpu_procs or host_cores())
+        cpu = cpu_baseline(a.mode, M, a.cpu_seconds or M['cpu_seconds'], a.cpu_procs or host_cores(), a.cpu_runs)
 
     import torch
     import torch.distributed as dist
@@ -481,7 +664,6 @@ def main():
         views = [pool[:, int(o) + s * HOP:int(o) + (s + 1) * HOP] for o in offsets]
         return torch.stack(views).permute(2, 0, 1).reshape(HOP, C).contiguous()
 
-    burst = bool(M.get('burst'))
     eng = ae.Engine(max_channels=C, device=local, flags=ae.F_TIMING)
     for _ in range(C):
         eng.open_channel(M['bitrate'], FS, burst=burst)
@@ -520,6 +702,48 @@ def main():
     tail_ms = (t_end - t_tail) * 1e3  # final drain: the last passes' decode, copy-back and host items
     samples = eng.samples_processed() - s0
     stats = {k: eng.stat(k) - v for k, v in st0.items()}
+    tag = M['timing'][:-len('demod')]
+    if burst:  # the burst path's kernels: Hilbert fast FIR, demod, trident FFT check, framing, R/T Viterbi
+        kt = {k: eng.timing('burst_' + k) for k in ('hilbert', 'demod', 'trident', 'frame', 'viterbi')}
+    else:
+        kt = {k: eng.timing(tag + k) for k in ('demod', 'coarse', 'frame', 'viterbi')}
+    ht = {k: eng.timing(k) for k in ('host_push', 'host_run', 'host_wait_njobs', 'host_wait_jobs', 'host_frames')}
+    del timed_inputs
+    h2d = None
+    if h2d_steps:
+        # the same step loop with every int16 block pushed from pinned host
+        # memory inside the timed region (H2D-inclusive), the
+        # blocks DMA'd straight into the PCM ring while the previous step runs
+        host_inputs = [step_input(pre + a.steps + s).cpu().pin_memory() for s in range(h2d_steps)]
+        eng.sync()
+        eng.drain_items()
+        torch.cuda.synchronize()
+        s1 = eng.samples_processed()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for xh in host_inputs:
+            eng.push_batch_host(xh.data_ptr(), HOP, C, C)
+            eng.run()
+            eng.drain_items()
+        eng.sync()
+        eng.drain_items()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        h_el = time.perf_counter() - t1
+        h_smp = eng.samples_processed() - s1
+        th = torch.tensor([h_el, float(h_smp)], dtype=torch.float64, device='cuda')
+        if world > 1:
+            dist.all_reduce(th[:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(th[1:], op=dist.ReduceOp.SUM)
+        h_el, h_smp = float(th[0]), float(th[1])
+        h2d = {'value': round(h_smp / h_el / 1e6, 3), 'unit': 'Msamples/s', 'steps': h2d_steps,
+               'ms_per_step': round(h_el / h2d_steps * 1e3, 3),
+               'pcie_bytes_per_step': 2 * HOP * C * world,
+               'note': 'same steps, int16 [hop, channels] blocks pushed from pinned host memory '
+                       '(aero_push_pcm_batch, dev=0) inside the timed region'}
+        del host_inputs
     stats['acars_items'] = items
     keys = sorted(stats)
     t = torch.tensor([elapsed, float(samples)] + [float(stats[k]) for k in keys], dtype=torch.float64,
@@ -530,20 +754,33 @@ def main():
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed, samples = float(tmax[0]), float(t[1])
         stats = {k: int(t[2 + i]) for i, k in enumerate(keys)}
-    tag = M['timing'][:-len('demod')]
-    if burst:  # the burst path's kernels: Hilbert fast FIR, demod, trident FFT check, framing, R/T Viterbi
-        kt = {k: eng.timing('burst_' + k) for k in ('hilbert', 'demod', 'trident', 'frame', 'viterbi')}
-    else:
-        kt = {k: eng.timing(tag + k) for k in ('demod', 'coarse', 'frame', 'viterbi')}
-    ht = {k: eng.timing(k) for k in ('host_push', 'host_run', 'host_wait_njobs', 'host_wait_jobs', 'host_frames')}
     if rank == 0:
         value = samples / elapsed / 1e6
-        dm_ms, dm_n = kt['demod']
-        per_launch_s = dm_ms / 1e3 / max(dm_n, 1)
-        samples_per_launch = C * HOP
-        achieved = M['bytes'] * samples_per_launch / per_launch_s / 1e9
+        # roofline of the dominant kernel (the most device time per step):
+        # the path's algorithmic bytes per step (bytes per
+        # input sample x samples of a step) over that kernel's summed time
+        # per step; the whole step's fraction beside it
+        steps = max(a.steps, 1)
+        dom = max(kt, key=lambda k: kt[k][0])
+        dom_ms = kt[dom][0] / steps
+        step_bytes = M['bytes'] * C * HOP
+        achieved = step_bytes / (dom_ms / 1e3) / 1e9
+        step_achieved = step_bytes / (elapsed / steps) / 1e9
         traffic, traffic_src = pmc_traffic(a.pmc or os.path.join(ROOT, 'profiles', 'pmc_%s.json' % a.mode),
-                                           a.mode, C)
+                                           a.mode, C, M['kernels'][dom])
+        total_ms = sum(v[0] for v in kt.values()) / steps
+        kernels = {}
+        for k, (ms, n) in kt.items():
+            kernels[M['kernels'][k]] = {'ms_per_step': round(ms / steps, 3), 'launches_per_step': round(n / steps, 2),
+                                        'share_of_device_time': round(ms / steps / total_ms, 3) if total_ms else None}
+        if 'nfft_log2' in M and kt['coarse'][1]:
+            # the coarse estimator's three radix-2 transforms, 5 N log2 N real flops each, per channel-hop
+            nf = 1 << M['nfft_log2']
+            fl = 3 * 5 * nf * M['nfft_log2']
+            kc = kernels[M['kernels']['coarse']]
+            tf = fl * C / (kc['ms_per_step'] / 1e3) / 1e12
+            kc['fp64'] = {'flop_per_channel_hop': fl, 'achieved_tflops': round(tf, 2), 'peak_tflops': FP64_PEAK_TFLOPS,
+                          'frac': round(tf / FP64_PEAK_TFLOPS, 4)}
         out = {
             'metric': M['metric'],
             'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world, 'steps': a.steps,
@@ -560,20 +797,25 @@ def main():
                                        FS, HOP)),
                        'channels_per_gpu': C, 'total_channels': C * world, 'hop_samples': HOP,
                        'parallelism': 'channel-sharded x%d' % world},
-            'roofline': {'bound': 'hbm', 'kernel': M['kernel'], 'achieved': round(achieved, 2),
+            'roofline': {'bound': 'hbm', 'kernel': M['kernels'][dom], 'achieved': round(achieved, 2),
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
                          'traffic': traffic, 'traffic_source': traffic_src, 'bytes_per_sample': M['bytes'],
-                         'avg_launch_ms': round(per_launch_s * 1e3, 3)},
+                         'bytes_per_step': int(step_bytes), 'kernel_ms_per_step': round(dom_ms, 3),
+                         'launches_per_step': round(kt[dom][1] / steps, 2),
+                         'step': {'achieved': round(step_achieved, 2), 'frac': round(step_achieved / HBM_PEAK_GBS, 5),
+                                  'ms_per_step': round(elapsed / steps * 1e3, 3)}},
+            'kernels': kernels,
             # SURVEY §8(d) / BASELINE.md: the path is FP64-VALU bound, so the whole-path FP64
             # rate (algorithmic flop per input sample x samples/s) is reported beside the HBM one
             'fp64_roofline': {'flop_per_sample': M['flops'], 'achieved': round(value * 1e6 * M['flops'] / 1e12, 3),
                               'peak': FP64_PEAK_TFLOPS * world, 'unit': 'TFLOP/s',
                               'frac': round(value * 1e6 * M['flops'] / 1e12 / (FP64_PEAK_TFLOPS * world), 5)},
-            'kernel_ms_per_step': {k: round(v[0] / max(a.steps, 1), 3) for k, v in kt.items()},
             'timed_region': stats,
             'host_ms_per_step': {k: round(v[0] / max(a.steps, 1), 3) for k, v in ht.items()},
             'drain_ms': round(tail_ms, 3),
         }
+        if h2d is not None:
+            out['h2d'] = h2d
         if cpu is not None:
             out['cpu_baseline'] = cpu
             out['vs_cpu'] = round(value / cpu['value'], 1)

@@ -165,6 +165,22 @@ int aero_stat(aero_engine *e, const char *name, uint64_t *value);
  * for the channel's queued GPU work. */
 int aero_channel_stat(aero_engine *e, int ch, const char *name, int64_t *value);
 
+/* Decoder status events of one channel since it opened, for aero-decode's
+ * verbose log (Decoder::handleDcdChange / handleNewFreqCenter,
+ * decode/decode.cpp:429-439).  dcd_edges: changes of AeroL's data carrier
+ * detect as SignalHunter::handleDcd passes them on (decode/hunter.cpp:14-19);
+ * they alternate and the first is "no signal => signal".  hunter_steps:
+ * SignalHunter::newFreqCenter emissions (decode/hunter.cpp:31-40), with the
+ * centre of step k (1-based) in hunter_fc[(k - 1) & 7] for the last eight
+ * steps (0 for burst channels: their hunter is disabled, decode/decode.cpp:175).
+ * Waits for the channel's queued GPU work. */
+typedef struct {
+  int64_t dcd_edges;
+  int64_t hunter_steps;
+  double hunter_fc[8];
+} aero_channel_events;
+int aero_channel_get_events(aero_engine *e, int ch, aero_channel_events *out);
+
 /* Total input samples demodulated across channels since creation. */
 uint64_t aero_samples_processed(aero_engine *e);
 

@@ -488,6 +488,7 @@ struct Hunter {
   bool enabled = true;
   uint32_t maxTries = 15, fullScans = 0, minFreq = 0, maxFreq = 25000,
            bandwidth = 10500, iterationsSinceSignal = 0;
+  std::vector<double> steps;  // every newFreqCenter emission
   void setParams(uint32_t mn, uint32_t mx, uint32_t bw) {  // hunter.cpp:14-19
     minFreq = mn;
     maxFreq = mx;
@@ -509,6 +510,7 @@ struct Hunter {
           fullScans++;
         }
         fc = new_freq_center;
+        steps.push_back(fc);  // Decoder::handleNewFreqCenter's value (decode/decode.cpp:437-439)
         return true;
       }
     }
@@ -1322,6 +1324,13 @@ struct AeroL {
   uint16_t frameinfo = 0, lastframeinfo = 0;
   bool datacd = false;
   int datacdcountdown = 0;
+  // DataCarrierDetect changes as SignalHunter::handleDcd passes them on to
+  // Decoder::handleDcdChange (decode/hunter.cpp:14-19, decode/decode.cpp:429-435)
+  long long dcd_edges = 0;
+  void set_dcd(bool v) {
+    if (v != datacd) dcd_edges++;
+    datacd = v;
+  }
   std::vector<int> block;
   std::vector<int> perm;  // interleaverowdepermute
   // JConvolutionalCodec state
@@ -1445,7 +1454,7 @@ struct AeroL {
       } else {
         if (datacdcountdown > 0) datacdcountdown -= 3;
       }
-      if (!datacd && datacdcountdown > 2) datacd = true;
+      if (!datacd && datacdcountdown > 2) set_dcd(true);
       decline += (char)(k + '0');
       for (int j = 0; j < 10; j++) {
         char b[8];
@@ -1695,7 +1704,7 @@ struct AeroL {
       if (gotsync) {
         if (!burstmode && cntr + 1 != TotalNumberOfBits) isudata.reset();
         cntr = -1;
-        datacd = true;
+        set_dcd(true);
         datacdcountdown = 12;
         scr_pos = 0;
       }
@@ -1704,7 +1713,7 @@ struct AeroL {
         cntr = -1;
         if (burstmode) {  // end of the burst window: stop this call (aerol.cpp:2018-2029)
           cntr = 1000000000;
-          datacd = false;
+          set_dcd(false);
           datacdcountdown = 0;
           return;
         }
@@ -2994,6 +3003,11 @@ size_t oracle_rt_tests(const oracle_chan *c, uint8_t *dst, size_t cap) { return 
 size_t oracle_rt_packets(const oracle_chan *c, uint8_t *dst, size_t cap) { return copy_out(c->rt_packets, dst, cap); }
 size_t oracle_softbits(const oracle_chan *c, uint8_t *dst, size_t cap) {
   return copy_out(c->soft(), dst, cap);
+}
+size_t oracle_events(oracle_chan *c, long long *dcd_edges, double *fc, size_t cap) {
+  *dcd_edges = c->aerol().dcd_edges;
+  static const std::vector<double> none;
+  return copy_out(c->oq ? c->oq->hunter.steps : (c->msk ? c->msk->hunter.steps : none), fc, cap);
 }
 size_t oracle_hops(const oracle_chan *c, double *dst, size_t cap_records) {
   return copy_out(c->hops(), dst, cap_records * 6) / 6;

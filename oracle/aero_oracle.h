@@ -48,6 +48,11 @@ size_t oracle_rt_packets(const oracle_chan *c, uint8_t *dst, size_t cap);
  * mixer2 freq, mixer_center freq (after the slot ran), mse, signal flag. */
 size_t oracle_hops(const oracle_chan *c, double *dst, size_t cap_records);
 
+/* Decoder status events (decode/decode.cpp:429-439): *dcd_edges = the data
+ * carrier detect changes SignalHunter::handleDcd passes on; returns the
+ * number of newFreqCenter emissions and copies their centres (at most cap). */
+size_t oracle_events(oracle_chan *c, long long *dcd_edges, double *fc, size_t cap);
+
 /* rotated pt_qpsk trace (2 doubles per carrier event), only with ORACLE_TRACE_PT */
 size_t oracle_pt(const oracle_chan *c, double *dst, size_t cap_records);
 

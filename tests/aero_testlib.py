@@ -170,6 +170,9 @@ class Oracle:
             for f in ('oracle_softbits16', 'oracle_rt_tests', 'oracle_rt_packets'):
                 getattr(L, f).restype = ctypes.c_size_t
                 getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+            L.oracle_events.restype = ctypes.c_size_t
+            L.oracle_events.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_void_p,
+                                        ctypes.c_size_t]
             cls._lib = L
         return cls._lib
 
@@ -225,6 +228,14 @@ class Oracle:
 
     def frames(self):
         return self._get(self.L.oracle_frames, np.uint8)
+
+    def events(self):
+        """(dcd_edges, [centre of every SignalHunter step]) (decode/decode.cpp:429-439)"""
+        e = ctypes.c_longlong()
+        n = self.L.oracle_events(self.h, ctypes.byref(e), None, 0)
+        fc = np.zeros(n, dtype=np.float64)
+        self.L.oracle_events(self.h, ctypes.byref(e), fc.ctypes.data, n)
+        return int(e.value), [float(v) for v in fc]
 
     def item_lines(self, kind='A'):
         n = self.L.oracle_items(self.h, None, 0)

@@ -52,7 +52,7 @@ def parse_line(line):
     return it
 
 
-def expected(lines, fmt_id):
+def expected(lines, fmt_id, station=STATION):
     L = ctypes.CDLL(os.path.join(BIN, 'libaero_host.so'))
     L.aero_host_format.restype = ctypes.c_long
     L.aero_host_format.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong,
@@ -61,7 +61,7 @@ def expected(lines, fmt_id):
     for ln in lines:
         it = parse_line(ln)
         buf = ctypes.create_string_buffer(65536)
-        n = L.aero_host_format(fmt_id, STATION.encode(), 0, ctypes.byref(it), FIXED_MS, buf, len(buf))
+        n = L.aero_host_format(fmt_id, station.encode(), 0, ctypes.byref(it), FIXED_MS, buf, len(buf))
         out.append(buf.raw[:n].decode())
     return out
 
@@ -166,6 +166,8 @@ def test_zmq_to_acars_json_end_to_end(engine_lib, cpu_libs, tmp_path):
     assert rc == 0, '\n'.join(lines[-20:])
     console = [l for l in lines if l.startswith('{')]
     assert console == expected(want, 3)
+    # -v: Decoder::handleDcdChange once the first frame synchronises (decode/decode.cpp:429-435)
+    assert sum('Data carrier detected: no signal => signal' in l for l in lines) == 1
     assert tcp.data.decode('latin-1').splitlines() == [s for s in expected(want, 1)]
     assert [m.decode('latin-1').rstrip('\n') for m in udp.msgs] == expected(want, 2)
 
@@ -192,6 +194,9 @@ def test_no_signal_exit(engine_lib, tmp_path):
             dec.kill()
     th.join(timeout=10)
     text = '\n'.join(lines)
+    # -v: Decoder::handleNewFreqCenter, SignalHunter's unclamped centres (decode/hunter.cpp:31-40)
+    steps = re.findall(r'Trying frequency center ([0-9.]+) in search of signal', text)
+    assert steps[:4] == ['5250.0', '10500.0', '15750.0', '0.0'], steps
     assert 'Scanned entire VFO bandwidth and could not find a signal.' in text
     assert 'Exiting because of no signal' in text
     assert rc == 0
@@ -246,3 +251,61 @@ def test_publish_to_decode_pipeline(engine_lib, cpu_libs, tmp_path):
         assert rc == 0, '\n'.join(lines[-10:])
         console = [l for l in lines if l.startswith('{')]
         assert console == expected(want, 3)
+
+
+def test_multi_topic_decoder(engine_lib, cpu_libs, tmp_path):
+    """One aero-decode process for all 64 VFO topics of the C5 receiver
+    (repeated -t, per-topic -b and -s): aero-publish (GPU channeliser) ->
+    ZeroMQ -> one SUB socket with 64 subscriptions -> one engine channel per
+    topic, one aero_run per batch of queued messages.  Each topic's jsondump
+    lines (told apart by their station id) equal what a separate reference
+    aero-decode would print: the oracle publisher's audio through the oracle
+    decoder (publish/vfo.cpp -> decode/decode.cpp, config C5)."""
+    import build
+    import aero_engine as ae
+    build.build_host()
+    cfg = tl.c5_config()
+    x = tl.c5_wideband(cfg, 8.0)
+    ref = tl.OraclePublisher(cfg['sample_rate'], cfg['center_frequency'], cfg['mains'], cfg['vfos'])
+    nb = len(x) // ref.block_len
+    ref.process(x[:nb * ref.block_len])
+    wb = tmp_path / 'wideband.cf32'
+    x[:nb * ref.block_len].astype(np.complex64).tofile(str(wb))
+    port = free_port()
+    ini = tmp_path / 'c5.ini'
+    ini.write_text(tl.c5_ini(cfg).replace('tcp://*:6004', 'tcp://127.0.0.1:%d' % port))
+    nv = len(cfg['vfos'])
+    wants = []
+    for v in range(nv):
+        o = tl.Oracle(bitrate=ae.vfo_bitrate(cfg['vfos'][v]['data_rate']))
+        o.push_chunked(ref.usb(v), ref.info(v)['samples_per_block'])
+        wants.append(o.item_lines('A'))
+    assert sum(len(w) for w in wants) >= 40
+    args = ['-p', 'tcp://127.0.0.1:%d' % port, '--format', 'jsondump', '-v']
+    for v in range(nv):
+        args += ['-t', 'VFO%02d' % (v + 1), '-b', str(cfg['vfos'][v]['data_rate']), '-s', 'ST%02d' % (v + 1)]
+    dec, lines, th = _start_decoder(args, {})
+    try:
+        r = subprocess.run([os.path.join(BIN, 'aero-publish'), '-d',
+                            'driver=file,path=%s,start_delay_ms=1500' % wb, str(ini)],
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-3000:]
+        t0 = time.time()
+        want_n = sum(len(w) for w in wants)
+        while sum(l.startswith('{') for l in lines) < want_n - 4 * nv and time.time() - t0 < 90:
+            time.sleep(0.2)
+        time.sleep(2.0)
+    finally:
+        dec.send_signal(signal.SIGTERM)
+        rc = dec.wait(timeout=120)
+    th.join(timeout=10)
+    assert rc == 0, '\n'.join(lines[-10:])
+    console = [l for l in lines if l.startswith('{')]
+    for v in range(nv):
+        st = '"ST%02d"' % (v + 1)
+        got = [l for l in console if st in l]
+        assert got == expected(wants[v], 3, 'ST%02d' % (v + 1)), 'VFO%02d' % (v + 1)
+    # every topic's data carrier came up once, each line naming its topic
+    for v in range(nv):
+        if wants[v]:
+            assert sum(('Data carrier detected' in l and '[VFO%02d]' % (v + 1) in l) for l in lines) == 1

@@ -37,5 +37,8 @@ def test_pmc_json(tmp_path):
     assert d['algorithmic_bytes_per_launch'] == int(18.22 * 65536 * 4096)
     sys.path.insert(0, ROOT)
     import bench
-    assert bench.pmc_traffic(str(out), 'oqpsk10500', 65536)[0] == d['hbm_bytes_per_launch']
-    assert bench.pmc_traffic(str(out), 'oqpsk10500', 1024) == (None, None)   # another configuration
+    assert bench.pmc_traffic(str(out), 'oqpsk10500', 65536, 'demod_oqpsk_kernel')[0] == d['hbm_bytes_per_launch']
+    kc = d['kernels']['coarse_kernel<0>']
+    assert bench.pmc_traffic(str(out), 'oqpsk10500', 65536, 'coarse_kernel')[0] == kc['hbm_bytes_per_launch']
+    assert bench.pmc_traffic(str(out), 'oqpsk10500', 1024, 'coarse_kernel') == (None, None)   # another configuration
+    assert bench.pmc_traffic(str(out), 'oqpsk10500', 65536, 'viterbi_kernel') == (None, None)  # not captured
