@@ -85,6 +85,15 @@ def build_synth():
 
 
 MATHHOST_SO = os.path.join(ROOT, 'tools', 'libaero_mathhost.so')
+FFTSIM_SO = os.path.join(ROOT, 'tools', 'libfft_chain_sim.so')
+
+
+def build_fftsim():
+    """Test-only host model of the coarse kernel's FFT layouts (tests/test_fft_chain_sim.py)."""
+    src = os.path.join(ROOT, 'tools', 'fft_chain_sim.cpp')
+    if _stale(FFTSIM_SO, [src, os.path.join(CSRC, 'fft_layout.h')]):
+        _run(['g++', '-O2', '-std=c++17', '-fPIC', '-shared', '-ffp-contract=off', '-o', FFTSIM_SO, src])
+    return FFTSIM_SO
 
 
 def build_mathhost():
@@ -157,6 +166,7 @@ def build_all(jobs=4):
     build_oracle()
     build_synth()
     build_mathhost()
+    build_fftsim()
     so = build_engine(jobs)
     build_host(jobs)
     return so

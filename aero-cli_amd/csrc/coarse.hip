@@ -6,12 +6,13 @@
  * CenterFreqChangedSlot (decode/oqpskdemodulator.cpp:256-280), for every
  * channel whose 4096-sample hop is due.
  *
- * One 1024-thread workgroup per channel.  The 16384-point FP64 FFT keeps 16
- * complex values per thread in registers and runs JFFT's radix-2 DIT
- * butterflies (decode/jfft.cpp:114-212) in four register phases (stages 0-3,
- * 4-7, 8-11, 12-13) with LDS transposes between them; every butterfly uses
- * the same operands and twiddle as the reference, so the output is
- * bit-identical regardless of how butterflies are scheduled.
+ * One 1024-thread workgroup per channel.  The 16384-point FP64 FFTs keep 16
+ * complex values per thread in registers and run JFFT's radix-2 DIT
+ * butterflies (decode/jfft.cpp:114-212) chained through register stages, a
+ * wave-local LDS transpose, lane permutes and one workgroup exchange per
+ * transform (fft_chain.h); every butterfly uses the same operands and
+ * twiddle as the reference, so the output is bit-identical regardless of how
+ * butterflies are scheduled.
  */
 #include <hip/hip_runtime.h>
 
@@ -19,7 +20,7 @@
 
 #include "aero_math.h"
 #include "engine_common.h"
-#include "fft_dit.h"
+#include "fft_chain.h"
 
 namespace aero {
 
@@ -239,14 +240,16 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
       x[i] = make_double2(cs.x * dval, cs.y * dval);
     }
   }
+  __syncthreads();  // the ring image is read: the LDS is the transforms' from here on
   CSTAMP(0);
   // forward FFT
-  fft_dit<L, false, true>(x, t, lds, T.tw, s_tw);
+  chain::fft<L, true, false>(x, t, lds, T.tw, s_tw);
   CSTAMP(1);
   // boxcar: zero bins startbin..stopbin (coarsefreqestimate.cpp:143-146)
+  const int bin_t = chain::out_bin_thread<L>(t);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int p = epos<L, 3>(t, i);
+    const int p = bin_t | chain::out_bin_reg<L>(i);
     if (p >= K::START && p <= K::STOP) x[i] = make_double2(0.0, 0.0);
   }
   // inverse FFT.  JFFT scales by 1/N and FFTWrapper multiplies by N
@@ -254,8 +257,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   // x with |x| >= 2^-1008, and a nonzero value of this path is far above that
   // (magnitudes >= ~2^-200: sums and products of pcm/32768, CIS and twiddle
   // values), so both multiplies are the identity here and are skipped.
-  exchange<L, 3, 0, true>(x, t, lds);
-  fft_dit<L, true, true>(x, t, lds, T.twi, s_tw);
+  chain::fft<L, false, true>(x, t, lds, T.twi, s_tw);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     // square
@@ -265,9 +267,8 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     const double im = 2.0 * (x[i].x * x[i].y);
     x[i] = make_double2(r, im);
   }
-  exchange<L, 3, 0, true>(x, t, lds);
   CSTAMP(2);
-  fft_dit<L, false, true>(x, t, lds, T.tw, s_tw);
+  chain::fft<L, false, false>(x, t, lds, T.tw, s_tw);
   CSTAMP(3);
   // fftshift + smoothing y = 0.9 y + 10 log10(max(|X|,1)) over the bins the fold reads:
   // |X| per bin to LDS first (keeps the log10 out of the register-heavy FFT scope)
@@ -278,11 +279,11 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   auto yload = [&](int k) { return (k < YLEN && !yreset) ? yg[k] : 20.0; };
   double yp0 = yload(t), yp1 = yload(t + FT);
   __syncthreads();
-  double *ylds = lds;  // [YLEN]
+  double *ylds = lds;  // [ypad(YLEN)]: bin k - YLO at ypad(k - YLO)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int yi = epos<L, 3>(t, i) ^ (N / 2);
-    if (yi >= K::YLO && yi <= K::YHI) ylds[yi - K::YLO] = CO_HYPOT(x[i].x, x[i].y);
+    const int yi = (bin_t | chain::out_bin_reg<L>(i)) ^ (N / 2);
+    if (yi >= K::YLO && yi <= K::YHI) ylds[fftl::ypad(yi - K::YLO)] = CO_HYPOT(x[i].x, x[i].y);
   }
   double yp2 = yload(t + 2 * FT);
   __syncthreads();
@@ -293,9 +294,9 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     yp0 = yp1;
     yp1 = yp2;
     yp2 = yload(k + 3 * FT);
-    const double ynew = yold * 0.9 + 0.1 * 10 * CO_LOG10(fmax(ylds[k], 1.0));
+    const double ynew = yold * 0.9 + 0.1 * 10 * CO_LOG10(fmax(ylds[fftl::ypad(k)], 1.0));
     yg[k] = ynew;
-    ylds[k] = ynew;
+    ylds[fftl::ypad(k)] = ynew;
   }
   __syncthreads();
   CSTAMP(5);
@@ -306,7 +307,8 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     const int i = K::ILO + t + FT * r;
     if (i >= K::IHI) break;
     double val = 0;
-    for (int j = -1; j <= 1; j++) val += (ylds[i - K::EPB - j - K::YLO] + ylds[i + K::EPB + j - K::YLO]);
+    for (int j = -1; j <= 1; j++)
+      val += (ylds[fftl::ypad(i - K::EPB - j - K::YLO)] + ylds[fftl::ypad(i + K::EPB + j - K::YLO)]);
     if (val > bv) {
       bv = val;
       bi = i;

@@ -31,6 +31,7 @@ def build_cpu_only():
     import build
     build.build_oracle()
     build.build_synth()
+    build.build_fftsim()
 
 
 _synth = None
