@@ -134,24 +134,68 @@ __global__ __launch_bounds__(512) void hilbert_kernel(BurstState S, BurstTables 
 // 40 x 2 x 8 B x 64 = 40 KB per wave, so four waves (one per SIMD) share a
 // CU and 65536 channels run in one round instead of two.
 constexpr int BD_BLOCK = 64;
-constexpr int BD_LDS_TAPS = 40, BD_REG_TAPS = NTAPS - BD_LDS_TAPS;
+#ifndef AERO_BD_LDS_TAPS
+#define AERO_BD_LDS_TAPS 40
+#endif
+constexpr int BD_LDS_TAPS = AERO_BD_LDS_TAPS, BD_REG_TAPS = NTAPS - BD_LDS_TAPS;
+
+// AERO_X_BSTAMPS (diagnostic build only): s_memtime cycle totals per section
+// of the demod loop, each wave's maximum over its lanes (the wave's time in
+// the section while the lane was in the loop), summed over waves: [0] loop
+// control, [1] part A (AGC, burst statistic), [2] peak detector incl.
+// findmaxpos, [3] trident store / resume, [4] part B loads + RRC, [5] PLL,
+// rotators, AGC2, clip, [6] symbol timing + step + NCOs, [7] entry + exit
+// (state); counters summed over lanes: [8] samples advanced, [9] findmaxpos
+// scans, [10] lanes that entered the loop, [11] waves, [12] loop iterations
+// (max over the wave's lanes)
+#ifdef AERO_X_BSTAMPS
+__device__ unsigned long long g_bstamps[16];
+#define BSTAMP(k)                                                  \
+  do {                                                             \
+    __builtin_amdgcn_sched_barrier(0);                             \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
+    bst_[k] += t_ - btime_;                                        \
+    btime_ = t_;                                                   \
+    __builtin_amdgcn_sched_barrier(0);                             \
+  } while (0)
+#define BCOUNT(k, v) (bcnt_[k] += (v))
+#else
+#define BSTAMP(k) \
+  do {            \
+  } while (0)
+#define BCOUNT(k, v) \
+  do {               \
+  } while (0)
+#endif
 
 __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, BurstTables T, int nch, int max_n,
                                                                int trace) {
-  __shared__ double s_qre[BD_LDS_TAPS][BD_BLOCK];
-  __shared__ double s_qim[BD_LDS_TAPS][BD_BLOCK];
+  __shared__ double s_qre[BD_LDS_TAPS > 0 ? BD_LDS_TAPS : 1][BD_BLOCK];
+  __shared__ double s_qim[BD_LDS_TAPS > 0 ? BD_LDS_TAPS : 1][BD_BLOCK];
   const int c = blockIdx.x * BD_BLOCK + threadIdx.x, col = threadIdx.x;
   if (c >= nch) return;
+#ifdef AERO_X_BSTAMPS
+  unsigned long long bst_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bcnt_[5] = {0, 0, 0, 0, 0};
+  unsigned long long btime_ = __builtin_amdgcn_s_memtime();
+  bool bactive_ = false;
+#endif
   const int C = S.C;
   double *ds = S.ds + c;
   int *is = S.is + c;
   long long *ls = S.ls + c;
   int pend = is[BI_PEND * C];
-  if (pend == 1) return;  // trident check outstanding
   const long long n0 = ls[BL_NSAMP * C];
   long long end = ls[BL_AVAIL * C];
   if (end - n0 > max_n) end = n0 + max_n;
+#ifdef AERO_X_BSTAMPS
+  // every lane reaches the wave reduction at the end
+  if (!(pend == 1 || (n0 >= end && pend != 2))) {
+    bactive_ = true;
+#else
+  if (pend == 1) return;  // trident check outstanding
   if (n0 >= end && pend != 2) return;
+  {
+#endif
 
   double m2_ptr = ds[BD_M2_PTR * C], m2_step = ds[BD_M2_STEP * C], m2_freq = ds[BD_M2_FREQ * C];
   double so_ptr = ds[BD_SO_PTR * C], so_last = ds[BD_SO_LAST * C], so_step = ds[BD_SO_STEP * C];
@@ -200,7 +244,10 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
 
   long long n = n0;
   bool resume = pend == 2;
+  BSTAMP(7);
   while (resume || n < end) {
+    BSTAMP(0);
+    BCOUNT(4, 1);
     double vtd;  // val_to_demod
     if (!resume) {
       if (sp - scons > B_SOFT_RING - 64) break;  // soft ring full: framing frees it next
@@ -261,6 +308,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       }
       double bt = fastarm * fastarm;
       if (bt > 500) bt = 500;
+      BSTAMP(1);
       {  // PeakDetector::update (DSP.h:491-566)
         double val = bt;
         double *r3 = S.pd3 + (size_t)pd3_p * C + c;
@@ -274,6 +322,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         val = pd2_old;  // d2.update(val)
         if ((!pd_cntdown) && (val > 0.2) && ((pd_lastdy >= 0 && dy < 0))) {
           pd_cntdown = B_PD_MAXCD;
+          BCOUNT(1, 1);
           // d3.findmaxpos: first maximum, scanning from the oldest slot
           int q = pd3_p, maxpos = 0;
           double maxval = S.pd3[(size_t)q * C + c];
@@ -298,6 +347,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         }
         if (hit) tri_ptr = 0;
       }
+      BSTAMP(2);
       if (tri_ptr < B_TRI) {
         S.tri[(size_t)c * B_TRI + tri_ptr] = cvd.x;
         tri_ptr++;
@@ -345,6 +395,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       resume = false;
       pend = 0;
     }
+    BSTAMP(3);
     // ---- part B (:450-702); its ring and weight reads first (a1's whatever
     // the symbol-tone window says: a read changes nothing)
     const double agc2_old = S.agc2[(size_t)agc2_p * C + c];
@@ -366,6 +417,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         hre[j - BD_LDS_TAPS] = hre[j - 1 - BD_LDS_TAPS] + c_btaps[j] * ddr;
         him[j - BD_LDS_TAPS] = him[j - 1 - BD_LDS_TAPS] + c_btaps[j] * ddi;
       }
+#if AERO_BD_LDS_TAPS > 0
       hre[0] = s_qre[BD_LDS_TAPS - 1][col] + c_btaps[BD_LDS_TAPS] * ddr;
       him[0] = s_qim[BD_LDS_TAPS - 1][col] + c_btaps[BD_LDS_TAPS] * ddi;
       for (int j = BD_LDS_TAPS - 1; j >= 1; --j) {
@@ -374,7 +426,12 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       }
       s_qre[0][col] = 0.0 + c_btaps[0] * ddr;
       s_qim[0][col] = 0.0 + c_btaps[0] * ddi;
+#else
+      hre[0] = 0.0 + c_btaps[0] * ddr;
+      him[0] = 0.0 + c_btaps[0] * ddi;
+#endif
     }
+    BSTAMP(4);
     if (startstop > 0) {
       startstop--;
       if (cntr < 1000000) cntr++;
@@ -434,6 +491,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       s2r = k * s2r;
       s2i = k * s2i;
     }
+    BSTAMP(5);
     {  // symbol timing (:482-496)
       const double st_diff = dly_commit(S.dl[BDL_S] + c, C, dlp[BDL_S], pS, abval * abval) - (abval * abval);
       const double st_d1out = dly_commit(S.dl[BDL_41] + c, C, dlp[BDL_41], p41, st_diff);
@@ -543,7 +601,9 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     b_nco_next(so_ptr, so_step);
     b_nco_next(q_ptr, q_step);
     n++;
+    BSTAMP(6);
   }
+  BCOUNT(0, (unsigned long long)(n - n0));
   // state back
 #pragma unroll 1
   for (int j = 0; j < BD_LDS_TAPS; ++j) {
@@ -614,6 +674,43 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   ls[BL_SP * C] = sp;
   ls[BL_SCOMMIT * C] = scommit;
   ls[BL_CHUNK_H * C] = chunk_h;
+  BSTAMP(7);
+  }
+#ifdef AERO_X_BSTAMPS
+  {  // per wave: section maxima over lanes, counters summed
+    unsigned long long v[13];
+    for (int k = 0; k < 8; k++) v[k] = bst_[k];
+    v[8] = bcnt_[0];
+    v[9] = bcnt_[1];
+    v[10] = bactive_ ? 1 : 0;
+    v[11] = 0;
+    v[12] = bcnt_[4];
+    for (int off = 32; off > 0; off >>= 1) {
+      for (int k = 0; k < 13; k++) {
+        const unsigned long long o = __shfl_xor(v[k], off, 64);
+        v[k] = (k < 8 || k == 12) ? (o > v[k] ? o : v[k]) : v[k] + o;
+      }
+    }
+    if (threadIdx.x == 0 && v[10]) {
+      for (int k = 0; k < 8; k++) atomicAdd(&g_bstamps[k], v[k]);
+      atomicAdd(&g_bstamps[8], v[8]);
+      atomicAdd(&g_bstamps[9], v[9]);
+      atomicAdd(&g_bstamps[10], v[10]);
+      atomicAdd(&g_bstamps[11], 1ull);
+      atomicAdd(&g_bstamps[12], v[12]);
+    }
+  }
+#endif
+}
+
+void burst_read_stamps(unsigned long long *out) {
+#ifdef AERO_X_BSTAMPS
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bstamps), sizeof(unsigned long long) * 16);
+  unsigned long long z[16] = {0};
+  hipMemcpyToSymbol(HIP_SYMBOL(g_bstamps), z, sizeof z);
+#else
+  for (int k = 0; k < 16; ++k) out[k] = 0;
+#endif
 }
 
 // --------------------------------------------------------- trident check

@@ -48,6 +48,7 @@ void upload_msk_constants(const double *, const double *, const double *);
 void demod_read_stamps(unsigned long long *);
 void coarse_read_stamps(unsigned long long *);
 void viterbi_read_stamps(unsigned long long *);
+void burst_read_stamps(unsigned long long *);
 void launch_coarse(hipStream_t, int, const DevState &, const DevTables &, int);
 void launch_frame(hipStream_t, int, const DevState &, int);
 void launch_viterbi(hipStream_t, int, const DevState &, const DevTables &, int, int);
@@ -1643,4 +1644,6 @@ extern "C" void aero_x_demod_stamps(unsigned long long *out7) { demod_read_stamp
 extern "C" void aero_x_coarse_stamps(unsigned long long *out8) { coarse_read_stamps(out8); }
 // the Viterbi kernel's per-section cycle totals over every job (3 sections + job count)
 extern "C" void aero_x_viterbi_stamps(unsigned long long *out4) { viterbi_read_stamps(out4); }
+// the burst OQPSK demod's per-section cycle totals (AERO_X_BSTAMPS build; burst.hip)
+extern "C" void aero_x_burst_stamps(unsigned long long *out16) { burst_read_stamps(out16); }
 

@@ -22,7 +22,9 @@
  *    are printed after each engine run, not as the demodulator emits them;
  *  - extension: several -t options decode several topics in one process,
  *    one engine channel per topic (-b / -s once, or once per topic); every
- *    message queued on the socket is pushed before one aero_run.
+ *    message queued on the socket is pushed before one aero_run;
+ *  - AERO_ZMQ_HWM sets the SUB socket's receive high-water mark (0 =
+ *    unbounded) for publishers running faster than real time.
  */
 #include <execinfo.h>
 #include <signal.h>
@@ -402,6 +404,10 @@ int main(int argc, char **argv) {
   std::vector<char> samples(buf_size);
   int rc_exit = 0;
   AH_DBG("Connecting to ZMQ endpoint at %s", publisher.c_str());
+  if (const char *h = getenv("AERO_ZMQ_HWM")) {  // as aero-publish: 0 = unbounded receive queue
+    const int hwm = atoi(h);
+    z->setsockopt(sub, ZMQ_RCVHWM_, &hwm, sizeof hwm);
+  }
   if (z->connect(sub, publisher.c_str()) == -1) {
     AH_CRIT("Failed to connect to publisher, error code: %d; is aero-publish or SDRReceiver running?", -1);
     g_running.store(0);

@@ -107,6 +107,13 @@ struct Publisher {
     z->setsockopt(sock, 37 /* ZMQ_TCP_KEEPALIVE_INTVL */, &intvl, sizeof intvl);
     z->setsockopt(sock, ZMQ_RECONNECT_IVL_, &reconnect, sizeof reconnect);
     z->setsockopt(sock, ZMQ_RECONNECT_IVL_MAX_, &reconnect_max, sizeof reconnect_max);
+    // AERO_ZMQ_HWM (not in the reference, which keeps ZeroMQ's default 1000):
+    // a send queue bound for runs that publish faster than real time (a file
+    // source without pacing); 0 = unbounded, nothing is dropped
+    if (const char *h = getenv("AERO_ZMQ_HWM")) {
+      const int hwm = atoi(h);
+      z->setsockopt(sock, ZMQ_SNDHWM_, &hwm, sizeof hwm);
+    }
     return (bind ? z->bind(sock, addr.c_str()) : z->connect(sock, addr.c_str())) == 0;
   }
   // the topic goes out as exactly 5 bytes (zmqpublisher.cpp:69), NUL-padded

@@ -542,7 +542,10 @@ def run_c5bin(a):
     args = [os.path.join(bindir, 'aero-decode'), '-p', 'tcp://127.0.0.1:%d' % port, '--format', 'jsondump', '-v']
     for v in range(nv):
         args += ['-t', 'VFO%02d' % (v + 1), '-b', str(cfg['vfos'][v]['data_rate']), '-s', 'BENCH']
-    dec = subprocess.Popen(args, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    # the publisher reads the file without pacing: unbounded ZeroMQ queues on
+    # both ends (AERO_ZMQ_HWM=0) so nothing is dropped while the decoder catches up
+    env = dict(os.environ, AERO_ZMQ_HWM='0')
+    dec = subprocess.Popen(args, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env)
     lines, stamps = [], []
 
     def pump(pipe, out, st):
@@ -558,7 +561,7 @@ def run_c5bin(a):
         time.sleep(0.05)
     pub = subprocess.Popen([os.path.join(bindir, 'aero-publish'), '-v', '-d',
                             'driver=file,path=%s,start_delay_ms=1500' % wb, ini], stdout=subprocess.DEVNULL,
-                           stderr=subprocess.PIPE)
+                           stderr=subprocess.PIPE, env=env)
     plines, pstamps = [], []
     tp = threading.Thread(target=pump, args=(pub.stderr, plines, pstamps), daemon=True)
     tp.start()

@@ -74,7 +74,9 @@ def test_events_burst(engine_lib, cpu_libs):
         ref.push_chunked(pcm, 12000)
         want_dcd, want_fc = ref.events()
         dcd, steps, _ = eng.channel_events(ch)
-        assert want_dcd >= 4, 'the synthetic stream carries several bursts'
+        # the burst window (10500 bits) only ends after many bursts, so the
+        # carrier usually stays detected after the first one
+        assert want_dcd >= 1, 'the synthetic stream carries bursts'
         assert (dcd, steps) == (want_dcd, 0), (b, dcd, want_dcd)
     eng.close()
 

@@ -284,11 +284,12 @@ def test_multi_topic_decoder(engine_lib, cpu_libs, tmp_path):
     args = ['-p', 'tcp://127.0.0.1:%d' % port, '--format', 'jsondump', '-v']
     for v in range(nv):
         args += ['-t', 'VFO%02d' % (v + 1), '-b', str(cfg['vfos'][v]['data_rate']), '-s', 'ST%02d' % (v + 1)]
-    dec, lines, th = _start_decoder(args, {})
+    # unpaced file source: unbounded ZeroMQ queues (AERO_ZMQ_HWM=0) so no message is dropped
+    dec, lines, th = _start_decoder(args, {'AERO_ZMQ_HWM': '0'})
     try:
         r = subprocess.run([os.path.join(BIN, 'aero-publish'), '-d',
                             'driver=file,path=%s,start_delay_ms=1500' % wb, str(ini)],
-                           capture_output=True, text=True, timeout=180)
+                           capture_output=True, text=True, timeout=180, env=dict(os.environ, AERO_ZMQ_HWM='0'))
         assert r.returncode == 0, r.stderr[-3000:]
         t0 = time.time()
         want_n = sum(len(w) for w in wants)
