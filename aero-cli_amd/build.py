@@ -32,6 +32,13 @@ CXX_FLAGS = ['-O2', '-std=c++17', '-fPIC', '-Wall'] + FP
 HIP_SRCS = ['demod_oqpsk.hip', 'demod_msk.hip', 'coarse.hip', 'aerol.hip', 'engine.hip', 'chan.hip', 'burst.hip', 'burst_msk.hip',
             'burst_engine.hip']
 CXX_SRCS = ['tables_host.cpp', 'acars_host.cpp']
+# Per-file codegen: the burst demodulators' loops hold their state in
+# registers; LLVM's machine LICM hoists every FP64 constant of the inlined
+# libm ports out of the loop into SGPRs, hundreds of them, which then spill
+# (AGPR / VGPR-lane round trips every sample).  Without it they stay
+# rematerialised at their use.
+FILE_FLAGS = {'burst.hip': ['-mllvm', '-disable-machine-licm'],
+              'burst_msk.hip': ['-mllvm', '-disable-machine-licm']}
 
 
 def _run(cmd):
@@ -48,10 +55,12 @@ def _stale(out, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_engine(jobs=4, variant=None, defines=()):
-    """Builds aero-cli_amd/libaero_engine.so.  `variant`/`defines` build an
-    experimental copy (libaero_engine_<variant>.so, objects in build/<variant>)
-    for A/B kernel measurements; select it with AERO_ENGINE_SO=<path>."""
+def build_engine(jobs=4, variant=None, defines=(), file_flags=None):
+    """Builds aero-cli_amd/libaero_engine.so.  `variant`/`defines`/`file_flags`
+    build an experimental copy (libaero_engine_<variant>.so, objects in
+    build/<variant>) for A/B kernel measurements; select it with
+    AERO_ENGINE_SO=<path>."""
+    ff = dict(FILE_FLAGS, **(file_flags or {}))
     bdir = BUILD if variant is None else os.path.join(BUILD, variant)
     out = ENGINE_SO if variant is None else os.path.join(HERE, 'libaero_engine_%s.so' % variant)
     os.makedirs(bdir, exist_ok=True)
@@ -65,7 +74,7 @@ def build_engine(jobs=4, variant=None, defines=()):
         objs.append(obj)
         if _stale(obj, [src] + headers):
             if s.endswith('.hip'):
-                cmd = [HIPCC] + HIP_FLAGS + dflags + ['-c', src, '-o', obj]
+                cmd = [HIPCC] + HIP_FLAGS + ff.get(s, []) + dflags + ['-c', src, '-o', obj]
             else:
                 cmd = ['g++'] + CXX_FLAGS + dflags + ['-c', src, '-o', obj]
             tasks.append(cmd)

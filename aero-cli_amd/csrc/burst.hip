@@ -8,14 +8,19 @@
  *                      decode/jfft.cpp:445-495): 8192-point overlap-add blocks of
  *                      6145 samples, one workgroup per channel, into a
  *                      time-major analytic-signal ring.
- *  demod_burst_kernel  the per-sample recurrence, one channel per lane.  A lane
- *                      stops where the reference runs its trident check
- *                      (burstoqpskdemodulator.cpp:343-440) and resumes after
- *                      trident_kernel has decided, at the same sample.
+ *  front_burst_kernel  part A of the per-sample recurrence (AGC, d1/d2, burst
+ *                      statistic, peak detector, trident buffer), one channel
+ *                      per lane, ahead of the demodulator: it never reads the
+ *                      demodulator's state.  It records each completed trident
+ *                      buffer and the sample the reference checks it at
+ *                      (burstoqpskdemodulator.cpp:343-440).
  *  trident_kernel      FFTrWrapper<double>(32768) of both trident halves (a
  *                      16384-point JFFT + split), |top| - |base|, the +-1792-bin
  *                      trident search and the strongest base bin; one
- *                      1024-thread workgroup per waiting channel.
+ *                      1024-thread workgroup per recorded check.
+ *  demod_burst_kernel  part B, one channel per lane, from the front end's
+ *                      val_to_demod ring, each trident decision applied at
+ *                      its sample.
  *  frame_burst_kernel  AeroL burst framing (UW tolerance 4 within the muw window,
  *                      dummy header, R/T block fill, tests at blockptr 320+192k).
  *  rt_viterbi_kernel   one wave per R/T test: deinterleave 64 x blockptr/64 and
@@ -26,6 +31,9 @@
  * operation order, GCC complex products, aero_math.h for libm.
  */
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
 
 #include "aero_math.h"
 #include "burst_common.h"
@@ -142,12 +150,11 @@ constexpr int BD_LDS_TAPS = AERO_BD_LDS_TAPS, BD_REG_TAPS = NTAPS - BD_LDS_TAPS;
 // AERO_X_BSTAMPS (diagnostic build only): s_memtime cycle totals per section
 // of the demod loop, each wave's maximum over its lanes (the wave's time in
 // the section while the lane was in the loop), summed over waves: [0] loop
-// control, [1] part A (AGC, burst statistic), [2] peak detector incl.
-// findmaxpos, [3] trident store / resume, [4] part B loads + RRC, [5] PLL,
-// rotators, AGC2, clip, [6] symbol timing + step + NCOs, [7] entry + exit
-// (state); counters summed over lanes: [8] samples advanced, [9] findmaxpos
-// scans, [10] lanes that entered the loop, [11] waves, [12] loop iterations
-// (max over the wave's lanes)
+// control, [1] message start + val_to_demod, [3] trident decision, [4] part
+// B loads + RRC, [5] PLL, rotators, AGC2, clip, [6] symbol timing + step +
+// NCOs, [7] entry + exit (state); counters summed over lanes: [8] samples
+// advanced, [10] lanes that entered the loop, [11] waves, [12] loop
+// iterations (max over the wave's lanes)
 #ifdef AERO_X_BSTAMPS
 __device__ unsigned long long g_bstamps[16];
 #define BSTAMP(k)                                                  \
@@ -168,8 +175,165 @@ __device__ unsigned long long g_bstamps[16];
   } while (0)
 #endif
 
-__global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, BurstTables T, int nch, int max_n,
-                                                               int trace) {
+// ------------------------------------------------------------- front end
+// Part A of BurstOqpskDemodulator::writeDataSlot (decode/burstoqpskdemodulator.cpp:
+// 300-345): AGC, the delays d1 / d2, the burst-timing statistic, the peak
+// detector and the trident buffer.  It reads the analytic signal only, never
+// the demodulator's state, so it runs ahead of the demodulator proper over
+// the pass's samples: d2's output (val_to_demod, the demodulator's input
+// B_D2 - 1 samples later) goes to a ring indexed by sample, and each
+// completed trident buffer stays in its own slot with the sample at which
+// the reference checks it, for trident_kernel to decide before the
+// demodulator reaches that sample.  One channel per lane, no LDS.
+__global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTables T, int nch) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= nch) return;
+  const int C = S.C;
+  double *ds = S.ds + c;
+  int *is = S.is + c;
+  long long *ls = S.ls + c;
+  const long long n0 = ls[BL_NSAMP_A * C];
+  long long end = ls[BL_AVAIL * C];
+  // the ring keeps what the demodulator has not read yet
+  const long long lim = ls[BL_NSAMP * C] + (BV_LEN - (B_D2 - 1));
+  if (end > lim) end = lim;
+  long long chk_n = ls[BL_CHK_N * C];
+  const long long chk_done = ls[BL_CHK_DONE * C];
+  if (n0 >= end) return;
+  double agc_sum = ds[BD_AGC_SUM * C];
+  double ma1r = ds[BD_MA1_RE * C], ma1i = ds[BD_MA1_IM * C], mav1_sum = ds[BD_MAV1_SUM * C];
+  double pd_lastdy = ds[BD_PD_LASTDY * C];
+  int agc_p = is[BI_AGC_P * C], d1_p = is[BI_D1_P * C];
+  int ma1_p = is[BI_MA1_P * C], mav1_p = is[BI_MAV1_P * C];
+  int dl_bt = is[(BI_DL_P0 + BDL_BT) * C], dl_md = is[(BI_DL_P0 + BDL_MADIFF) * C];
+  int pd1_p = is[BI_PD1_P * C], pd2_p = is[BI_PD2_P * C], pd3_p = is[BI_PD3_P * C];
+  int pd_cntdown = is[BI_PD_CNTDOWN * C], pd_maxposcd = is[BI_PD_MAXPOSCD * C];
+  int tri_ptr = is[BI_TRI_PTR * C];
+  double *tri = S.tri + ((size_t)c * TRI_SLOTS + (chk_n & (TRI_SLOTS - 1))) * B_TRI;
+  const DlyRef dBT = dref(T, BDL_BT), dMD = dref(T, BDL_MADIFF);
+  double2 *btr = reinterpret_cast<double2 *>(S.dl[BDL_BT]) + c;
+  long long n = n0;
+  while (n < end) {
+    // every slot holds a check the demodulator has not applied: the buffer
+    // this sample may start filling is one of them
+    if (chk_n - chk_done >= TRI_SLOTS) break;
+    // every ring slot (and Delay weight) this sample reads, loaded before any
+    // of its stores so the round trips overlap; none is the slot written
+    // this sample (burst_dev.h dly_pre)
+    const int d1r = d1_p + 1 == B_D1 ? 0 : d1_p + 1;
+    const int p1r = pd1_p + 1 == B_PD1 ? 0 : pd1_p + 1, p2r = pd2_p + 1 == B_PD2 ? 0 : pd2_p + 1;
+    const double2 a = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
+    const double agc_old = S.agc[(size_t)agc_p * C + c];
+    const double2 cvd = S.d1[(size_t)d1r * C + c];  // d1.update_dont_touch(cval)
+    const DlyPre2 btp = dly_pre2(btr, C, dl_bt, dBT);
+    const double2 ma_old = S.ma1[(size_t)ma1_p * C + c];
+    const double mv_old = S.mav1[(size_t)mav1_p * C + c];
+    const DlyPre mdp = dly_pre(S.dl[BDL_MADIFF] + c, C, dl_md, dMD);
+    const double pd1_old = S.pd1[(size_t)p1r * C + c], pd2_old = S.pd2[(size_t)p2r * C + c];
+    double cr = a.x, ci = a.y;
+    {  // agc.Update(|cval|); cval *= AGCVal (:316-317)
+      const double av = aero_hypot(cr, ci);
+      agc_sum = agc_sum - agc_old;
+      agc_sum = agc_sum + fabs(av);
+      S.agc[(size_t)agc_p * C + c] = fabs(av);
+      agc_p = agc_p + 1 == B_AGC ? 0 : agc_p + 1;
+      double g = 1.414213562 / fmax(agc_sum / ((double)B_AGC), 0.000001);
+      g = fmax(g, 0.000001);
+      cr *= g;
+      ci *= g;
+    }
+    S.d1[(size_t)d1_p * C + c] = make_double2(cr, ci);
+    d1_p = d1r;
+    // d2.update_dont_touch(real(cval_d)): the demodulator reads it back B_D2 - 1 samples later
+    S.vring[(size_t)(n & (BV_LEN - 1)) * C + c] = cvd.x;
+    double fastarm;
+    {  // burst-timing statistic (:326-339)
+      const double2 bd = dly_commit2(btr, C, dl_bt, btp, make_double2(cr, ci));
+      const double pr = cr * bd.x - ci * (-bd.y), pi = cr * (-bd.y) + ci * bd.x;  // cval * conj(bd)
+      ma1r = ma1r - ma_old.x;
+      ma1i = ma1i - ma_old.y;
+      ma1r = ma1r + pr;
+      ma1i = ma1i + pi;
+      S.ma1[(size_t)ma1_p * C + c] = make_double2(pr, pi);
+      ma1_p = ma1_p + 1 == B_MA ? 0 : ma1_p + 1;
+      fastarm = aero_hypot(ma1r / ((double)B_MA), ma1i / ((double)B_MA));
+      mav1_sum = mav1_sum - mv_old;
+      mav1_sum = mav1_sum + (fastarm);
+      S.mav1[(size_t)mav1_p * C + c] = fastarm;
+      mav1_p = mav1_p + 1 == B_MA ? 0 : mav1_p + 1;
+      fastarm = mav1_sum / ((double)B_MA);
+      fastarm -= dly_commit(S.dl[BDL_MADIFF] + c, C, dl_md, mdp, fastarm);
+      if (fastarm < 0) fastarm = 0;
+    }
+    double bt = fastarm * fastarm;
+    if (bt > 500) bt = 500;
+    {  // PeakDetector::update (DSP.h:491-566)
+      double val = bt;
+      S.pd3[(size_t)pd3_p * C + c] = val;
+      pd3_p = pd3_p + 1 == B_PD3 ? 0 : pd3_p + 1;
+      S.pd1[(size_t)pd1_p * C + c] = val;
+      pd1_p = p1r;
+      const double dy = val - pd1_old;
+      S.pd2[(size_t)pd2_p * C + c] = val;
+      pd2_p = p2r;
+      val = pd2_old;  // d2.update(val)
+      if ((!pd_cntdown) && (val > 0.2) && ((pd_lastdy >= 0 && dy < 0))) {
+        pd_cntdown = B_PD_MAXCD;
+        pd_maxposcd = pd3_findmaxpos(S.pd3 + c, C, pd3_p, B_PD3);
+      }
+      if (pd_cntdown > 0) pd_cntdown--;
+      pd_lastdy = dy;
+      bool hit = false;
+      if (!pd_maxposcd) {
+        pd_maxposcd--;
+        hit = true;
+      } else if (pd_maxposcd > 0) {
+        pd_maxposcd--;
+      }
+      if (hit) tri_ptr = 0;
+    }
+    if (tri_ptr < B_TRI) {
+      tri[tri_ptr] = cvd.x;
+      tri_ptr++;
+    } else if (tri_ptr == B_TRI) {
+      // the reference checks the buffer at this sample (:343-440); the
+      // demodulator applies trident_kernel's decision before its part B here
+      tri_ptr++;
+      const int slot = (int)(chk_n & (TRI_SLOTS - 1));
+      S.chk_n[(size_t)c * TRI_SLOTS + slot] = n;
+      S.tjobs[atomicAdd(S.ntjobs, 1)] = c | (slot << 24);
+      chk_n++;
+      tri = S.tri + ((size_t)c * TRI_SLOTS + (chk_n & (TRI_SLOTS - 1))) * B_TRI;
+    }
+    n++;
+  }
+  ds[BD_AGC_SUM * C] = agc_sum;
+  ds[BD_MA1_RE * C] = ma1r;
+  ds[BD_MA1_IM * C] = ma1i;
+  ds[BD_MAV1_SUM * C] = mav1_sum;
+  ds[BD_PD_LASTDY * C] = pd_lastdy;
+  is[BI_AGC_P * C] = agc_p;
+  is[BI_D1_P * C] = d1_p;
+  is[BI_MA1_P * C] = ma1_p;
+  is[BI_MAV1_P * C] = mav1_p;
+  is[(BI_DL_P0 + BDL_BT) * C] = dl_bt;
+  is[(BI_DL_P0 + BDL_MADIFF) * C] = dl_md;
+  is[BI_PD1_P * C] = pd1_p;
+  is[BI_PD2_P * C] = pd2_p;
+  is[BI_PD3_P * C] = pd3_p;
+  is[BI_PD_CNTDOWN * C] = pd_cntdown;
+  is[BI_PD_MAXPOSCD * C] = pd_maxposcd;
+  is[BI_TRI_PTR * C] = tri_ptr;
+  ls[BL_NSAMP_A * C] = n;
+  ls[BL_CHK_N * C] = chk_n;
+}
+
+// ----------------------------------------------------------------- demod
+// Part B of writeDataSlot (:450-702) from the front end's val_to_demod, the
+// trident decisions applied at the samples the front end recorded.  One
+// wave per workgroup.  The transposed RRC partial sums of taps
+// [BD_LDS_TAPS, 55) live in registers, the rest (real and imaginary) in LDS.
+__global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, BurstTables T, int nch, int trace) {
   __shared__ double s_qre[BD_LDS_TAPS > 0 ? BD_LDS_TAPS : 1][BD_BLOCK];
   __shared__ double s_qim[BD_LDS_TAPS > 0 ? BD_LDS_TAPS : 1][BD_BLOCK];
   const int c = blockIdx.x * BD_BLOCK + threadIdx.x, col = threadIdx.x;
@@ -183,41 +347,31 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   double *ds = S.ds + c;
   int *is = S.is + c;
   long long *ls = S.ls + c;
-  int pend = is[BI_PEND * C];
   const long long n0 = ls[BL_NSAMP * C];
-  long long end = ls[BL_AVAIL * C];
-  if (end - n0 > max_n) end = n0 + max_n;
+  const long long end = ls[BL_NSAMP_A * C];  // the front end's progress
 #ifdef AERO_X_BSTAMPS
   // every lane reaches the wave reduction at the end
-  if (!(pend == 1 || (n0 >= end && pend != 2))) {
+  if (n0 < end) {
     bactive_ = true;
 #else
-  if (pend == 1) return;  // trident check outstanding
-  if (n0 >= end && pend != 2) return;
+  if (n0 >= end) return;
   {
 #endif
-
   double m2_ptr = ds[BD_M2_PTR * C], m2_step = ds[BD_M2_STEP * C], m2_freq = ds[BD_M2_FREQ * C];
   double so_ptr = ds[BD_SO_PTR * C], so_last = ds[BD_SO_LAST * C], so_step = ds[BD_SO_STEP * C];
   double so_freq = ds[BD_SO_FREQ * C];
   double q_ptr = ds[BD_Q_PTR * C], q_step = ds[BD_Q_STEP * C];
-  double agc_sum = ds[BD_AGC_SUM * C], agc2_sum = ds[BD_AGC2_SUM * C];
-  double ma1r = ds[BD_MA1_RE * C], ma1i = ds[BD_MA1_IM * C], mav1_sum = ds[BD_MAV1_SUM * C];
-  double pd_lastdy = ds[BD_PD_LASTDY * C], vol_gain = ds[BD_VOL_GAIN * C];
+  double agc2_sum = ds[BD_AGC2_SUM * C], vol_gain = ds[BD_VOL_GAIN * C];
   double srx1 = ds[BD_SR_X1 * C], srx2 = ds[BD_SR_X2 * C], sry1 = ds[BD_SR_Y1 * C], sry2 = ds[BD_SR_Y2 * C];
   double ave_r = ds[BD_AVE_RE * C], ave_i = ds[BD_AVE_IM * C], rot_r = ds[BD_ROT_RE * C], rot_i = ds[BD_ROT_IM * C];
   double str_r = ds[BD_STR_RE * C], str_i = ds[BD_STR_IM * C];
   double ptd_r = ds[BD_PTD_RE * C], ptd_i = ds[BD_PTD_IM * C], s2l_r = ds[BD_S2L_RE * C], s2l_i = ds[BD_S2L_IM * C];
   double rotf = ds[BD_ROTF * C], mse = ds[BD_MSE * C], lastmse = ds[BD_LASTMSE * C];
   double msema_sum = ds[BD_MSEMA_SUM * C];
-  int agc_p = is[BI_AGC_P * C], agc2_p = is[BI_AGC2_P * C], d1_p = is[BI_D1_P * C], d2_p = is[BI_D2_P * C];
-  int ma1_p = is[BI_MA1_P * C], mav1_p = is[BI_MAV1_P * C];
-  int dlp[BDL_COUNT];
-#pragma unroll
-  for (int k = 0; k < BDL_COUNT; ++k) dlp[k] = is[(BI_DL_P0 + k) * C];
-  int pd1_p = is[BI_PD1_P * C], pd2_p = is[BI_PD2_P * C], pd3_p = is[BI_PD3_P * C];
-  int pd_cntdown = is[BI_PD_CNTDOWN * C], pd_maxposcd = is[BI_PD_MAXPOSCD * C];
-  int tri_ptr = is[BI_TRI_PTR * C], msema_p = is[BI_MSEMA_P * C];
+  int agc2_p = is[BI_AGC2_P * C];
+  int dl_s = is[(BI_DL_P0 + BDL_S) * C], dl_41 = is[(BI_DL_P0 + BDL_41) * C], dl_42 = is[(BI_DL_P0 + BDL_42) * C];
+  int dl_8 = is[(BI_DL_P0 + BDL_8) * C], dl_a1 = is[(BI_DL_P0 + BDL_A1) * C];
+  int msema_p = is[BI_MSEMA_P * C];
   int startstop = is[BI_STARTSTOP * C], cntr = is[BI_CNTR * C], insertpre = is[BI_INSERTPRE * C];
   int yui = is[BI_YUI * C];
   int hop_n = S.hop_n[c];
@@ -225,6 +379,9 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   const long long scons = ls[BL_SCONS * C];
   long long chunk_h = ls[BL_CHUNK_H * C];
   const long long chunk_n = ls[BL_CHUNK_N * C];
+  long long chk_done = ls[BL_CHK_DONE * C];
+  const long long chk_n = ls[BL_CHK_N * C];
+  long long next_chk = chk_done < chk_n ? S.chk_n[(size_t)c * TRI_SLOTS + (chk_done & (TRI_SLOTS - 1))] : LLONG_MAX;
 #pragma unroll 1
   for (int j = 0; j < BD_LDS_TAPS; ++j) {
     s_qre[j][col] = S.fir[(size_t)j * C + c];
@@ -240,131 +397,30 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   const long long *chunks = S.chunks + (size_t)c * CHUNK_RING;
   const double PT = 0.4 * WTSIZE;  // IfHavePassedPoint(ee), ee = 0.4
   const DlyRef dS = dref(T, BDL_S), d41 = dref(T, BDL_41), d42 = dref(T, BDL_42), d8 = dref(T, BDL_8);
-  const DlyRef dA1 = dref(T, BDL_A1), dBT = dref(T, BDL_BT), dMD = dref(T, BDL_MADIFF);
+  const DlyRef dA1 = dref(T, BDL_A1);
 
   long long n = n0;
-  bool resume = pend == 2;
   BSTAMP(7);
-  while (resume || n < end) {
+  while (n < end) {
     BSTAMP(0);
     BCOUNT(4, 1);
-    double vtd;  // val_to_demod
-    if (!resume) {
-      if (sp - scons > B_SOFT_RING - 64) break;  // soft ring full: framing frees it next
-      // lastmse is captured at the start of every message (burstoqpskdemodulator.cpp:264)
-      while (chunk_h < chunk_n && chunks[chunk_h & (CHUNK_RING - 1)] == n) {
-        lastmse = mse;
-        chunk_h++;
-      }
-      // every ring slot (and Delay weight) this sample reads, loaded before
-      // any of its stores so the round trips overlap; none is the slot
-      // written this sample (burst_dev.h dly_pre)
-      const int d1r = d1_p + 1 == B_D1 ? 0 : d1_p + 1, d2r = d2_p + 1 == B_D2 ? 0 : d2_p + 1;
-      const int p1r = pd1_p + 1 == B_PD1 ? 0 : pd1_p + 1, p2r = pd2_p + 1 == B_PD2 ? 0 : pd2_p + 1;
-      double2 *btr = reinterpret_cast<double2 *>(S.dl[BDL_BT]) + c;
-      const double2 a = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
-      const double agc_old = S.agc[(size_t)agc_p * C + c];
-      const double2 cvd = S.d1[(size_t)d1r * C + c];  // d1.update_dont_touch(cval)
-      vtd = S.d2[(size_t)d2r * C + c];                 // d2.update_dont_touch(real(cval_d))
-      const DlyPre2 btp = dly_pre2(btr, C, dlp[BDL_BT], dBT);
-      const double2 ma_old = S.ma1[(size_t)ma1_p * C + c];
-      const double mv_old = S.mav1[(size_t)mav1_p * C + c];
-      const DlyPre mdp = dly_pre(S.dl[BDL_MADIFF] + c, C, dlp[BDL_MADIFF], dMD);
-      const double pd1_old = S.pd1[(size_t)p1r * C + c], pd2_old = S.pd2[(size_t)p2r * C + c];
-      double cr = a.x, ci = a.y;
-      {  // agc.Update(|cval|); cval *= AGCVal (:316-317)
-        const double av = aero_hypot(cr, ci);
-        agc_sum = agc_sum - agc_old;
-        agc_sum = agc_sum + fabs(av);
-        S.agc[(size_t)agc_p * C + c] = fabs(av);
-        agc_p = agc_p + 1 == B_AGC ? 0 : agc_p + 1;
-        double g = 1.414213562 / fmax(agc_sum / ((double)B_AGC), 0.000001);
-        g = fmax(g, 0.000001);
-        cr *= g;
-        ci *= g;
-      }
-      S.d1[(size_t)d1_p * C + c] = make_double2(cr, ci);
-      d1_p = d1r;
-      S.d2[(size_t)d2_p * C + c] = cvd.x;
-      d2_p = d2r;
-      double fastarm;
-      {  // burst-timing statistic (:326-339)
-        const double2 bd = dly_commit2(btr, C, dlp[BDL_BT], btp, make_double2(cr, ci));
-        const double pr = cr * bd.x - ci * (-bd.y), pi = cr * (-bd.y) + ci * bd.x;  // cval * conj(bd)
-        ma1r = ma1r - ma_old.x;
-        ma1i = ma1i - ma_old.y;
-        ma1r = ma1r + pr;
-        ma1i = ma1i + pi;
-        S.ma1[(size_t)ma1_p * C + c] = make_double2(pr, pi);
-        ma1_p = ma1_p + 1 == B_MA ? 0 : ma1_p + 1;
-        fastarm = aero_hypot(ma1r / ((double)B_MA), ma1i / ((double)B_MA));
-        mav1_sum = mav1_sum - mv_old;
-        mav1_sum = mav1_sum + (fastarm);
-        S.mav1[(size_t)mav1_p * C + c] = fastarm;
-        mav1_p = mav1_p + 1 == B_MA ? 0 : mav1_p + 1;
-        fastarm = mav1_sum / ((double)B_MA);
-        fastarm -= dly_commit(S.dl[BDL_MADIFF] + c, C, dlp[BDL_MADIFF], mdp, fastarm);
-        if (fastarm < 0) fastarm = 0;
-      }
-      double bt = fastarm * fastarm;
-      if (bt > 500) bt = 500;
-      BSTAMP(1);
-      {  // PeakDetector::update (DSP.h:491-566)
-        double val = bt;
-        double *r3 = S.pd3 + (size_t)pd3_p * C + c;
-        *r3 = val;
-        pd3_p = pd3_p + 1 == B_PD3 ? 0 : pd3_p + 1;
-        S.pd1[(size_t)pd1_p * C + c] = val;
-        pd1_p = p1r;
-        const double dy = val - pd1_old;
-        S.pd2[(size_t)pd2_p * C + c] = val;
-        pd2_p = p2r;
-        val = pd2_old;  // d2.update(val)
-        if ((!pd_cntdown) && (val > 0.2) && ((pd_lastdy >= 0 && dy < 0))) {
-          pd_cntdown = B_PD_MAXCD;
-          BCOUNT(1, 1);
-          // d3.findmaxpos: first maximum, scanning from the oldest slot
-          int q = pd3_p, maxpos = 0;
-          double maxval = S.pd3[(size_t)q * C + c];
-          for (int i = 0; i < B_PD3; i++) {
-            const double v = S.pd3[(size_t)q * C + c];
-            if (v > maxval) {
-              maxval = v;
-              maxpos = i;
-            }
-            q = q + 1 == B_PD3 ? 0 : q + 1;
-          }
-          pd_maxposcd = maxpos;
-        }
-        if (pd_cntdown > 0) pd_cntdown--;
-        pd_lastdy = dy;
-        bool hit = false;
-        if (!pd_maxposcd) {
-          pd_maxposcd--;
-          hit = true;
-        } else if (pd_maxposcd > 0) {
-          pd_maxposcd--;
-        }
-        if (hit) tri_ptr = 0;
-      }
-      BSTAMP(2);
-      if (tri_ptr < B_TRI) {
-        S.tri[(size_t)c * B_TRI + tri_ptr] = cvd.x;
-        tri_ptr++;
-      } else if (tri_ptr == B_TRI) {
-        tri_ptr++;
-        ds[BD_RESUME_VAL * C] = vtd;
-        pend = 1;  // trident_kernel decides, this sample resumes after it
-        break;
-      }
-    } else {
-      vtd = ds[BD_RESUME_VAL * C];
-      // trident decision (burstoqpskdemodulator.cpp:393-411)
-      if (is[BI_TRI_DET * C]) {
-        const double carrierphase = aero_atan2(ds[BD_TRI_BIM * C], ds[BD_TRI_BRE * C]) - (M_PI / 4.0);
-        b_set_freq(m2_freq, m2_step, (48000.0 / 32768.0) * (double)is[BI_TRI_MINBIN * C]);
+    if (sp - scons > B_SOFT_RING - 64) break;  // soft ring full: framing frees it next
+    // lastmse is captured at the start of every message (burstoqpskdemodulator.cpp:264)
+    while (chunk_h < chunk_n && chunks[chunk_h & (CHUNK_RING - 1)] == n) {
+      lastmse = mse;
+      chunk_h++;
+    }
+    // val_to_demod = d2.update_dont_touch(...): the front end's value of B_D2 - 1 samples ago (zeros before)
+    const double vtd = n >= B_D2 - 1 ? S.vring[(size_t)((n - (B_D2 - 1)) & (BV_LEN - 1)) * C + c] : 0.0;
+    BSTAMP(1);
+    if (n == next_chk) {
+      // trident decision (burstoqpskdemodulator.cpp:393-411), computed by trident_kernel
+      const double *r = S.chk + ((size_t)c * TRI_SLOTS + (chk_done & (TRI_SLOTS - 1))) * CHK_REC;
+      if (r[0] != 0.0) {
+        const double carrierphase = aero_atan2(r[6], r[5]) - (M_PI / 4.0);
+        b_set_freq(m2_freq, m2_step, (48000.0 / 32768.0) * r[1]);
         b_set_phase_deg(m2_ptr, (180.0 / M_PI) * carrierphase);
-        vol_gain = 1.4142 * 500.0 / ds[BD_TRI_MINVAL * C];
+        vol_gain = 1.4142 * 500.0 / r[3];
         b_set_freq(so_freq, so_step, 10500.0);
         b_set_phase_deg(so_ptr, 0);
         srx1 = srx2 = sry1 = sry2 = 0;
@@ -385,27 +441,31 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       if (trace && hop_n < S.hop_cap) {
         double *h = S.hops + ((size_t)c * S.hop_cap + hop_n) * 6;
         h[0] = (double)n;
-        h[1] = is[BI_TRI_DET * C] ? 1.0 : 0.0;
+        h[1] = r[0] != 0.0 ? 1.0 : 0.0;
         h[2] = m2_freq;
         h[3] = vol_gain;
-        h[4] = ds[BD_TRI_MAXVAL * C];
-        h[5] = (double)is[BI_TRI_MINBIN * C];
+        h[4] = r[4];
+        h[5] = r[1];
       }
       hop_n++;
-      resume = false;
-      pend = 0;
+      chk_done++;
+      next_chk = chk_done < chk_n ? S.chk_n[(size_t)c * TRI_SLOTS + (chk_done & (TRI_SLOTS - 1))] : LLONG_MAX;
     }
     BSTAMP(3);
     // ---- part B (:450-702); its ring and weight reads first (a1's whatever
     // the symbol-tone window says: a read changes nothing)
     const double agc2_old = S.agc2[(size_t)agc2_p * C + c];
-    const DlyPre pS = dly_pre(S.dl[BDL_S] + c, C, dlp[BDL_S], dS);
-    const DlyPre p41 = dly_pre(S.dl[BDL_41] + c, C, dlp[BDL_41], d41);
-    const DlyPre p42 = dly_pre(S.dl[BDL_42] + c, C, dlp[BDL_42], d42);
-    const DlyPre p8 = dly_pre(S.dl[BDL_8] + c, C, dlp[BDL_8], d8);
-    const DlyPre pA1 = dly_pre(S.dl[BDL_A1] + c, C, dlp[BDL_A1], dA1);
+    const DlyPre pS = dly_pre(S.dl[BDL_S] + c, C, dl_s, dS);
+    const DlyPre p41 = dly_pre(S.dl[BDL_41] + c, C, dl_41, d41);
+    const DlyPre p42 = dly_pre(S.dl[BDL_42] + c, C, dl_42, d42);
+    const DlyPre p8 = dly_pre(S.dl[BDL_8] + c, C, dl_8, d8);
+    const DlyPre pA1 = dly_pre(S.dl[BDL_A1] + c, C, dl_a1, dA1);
     double s2r, s2i;
     {
+      // the taps are reloaded (scalar loads) every sample rather than held
+      // in 110 SGPRs across the loop, which spilled
+      const double *tp = c_btaps;
+      asm volatile("" : "+s"(tp));
       const double2 m2 = T.cis[b_cis_index(m2_ptr)];
       const double sc = vol_gain * vtd;
       const double ddr = m2.x * sc, ddi = m2.y * sc;
@@ -414,21 +474,21 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       s2i = him[BD_REG_TAPS - 1];
 #pragma unroll
       for (int j = NTAPS - 1; j > BD_LDS_TAPS; --j) {  // register part, descending: q[j - 1] read before rewritten
-        hre[j - BD_LDS_TAPS] = hre[j - 1 - BD_LDS_TAPS] + c_btaps[j] * ddr;
-        him[j - BD_LDS_TAPS] = him[j - 1 - BD_LDS_TAPS] + c_btaps[j] * ddi;
+        hre[j - BD_LDS_TAPS] = hre[j - 1 - BD_LDS_TAPS] + tp[j] * ddr;
+        him[j - BD_LDS_TAPS] = him[j - 1 - BD_LDS_TAPS] + tp[j] * ddi;
       }
 #if AERO_BD_LDS_TAPS > 0
-      hre[0] = s_qre[BD_LDS_TAPS - 1][col] + c_btaps[BD_LDS_TAPS] * ddr;
-      him[0] = s_qim[BD_LDS_TAPS - 1][col] + c_btaps[BD_LDS_TAPS] * ddi;
+      hre[0] = s_qre[BD_LDS_TAPS - 1][col] + tp[BD_LDS_TAPS] * ddr;
+      him[0] = s_qim[BD_LDS_TAPS - 1][col] + tp[BD_LDS_TAPS] * ddi;
       for (int j = BD_LDS_TAPS - 1; j >= 1; --j) {
-        s_qre[j][col] = s_qre[j - 1][col] + c_btaps[j] * ddr;
-        s_qim[j][col] = s_qim[j - 1][col] + c_btaps[j] * ddi;
+        s_qre[j][col] = s_qre[j - 1][col] + tp[j] * ddr;
+        s_qim[j][col] = s_qim[j - 1][col] + tp[j] * ddi;
       }
-      s_qre[0][col] = 0.0 + c_btaps[0] * ddr;
-      s_qim[0][col] = 0.0 + c_btaps[0] * ddi;
+      s_qre[0][col] = 0.0 + tp[0] * ddr;
+      s_qim[0][col] = 0.0 + tp[0] * ddi;
 #else
-      hre[0] = 0.0 + c_btaps[0] * ddr;
-      him[0] = 0.0 + c_btaps[0] * ddi;
+      hre[0] = 0.0 + tp[0] * ddr;
+      him[0] = 0.0 + tp[0] * ddi;
 #endif
     }
     BSTAMP(4);
@@ -456,7 +516,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       str_i = ni;
       ave_r = ave_r * 0.95 + 0.05 * str_r;
       ave_i = ave_i * 0.95 + 0.05 * str_i;
-      const double spi2 = dly_commit(S.dl[BDL_A1] + c, C, dlp[BDL_A1], pA1, spr);
+      const double spi2 = dly_commit(S.dl[BDL_A1] + c, C, dl_a1, pA1, spr);
       const double2 qv = T.cis[b_cis_index(q_ptr)];
       const double er_r = qv.x * spr - qv.y * (-spi2), er_i = qv.x * (-spi2) + qv.y * spr;
       double st_err = aero_atan2(er_i, er_r);
@@ -493,9 +553,9 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     }
     BSTAMP(5);
     {  // symbol timing (:482-496)
-      const double st_diff = dly_commit(S.dl[BDL_S] + c, C, dlp[BDL_S], pS, abval * abval) - (abval * abval);
-      const double st_d1out = dly_commit(S.dl[BDL_41] + c, C, dlp[BDL_41], p41, st_diff);
-      const double st_d2out = dly_commit(S.dl[BDL_42] + c, C, dlp[BDL_42], p42, st_d1out);
+      const double st_diff = dly_commit(S.dl[BDL_S] + c, C, dl_s, pS, abval * abval) - (abval * abval);
+      const double st_d1out = dly_commit(S.dl[BDL_41] + c, C, dl_41, p41, st_diff);
+      const double st_d2out = dly_commit(S.dl[BDL_42] + c, C, dl_42, p42, st_d1out);
       double st_eta = (st_d2out - st_diff) * st_d1out;
       {  // st_iir_resonator.update(st_eta)
         double y = 0;
@@ -510,7 +570,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         sry1 = y;
         if (cntr > SPS * (128 + 128)) st_eta = y;
       }
-      const double m1r = st_eta, m1i = -dly_commit(S.dl[BDL_8] + c, C, dlp[BDL_8], p8, st_eta);
+      const double m1r = st_eta, m1i = -dly_commit(S.dl[BDL_8] + c, C, dl_8, p8, st_eta);
       const double2 so = T.cis[b_cis_index(so_ptr)];
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
       const double st_angle_error = aero_atan2(oim, ore);
@@ -624,12 +684,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   ds[BD_SO_FREQ * C] = so_freq;
   ds[BD_Q_PTR * C] = q_ptr;
   ds[BD_Q_STEP * C] = q_step;
-  ds[BD_AGC_SUM * C] = agc_sum;
   ds[BD_AGC2_SUM * C] = agc2_sum;
-  ds[BD_MA1_RE * C] = ma1r;
-  ds[BD_MA1_IM * C] = ma1i;
-  ds[BD_MAV1_SUM * C] = mav1_sum;
-  ds[BD_PD_LASTDY * C] = pd_lastdy;
   ds[BD_VOL_GAIN * C] = vol_gain;
   ds[BD_SR_X1 * C] = srx1;
   ds[BD_SR_X2 * C] = srx2;
@@ -649,31 +704,23 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   ds[BD_MSE * C] = mse;
   ds[BD_LASTMSE * C] = lastmse;
   ds[BD_MSEMA_SUM * C] = msema_sum;
-  is[BI_AGC_P * C] = agc_p;
   is[BI_AGC2_P * C] = agc2_p;
-  is[BI_D1_P * C] = d1_p;
-  is[BI_D2_P * C] = d2_p;
-  is[BI_MA1_P * C] = ma1_p;
-  is[BI_MAV1_P * C] = mav1_p;
-#pragma unroll
-  for (int k = 0; k < BDL_COUNT; ++k) is[(BI_DL_P0 + k) * C] = dlp[k];
-  is[BI_PD1_P * C] = pd1_p;
-  is[BI_PD2_P * C] = pd2_p;
-  is[BI_PD3_P * C] = pd3_p;
-  is[BI_PD_CNTDOWN * C] = pd_cntdown;
-  is[BI_PD_MAXPOSCD * C] = pd_maxposcd;
-  is[BI_TRI_PTR * C] = tri_ptr;
+  is[(BI_DL_P0 + BDL_S) * C] = dl_s;
+  is[(BI_DL_P0 + BDL_41) * C] = dl_41;
+  is[(BI_DL_P0 + BDL_42) * C] = dl_42;
+  is[(BI_DL_P0 + BDL_8) * C] = dl_8;
+  is[(BI_DL_P0 + BDL_A1) * C] = dl_a1;
   is[BI_MSEMA_P * C] = msema_p;
   is[BI_STARTSTOP * C] = startstop;
   is[BI_CNTR * C] = cntr;
   is[BI_INSERTPRE * C] = insertpre;
   is[BI_YUI * C] = yui;
-  is[BI_PEND * C] = pend;
   S.hop_n[c] = hop_n;
   ls[BL_NSAMP * C] = n;
   ls[BL_SP * C] = sp;
   ls[BL_SCOMMIT * C] = scommit;
   ls[BL_CHUNK_H * C] = chunk_h;
+  ls[BL_CHK_DONE * C] = chk_done;
   BSTAMP(7);
   }
 #ifdef AERO_X_BSTAMPS
@@ -681,7 +728,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     unsigned long long v[13];
     for (int k = 0; k < 8; k++) v[k] = bst_[k];
     v[8] = bcnt_[0];
-    v[9] = bcnt_[1];
+    v[9] = 0;
     v[10] = bactive_ ? 1 : 0;
     v[11] = 0;
     v[12] = bcnt_[4];
@@ -714,21 +761,23 @@ void burst_read_stamps(unsigned long long *out) {
 }
 
 // --------------------------------------------------------- trident check
-// burstoqpskdemodulator.cpp:343-392 for every channel waiting on it
-__global__ __launch_bounds__(1024) void trident_kernel(BurstState S, BurstTables T, int nch) {
+// burstoqpskdemodulator.cpp:343-392 for every check the front end recorded
+// this pass (S.tjobs); each workgroup takes checks blockIdx.x, + gridDim.x, ...
+__global__ __launch_bounds__(1024) void trident_kernel(BurstState S, BurstTables T) {
   constexpr int L = 14, N = TRI_N, FT = N / 16, PADDED = N + N / 16;
   __shared__ double lds[PADDED];
   __shared__ double2 s_tw[TwLds<L>::LEN];
   __shared__ double red_v[FT / 64];
   __shared__ int red_i[FT / 64];
   __shared__ double2 s_best;
-  const int c = blockIdx.x, t = threadIdx.x;
-  if (c >= nch) return;
-  const int C = S.C;
-  if (S.is[BI_PEND * C + c] != 1) return;  // uniform per workgroup
+  const int t = threadIdx.x;
+  const int njobs = *S.ntjobs;  // uniform
+  if ((int)blockIdx.x >= njobs) return;
   load_tw_lds<L>(s_tw, T.tw16, t, FT);
-  const double *tb = S.tri + (size_t)c * B_TRI;
-  double *absb = S.tri_abs + (size_t)c * N;
+  double *absb = S.tri_abs + (size_t)blockIdx.x * N;
+  for (int job = blockIdx.x; job < njobs; job += gridDim.x) {
+  const int c = S.tjobs[job] & 0xFFFFFF, slot = S.tjobs[job] >> 24;
+  const double *tb = S.tri + ((size_t)c * TRI_SLOTS + slot) * B_TRI;
   // block reduction: larger value, then smaller index
   auto reduce = [&](double v, int idx, double &bv, int &bi) {
     for (int off = 32; off > 0; off >>= 1) {
@@ -835,17 +884,19 @@ __global__ __launch_bounds__(1024) void trident_kernel(BurstState S, BurstTables
   double maxval;
   int maxbin;
   reduce(lv, li, maxval, maxbin);
-  if (t == 0) {
+  if (t == 0) {  // the decision record demod_burst_kernel applies at the check's sample
     const double hzperbin = 48000.0 / 32768.0;
     const int det = (maxval > 500.0) && (fabs((((double)maxbin - (double)minbin)) * hzperbin) < 20.0);
-    S.is[BI_TRI_DET * C + c] = det;
-    S.is[BI_TRI_MINBIN * C + c] = minbin;
-    S.is[BI_TRI_MAXBIN * C + c] = maxbin;
-    S.ds[BD_TRI_MINVAL * C + c] = minval;
-    S.ds[BD_TRI_MAXVAL * C + c] = maxval;
-    S.ds[BD_TRI_BRE * C + c] = s_best.x;
-    S.ds[BD_TRI_BIM * C + c] = s_best.y;
-    S.is[BI_PEND * C + c] = 2;
+    double *r = S.chk + ((size_t)c * TRI_SLOTS + slot) * CHK_REC;
+    r[0] = det;
+    r[1] = minbin;
+    r[2] = maxbin;
+    r[3] = minval;
+    r[4] = maxval;
+    r[5] = s_best.x;
+    r[6] = s_best.y;
+  }
+  __syncthreads();  // the LDS and s_best are the next check's
   }
 }
 
@@ -1025,13 +1076,17 @@ void launch_hilbert(hipStream_t st, const BurstState &S, const BurstTables &T, i
   hipLaunchKernelGGL(hilbert_kernel, dim3(nch), dim3(512), 0, st, S, T, nch);
 }
 
-void launch_demod_burst(hipStream_t st, const BurstState &S, const BurstTables &T, int nch, int max_n, int trace) {
+void launch_front_burst(hipStream_t st, const BurstState &S, const BurstTables &T, int nch) {
+  hipLaunchKernelGGL(front_burst_kernel, dim3((nch + 63) / 64), dim3(64), 0, st, S, T, nch);
+}
+
+void launch_demod_burst(hipStream_t st, const BurstState &S, const BurstTables &T, int nch, int trace) {
   hipLaunchKernelGGL(demod_burst_kernel, dim3((nch + BD_BLOCK - 1) / BD_BLOCK), dim3(BD_BLOCK), 0, st, S, T, nch,
-                     max_n, trace);
+                     trace);
 }
 
 void launch_trident(hipStream_t st, const BurstState &S, const BurstTables &T, int nch) {
-  hipLaunchKernelGGL(trident_kernel, dim3(nch), dim3(1024), 0, st, S, T, nch);
+  hipLaunchKernelGGL(trident_kernel, dim3(std::min(nch * TRI_SLOTS, TRI_GRID)), dim3(1024), 0, st, S, T);
 }
 
 void launch_frame_burst(hipStream_t st, const BurstState &S, int nch) {

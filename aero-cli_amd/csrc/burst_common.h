@@ -36,6 +36,16 @@ constexpr int RT_BLOCK = 6080;   // 64 x 95 R/T block
 constexpr int RT_JOB_OUT = 400;  // int4 header + decoded bits, MSB first
 constexpr int RT_TESTS_PER_PASS = 8;
 constexpr int TRI_N = 16384;     // complex FFT inside FFTrWrapper<double>(32768)
+// The front end (AGC, burst statistic, peak detector, trident buffer) runs
+// ahead of the demodulator proper: d2's output, the demodulator's input
+// val_to_demod, goes to a time-indexed ring (B_D2 - 1 samples of delay plus
+// the run-ahead), and every completed trident buffer to one of TRI_SLOTS
+// slots with the sample the reference checks it at.
+constexpr int TRI_SLOTS = 4;     // trident checks a channel may have recorded and not yet applied
+constexpr int BV_LEN = 16384;    // OQPSK val_to_demod ring (>= B_D2 - 1 + a pass of 12000 samples)
+constexpr int MV_LEN = 32768;    // MSK (M_D2 - 1 = 7680)
+constexpr int CHK_REC = 8;       // doubles per trident decision record
+constexpr int TRI_GRID = 1024;   // trident workgroups (each loops over the pass's checks)
 
 // Delay<T> instances (ring size, fractional delay): delays(1), delayt41/42(T/4),
 // delayt8(T/8), a1(T/2), bt_d1(T, complex), bt_ma_diff(128 T)
@@ -52,20 +62,16 @@ enum BDS : int {
   BD_AVE_RE, BD_AVE_IM, BD_ROT_RE, BD_ROT_IM, BD_STR_RE, BD_STR_IM,
   BD_PTD_RE, BD_PTD_IM, BD_S2L_RE, BD_S2L_IM, BD_ROTF,
   BD_MSE, BD_LASTMSE, BD_MSEMA_SUM,
-  BD_RESUME_VAL,
-  BD_TRI_MINVAL, BD_TRI_MAXVAL, BD_TRI_BRE, BD_TRI_BIM,
   BD_COUNT
 };
 
 // int state fields
 enum BIS : int {
-  BI_AGC_P, BI_AGC2_P, BI_D1_P, BI_D2_P, BI_MA1_P, BI_MAV1_P,
+  BI_AGC_P, BI_AGC2_P, BI_D1_P, BI_MA1_P, BI_MAV1_P,
   BI_DL_P0,  // .. BI_DL_P0 + BDL_COUNT - 1: Delay write pointers
   BI_PD1_P = BI_DL_P0 + BDL_COUNT, BI_PD2_P, BI_PD3_P, BI_PD_CNTDOWN, BI_PD_MAXPOSCD,
   BI_TRI_PTR, BI_MSEMA_P,
   BI_STARTSTOP, BI_CNTR, BI_INSERTPRE, BI_YUI,
-  BI_PEND,  // 0 running, 1 trident check requested, 2 trident decision ready
-  BI_TRI_DET, BI_TRI_MINBIN, BI_TRI_MAXBIN,
   // AeroL burst framing
   BI_RI, BI_MUW, BI_FCNTR, BI_GSL, BI_UWI, BI_UWR, BI_UWI_INV, BI_UWR_INV, BI_DATACD, BI_BLOCKPTR, BI_BURST_ID,
   BI_SKIP_GROUP,
@@ -100,16 +106,12 @@ enum BMDS : int {
   BM_SR_X1, BM_SR_X2, BM_SR_Y1, BM_SR_Y2,
   BM_AVE_RE, BM_AVE_IM, BM_ROT_RE, BM_ROT_IM, BM_STR_RE, BM_STR_IM, BM_ROTF,
   BM_MSE, BM_MSEMA_SUM, BM_DIFF_LAST,
-  BM_RESUME_VAL,
-  BM_TRI_MINVAL, BM_TRI_BRE, BM_TRI_BIM,
   BM_COUNT
 };
 enum BMIS : int {
-  BMI_AGC_P, BMI_AGC2_P, BMI_D1_P, BMI_D2_P, BMI_MA1_P, BMI_MAV1_P, BMI_MADIFF_P, BMI_BTD_P, BMI_A1_P, BMI_D8_P,
+  BMI_AGC_P, BMI_AGC2_P, BMI_D1_P, BMI_MA1_P, BMI_MAV1_P, BMI_MADIFF_P, BMI_BTD_P, BMI_A1_P, BMI_D8_P,
   BMI_DSM_P, BMI_PD1_P, BMI_PD2_P, BMI_PD3_P, BMI_PD_CNTDOWN, BMI_PD_MAXPOSCD,
   BMI_TRI_PTR, BMI_MSEMA_P, BMI_STARTSTOP, BMI_CNTR,
-  BMI_PEND,  // 0 running, 1 trident check requested, 2 trident spectra ready
-  BMI_TRI_MINBIN, BMI_TRI_TOPLO, BMI_TRI_TOPHI,
   // AeroL MSK burst framing
   BMI_MUW, BMI_FCNTR, BMI_UW, BMI_UW_INV, BMI_BLOCKPTR, BMI_BURST_ID, BMI_SKIP_GROUP, BMI_TOTAL,
   BMI_DATACD, BMI_DCD_EDGES,  // AeroL datacd (aerol.cpp:2010-2028) and its changes
@@ -128,6 +130,9 @@ enum BLS : int {
   BL_SCONS,    // soft entries consumed by the framing
   BL_CHUNK_N,  // message starts recorded
   BL_CHUNK_H,  // message starts passed
+  BL_NSAMP_A,  // samples through the front end
+  BL_CHK_N,    // trident checks recorded by the front end
+  BL_CHK_DONE, // trident decisions applied by the demodulator
   BL_COUNT
 };
 
@@ -144,13 +149,17 @@ struct BurstState {
   double2 *hb_rem;  // [C][HB_REM]
   double *agc, *agc2;           // [len][C]
   double2 *d1;                  // [B_D1][C]
-  double *d2;                   // [B_D2][C]
+  double *vring;                // [BV_LEN or MV_LEN][C] val_to_demod of sample n at n & (len - 1)
   double2 *ma1;                 // [B_MA][C]
   double *mav1;                 // [B_MA][C]
   double *dl[BDL_COUNT];        // Delay rings [size][C] (BDL_BT holds double2); MSK: bt_d1 (double2),
                                 // bt_ma_diff, a1, delayt8, delayedsmpl (double2) in slots 0-4
   double *pd1, *pd2, *pd3;      // [len][C]
-  double *tri;                  // [C][B_TRI]
+  double *tri;                  // [C][TRI_SLOTS][B_TRI or M_TRI] completed trident buffers
+  long long *chk_n;             // [C][TRI_SLOTS] sample of each recorded check
+  double *chk;                  // [C][TRI_SLOTS][CHK_REC] its decision (trident kernels)
+  int *tjobs;                   // [C * TRI_SLOTS] this pass's checks: channel | slot << 24
+  int *ntjobs;
   double *msema;                // [C][B_MSEMA]
   long long *chunks;            // [C][CHUNK_RING]
   int16_t *soft;                // [C][B_SOFT_RING]
@@ -160,7 +169,7 @@ struct BurstState {
   int *jobs;                    // [C * RT_TESTS_PER_PASS] int4 (c, blockptr, burst id, 0)
   int *njobs;
   uint8_t *jobout;              // [C * RT_TESTS_PER_PASS][RT_JOB_OUT]
-  double *tri_abs;              // [C][TRI_N] |base| scratch of the trident check
+  double *tri_abs;              // [TRI_GRID][TRI_N] |base| scratch of the trident check
 };
 
 struct BurstTables {

@@ -60,6 +60,31 @@ __device__ __forceinline__ void b_cexp_i(double y, double &c, double &s) {
   }
 }
 
+// PeakDetector's d3.findmaxpos (DSP.h:491-566): the position of the first
+// maximum of a time-major ring of len slots, scanning from the oldest slot p
+// (the next one written); 16 slots are loaded at a time so their round trips
+// overlap instead of one per slot
+__device__ __forceinline__ int pd3_findmaxpos(const double *ring, int C, int p, int len) {
+  double maxval = ring[(size_t)p * C];
+  int maxpos = 0;
+  for (int i0 = 0; i0 < len; i0 += 16) {
+    double v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      int q = p + i0 + k;
+      if (q >= len) q -= len;
+      v[k] = i0 + k < len ? ring[(size_t)q * C] : -1.7976931348623157e308;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (v[k] > maxval) {
+        maxval = v[k];
+        maxpos = i0 + k;
+      }
+  }
+  return maxpos;
+}
+
 // Delay<T>::update (DSP.h:365-384) on a time-major ring with per-pointer weights
 struct DlyRef {
   const double *w, *omw;

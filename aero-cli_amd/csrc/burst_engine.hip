@@ -35,12 +35,14 @@ namespace aero {
 void burst_upload_constants(const double *sr_b, const double *sr_a, const double *taps);
 void launch_hk_spectrum(hipStream_t st, const BurstTables &T, double2 *hk);
 void launch_hilbert(hipStream_t st, const BurstState &S, const BurstTables &T, int nch);
-void launch_demod_burst(hipStream_t st, const BurstState &S, const BurstTables &T, int nch, int max_n, int trace);
+void launch_front_burst(hipStream_t st, const BurstState &S, const BurstTables &T, int nch);
+void launch_demod_burst(hipStream_t st, const BurstState &S, const BurstTables &T, int nch, int trace);
 void launch_trident(hipStream_t st, const BurstState &S, const BurstTables &T, int nch);
 void launch_frame_burst(hipStream_t st, const BurstState &S, int nch);
 void launch_rt_viterbi(hipStream_t st, const BurstState &S, int max_jobs);
 void burst_msk_upload_constants(const double *sr_b, const double *sr_a, const double *taps);
-void launch_demod_bmsk(hipStream_t st, const BurstState &S, const BurstTables &T, int nch, int max_n, int trace);
+void launch_front_bmsk(hipStream_t st, const BurstState &S, const BurstTables &T, int nch);
+void launch_demod_bmsk(hipStream_t st, const BurstState &S, const BurstTables &T, int nch, int trace);
 void launch_trident_bmsk(hipStream_t st, const BurstState &S, const BurstTables &T, int nch);
 void launch_frame_bmsk(hipStream_t st, const BurstState &S, int nch);
 
@@ -57,7 +59,6 @@ namespace {
 
 constexpr long long B_PCM_CAP = 32768;
 constexpr int B_HOP_CAP = 256;
-constexpr int DEMOD_ROUNDS = 8;  // demod / trident alternations per pass
 
 __global__ void b_scatter_kernel(int16_t *ring, int C, long long capm, const int16_t *src, long long n, int c,
                                  long long start) {
@@ -185,7 +186,7 @@ size_t burst_layout(int kind, BurstState &S, BurstTables &T, int C, char *base, 
   S.agc = carve<double>(p, (size_t)B_AGC * C);
   S.agc2 = carve<double>(p, (size_t)(msk ? M_AGC2 : B_AGC2) * C);
   S.d1 = carve<double2>(p, (size_t)(msk ? M_D1 : B_D1) * C);
-  S.d2 = carve<double>(p, (size_t)(msk ? M_D2 : B_D2) * C);
+  S.vring = carve<double>(p, (size_t)(msk ? MV_LEN : BV_LEN) * C);
   S.ma1 = carve<double2>(p, (size_t)(msk ? M_MA : B_MA) * C);
   S.mav1 = carve<double>(p, (size_t)(msk ? M_MA : B_MA) * C);
   if (msk) {  // bt_d1 (complex), bt_ma_diff, a1, delayt8, delayedsmpl (complex)
@@ -198,7 +199,11 @@ size_t burst_layout(int kind, BurstState &S, BurstTables &T, int C, char *base, 
   S.pd1 = carve<double>(p, (size_t)(msk ? M_PD1 : B_PD1) * C);
   S.pd2 = carve<double>(p, (size_t)(msk ? M_PD2 : B_PD2) * C);
   S.pd3 = carve<double>(p, (size_t)(msk ? M_PD3 : B_PD3) * C);
-  S.tri = carve<double>(p, (size_t)(msk ? M_TRI : B_TRI) * C);
+  S.tri = carve<double>(p, (size_t)TRI_SLOTS * (msk ? M_TRI : B_TRI) * C);
+  S.chk_n = carve<long long>(p, (size_t)TRI_SLOTS * C);
+  S.chk = carve<double>(p, (size_t)TRI_SLOTS * CHK_REC * C);
+  S.tjobs = carve<int>(p, (size_t)TRI_SLOTS * C);
+  S.ntjobs = carve<int>(p, 16);
   S.msema = carve<double>(p, (size_t)(msk ? M_MSEMA : B_MSEMA) * C);
   S.chunks = carve<long long>(p, (size_t)CHUNK_RING * C);
   S.soft = carve<int16_t>(p, (size_t)B_SOFT_RING * C);
@@ -208,7 +213,7 @@ size_t burst_layout(int kind, BurstState &S, BurstTables &T, int C, char *base, 
   S.jobs = carve<int>(p, (size_t)4 * RT_TESTS_PER_PASS * C);
   S.njobs = carve<int>(p, 16);
   S.jobout = carve<uint8_t>(p, (size_t)RT_JOB_OUT * RT_TESTS_PER_PASS * C);
-  S.tri_abs = carve<double>(p, (size_t)(msk ? 1 : TRI_N) * C);
+  S.tri_abs = carve<double>(p, (size_t)(msk ? 1 : TRI_N) * TRI_GRID);
   T.cis = carve<double2>(p, WTSIZE);
   T.tw8 = carve<double2>(p, 8192);
   T.twi8 = carve<double2>(p, 8192);
@@ -268,15 +273,19 @@ int run_once(BurstGroup *g, bool trace, bool &progress) {
   const int nch = g->nch;
   progress = false;
   const bool msk = g->kind == BURST_MSK;
+  // Hilbert FIR -> front end (runs ahead, records the trident checks it
+  // completes) -> the checks' decisions -> the demodulator up to the front
+  // end, applying each decision at its sample
   timed(g, "burst_hilbert", [&] { launch_hilbert(g->st, g->S, g->T, nch); });
-  for (int r = 0; r < DEMOD_ROUNDS; r++) {
-    if (msk) {
-      timed(g, "burst_demod", [&] { launch_demod_bmsk(g->st, g->S, g->T, nch, (int)B_PCM_CAP, trace ? 1 : 0); });
-      timed(g, "burst_trident", [&] { launch_trident_bmsk(g->st, g->S, g->T, nch); });
-    } else {
-      timed(g, "burst_demod", [&] { launch_demod_burst(g->st, g->S, g->T, nch, (int)B_PCM_CAP, trace ? 1 : 0); });
-      timed(g, "burst_trident", [&] { launch_trident(g->st, g->S, g->T, nch); });
-    }
+  BCHK(hipMemsetAsync(g->S.ntjobs, 0, sizeof(int), g->st));
+  if (msk) {
+    timed(g, "burst_front", [&] { launch_front_bmsk(g->st, g->S, g->T, nch); });
+    timed(g, "burst_trident", [&] { launch_trident_bmsk(g->st, g->S, g->T, nch); });
+    timed(g, "burst_demod", [&] { launch_demod_bmsk(g->st, g->S, g->T, nch, trace ? 1 : 0); });
+  } else {
+    timed(g, "burst_front", [&] { launch_front_burst(g->st, g->S, g->T, nch); });
+    timed(g, "burst_trident", [&] { launch_trident(g->st, g->S, g->T, nch); });
+    timed(g, "burst_demod", [&] { launch_demod_burst(g->st, g->S, g->T, nch, trace ? 1 : 0); });
   }
   BCHK(hipMemsetAsync(g->S.njobs, 0, sizeof(int), g->st));
   if (msk)

@@ -8,22 +8,25 @@
  *
  *  hilbert_kernel         shared with burst OQPSK (burst.hip): the same
  *                         2048-tap QJHilbertFilter.
- *  demod_bmsk_kernel      the per-sample recurrence, one channel per lane: AGC,
- *                         the d1 / d2 alignment delays, the burst-timing
- *                         statistic and peak detector, trident-buffer fill, and
- *                         while a burst is on (startstop > 0 || mse < 0.6) the
- *                         80-tap matched filter (transposed form, partial
- *                         sums in LDS [tap][lane]), symbol-tone PLL,
- *                         carrier rotation, AGC2, symbol timing and the
- *                         differential soft bits, grouped 12 at a time.  A lane
- *                         stops at a trident check and resumes at the same
- *                         sample once trident_bmsk_kernel has its spectra.
+ *  front_bmsk_kernel      the front end, one channel per lane, ahead of the
+ *                         demodulator (it never reads its state): AGC, the d1 /
+ *                         d2 alignment delays (d2's output to a ring indexed by
+ *                         sample), the burst-timing statistic and peak detector,
+ *                         trident-buffer fill; each completed buffer is kept
+ *                         with the sample the reference checks it at.
  *  trident_bmsk_kernel    FFTrWrapper<double>(32768) of the start-tone window
  *                         (5040 samples) and the 0-1 preamble window (2960): the
  *                         strongest base bin and the strongest top bins either
  *                         side of it (:414-473); one 1024-thread workgroup per
- *                         waiting channel.  The detection decision needs cntr
- *                         and runs in the demod when it resumes.
+ *                         recorded check.  The detection decision needs cntr
+ *                         and runs in the demodulator.
+ *  demod_bmsk_kernel      the demodulator, one channel per lane: at each
+ *                         check's sample the trident decision, and while a
+ *                         burst is on (startstop > 0 || mse < 0.6) the 80-tap
+ *                         matched filter (transposed form, partial sums of taps
+ *                         0-39 in LDS [tap][lane], 40-79 in registers),
+ *                         symbol-tone PLL, carrier rotation, AGC2, symbol timing
+ *                         and the differential soft bits, grouped 12 at a time.
  *  frame_bmsk_kernel      AeroL MSK burst framing: phase-invariant UW (4 bit
  *                         errors) accepted within 250 bits of the start-of-burst
  *                         marker, dummy header, R/T block fill, Viterbi jobs at
@@ -35,6 +38,9 @@
  * operation order, GCC complex products, aero_math.h for libm.
  */
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
 
 #include "aero_math.h"
 #include "burst_common.h"
@@ -77,8 +83,161 @@ __device__ __forceinline__ double m_diff_soft(double &last, double soft) {  // D
 constexpr int BM_BLOCK = 64;
 constexpr int BM_LDS_TAPS = 40, BM_REG_TAPS = M_NT - BM_LDS_TAPS;
 
-__global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, BurstTables T, int nch, int max_n,
-                                                              int trace) {
+// ------------------------------------------------------------- front end
+// The part of BurstMskDemodulator::writeData before the demodulator proper
+// (decode/burstmskdemodulator.cpp:356-413): AGC, d1 / d2, the burst-timing
+// statistic, the peak detector and the trident buffer.  It never reads the
+// demodulator's state and runs ahead of it (as burst.hip's
+// front_burst_kernel): val_to_demod to a ring indexed by sample, completed
+// trident buffers to slots with the sample the reference checks them at.
+__global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTables T, int nch) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= nch) return;
+  const int C = S.C;
+  double *ds = S.ds + c;
+  int *is = S.is + c;
+  long long *ls = S.ls + c;
+  const long long n0 = ls[BL_NSAMP_A * C];
+  long long end = ls[BL_AVAIL * C];
+  const long long lim = ls[BL_NSAMP * C] + (MV_LEN - (M_D2 - 1));  // what the demodulator has not read
+  if (end > lim) end = lim;
+  long long chk_n = ls[BL_CHK_N * C];
+  const long long chk_done = ls[BL_CHK_DONE * C];
+  if (n0 >= end) return;
+  double agc_sum = ds[BM_AGC_SUM * C];
+  double ma1r = ds[BM_MA1_RE * C], ma1i = ds[BM_MA1_IM * C], mav1_sum = ds[BM_MAV1_SUM * C];
+  double pd_lastdy = ds[BM_PD_LASTDY * C];
+  int agc_p = is[BMI_AGC_P * C], d1_p = is[BMI_D1_P * C];
+  int ma1_p = is[BMI_MA1_P * C], mav1_p = is[BMI_MAV1_P * C], madiff_p = is[BMI_MADIFF_P * C];
+  int btd_p = is[BMI_BTD_P * C];
+  int pd1_p = is[BMI_PD1_P * C], pd2_p = is[BMI_PD2_P * C], pd3_p = is[BMI_PD3_P * C];
+  int pd_cntdown = is[BMI_PD_CNTDOWN * C], pd_maxposcd = is[BMI_PD_MAXPOSCD * C];
+  int tri_ptr = is[BMI_TRI_PTR * C];
+  double *tri = S.tri + ((size_t)c * TRI_SLOTS + (chk_n & (TRI_SLOTS - 1))) * M_TRI;
+  double2 *btd = reinterpret_cast<double2 *>(S.dl[0]) + c;
+  double *madiff = S.dl[1] + c;
+  long long n = n0;
+  while (n < end) {
+    if (chk_n - chk_done >= TRI_SLOTS) break;  // every slot holds a check not yet applied
+    // every ring slot this sample reads, loaded before any of its stores so
+    // the round trips overlap; no slot read here is the one written this
+    // sample (rings hold > 2 slots)
+    const int d1r = d1_p + 1 == M_D1 ? 0 : d1_p + 1;
+    const int bto = btd_p + 1 == M_BTD ? 0 : btd_p + 1, btn = bto + 1 == M_BTD ? 0 : bto + 1;
+    const int mdo = madiff_p + 1 == M_MADIFF ? 0 : madiff_p + 1, mdn = mdo + 1 == M_MADIFF ? 0 : mdo + 1;
+    const int p1r = pd1_p + 1 == M_PD1 ? 0 : pd1_p + 1, p2r = pd2_p + 1 == M_PD2 ? 0 : pd2_p + 1;
+    const double2 a = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
+    const double agc_old = S.agc[(size_t)agc_p * C + c];
+    const double2 cvd = S.d1[(size_t)d1r * C + c];  // d1.update_dont_touch(cval)
+    const double2 bt_old = btd[(size_t)bto * C], bt_new = btd[(size_t)btn * C];
+    const double2 ma_old = S.ma1[(size_t)ma1_p * C + c];
+    const double mv_old = S.mav1[(size_t)mav1_p * C + c];
+    const double md_old = madiff[(size_t)mdo * C], md_new = madiff[(size_t)mdn * C];
+    const double pd1_old = S.pd1[(size_t)p1r * C + c], pd2_old = S.pd2[(size_t)p2r * C + c];
+    double cr = a.x, ci = a.y;
+    {  // agc->Update(abs(cval)); cval *= agc->AGCVal (:366-368)
+      const double av = aero_hypot(cr, ci);
+      agc_sum = agc_sum - agc_old;
+      agc_sum = agc_sum + fabs(av);
+      S.agc[(size_t)agc_p * C + c] = fabs(av);
+      agc_p = agc_p + 1 == B_AGC ? 0 : agc_p + 1;
+      double g = 1.414213562 / fmax(agc_sum / ((double)B_AGC), 0.000001);
+      g = fmax(g, 0.000001);
+      cr *= g;
+      ci *= g;
+    }
+    S.d1[(size_t)d1_p * C + c] = make_double2(cr, ci);
+    d1_p = d1r;
+    // d2.update_dont_touch(real(cval_d)): the demodulator reads it back M_D2 - 1 samples later
+    S.vring[(size_t)(n & (MV_LEN - 1)) * C + c] = cvd.x;
+    double fastarm;
+    {  // burst-timing statistic (:376-385); bt_d1 = Delay(SPS): weights 0 / 1 (dly_int2)
+      btd[(size_t)btd_p * C] = make_double2(cr, ci);
+      btd_p = bto;
+      const double2 bd = make_double2(0.0 * bt_new.x + (1.0 - 0.0) * bt_old.x,
+                                      0.0 * bt_new.y + (1.0 - 0.0) * bt_old.y);
+      const double pr = cr * bd.x - ci * (-bd.y), pi = cr * (-bd.y) + ci * bd.x;  // cval * conj(bd)
+      ma1r = ma1r - ma_old.x;
+      ma1i = ma1i - ma_old.y;
+      ma1r = ma1r + pr;
+      ma1i = ma1i + pi;
+      S.ma1[(size_t)ma1_p * C + c] = make_double2(pr, pi);
+      ma1_p = ma1_p + 1 == M_MA ? 0 : ma1_p + 1;
+      fastarm = aero_hypot(ma1r / ((double)M_MA), ma1i / ((double)M_MA));
+      mav1_sum = mav1_sum - mv_old;
+      mav1_sum = mav1_sum + (fastarm);
+      S.mav1[(size_t)mav1_p * C + c] = fastarm;
+      mav1_p = mav1_p + 1 == M_MA ? 0 : mav1_p + 1;
+      fastarm = mav1_sum / ((double)M_MA);
+      madiff[(size_t)madiff_p * C] = fastarm;  // bt_ma_diff.update(fastarm), whole-sample delay
+      madiff_p = mdo;
+      fastarm -= (0.0 * md_new + (1.0 - 0.0) * md_old);
+      if (fastarm < 0) fastarm = 0;
+    }
+    double bt = fastarm * fastarm;
+    if (bt > 500) bt = 500;
+    {  // PeakDetector::update (DSP.h:491-566), setSettings(2520, 0.1)
+      double val = bt;
+      S.pd3[(size_t)pd3_p * C + c] = val;
+      pd3_p = pd3_p + 1 == M_PD3 ? 0 : pd3_p + 1;
+      S.pd1[(size_t)pd1_p * C + c] = val;
+      pd1_p = p1r;
+      const double dy = val - pd1_old;
+      S.pd2[(size_t)pd2_p * C + c] = val;
+      pd2_p = p2r;
+      val = pd2_old;  // d2.update(val)
+      if ((!pd_cntdown) && (val > 0.1) && ((pd_lastdy >= 0 && dy < 0))) {
+        pd_cntdown = M_PD_MAXCD;
+        pd_maxposcd = pd3_findmaxpos(S.pd3 + c, C, pd3_p, M_PD3);
+      }
+      if (pd_cntdown > 0) pd_cntdown--;
+      pd_lastdy = dy;
+      bool hit = false;
+      if (!pd_maxposcd) {
+        pd_maxposcd--;
+        hit = true;
+      } else if (pd_maxposcd > 0) {
+        pd_maxposcd--;
+      }
+      if (hit) tri_ptr = 0;
+    }
+    if (tri_ptr < M_TRI) {
+      tri[tri_ptr] = cvd.x;
+      tri_ptr++;
+    } else if (tri_ptr == M_TRI) {
+      // the reference computes the trident spectra at this sample
+      // (:414-473); the demodulator takes the decision before the rest of it
+      tri_ptr++;
+      const int slot = (int)(chk_n & (TRI_SLOTS - 1));
+      S.chk_n[(size_t)c * TRI_SLOTS + slot] = n;
+      S.tjobs[atomicAdd(S.ntjobs, 1)] = c | (slot << 24);
+      chk_n++;
+      tri = S.tri + ((size_t)c * TRI_SLOTS + (chk_n & (TRI_SLOTS - 1))) * M_TRI;
+    }
+    n++;
+  }
+  ds[BM_AGC_SUM * C] = agc_sum;
+  ds[BM_MA1_RE * C] = ma1r;
+  ds[BM_MA1_IM * C] = ma1i;
+  ds[BM_MAV1_SUM * C] = mav1_sum;
+  ds[BM_PD_LASTDY * C] = pd_lastdy;
+  is[BMI_AGC_P * C] = agc_p;
+  is[BMI_D1_P * C] = d1_p;
+  is[BMI_MA1_P * C] = ma1_p;
+  is[BMI_MAV1_P * C] = mav1_p;
+  is[BMI_MADIFF_P * C] = madiff_p;
+  is[BMI_BTD_P * C] = btd_p;
+  is[BMI_PD1_P * C] = pd1_p;
+  is[BMI_PD2_P * C] = pd2_p;
+  is[BMI_PD3_P * C] = pd3_p;
+  is[BMI_PD_CNTDOWN * C] = pd_cntdown;
+  is[BMI_PD_MAXPOSCD * C] = pd_maxposcd;
+  is[BMI_TRI_PTR * C] = tri_ptr;
+  ls[BL_NSAMP_A * C] = n;
+  ls[BL_CHK_N * C] = chk_n;
+}
+
+__global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, BurstTables T, int nch, int trace) {
   __shared__ double s_qre[BM_LDS_TAPS][BM_BLOCK];
   __shared__ double s_qim[BM_LDS_TAPS][BM_BLOCK];
   const int c = blockIdx.x * BM_BLOCK + threadIdx.x, col = threadIdx.x;
@@ -87,33 +246,28 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
   double *ds = S.ds + c;
   int *is = S.is + c;
   long long *ls = S.ls + c;
-  int pend = is[BMI_PEND * C];
-  if (pend == 1) return;  // trident spectra outstanding
   const long long n0 = ls[BL_NSAMP * C];
-  long long end = ls[BL_AVAIL * C];
-  if (end - n0 > max_n) end = n0 + max_n;
-  if (n0 >= end && pend != 2) return;
+  const long long end = ls[BL_NSAMP_A * C];  // the front end's progress
+  if (n0 >= end) return;
 
   double m2_ptr = ds[BM_M2_PTR * C], m2_step = ds[BM_M2_STEP * C], m2_freq = ds[BM_M2_FREQ * C];
   double so_ptr = ds[BM_SO_PTR * C], so_last = ds[BM_SO_LAST * C], so_step = ds[BM_SO_STEP * C];
   double sh_ptr = ds[BM_SH_PTR * C], sh_step = ds[BM_SH_STEP * C];
-  double agc_sum = ds[BM_AGC_SUM * C], agc2_sum = ds[BM_AGC2_SUM * C];
-  double ma1r = ds[BM_MA1_RE * C], ma1i = ds[BM_MA1_IM * C], mav1_sum = ds[BM_MAV1_SUM * C];
-  double pd_lastdy = ds[BM_PD_LASTDY * C], vol_gain = ds[BM_VOL_GAIN * C];
+  double agc2_sum = ds[BM_AGC2_SUM * C], vol_gain = ds[BM_VOL_GAIN * C];
   double srx1 = ds[BM_SR_X1 * C], srx2 = ds[BM_SR_X2 * C], sry1 = ds[BM_SR_Y1 * C], sry2 = ds[BM_SR_Y2 * C];
   double ave_r = ds[BM_AVE_RE * C], ave_i = ds[BM_AVE_IM * C], rot_r = ds[BM_ROT_RE * C], rot_i = ds[BM_ROT_IM * C];
   double str_r = ds[BM_STR_RE * C], str_i = ds[BM_STR_IM * C], rotf = ds[BM_ROTF * C];
   double mse = ds[BM_MSE * C], msema_sum = ds[BM_MSEMA_SUM * C], diff_last = ds[BM_DIFF_LAST * C];
-  int agc_p = is[BMI_AGC_P * C], agc2_p = is[BMI_AGC2_P * C], d1_p = is[BMI_D1_P * C], d2_p = is[BMI_D2_P * C];
-  int ma1_p = is[BMI_MA1_P * C], mav1_p = is[BMI_MAV1_P * C], madiff_p = is[BMI_MADIFF_P * C];
-  int btd_p = is[BMI_BTD_P * C], a1_p = is[BMI_A1_P * C], d8_p = is[BMI_D8_P * C], dsm_p = is[BMI_DSM_P * C];
-  int pd1_p = is[BMI_PD1_P * C], pd2_p = is[BMI_PD2_P * C], pd3_p = is[BMI_PD3_P * C];
-  int pd_cntdown = is[BMI_PD_CNTDOWN * C], pd_maxposcd = is[BMI_PD_MAXPOSCD * C];
-  int tri_ptr = is[BMI_TRI_PTR * C], msema_p = is[BMI_MSEMA_P * C];
+  int agc2_p = is[BMI_AGC2_P * C];
+  int a1_p = is[BMI_A1_P * C], d8_p = is[BMI_D8_P * C], dsm_p = is[BMI_DSM_P * C];
+  int msema_p = is[BMI_MSEMA_P * C];
   int startstop = is[BMI_STARTSTOP * C], cntr = is[BMI_CNTR * C];
   int hop_n = S.hop_n[c];
   long long sp = ls[BL_SP * C], scommit = ls[BL_SCOMMIT * C];
   const long long scons = ls[BL_SCONS * C];
+  long long chk_done = ls[BL_CHK_DONE * C];
+  const long long chk_n = ls[BL_CHK_N * C];
+  long long next_chk = chk_done < chk_n ? S.chk_n[(size_t)c * TRI_SLOTS + (chk_done & (TRI_SLOTS - 1))] : LLONG_MAX;
 #pragma unroll 1
   for (int j = 0; j < BM_LDS_TAPS; ++j) {
     s_qre[j][col] = S.fir[(size_t)j * C + c];
@@ -126,128 +280,21 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
     him[j] = S.fir[(size_t)(M_NT + BM_LDS_TAPS + j) * C + c];
   }
   int16_t *soft = S.soft + (size_t)c * B_SOFT_RING;
-  double2 *btd = reinterpret_cast<double2 *>(S.dl[0]) + c;
-  double *madiff = S.dl[1] + c, *a1 = S.dl[2] + c, *d8 = S.dl[3] + c;
+  double *a1 = S.dl[2] + c, *d8 = S.dl[3] + c;
   double2 *dsm = reinterpret_cast<double2 *>(S.dl[4]) + c;
   const double PT = M_EE * WTSIZE;  // IfHavePassedPoint(ee)
 
   long long n = n0;
-  bool resume = pend == 2;
-  while (resume || n < end) {
-    double vtd;  // val_to_demod
-    if (!resume) {
-      if (sp - scons > B_SOFT_RING - 64) break;  // soft ring full: framing frees it next
-      // every ring slot this sample reads, loaded before any of its stores so
-      // the round trips overlap (the compiler cannot hoist a load above a
-      // store to another ring it cannot prove distinct); no slot read here is
-      // the one written this sample (rings hold > 2 slots)
-      const int d1r = d1_p + 1 == M_D1 ? 0 : d1_p + 1, d2r = d2_p + 1 == M_D2 ? 0 : d2_p + 1;
-      const int bto = btd_p + 1 == M_BTD ? 0 : btd_p + 1, btn = bto + 1 == M_BTD ? 0 : bto + 1;
-      const int mdo = madiff_p + 1 == M_MADIFF ? 0 : madiff_p + 1, mdn = mdo + 1 == M_MADIFF ? 0 : mdo + 1;
-      const int p1r = pd1_p + 1 == M_PD1 ? 0 : pd1_p + 1, p2r = pd2_p + 1 == M_PD2 ? 0 : pd2_p + 1;
-      const double2 a = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
-      const double agc_old = S.agc[(size_t)agc_p * C + c];
-      const double2 cvd = S.d1[(size_t)d1r * C + c];  // d1.update_dont_touch(cval)
-      vtd = S.d2[(size_t)d2r * C + c];                 // d2.update_dont_touch(real(cval_d))
-      const double2 bt_old = btd[(size_t)bto * C], bt_new = btd[(size_t)btn * C];
-      const double2 ma_old = S.ma1[(size_t)ma1_p * C + c];
-      const double mv_old = S.mav1[(size_t)mav1_p * C + c];
-      const double md_old = madiff[(size_t)mdo * C], md_new = madiff[(size_t)mdn * C];
-      const double pd1_old = S.pd1[(size_t)p1r * C + c], pd2_old = S.pd2[(size_t)p2r * C + c];
-      double cr = a.x, ci = a.y;
-      {  // agc->Update(abs(cval)); cval *= agc->AGCVal (:366-368)
-        const double av = aero_hypot(cr, ci);
-        agc_sum = agc_sum - agc_old;
-        agc_sum = agc_sum + fabs(av);
-        S.agc[(size_t)agc_p * C + c] = fabs(av);
-        agc_p = agc_p + 1 == B_AGC ? 0 : agc_p + 1;
-        double g = 1.414213562 / fmax(agc_sum / ((double)B_AGC), 0.000001);
-        g = fmax(g, 0.000001);
-        cr *= g;
-        ci *= g;
-      }
-      S.d1[(size_t)d1_p * C + c] = make_double2(cr, ci);
-      d1_p = d1r;
-      S.d2[(size_t)d2_p * C + c] = cvd.x;
-      d2_p = d2r;
-      double fastarm;
-      {  // burst-timing statistic (:376-385); bt_d1 = Delay(SPS): weights 0 / 1 (dly_int2)
-        btd[(size_t)btd_p * C] = make_double2(cr, ci);
-        btd_p = bto;
-        const double2 bd = make_double2(0.0 * bt_new.x + (1.0 - 0.0) * bt_old.x,
-                                        0.0 * bt_new.y + (1.0 - 0.0) * bt_old.y);
-        const double pr = cr * bd.x - ci * (-bd.y), pi = cr * (-bd.y) + ci * bd.x;  // cval * conj(bd)
-        ma1r = ma1r - ma_old.x;
-        ma1i = ma1i - ma_old.y;
-        ma1r = ma1r + pr;
-        ma1i = ma1i + pi;
-        S.ma1[(size_t)ma1_p * C + c] = make_double2(pr, pi);
-        ma1_p = ma1_p + 1 == M_MA ? 0 : ma1_p + 1;
-        fastarm = aero_hypot(ma1r / ((double)M_MA), ma1i / ((double)M_MA));
-        mav1_sum = mav1_sum - mv_old;
-        mav1_sum = mav1_sum + (fastarm);
-        S.mav1[(size_t)mav1_p * C + c] = fastarm;
-        mav1_p = mav1_p + 1 == M_MA ? 0 : mav1_p + 1;
-        fastarm = mav1_sum / ((double)M_MA);
-        madiff[(size_t)madiff_p * C] = fastarm;  // bt_ma_diff.update(fastarm), whole-sample delay
-        madiff_p = mdo;
-        fastarm -= (0.0 * md_new + (1.0 - 0.0) * md_old);
-        if (fastarm < 0) fastarm = 0;
-      }
-      double bt = fastarm * fastarm;
-      if (bt > 500) bt = 500;
-      {  // PeakDetector::update (DSP.h:491-566), setSettings(2520, 0.1)
-        double val = bt;
-        double *r3 = S.pd3 + (size_t)pd3_p * C + c;
-        *r3 = val;
-        pd3_p = pd3_p + 1 == M_PD3 ? 0 : pd3_p + 1;
-        S.pd1[(size_t)pd1_p * C + c] = val;
-        pd1_p = p1r;
-        const double dy = val - pd1_old;
-        S.pd2[(size_t)pd2_p * C + c] = val;
-        pd2_p = p2r;
-        val = pd2_old;  // d2.update(val)
-        if ((!pd_cntdown) && (val > 0.1) && ((pd_lastdy >= 0 && dy < 0))) {
-          pd_cntdown = M_PD_MAXCD;
-          // d3.findmaxpos: first maximum, scanning from the oldest slot
-          int qq = pd3_p, maxpos = 0;
-          double maxval = S.pd3[(size_t)qq * C + c];
-          for (int i = 0; i < M_PD3; i++) {
-            const double v = S.pd3[(size_t)qq * C + c];
-            if (v > maxval) {
-              maxval = v;
-              maxpos = i;
-            }
-            qq = qq + 1 == M_PD3 ? 0 : qq + 1;
-          }
-          pd_maxposcd = maxpos;
-        }
-        if (pd_cntdown > 0) pd_cntdown--;
-        pd_lastdy = dy;
-        bool hit = false;
-        if (!pd_maxposcd) {
-          pd_maxposcd--;
-          hit = true;
-        } else if (pd_maxposcd > 0) {
-          pd_maxposcd--;
-        }
-        if (hit) tri_ptr = 0;
-      }
-      if (tri_ptr < M_TRI) {
-        S.tri[(size_t)c * M_TRI + tri_ptr] = cvd.x;
-        tri_ptr++;
-      } else if (tri_ptr == M_TRI) {
-        tri_ptr++;
-        ds[BM_RESUME_VAL * C] = vtd;
-        pend = 1;  // trident_bmsk_kernel computes the spectra, this sample resumes after it
-        break;
-      }
-    } else {
-      vtd = ds[BM_RESUME_VAL * C];
-      // trident decision (burstmskdemodulator.cpp:475-522); dcd is false
-      const double minval = ds[BM_TRI_MINVAL * C];
-      const int minvalbin = is[BMI_TRI_MINBIN * C], maxtoppos = is[BMI_TRI_TOPLO * C];
-      const int maxtopposhigh = is[BMI_TRI_TOPHI * C];
+  while (n < end) {
+    if (sp - scons > B_SOFT_RING - 64) break;  // soft ring full: framing frees it next
+    // val_to_demod = d2.update_dont_touch(...): the front end's value M_D2 - 1 samples ago (zeros before)
+    const double vtd = n >= M_D2 - 1 ? S.vring[(size_t)((n - (M_D2 - 1)) & (MV_LEN - 1)) * C + c] : 0.0;
+    if (n == next_chk) {
+      // trident decision (burstmskdemodulator.cpp:475-522) from trident_bmsk_kernel's spectra; dcd is false
+      const double *r = S.chk + ((size_t)c * TRI_SLOTS + (chk_done & (TRI_SLOTS - 1))) * CHK_REC;
+      const double minval = r[0];
+      const int minvalbin = (int)r[1], maxtoppos = (int)r[2];
+      const int maxtopposhigh = (int)r[3];
       const double hzperbin = 48000.0 / 32768.0;
       constexpr int peakspacingbins = 410;  // qRound((0.5 * fb) / hzperbin)
       const int distfrompeak = abs(maxtoppos - minvalbin);
@@ -255,7 +302,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
                        !(cntr > 0 && cntr < (500 * MSPS));
       if (det) {
         vol_gain = 1.4142 * (500.0 / (minval / 3));
-        const double carrierphase = aero_atan2(ds[BM_TRI_BIM * C], ds[BM_TRI_BRE * C]) - (M_PI / 4.0);
+        const double carrierphase = aero_atan2(r[5], r[4]) - (M_PI / 4.0);
         b_set_phase_deg(m2_ptr, (180.0 / M_PI) * carrierphase);
         // mixer2.SetFreq, then CenterFreqChangedSlot (:299-317) puts mixer2 on
         // mixer_center's clamped frequency
@@ -294,8 +341,8 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         h[5] = (double)minvalbin + 65536.0 * (double)maxtoppos;
       }
       hop_n++;
-      resume = false;
-      pend = 0;
+      chk_done++;
+      next_chk = chk_done < chk_n ? S.chk_n[(size_t)c * TRI_SLOTS + (chk_done & (TRI_SLOTS - 1))] : LLONG_MAX;
     }
     // sample counting and the signal-status timeout (:525-545)
     if (startstop > 0) {
@@ -501,12 +548,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
   ds[BM_SO_PTR * C] = so_ptr;
   ds[BM_SO_LAST * C] = so_last;
   ds[BM_SH_PTR * C] = sh_ptr;
-  ds[BM_AGC_SUM * C] = agc_sum;
   ds[BM_AGC2_SUM * C] = agc2_sum;
-  ds[BM_MA1_RE * C] = ma1r;
-  ds[BM_MA1_IM * C] = ma1i;
-  ds[BM_MAV1_SUM * C] = mav1_sum;
-  ds[BM_PD_LASTDY * C] = pd_lastdy;
   ds[BM_VOL_GAIN * C] = vol_gain;
   ds[BM_SR_X1 * C] = srx1;
   ds[BM_SR_X2 * C] = srx2;
@@ -522,31 +564,18 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
   ds[BM_MSE * C] = mse;
   ds[BM_MSEMA_SUM * C] = msema_sum;
   ds[BM_DIFF_LAST * C] = diff_last;
-  is[BMI_AGC_P * C] = agc_p;
   is[BMI_AGC2_P * C] = agc2_p;
-  is[BMI_D1_P * C] = d1_p;
-  is[BMI_D2_P * C] = d2_p;
-  is[BMI_MA1_P * C] = ma1_p;
-  is[BMI_MAV1_P * C] = mav1_p;
-  is[BMI_MADIFF_P * C] = madiff_p;
-  is[BMI_BTD_P * C] = btd_p;
   is[BMI_A1_P * C] = a1_p;
   is[BMI_D8_P * C] = d8_p;
   is[BMI_DSM_P * C] = dsm_p;
-  is[BMI_PD1_P * C] = pd1_p;
-  is[BMI_PD2_P * C] = pd2_p;
-  is[BMI_PD3_P * C] = pd3_p;
-  is[BMI_PD_CNTDOWN * C] = pd_cntdown;
-  is[BMI_PD_MAXPOSCD * C] = pd_maxposcd;
-  is[BMI_TRI_PTR * C] = tri_ptr;
   is[BMI_MSEMA_P * C] = msema_p;
   is[BMI_STARTSTOP * C] = startstop;
   is[BMI_CNTR * C] = cntr;
-  is[BMI_PEND * C] = pend;
   S.hop_n[c] = hop_n;
   ls[BL_NSAMP * C] = n;
   ls[BL_SP * C] = sp;
   ls[BL_SCOMMIT * C] = scommit;
+  ls[BL_CHK_DONE * C] = chk_done;
 }
 
 // --------------------------------------------------------- trident check
@@ -554,19 +583,20 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
 // FFTr of tridentbuffer[0, 5040), top = FFTr of [5040, 8000); the first
 // strict maximum of |base| over bins [0, 16384), and of |top| over bins
 // (50, minvalbin - 205) and (minvalbin + 205, 16384), each starting from 0.
-__global__ __launch_bounds__(1024) void trident_bmsk_kernel(BurstState S, BurstTables T, int nch) {
+__global__ __launch_bounds__(1024) void trident_bmsk_kernel(BurstState S, BurstTables T) {
   constexpr int L = 14, N = TRI_N, FT = N / 16, PADDED = N + N / 16;
   __shared__ double lds[PADDED];
   __shared__ double2 s_tw[TwLds<L>::LEN];
   __shared__ double red_v[FT / 64];
   __shared__ int red_i[FT / 64];
   __shared__ double2 s_best;
-  const int c = blockIdx.x, t = threadIdx.x;
-  if (c >= nch) return;
-  const int C = S.C;
-  if (S.is[BMI_PEND * C + c] != 1) return;  // uniform per workgroup
+  const int t = threadIdx.x;
+  const int njobs = *S.ntjobs;  // uniform
+  if ((int)blockIdx.x >= njobs) return;
   load_tw_lds<L>(s_tw, T.tw16, t, FT);
-  const double *tb = S.tri + (size_t)c * M_TRI;
+  for (int job = blockIdx.x; job < njobs; job += gridDim.x) {
+  const int c = S.tjobs[job] & 0xFFFFFF, slot = S.tjobs[job] >> 24;
+  const double *tb = S.tri + ((size_t)c * TRI_SLOTS + slot) * M_TRI;
   // block reduction of (value, bin) candidates: larger value, then smaller bin
   auto reduce = [&](double v, int idx, double &bv, int &bi) {
     for (int off = 32; off > 0; off >>= 1) {
@@ -668,14 +698,16 @@ __global__ __launch_bounds__(1024) void trident_bmsk_kernel(BurstState S, BurstT
       tophi = bi == NONE ? 0 : bi;
     }
   }
-  if (t == 0) {
-    S.ds[BM_TRI_MINVAL * C + c] = minval;
-    S.ds[BM_TRI_BRE * C + c] = s_best.x;
-    S.ds[BM_TRI_BIM * C + c] = s_best.y;
-    S.is[BMI_TRI_MINBIN * C + c] = minbin;
-    S.is[BMI_TRI_TOPLO * C + c] = toplo;
-    S.is[BMI_TRI_TOPHI * C + c] = tophi;
-    S.is[BMI_PEND * C + c] = 2;
+  if (t == 0) {  // the record demod_bmsk_kernel decides on at the check's sample
+    double *r = S.chk + ((size_t)c * TRI_SLOTS + slot) * CHK_REC;
+    r[0] = minval;
+    r[1] = minbin;
+    r[2] = toplo;
+    r[3] = tophi;
+    r[4] = s_best.x;
+    r[5] = s_best.y;
+  }
+  __syncthreads();  // the LDS and s_best are the next check's
   }
 }
 
@@ -787,13 +819,17 @@ void burst_msk_upload_constants(const double *sr_b, const double *sr_a, const do
   hipMemcpyToSymbol(HIP_SYMBOL(c_mtaps), taps, sizeof(double) * M_NT);
 }
 
-void launch_demod_bmsk(hipStream_t st, const BurstState &S, const BurstTables &T, int nch, int max_n, int trace) {
+void launch_front_bmsk(hipStream_t st, const BurstState &S, const BurstTables &T, int nch) {
+  hipLaunchKernelGGL(front_bmsk_kernel, dim3((nch + 63) / 64), dim3(64), 0, st, S, T, nch);
+}
+
+void launch_demod_bmsk(hipStream_t st, const BurstState &S, const BurstTables &T, int nch, int trace) {
   hipLaunchKernelGGL(demod_bmsk_kernel, dim3((nch + BM_BLOCK - 1) / BM_BLOCK), dim3(BM_BLOCK), 0, st, S, T, nch,
-                     max_n, trace);
+                     trace);
 }
 
 void launch_trident_bmsk(hipStream_t st, const BurstState &S, const BurstTables &T, int nch) {
-  hipLaunchKernelGGL(trident_bmsk_kernel, dim3(nch), dim3(1024), 0, st, S, T, nch);
+  hipLaunchKernelGGL(trident_bmsk_kernel, dim3(std::min(nch * TRI_SLOTS, TRI_GRID)), dim3(1024), 0, st, S, T);
 }
 
 void launch_frame_bmsk(hipStream_t st, const BurstState &S, int nch) {

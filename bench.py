@@ -48,7 +48,7 @@ MODES = {
                        timing='burst_demod', burst=True, preroll=4,
                        metric='Msamples/s demod+Viterbi, 10500bps burst OQPSK (C4); R/T packets bit-exact vs ref',
                        cpu_seconds=240.0, config='C4', flops=1300.0,
-                       kernels={'hilbert': 'hilbert_kernel', 'demod': 'demod_burst_kernel',
+                       kernels={'hilbert': 'hilbert_kernel', 'front': 'front_burst_kernel', 'demod': 'demod_burst_kernel',
                                 'trident': 'trident_kernel', 'frame': 'frame_burst_kernel',
                                 'viterbi': 'rt_viterbi_kernel'}),
     # burst MSK (aero-decode -b 1200 --burst: one fb = 1200 demodulator at 48 kHz), the C4
@@ -58,7 +58,7 @@ MODES = {
                          timing='burst_demod', burst=True, preroll=4,
                          metric='Msamples/s demod+Viterbi, 1200bps burst MSK; R/T packets bit-exact vs ref',
                          cpu_seconds=240.0, config='f1 (burst MSK 1200)', flops=900.0,
-                         kernels={'hilbert': 'hilbert_kernel', 'demod': 'demod_bmsk_kernel',
+                         kernels={'hilbert': 'hilbert_kernel', 'front': 'front_bmsk_kernel', 'demod': 'demod_bmsk_kernel',
                                   'trident': 'trident_bmsk_kernel', 'frame': 'frame_bmsk_kernel',
                                   'viterbi': 'rt_viterbi_kernel'}),
     # 2 B int16 in + 0.025 B soft bits out (fb stays 600 at 24 kHz, decode/decode.cpp:142-150)
@@ -707,7 +707,7 @@ def main():
     stats = {k: eng.stat(k) - v for k, v in st0.items()}
     tag = M['timing'][:-len('demod')]
     if burst:  # the burst path's kernels: Hilbert fast FIR, demod, trident FFT check, framing, R/T Viterbi
-        kt = {k: eng.timing('burst_' + k) for k in ('hilbert', 'demod', 'trident', 'frame', 'viterbi')}
+        kt = {k: eng.timing('burst_' + k) for k in ('hilbert', 'front', 'demod', 'trident', 'frame', 'viterbi')}
     else:
         kt = {k: eng.timing(tag + k) for k in ('demod', 'coarse', 'frame', 'viterbi')}
     ht = {k: eng.timing(k) for k in ('host_push', 'host_run', 'host_wait_njobs', 'host_wait_jobs', 'host_frames')}
