@@ -137,15 +137,35 @@ __global__ __launch_bounds__(512) void hilbert_kernel(BurstState S, BurstTables 
 }
 
 // ----------------------------------------------------------------- demod
-// One wave per workgroup.  The transposed RRC partial sums of taps
-// [BD_LDS_TAPS, 55) live in registers, the rest (real and imaginary) in LDS:
-// 40 x 2 x 8 B x 64 = 40 KB per wave, so four waves (one per SIMD) share a
-// CU and 65536 channels run in one round instead of two.
+// One wave per workgroup, at most 40 KB of LDS per wave, so four waves (one
+// per SIMD) share a CU and 65536 channels run in one round instead of two.
+//
+// The RRC (FIR::FIRUpdateAndProcess, transposed form: the output is
+// ((0 + h0 d[n-55]) + h1 d[n-54]) + ... + h54 d[n-1], oldest term first).
+// AERO_BD_DIRECT (default): the partial sum of the oldest BD_LDS_TAPS taps is
+// formed directly, oldest first, from a per-lane LDS line of the last
+// BD_LDS_TAPS mixer outputs d (one 16-B read per tap and one write per
+// sample); the line slides back every BD_DBLK samples.  The same products are
+// added in the same order as in the transposed form, so every partial sum is
+// the same double.  The newest taps keep their transposed partial sums in
+// registers.  The state between launches holds the line (oldest first) in
+// place of those taps' partial sums: all zero at start in either form.
+// AERO_BD_DIRECT=0: the transposed partial sums of taps [0, BD_LDS_TAPS) in
+// LDS (a read and a write per tap and sample).
 constexpr int BD_BLOCK = 64;
+#ifndef AERO_BD_DIRECT
+#define AERO_BD_DIRECT 1
+#endif
 #ifndef AERO_BD_LDS_TAPS
-#define AERO_BD_LDS_TAPS 40
+#define AERO_BD_LDS_TAPS (AERO_BD_DIRECT ? 36 : 40)
 #endif
 constexpr int BD_LDS_TAPS = AERO_BD_LDS_TAPS, BD_REG_TAPS = NTAPS - BD_LDS_TAPS;
+constexpr int BD_DBLK = 40 - BD_LDS_TAPS;  // direct form: samples per slide of the line
+#ifndef AERO_BD_DCH
+#define AERO_BD_DCH 8
+#endif
+constexpr int BD_DCH = AERO_BD_DCH;  // direct form: line entries read per chunk
+static_assert(!AERO_BD_DIRECT || (BD_LDS_TAPS >= 1 && BD_DBLK >= 1), "direct line within 40 KB per wave");
 
 // AERO_X_BSTAMPS (diagnostic build only): s_memtime cycle totals per section
 // of the demod loop, each wave's maximum over its lanes (the wave's time in
@@ -334,8 +354,12 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
 // wave per workgroup.  The transposed RRC partial sums of taps
 // [BD_LDS_TAPS, 55) live in registers, the rest (real and imaginary) in LDS.
 __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, BurstTables T, int nch, int trace) {
+#if AERO_BD_DIRECT
+  __shared__ double2 s_d[BD_LDS_TAPS + BD_DBLK][BD_BLOCK];  // [slot][lane]: d of past samples
+#else
   __shared__ double s_qre[BD_LDS_TAPS > 0 ? BD_LDS_TAPS : 1][BD_BLOCK];
   __shared__ double s_qim[BD_LDS_TAPS > 0 ? BD_LDS_TAPS : 1][BD_BLOCK];
+#endif
   const int c = blockIdx.x * BD_BLOCK + threadIdx.x, col = threadIdx.x;
   if (c >= nch) return;
 #ifdef AERO_X_BSTAMPS
@@ -382,11 +406,18 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   long long chk_done = ls[BL_CHK_DONE * C];
   const long long chk_n = ls[BL_CHK_N * C];
   long long next_chk = chk_done < chk_n ? S.chk_n[(size_t)c * TRI_SLOTS + (chk_done & (TRI_SLOTS - 1))] : LLONG_MAX;
+#if AERO_BD_DIRECT
+#pragma unroll 1
+  for (int j = 0; j < BD_LDS_TAPS; ++j)
+    s_d[j][col] = make_double2(S.fir[(size_t)j * C + c], S.fir[(size_t)(NTAPS + j) * C + c]);
+  int dt = 0;  // the line's oldest entry is slot dt
+#else
 #pragma unroll 1
   for (int j = 0; j < BD_LDS_TAPS; ++j) {
     s_qre[j][col] = S.fir[(size_t)j * C + c];
     s_qim[j][col] = S.fir[(size_t)(NTAPS + j) * C + c];
   }
+#endif
   double hre[BD_REG_TAPS], him[BD_REG_TAPS];  // partial sums of taps BD_LDS_TAPS..54
 #pragma unroll
   for (int j = 0; j < BD_REG_TAPS; ++j) {
@@ -400,6 +431,16 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   const DlyRef dA1 = dref(T, BDL_A1);
 
   long long n = n0;
+  // the loads a sample's FIR and AGC2 need are issued one sample ahead (their
+  // indices advance by one per sample; a trident decision that moves mixer2
+  // reloads its table entry): val_to_demod (front end's ring), mixer2's cis
+  // entry, the agc2 slot about to be replaced
+  auto vtd_at = [&](long long k) {
+    return k >= B_D2 - 1 ? S.vring[(size_t)((k - (B_D2 - 1)) & (BV_LEN - 1)) * C + c] : 0.0;
+  };
+  double vtd_n = vtd_at(n);
+  double2 m2_n = T.cis[b_cis_index(m2_ptr)];
+  double agc2_n = S.agc2[(size_t)agc2_p * C + c];
   BSTAMP(7);
   while (n < end) {
     BSTAMP(0);
@@ -411,7 +452,8 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       chunk_h++;
     }
     // val_to_demod = d2.update_dont_touch(...): the front end's value of B_D2 - 1 samples ago (zeros before)
-    const double vtd = n >= B_D2 - 1 ? S.vring[(size_t)((n - (B_D2 - 1)) & (BV_LEN - 1)) * C + c] : 0.0;
+    const double vtd = vtd_n;
+    vtd_n = vtd_at(n + 1);  // past the front end's progress: unused
     BSTAMP(1);
     if (n == next_chk) {
       // trident decision (burstoqpskdemodulator.cpp:393-411), computed by trident_kernel
@@ -420,6 +462,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         const double carrierphase = aero_atan2(r[6], r[5]) - (M_PI / 4.0);
         b_set_freq(m2_freq, m2_step, (48000.0 / 32768.0) * r[1]);
         b_set_phase_deg(m2_ptr, (180.0 / M_PI) * carrierphase);
+        m2_n = T.cis[b_cis_index(m2_ptr)];
         vol_gain = 1.4142 * 500.0 / r[3];
         b_set_freq(so_freq, so_step, 10500.0);
         b_set_phase_deg(so_ptr, 0);
@@ -454,7 +497,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     BSTAMP(3);
     // ---- part B (:450-702); its ring and weight reads first (a1's whatever
     // the symbol-tone window says: a read changes nothing)
-    const double agc2_old = S.agc2[(size_t)agc2_p * C + c];
+    const double agc2_old = agc2_n;
     const DlyPre pS = dly_pre(S.dl[BDL_S] + c, C, dl_s, dS);
     const DlyPre p41 = dly_pre(S.dl[BDL_41] + c, C, dl_41, d41);
     const DlyPre p42 = dly_pre(S.dl[BDL_42] + c, C, dl_42, d42);
@@ -463,21 +506,73 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     double s2r, s2i;
     {
       // the taps are reloaded (scalar loads) every sample rather than held
-      // in 110 SGPRs across the loop, which spilled
-      const double *tp = c_btaps;
-      asm volatile("" : "+s"(tp));
-      const double2 m2 = T.cis[b_cis_index(m2_ptr)];
+      // in 110 SGPRs across the loop, which spilled: the laundered value is
+      // a zero offset, not the pointer, so the loads stay scalar loads from
+      // constant memory (a laundered pointer loses its address space and
+      // turns them into flat vector loads, each waited for in turn)
+      // (the offset is laundered again after each chunk of taps, so a chunk's
+      // scalar loads are issued when it is due and 16 SGPRs hold its taps)
+      int tz = 0;
+      asm volatile("" : "+s"(tz));
+      const double2 m2 = m2_n;
       const double sc = vol_gain * vtd;
       const double ddr = m2.x * sc, ddi = m2.y * sc;
-      // RRC, transposed form (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
+      // RRC (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
+#if AERO_BD_DIRECT
+      // partial sum of taps 0..BD_LDS_TAPS-1 at sample n-1, oldest term first
+      const int lbase = dt * BD_BLOCK + col;  // element index of the oldest entry in s_d
+      double ar = 0.0, ai = 0.0;
+      {
+        // in chunks of BD_DCH entries, each chunk's reads issued after the
+        // previous chunk's sums (the scheduler would otherwise issue all
+        // reads at once and hold 4 registers per tap); the laundered value is
+        // an index, so the reads stay LDS reads
+        const double2 *sd = &s_d[0][0];
+        int lp = lbase;
+#pragma unroll
+        for (int i0 = 0; i0 < BD_LDS_TAPS; i0 += BD_DCH) {
+          double2 v[BD_DCH];
+#pragma unroll
+          for (int u = 0; u < BD_DCH; ++u)
+            if (i0 + u < BD_LDS_TAPS) v[u] = sd[lp + (i0 + u) * BD_BLOCK];
+#pragma unroll
+          for (int u = 0; u < BD_DCH; ++u) {
+            if (i0 + u >= BD_LDS_TAPS) break;
+            const double tap = c_btaps[tz + i0 + u];
+            if (i0 + u == 0) {
+              ar = 0.0 + tap * v[0].x;
+              ai = 0.0 + tap * v[0].y;
+            } else {
+              ar = ar + tap * v[u].x;
+              ai = ai + tap * v[u].y;
+            }
+          }
+          asm volatile("" : "+v"(lp), "+s"(tz) : "v"(ar), "v"(ai));
+        }
+      }
+#endif
+      const double *tp = c_btaps + tz;
       s2r = hre[BD_REG_TAPS - 1];
       s2i = him[BD_REG_TAPS - 1];
 #pragma unroll
       for (int j = NTAPS - 1; j > BD_LDS_TAPS; --j) {  // register part, descending: q[j - 1] read before rewritten
         hre[j - BD_LDS_TAPS] = hre[j - 1 - BD_LDS_TAPS] + tp[j] * ddr;
         him[j - BD_LDS_TAPS] = him[j - 1 - BD_LDS_TAPS] + tp[j] * ddi;
+        if ((NTAPS - 1 - j) % 8 == 7) {
+          asm volatile("" : "+s"(tz) : "v"(hre[j - BD_LDS_TAPS]));
+          tp = c_btaps + tz;
+        }
       }
-#if AERO_BD_LDS_TAPS > 0
+#if AERO_BD_DIRECT
+      hre[0] = ar + tp[BD_LDS_TAPS] * ddr;
+      him[0] = ai + tp[BD_LDS_TAPS] * ddi;
+      (&s_d[0][0])[lbase + BD_LDS_TAPS * BD_BLOCK] = make_double2(ddr, ddi);
+      if (++dt == BD_DBLK) {  // slide the line back to slot 0 (ascending: no entry overwritten before it is moved)
+        dt = 0;
+#pragma unroll 8
+        for (int i = 0; i < BD_LDS_TAPS; ++i) s_d[i][col] = s_d[BD_DBLK + i][col];
+      }
+#elif AERO_BD_LDS_TAPS > 0
       hre[0] = s_qre[BD_LDS_TAPS - 1][col] + tp[BD_LDS_TAPS] * ddr;
       him[0] = s_qim[BD_LDS_TAPS - 1][col] + tp[BD_LDS_TAPS] * ddi;
       for (int j = BD_LDS_TAPS - 1; j >= 1; --j) {
@@ -540,6 +635,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       agc2_sum = agc2_sum + fabs(sa);
       S.agc2[(size_t)agc2_p * C + c] = fabs(sa);
       agc2_p = agc2_p + 1 == B_AGC2 ? 0 : agc2_p + 1;
+      agc2_n = S.agc2[(size_t)agc2_p * C + c];  // written B_AGC2 samples ago
       double g = 1.414213562 / fmax(agc2_sum / ((double)B_AGC2), 0.000001);
       g = fmax(g, 0.000001);
       s2r *= g;
@@ -657,6 +753,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     s2l_r = s2r;
     s2l_i = s2i;
     b_nco_next(m2_ptr, m2_step);
+    m2_n = T.cis[b_cis_index(m2_ptr)];
     so_last = so_ptr;
     b_nco_next(so_ptr, so_step);
     b_nco_next(q_ptr, q_step);
@@ -665,11 +762,20 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   }
   BCOUNT(0, (unsigned long long)(n - n0));
   // state back
+#if AERO_BD_DIRECT
+#pragma unroll 1
+  for (int j = 0; j < BD_LDS_TAPS; ++j) {
+    const double2 v = s_d[dt + j][col];
+    S.fir[(size_t)j * C + c] = v.x;
+    S.fir[(size_t)(NTAPS + j) * C + c] = v.y;
+  }
+#else
 #pragma unroll 1
   for (int j = 0; j < BD_LDS_TAPS; ++j) {
     S.fir[(size_t)j * C + c] = s_qre[j][col];
     S.fir[(size_t)(NTAPS + j) * C + c] = s_qim[j][col];
   }
+#endif
 #pragma unroll
   for (int j = 0; j < BD_REG_TAPS; ++j) {
     S.fir[(size_t)(BD_LDS_TAPS + j) * C + c] = hre[j];

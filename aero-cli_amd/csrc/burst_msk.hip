@@ -285,10 +285,19 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
   const double PT = M_EE * WTSIZE;  // IfHavePassedPoint(ee)
 
   long long n = n0;
+  // loads issued one sample ahead, as in demod_burst_kernel: val_to_demod,
+  // mixer2's cis entry (reloaded when a decision moves mixer2), the agc2 slot
+  auto vtd_at = [&](long long k) {
+    return k >= M_D2 - 1 ? S.vring[(size_t)((k - (M_D2 - 1)) & (MV_LEN - 1)) * C + c] : 0.0;
+  };
+  double vtd_n = vtd_at(n);
+  double2 m2_n = T.cis[b_cis_index(m2_ptr)];
+  double agc2_n = S.agc2[(size_t)agc2_p * C + c];
   while (n < end) {
     if (sp - scons > B_SOFT_RING - 64) break;  // soft ring full: framing frees it next
     // val_to_demod = d2.update_dont_touch(...): the front end's value M_D2 - 1 samples ago (zeros before)
-    const double vtd = n >= M_D2 - 1 ? S.vring[(size_t)((n - (M_D2 - 1)) & (MV_LEN - 1)) * C + c] : 0.0;
+    const double vtd = vtd_n;
+    vtd_n = vtd_at(n + 1);  // past the front end's progress: unused
     if (n == next_chk) {
       // trident decision (burstmskdemodulator.cpp:475-522) from trident_bmsk_kernel's spectra; dcd is false
       const double *r = S.chk + ((size_t)c * TRI_SLOTS + (chk_done & (TRI_SLOTS - 1))) * CHK_REC;
@@ -304,6 +313,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         vol_gain = 1.4142 * (500.0 / (minval / 3));
         const double carrierphase = aero_atan2(r[5], r[4]) - (M_PI / 4.0);
         b_set_phase_deg(m2_ptr, (180.0 / M_PI) * carrierphase);
+        m2_n = T.cis[b_cis_index(m2_ptr)];
         // mixer2.SetFreq, then CenterFreqChangedSlot (:299-317) puts mixer2 on
         // mixer_center's clamped frequency
         double fc = ((maxtopposhigh + maxtoppos) / 2) * hzperbin;
@@ -361,7 +371,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       const int dsr = dsm_p + 1 == M_DSM ? 0 : dsm_p + 1;
       const int d8o = d8_p + 1 == M_D8 ? 0 : d8_p + 1, d8n = d8o + 1 == M_D8 ? 0 : d8o + 1;
       const int a1o = a1_p + 1 == M_A1 ? 0 : a1_p + 1, a1n = a1o + 1 == M_A1 ? 0 : a1o + 1;
-      const double agc2_old = S.agc2[(size_t)agc2_p * C + c];
+      const double agc2_old = agc2_n;
       const double2 pd_slot = dsm[(size_t)dsr * C];
       const double d8_old = d8[(size_t)d8o * C], d8_new = d8[(size_t)d8n * C];
       double a1_old = 0.0, a1_new = 0.0;
@@ -371,26 +381,40 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       }
       double s2r, s2i;
       {
-        const double2 m2 = T.cis[b_cis_index(m2_ptr)];
+        const double2 m2 = m2_n;
         double cr = m2.x * vtd, ci = m2.y * vtd;  // mixer2.WTCISValue() * (val_to_demod) * vol_gain
         cr = cr * vol_gain;
         ci = ci * vol_gain;
-        // matched filter, transposed form (FIR::FIRUpdateAndProcess reads the 80 samples before the newest)
+        // matched filter, transposed form (FIR::FIRUpdateAndProcess reads the 80 samples before the newest);
+        // taps reloaded by scalar loads every sample, 8 at a time (a zero
+        // offset laundered after each 8 taps: held across the loop they took
+        // 160 SGPRs and spilled)
+        int tz = 0;
+        asm volatile("" : "+s"(tz));
+        const double *tp = c_mtaps + tz;
         s2r = hre[BM_REG_TAPS - 1];
         s2i = him[BM_REG_TAPS - 1];
 #pragma unroll
         for (int j = M_NT - 1; j > BM_LDS_TAPS; --j) {  // register part, descending: q[j - 1] read before rewritten
-          hre[j - BM_LDS_TAPS] = hre[j - 1 - BM_LDS_TAPS] + c_mtaps[j] * cr;
-          him[j - BM_LDS_TAPS] = him[j - 1 - BM_LDS_TAPS] + c_mtaps[j] * ci;
+          hre[j - BM_LDS_TAPS] = hre[j - 1 - BM_LDS_TAPS] + tp[j] * cr;
+          him[j - BM_LDS_TAPS] = him[j - 1 - BM_LDS_TAPS] + tp[j] * ci;
+          if ((M_NT - 1 - j) % 8 == 7) {
+            asm volatile("" : "+s"(tz) : "v"(hre[j - BM_LDS_TAPS]));
+            tp = c_mtaps + tz;
+          }
         }
-        hre[0] = s_qre[BM_LDS_TAPS - 1][col] + c_mtaps[BM_LDS_TAPS] * cr;
-        him[0] = s_qim[BM_LDS_TAPS - 1][col] + c_mtaps[BM_LDS_TAPS] * ci;
+        hre[0] = s_qre[BM_LDS_TAPS - 1][col] + tp[BM_LDS_TAPS] * cr;
+        him[0] = s_qim[BM_LDS_TAPS - 1][col] + tp[BM_LDS_TAPS] * ci;
         for (int j = BM_LDS_TAPS - 1; j >= 1; --j) {
-          s_qre[j][col] = s_qre[j - 1][col] + c_mtaps[j] * cr;
-          s_qim[j][col] = s_qim[j - 1][col] + c_mtaps[j] * ci;
+          s_qre[j][col] = s_qre[j - 1][col] + tp[j] * cr;
+          s_qim[j][col] = s_qim[j - 1][col] + tp[j] * ci;
+          if ((BM_LDS_TAPS - 1 - j) % 8 == 7) {
+            asm volatile("" : "+s"(tz) : "v"(cr));
+            tp = c_mtaps + tz;
+          }
         }
-        s_qre[0][col] = 0.0 + c_mtaps[0] * cr;
-        s_qim[0][col] = 0.0 + c_mtaps[0] * ci;
+        s_qre[0][col] = 0.0 + tp[0] * cr;
+        s_qim[0][col] = 0.0 + tp[0] * ci;
       }
       if (tone) {  // symbol-tone x4 PLL (:555-578)
         const double t1r = s2r * str_r - s2i * str_i, t1i = s2r * str_i + s2i * str_r;
@@ -432,6 +456,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         agc2_sum = agc2_sum + fabs(sa);
         S.agc2[(size_t)agc2_p * C + c] = fabs(sa);
         agc2_p = agc2_p + 1 == M_AGC2 ? 0 : agc2_p + 1;
+        agc2_n = S.agc2[(size_t)agc2_p * C + c];  // written M_AGC2 samples ago
         double g = 1.414213562 / fmax(agc2_sum / ((double)M_AGC2), 0.000001);
         g = fmax(g, 0.000001);
         s2r *= g;
@@ -528,6 +553,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       b_nco_next(so_ptr, so_step);
       b_nco_next(sh_ptr, sh_step);
       b_nco_next(m2_ptr, m2_step);
+      m2_n = T.cis[b_cis_index(m2_ptr)];
     }
     n++;
   }

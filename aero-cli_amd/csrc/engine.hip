@@ -1055,11 +1055,17 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
     }
     const long long r0 = start & (PCM_CAP - 1);
     const size_t n1 = (size_t)std::min<long long>((long long)n, PCM_CAP - r0);
-    HIPCHK(hipMemcpy2DAsync(e->S.pcm + r0 * e->C + c0, sizeof(int16_t) * e->C, src, sizeof(int16_t) * ld,
-                            sizeof(int16_t) * nch, n1, kind, e->st_in));
-    if (n1 < n)
-      HIPCHK(hipMemcpy2DAsync(e->S.pcm + c0, sizeof(int16_t) * e->C, src + n1 * ld, sizeof(int16_t) * ld,
-                              sizeof(int16_t) * nch, n - n1, kind, e->st_in));
+    // whole rows (every channel of the group, the source as wide as the ring)
+    // are one contiguous block: a 1-D copy, which the DMA engines run beside
+    // the kernels (a 2-D copy is a blit kernel that waits for CUs)
+    const bool rows = c0 == 0 && nch == e->C && ld == (size_t)e->C;
+    auto copy = [&](int16_t *dst, const int16_t *from, size_t nrows) -> hipError_t {
+      if (rows) return hipMemcpyAsync(dst, from, sizeof(int16_t) * e->C * nrows, kind, e->st_in);
+      return hipMemcpy2DAsync(dst, sizeof(int16_t) * e->C, from, sizeof(int16_t) * ld, sizeof(int16_t) * nch, nrows,
+                              kind, e->st_in);
+    };
+    HIPCHK(copy(e->S.pcm + r0 * e->C + c0, src, n1));
+    if (n1 < n) HIPCHK(copy(e->S.pcm + c0, src + n1 * ld, n - n1));
     HIPCHK(hipEventRecord(e->ev_in, e->st_in));
     HIPCHK(hipEventSynchronize(e->ev_in));  // the caller's buffer is free again
     HIPCHK(hipStreamWaitEvent(e->st, e->ev_in, 0));
@@ -1178,8 +1184,8 @@ int aero_engine_create(const aero_engine_cfg *cfg, aero_engine **out) {
     if (n < 1) n = 1;
     e->hpool.reset(new HostPool(n));
   }
-  // the 10500 group is created up front (the hot path), MSK groups on first use
-  if (int rc = group_create(e.get(), MODE_OQPSK, e->groups[MODE_OQPSK])) return rc;
+  // every group (continuous and burst) is created on its kind's first
+  // aero_channel_open: an engine of burst channels holds no continuous state
   *out = e.release();
   return AERO_OK;
 }
@@ -1593,7 +1599,7 @@ int aero_sync(aero_engine *e) {
 int aero_device_math(aero_engine *e, int fn, const double *x, const double *y, double *out, size_t n) {
   if (!e || !x || !y || !out) return AERO_E_INVALID;
   HIPCHK(hipSetDevice(e->device));
-  hipStream_t st = e->groups[MODE_OQPSK]->st;
+  hipStream_t st = nullptr;
   double *d = nullptr;
   HIPCHK(hipMalloc(&d, 3 * n * sizeof(double) + 64));
   HIPCHK(hipMemcpy(d, x, n * 8, hipMemcpyHostToDevice));

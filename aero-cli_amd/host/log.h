@@ -9,7 +9,8 @@ namespace aerohost {
 extern bool g_verbose;
 }
 
-#define AH_INF(...) (fprintf(stderr, __VA_ARGS__), fputc('\n', stderr))
+// the line and its newline under one stream lock (the forwarder thread logs too)
+#define AH_INF(...) (flockfile(stderr), fprintf(stderr, __VA_ARGS__), fputc('\n', stderr), funlockfile(stderr))
 #define AH_DBG(fmt, ...) \
   (aerohost::g_verbose ? (fprintf(stderr, "\033[1;34m[DEBUG] " fmt "\033[0m\n", ##__VA_ARGS__), 0) : 0)
 #define AH_WARN(fmt, ...) fprintf(stderr, "\033[1;33m[WARN] " fmt "\033[0m\n", ##__VA_ARGS__)

@@ -291,11 +291,18 @@ def test_multi_topic_decoder(engine_lib, cpu_libs, tmp_path):
                             'driver=file,path=%s,start_delay_ms=1500' % wb, str(ini)],
                            capture_output=True, text=True, timeout=180, env=dict(os.environ, AERO_ZMQ_HWM='0'))
         assert r.returncode == 0, r.stderr[-3000:]
+        # messages still queued at SIGTERM are dropped (as the reference
+        # does): wait until the decoder has taken them all, i.e. its output
+        # has stopped growing for a few seconds
         t0 = time.time()
-        want_n = sum(len(w) for w in wants)
-        while sum(l.startswith('{') for l in lines) < want_n - 4 * nv and time.time() - t0 < 90:
+        last, t_last = -1, time.time()
+        while time.time() - t0 < 150:
+            n_now = sum(l.startswith('{') for l in lines)
+            if n_now != last:
+                last, t_last = n_now, time.time()
+            elif time.time() - t_last > 6.0:
+                break
             time.sleep(0.2)
-        time.sleep(2.0)
     finally:
         dec.send_signal(signal.SIGTERM)
         rc = dec.wait(timeout=120)
