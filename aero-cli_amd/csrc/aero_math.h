@@ -467,7 +467,7 @@ AERO_HD double aero_cos(double x) {
 
 /* sin and cos of x together (one reduction, one table lookup); the same
  * correctly-rounded results as aero_sin / aero_cos */
-AERO_HD void aero_sincos(double x, double &so, double &co) {
+AERO_HD void aero_sincos_dd(double x, double &so, double &co) {
   if (!__builtin_isfinite(x) || __builtin_fabs(x) >= 0x1p20) {
     so = co = __builtin_nan("");
     return;
@@ -485,6 +485,59 @@ AERO_HD void aero_sincos(double x, double &so, double &co) {
   }
   if (__builtin_fabs(x) < 0x1p-26) so = x;
   if (__builtin_fabs(x) < 0x1p-27) co = 1.0;
+}
+
+/* sincos fast path (Ziv) for 2^-26 <= |x| <= 1/4, the demods' usual loop
+ * corrections.  Taylor series around 0 with the terms that matter at 2^-70
+ * kept exact or in double-double: x^2 exact by fma, x^3/6 and x^5/120 (sin),
+ * x^2/2 and x^4/24 (cos) as double-double products, the rest (|.| <= 2^-24
+ * |x| for sin, 2^-21 for cos) in double; their sum carries at most ~2^-72
+ * relative error, so when hi + (lo +- 2^-69 |hi|) round alike, hi + lo is the
+ * correctly rounded value (aero_sincos_dd's result).  Otherwise (and outside
+ * the range) the double-double path decides.  No IEEE division. */
+AERO_HD void aero_sincos(double x, double &so, double &co) {
+  const double ax = __builtin_fabs(x);
+  if (!(ax >= 0x1p-26 && ax <= 0.25)) {
+    aero_sincos_dd(x, so, co);
+    return;
+  }
+  const double x2 = ax * ax, x2l = fma(ax, ax, -x2);  // x^2 = x2 + x2l exactly
+  // sin |x| = |x| - x^3/6 + x^5/120 + x^7 P(x^2)
+  const double x3 = ax * x2, x3l = fma(ax, x2, -x3) + ax * x2l;
+  const double t3 = x3 * -AERO_INV6_HI, t3l = fma(x3, -AERO_INV6_HI, -t3) + (x3 * -AERO_INV6_LO + x3l * -AERO_INV6_HI);
+  const double x5 = x3 * x2, x5l = fma(x3, x2, -x5) + (x3 * x2l + x3l * x2);
+  const double t5 = x5 * AERO_INV120_HI, t5l = fma(x5, AERO_INV120_HI, -t5) + (x5 * AERO_INV120_LO + x5l * AERO_INV120_HI);
+  double p = fma(x2, 1.0 / 355687428096000.0, -1.0 / 1307674368000.0);
+  p = fma(x2, p, 1.0 / 6227020800.0);
+  p = fma(x2, p, -1.0 / 39916800.0);
+  p = fma(x2, p, 1.0 / 362880.0);
+  p = fma(x2, p, -1.0 / 5040.0);
+  const double r7 = (x5 * x2) * p;
+  const dd sa = two_sum(ax, t3);
+  const dd sb = two_sum(sa.hi, t5);
+  const double slo = (sa.lo + sb.lo) + ((t3l + t5l) + r7);
+  // cos x = 1 - x^2/2 + x^4/24 + x^6 Q(x^2)
+  const double h = 0.5 * x2, hl = 0.5 * x2l;  // exact
+  const double x4 = x2 * x2, x4l = fma(x2, x2, -x4) + 2.0 * (x2 * x2l);
+  const double t4 = x4 * AERO_INV24_HI, t4l = fma(x4, AERO_INV24_HI, -t4) + (x4 * AERO_INV24_LO + x4l * AERO_INV24_HI);
+  double q = fma(x2, 1.0 / 20922789888000.0, -1.0 / 87178291200.0);
+  q = fma(x2, q, 1.0 / 479001600.0);
+  q = fma(x2, q, -1.0 / 3628800.0);
+  q = fma(x2, q, 1.0 / 40320.0);
+  q = fma(x2, q, -1.0 / 720.0);
+  const double r6 = (x4 * x2) * q;
+  const dd ca = two_sum(1.0, -h);
+  const dd cb = two_sum(ca.hi, t4);
+  const double clo = (ca.lo + cb.lo) + ((t4l - hl) + r6);
+  const double sv = sb.hi + slo, cv = cb.hi + clo;
+  const double es = 0x1p-69 * sb.hi, ec = 0x1p-69 * cb.hi;
+  if (sv != sb.hi + (slo + es) || sv != sb.hi + (slo - es) || cv != cb.hi + (clo + ec) ||
+      cv != cb.hi + (clo - ec)) {
+    aero_sincos_dd(x, so, co);
+    return;
+  }
+  so = __builtin_signbit(x) ? -sv : sv;
+  co = cv;
 }
 
 /* natural log of m in [1, 2) as double-double */

@@ -440,6 +440,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   };
   double vtd_n = vtd_at(n);
   double2 m2_n = T.cis[b_cis_index(m2_ptr)];
+  double2 so_n = T.cis[b_cis_index(so_ptr)];  // st_osc's entry (reloaded where the phase is set)
   double agc2_n = S.agc2[(size_t)agc2_p * C + c];
   BSTAMP(7);
   while (n < end) {
@@ -466,6 +467,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         vol_gain = 1.4142 * 500.0 / r[3];
         b_set_freq(so_freq, so_step, 10500.0);
         b_set_phase_deg(so_ptr, 0);
+        so_n = T.cis[b_cis_index(so_ptr)];
         srx1 = srx2 = sry1 = sry2 = 0;
         startstop = B_STARTSTOP;
         cntr = 0;
@@ -618,6 +620,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       st_err *= 1.5 * (1.0 - progress * progress);
       b_advance(q_ptr, -(1.0 / (2.0 * M_PI)) * st_err * 0.1);
       b_set_phase_deg(so_ptr, (360.0 * q_ptr / ((double)WTSIZE)) * 4.0 + (360.0 * 0.4));
+      so_n = T.cis[b_cis_index(so_ptr)];
     }
     {  // sig2 *= symboltone_averotator; rotator *= exp(i rotator_freq); sig2 *= rotator
       const double ar = s2r * ave_r - s2i * ave_i, ai = s2r * ave_i + s2i * ave_r;
@@ -667,7 +670,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         if (cntr > SPS * (128 + 128)) st_eta = y;
       }
       const double m1r = st_eta, m1i = -dly_commit(S.dl[BDL_8] + c, C, dl_8, p8, st_eta);
-      const double2 so = T.cis[b_cis_index(so_ptr)];
+      const double2 so = so_n;
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
       const double st_angle_error = aero_atan2(oim, ore);
       if (cntr > SPS * (128 + 64)) {
@@ -756,6 +759,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     m2_n = T.cis[b_cis_index(m2_ptr)];
     so_last = so_ptr;
     b_nco_next(so_ptr, so_step);
+    so_n = T.cis[b_cis_index(so_ptr)];
     b_nco_next(q_ptr, q_step);
     n++;
     BSTAMP(6);
@@ -1127,8 +1131,8 @@ __global__ __launch_bounds__(256) void frame_burst_kernel(BurstState S, int nch)
 // soft values, decoded bits MSB-first
 __global__ __launch_bounds__(64) void rt_viterbi_kernel(BurstState S) {
   __shared__ uint8_t sbuf[RT_BLOCK];
-  __shared__ unsigned long long hist[HCAP];
-  __shared__ uint8_t obits[RT_BLOCK / 2 + 64];
+  __shared__ unsigned long long ow[64];  // decoded bit b: bit b & 63 of ow[b >> 6]
+  static_assert(RT_BLOCK / 2 <= 64 * 64, "decoded bits fit one 64-bit word per lane");
   const int njobs = *S.njobs;
   const int lane = threadIdx.x;
   for (int job = blockIdx.x; job < njobs; job += gridDim.x) {
@@ -1152,16 +1156,22 @@ __global__ __launch_bounds__(64) void rt_viterbi_kernel(BurstState S) {
         }
       }
     }
-    for (int k = lane; k < RT_BLOCK / 2 + 64; k += 64) obits[k] = 0;
     __syncthreads();
-    viterbi_decode_wave(sbuf, bp, hist, obits, lane);
+    // the register-history decoder (viterbi_dev.h), the same decoder as
+    // viterbi_decode_wave: the trellis steps need no LDS store or barrier
+    uint64_t obw;
+    viterbi_decode_regs(sbuf, bp, obw, lane);
+    ow[lane] = obw;
+    __syncthreads();
     uint8_t *out = S.jobout + (size_t)job * RT_JOB_OUT;
     const int nbits = bp / 2;
     if (lane == 0) *reinterpret_cast<int4 *>(out) = make_int4(c, bp, jd.z, nbits);
     for (int b = lane; b < (nbits + 7) / 8; b += 64) {
+      // bits 8b .. 8b+7 (one byte of one word), first bit as the MSB
+      const int byte = (int)((ow[b >> 3] >> (8 * (b & 7))) & 0xFFULL);
       int v = 0;
       for (int m = 0; m < 8; ++m)
-        if (8 * b + m < nbits) v |= obits[8 * b + m] << (7 - m);
+        if (8 * b + m < nbits) v |= ((byte >> m) & 1) << (7 - m);
       out[16 + b] = (uint8_t)v;
     }
   }

@@ -292,6 +292,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
   };
   double vtd_n = vtd_at(n);
   double2 m2_n = T.cis[b_cis_index(m2_ptr)];
+  double2 so_n = T.cis[b_cis_index(so_ptr)];  // st_osc's entry (reloaded where the phase is set)
   double agc2_n = S.agc2[(size_t)agc2_p * C + c];
   while (n < end) {
     if (sp - scons > B_SOFT_RING - 64) break;  // soft ring full: framing frees it next
@@ -339,6 +340,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         rotf = 0;
         srx1 = srx2 = sry1 = sry2 = 0;
         b_set_phase_deg(so_ptr, 0);
+        so_n = T.cis[b_cis_index(so_ptr)];
         b_set_phase_deg(sh_ptr, 0);
       }
       if (trace && hop_n < S.hop_cap) {
@@ -439,6 +441,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         st_err *= 0.5 * (1.0 - progress * progress);
         b_advance(sh_ptr, -(1.0 / (2.0 * M_PI)) * st_err * 0.05);
         b_set_phase_deg(so_ptr, (360.0 * sh_ptr / ((double)WTSIZE)) + (360.0 * (1.0 - M_EE)));
+        so_n = T.cis[b_cis_index(so_ptr)];
       }
       {  // sig2 *= symboltone_averotator; rotator *= exp(i rotator_freq); sig2 *= rotator
         const double ar = s2r * ave_r - s2i * ave_i, ai = s2r * ave_i + s2i * ave_r;
@@ -493,7 +496,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       d8[(size_t)d8_p * C] = st_eta;  // delayt8.update(st_eta), whole-sample delay (dly_int)
       d8_p = d8o;
       const double m1r = st_eta, m1i = -(0.0 * d8_new + (1.0 - 0.0) * d8_old);
-      const double2 so = T.cis[b_cis_index(so_ptr)];
+      const double2 so = so_n;
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
       const double st_angle_error = aero_atan2(oim, ore);
       if (cntr > M_ENDROT) b_advance(so_ptr, -st_angle_error * 0.002 / 360.0);
@@ -551,6 +554,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       }
       so_last = so_ptr;
       b_nco_next(so_ptr, so_step);
+      so_n = T.cis[b_cis_index(so_ptr)];
       b_nco_next(sh_ptr, sh_step);
       b_nco_next(m2_ptr, m2_step);
       m2_n = T.cis[b_cis_index(m2_ptr)];

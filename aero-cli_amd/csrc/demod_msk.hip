@@ -150,6 +150,11 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   int i = 0;
   // event operands carried out of the sample loop
   double e_s2r = 0, e_s2i = 0, e_pdr = 0, e_pdi = 0;
+  // PCM words two samples ahead (the coarse-ring entry staged during sample
+  // n holds sample n+1's word; loaded one sample ahead it would be waited for
+  // at once)
+  int16_t pcm_a = S.pcm[(size_t)(n0 & capm) * C + c];
+  int16_t pcm_b = S.pcm[(size_t)((n0 + 1) & capm) * C + c];
   while (i < ie) {
     bool pend = false;
     do {
@@ -157,7 +162,9 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       // this sample's ring reads before any of its stores, so their round
       // trips overlap (the rings are distinct, the compiler cannot prove it);
       // no slot read is the slot written this sample
-      const int16_t xs = S.pcm[(size_t)(n & capm) * C + c];
+      const int16_t xs = pcm_a;
+      pcm_a = pcm_b;
+      pcm_b = S.pcm[(size_t)((n + 2) & capm) * C + c];  // past the pushed samples: unused
       const double agc_old = S.agc[(size_t)(n % AGC) * C + c];
       const double2 dsm_old = S.dsm[(size_t)((n + 1) % DSM) * C + c];
       const double d8_older = S.d8[(size_t)((n + 1) % D8) * C + c];
@@ -252,7 +259,7 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       }
       if (i + 1 < ia) {
         const long long n1 = n + 1;
-        const int16_t x1 = S.pcm[(size_t)(n1 & capm) * C + c];
+        const int16_t x1 = pcm_a;
         S.cring[(size_t)c * NF + (n1 & (NF - 1))] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)x1 << 16);
         ifl = i + 2;
       }

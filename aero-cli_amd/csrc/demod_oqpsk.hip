@@ -235,8 +235,11 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
 
   const double PT = 0.4 * WTSIZE;  // IfHavePassedPoint(ee) with ee = 0.4 (oqpskdemodulator.cpp:225)
 
-  // sample n0+i's PCM word and AGC ring slot are always loaded one sample ahead
+  // sample n0+i's AGC ring slot is loaded one sample ahead, its PCM word two
+  // samples ahead: the coarse-ring entry staged during sample i holds sample
+  // i+1's PCM word, which one sample ahead would be waited for at once
   int16_t pcm_next = S.pcm[(size_t)pb * C + c];
+  int16_t pcm_next2 = S.pcm[(size_t)((pb + 1) & capm) * C + c];
   double agc_next = S.agc[(size_t)agc_ptr * C + c];
   // Event-aligned iteration.  The carrier/MSE/soft-bit step runs at every
   // second sample instant (one channel in ~9 samples), but in lockstep
@@ -256,13 +259,14 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
     do {
       XSTAMP(0);  // loop control
       const int16_t xs = pcm_next;
+      pcm_next = pcm_next2;
       const double agc_old = agc_next;
       // table lookups of this sample first, then the prefetch for the next
       const double2 cm = T.cis[cis_index(m2_ptr)];
       const double2 so = T.cis[cis_index(so_ptr)];
       {
         const int ap = agc_ptr + 1 == AGC_LEN ? 0 : agc_ptr + 1;
-        pcm_next = S.pcm[(size_t)((pb + i + 1) & capm) * C + c];
+        pcm_next2 = S.pcm[(size_t)((pb + i + 2) & capm) * C + c];  // past the pushed samples: unused
         agc_next = S.agc[(size_t)ap * C + c];
       }
       const double dval = ((double)xs) / 32768.0;

@@ -129,7 +129,7 @@ __device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nso
     const int prev = shfl_idx(m, s >> 1);
     if (s < (2 << i)) m = (soft_dist(conv_table(s), a, b) + prev) & 0xFFFF;
   }
-  int index = 0, len = 0, renorm = 0, outpos = 0;
+  int index = 0, len = 0, renorm = 0, outpos = 0;  // wave-uniform
   auto search = [&](int skip) -> int {
     int key = (s % skip == 0) ? ((m << 6) | s) : 0x7FFFFFFF;
     for (int off = 32; off > 0; off >>= 1) {
@@ -138,29 +138,40 @@ __device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nso
     }
     return __builtin_amdgcn_readfirstlane(key) & 63;
   };
+  // Traceback on the scalar unit: per column two v_readlane and a few scalar
+  // operations; the output bits (newest first, so bit b descends) are
+  // gathered in a 64-bit scalar word and merged into lane b >> 6 once per
+  // word.
   auto traceback = [&](int bestpath, int mintb) {
     const int nout = len - mintb;
     int idx = index;
     int j = 0;
-    // columns walked newest to oldest, one 64-column register block at a time
+    uint64_t acc = 0;
+    int accw = -1;
+    auto flush = [&]() {
+      if (accw >= 0 && lane == accw) obw |= acc;
+    };
     while (j < len) {
       idx = idx == 0 ? HCAP - 1 : idx - 1;
-      // steps inside this block: idx, idx - 1, ... down to the block start
-      int run = (idx & 63) + 1;
+      int run = (idx & 63) + 1;  // columns idx, idx - 1, ... down to this register's first
       if (run > len - j) run = len - j;
       auto walk = [&](const uint64_t hw) {
         for (int k = 0; k < run; ++k, ++j) {
-          const int col = idx - k;
-          const uint64_t hv = readlane64(hw, col & 63);
+          const uint64_t hv = readlane64(hw, (idx - k) & 63);
           const int hb = (int)((hv >> bestpath) & 1ULL);
           bestpath = (bestpath | (hb << 6)) >> 1;
           if (j >= mintb) {
-            const int b = outpos + (nout - 1 - (j - mintb));
-            if (lane == (b >> 6)) obw |= (uint64_t)hb << (b & 63);
+            const int bb = outpos + (nout - 1 - (j - mintb));
+            if ((bb >> 6) != accw) {
+              flush();
+              accw = bb >> 6;
+              acc = 0;
+            }
+            acc |= (uint64_t)hb << (bb & 63);
           }
         }
       };
-      // uniform branch per block (a selected copy would go through scratch)
+      // uniform branch per register (a selected copy would go through scratch)
       const int w = __builtin_amdgcn_readfirstlane(idx >> 6);
       if (w == 0)
         walk(h0);
@@ -170,6 +181,7 @@ __device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nso
         walk(h2);
       idx -= run - 1;
     }
+    flush();
     outpos += nout;
     len -= nout;
   };
@@ -188,11 +200,6 @@ __device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nso
       traceback(search(skip), MINTB);
     }
   };
-  int a = 0, b = 0;
-  if (6 < sets) {
-    a = sbuf[12];
-    b = sbuf[13];
-  }
   // the soft pairs of the next 64 steps: lane l holds step i0 + l's pair
   // (a | b << 8); a step takes its pair with one v_readlane, so no LDS read
   // sits on the step's dependency chain
@@ -200,57 +207,84 @@ __device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nso
     const int st = i0 + lane;
     return st < sets ? (uint32_t)sbuf[2 * st] | ((uint32_t)sbuf[2 * st + 1] << 8) : 0u;
   };
-  // Steps before the restricted tail (every state active), with the column
-  // register fixed per run of steps: soft_dist(tab_lo, a, b) = base + sa*a +
-  // sb*b for a, b in [0, 255], and the s | 64 edge carries the complementary
-  // code bits (both polynomials have bit 6 set: tab_hi == tab_lo ^ 3), so its
-  // metric is 510 minus that.  The decision mask is the compare itself and
-  // lands in column `index` through two v_writelane.
+  // Steps before the restricted tail (every state active) in runs that no
+  // event interrupts: a run ends where the column index leaves its register
+  // (64, 128, the wrap at 140), at the renormalisation (every 128 steps), at
+  // the traceback (140 columns held), at the end of the 64 buffered pairs
+  // or at the tail; the events are handled between runs exactly as
+  // process(1) handles them after a step.  Inside a run a step is: its pair
+  // by v_readlane, the two predecessor metrics by ds_bpermute, the branch
+  // metric soft_dist(tab_lo, a, b) = nbase - sa a - sb b (a, b in [0, 255];
+  // the s | 64 edge carries the complementary code bits, as both
+  // polynomials have bit 6 set: tab_hi == tab_lo ^ 3, so its metric is 510
+  // minus that), the compare (the decision mask) and the minimum, the mask
+  // into column index + k by two v_writelane.
   const int tail0 = sets - 6 > 6 ? sets - 6 : 6;
   {
-    const int sa = (tab_lo & 1) ? -1 : 1, sb = (tab_lo & 2) ? -1 : 1;
+    const int msa = (tab_lo & 1) ? 1 : -1, msb = (tab_lo & 2) ? 1 : -1;  // -sa, -sb
     const int nbase = -(((tab_lo & 1) ? 255 : 0) + ((tab_lo & 2) ? 255 : 0));
     const int src0 = (s >> 1) << 2, src1 = ((s >> 1) | 32) << 2;
     int i = 6;
     uint32_t pv = pairs(6);
     int pk = 0;  // step i's pair is lane pk of pv
-    auto steps = [&](uint64_t &hw, int run) {
-      for (int k = 0; k < run; ++k, ++i) {
-        if (pk == 64) {
-          pv = pairs(i);
-          pk = 0;
-        }
-        const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane((int)pv, pk);
-        ++pk;
-        const int ca = (int)(ab & 255u), cb = (int)(ab >> 8);
-        const int m0 = __builtin_amdgcn_ds_bpermute(src0, m), m1 = __builtin_amdgcn_ds_bpermute(src1, m);
-        const int nd = nbase - __mul24(sa, ca) - __mul24(sb, cb);  // -soft_dist(tab_lo, ca, cb)
-        const int e0 = (m0 - nd) & 0xFFFF;
-        const int e1 = (m1 + 510 + nd) & 0xFFFF;
-        const uint64_t mask = __ballot(e0 > e1);
-        m = e0 < e1 ? e0 : e1;
-        const int col = __builtin_amdgcn_readfirstlane(index & 63);
-        uint32_t lo = (uint32_t)hw, hi = (uint32_t)(hw >> 32);
-        asm("v_writelane_b32 %0, %1, m0" : "+v"(lo) : "s"((uint32_t)mask), "{m0}"(col));
-        asm("v_writelane_b32 %0, %1, m0" : "+v"(hi) : "s"((uint32_t)(mask >> 32)), "{m0}"(col));
-        hw = ((uint64_t)hi << 32) | lo;
-        process(1);
-      }
-    };
     while (i < tail0) {
-      // steps until the column index leaves its register (64, 128, wrap at 140)
       const int idx = __builtin_amdgcn_readfirstlane(index);
       const int w = idx >> 6;
       int run = (w == 2 ? HCAP : 64 * (w + 1)) - idx;
-      if (run > tail0 - i) run = tail0 - i;
+      run = min(run, tail0 - i);
+      run = min(run, RENORM - renorm);
+      run = min(run, HCAP - len);
+      run = min(run, 64 - pk);
+      run = __builtin_amdgcn_readfirstlane(run);
+      auto steps = [&](uint64_t &hw) {
+        uint32_t lo = (uint32_t)hw, hi = (uint32_t)(hw >> 32);
+        const int col0 = idx & 63;
+        for (int k = 0; k < run; ++k) {
+          const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane((int)pv, pk + k);
+          const int ca = (int)(ab & 255u), cb = (int)(ab >> 8);
+          const int m0 = __builtin_amdgcn_ds_bpermute(src0, m), m1 = __builtin_amdgcn_ds_bpermute(src1, m);
+          const int nd = nbase + __mul24(msa, ca) + __mul24(msb, cb);  // -soft_dist(tab_lo, ca, cb)
+          const int e0 = (m0 - nd) & 0xFFFF;
+          const int e1 = (m1 + 510 + nd) & 0xFFFF;
+          const uint64_t mask = __ballot(e0 > e1);
+          m = e0 < e1 ? e0 : e1;
+          const int col = col0 + k;
+          // the mask SGPRs were just written by a VALU compare: the hazard
+          // recognizer does not see into inline asm, so the wait states the
+          // v_writelane needs are explicit (without them the scheduler may
+          // place the compare right before it and a stale mask is written)
+          asm("s_nop 4\n\tv_writelane_b32 %0, %1, m0" : "+v"(lo) : "s"((uint32_t)mask), "{m0}"(col));
+          asm("v_writelane_b32 %0, %1, m0" : "+v"(hi) : "s"((uint32_t)(mask >> 32)), "{m0}"(col));
+        }
+        hw = ((uint64_t)hi << 32) | lo;
+      };
       if (w == 0)
-        steps(h0, run);
+        steps(h0);
       else if (w == 1)
-        steps(h1, run);
+        steps(h1);
       else
-        steps(h2, run);
+        steps(h2);
+      i += run;
+      pk += run;
+      index = idx + run == HCAP ? 0 : idx + run;
+      renorm += run;
+      len += run;
+      if (pk == 64) {
+        pv = pairs(i);
+        pk = 0;
+      }
+      if (renorm == RENORM) {
+        renorm = 0;
+        const int best = search(1);
+        const int mind = __builtin_amdgcn_readlane(m, best);
+        m = (m - mind) & 0xFFFF;
+        if (len == HCAP) traceback(best, MINTB);
+      } else if (len == HCAP) {
+        traceback(search(1), MINTB);
+      }
     }
   }
+  int a = 0, b = 0;
   if (tail0 < sets) {
     a = sbuf[2 * tail0];
     b = sbuf[2 * tail0 + 1];

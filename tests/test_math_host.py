@@ -71,3 +71,18 @@ def test_log_fast_path_equals_double_double():
         a = mathhost.evaluate('log', x).view(np.int64)
         b = mathhost.evaluate('log_dd', x).view(np.int64)
         assert np.array_equal(a, b)
+
+
+def test_sincos_fast_path_equals_double_double():
+    """aero_sincos's Ziv fast path (|x| <= 1/4) returns exactly what the
+    double-double path returns, for the loop corrections the demods pass it
+    (rotator frequency, PLL steps, averaged phase errors) and around the
+    range's edges."""
+    rng = np.random.default_rng(5)
+    xs = [rng.uniform(-0.25, 0.25, 1_000_000),
+          rng.standard_normal(1_000_000) * 1e-4,
+          np.exp(rng.uniform(np.log(2.0 ** -27), np.log(0.3), 1_000_000)) * rng.choice([-1.0, 1.0], 1_000_000),
+          rng.uniform(-0.6, 0.6, 200_000)]
+    for x in xs:
+        for a, b in (('sincos_s', 'sincos_dd_s'), ('sincos_c', 'sincos_dd_c')):
+            assert np.array_equal(mathhost.evaluate(a, x).view(np.int64), mathhost.evaluate(b, x).view(np.int64)), a

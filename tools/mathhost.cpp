@@ -24,6 +24,8 @@ extern "C" void aero_math_host_eval(int fn, const double *x, const double *y, do
       case 11: r = aero::aero_atan2_dd(a, b); break;
       case 12: r = aero::aero_log(a); break;
       case 13: r = aero::aero_log_dd(a); break;
+      case 14: { double s, c; aero::aero_sincos_dd(a, s, c); r = s; break; }
+      case 15: { double s, c; aero::aero_sincos_dd(a, s, c); r = c; break; }
       default: break;
     }
     out[i] = r;
