@@ -81,7 +81,7 @@ __global__ __launch_bounds__(512) void hilbert_kernel(BurstState S, BurstTables 
   constexpr int L = 13, PADDED = HB_N + HB_N / 16;
   __shared__ double lds[PADDED];
   __shared__ double2 s_tw[TwLds<L>::LEN];
-  const int c = blockIdx.x, t = threadIdx.x;
+  const int c = xcd_channel(blockIdx.x, gridDim.x), t = threadIdx.x;
   if (c >= nch) return;
   const int C = S.C;
   load_tw_lds<L>(s_tw, T.tw8, t, 512);

@@ -184,4 +184,17 @@ struct BurstTables {
   int dsize[BDL_COUNT];
 };
 
+// Workgroup -> channel map for kernels with one workgroup per channel that
+// read or write time-major [sample][C] arrays (a 128-B line holds 64 int16
+// or 8 complex samples of neighbouring channels).  Workgroups are dealt to
+// the 8 XCDs round-robin (blockIdx % 8), each with its own L2, so the
+// identity map has every line fetched (or partially written) by all 8 L2s;
+// this bijection of [0, n) gives XCD x the contiguous channels
+// [x q + min(x, r), ...) (q = n / 8, r = n % 8), so neighbouring channels
+// share one L2.
+__device__ __forceinline__ int xcd_channel(int b, int n) {
+  const int x = b & 7, k = b >> 3, q = n >> 3, r = n & 7;
+  return x * q + (x < r ? x : r) + k;
+}
+
 }  // namespace aero

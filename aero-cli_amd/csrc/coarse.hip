@@ -278,7 +278,9 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   const int yreset = S.is[IS_YRESET * C + c];
   auto yload = [&](int k) { return (k < YLEN && !yreset) ? yg[k] : 20.0; };
   double yp0 = yload(t), yp1 = yload(t + FT);
-  __syncthreads();
+  // no barrier here: the third transform's workgroup exchange ended with
+  // one (chain::gx), after which every wave only works in registers, so the
+  // LDS is free for |X| as soon as this wave gets here
   double *ylds = lds;  // [ypad(YLEN)]: bin k - YLO at ypad(k - YLO)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -288,7 +290,10 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   double yp2 = yload(t + 2 * FT);
   __syncthreads();
   CSTAMP(4);
-#pragma unroll 1
+#ifndef AERO_CO_LOG_UNROLL
+#define AERO_CO_LOG_UNROLL 1
+#endif
+#pragma unroll AERO_CO_LOG_UNROLL
   for (int k = t; k < YLEN; k += FT) {
     const double yold = yp0;
     yp0 = yp1;
