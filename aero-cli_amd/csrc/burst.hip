@@ -233,6 +233,10 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
   const DlyRef dBT = dref(T, BDL_BT), dMD = dref(T, BDL_MADIFF);
   double2 *btr = reinterpret_cast<double2 *>(S.dl[BDL_BT]) + c;
   long long n = n0;
+  // the analytic sample and the AGC slot it replaces are loaded one sample
+  // ahead: the sample's whole chain starts from them
+  double2 a_n = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
+  double agc_n = S.agc[(size_t)agc_p * C + c];
   while (n < end) {
     // every slot holds a check the demodulator has not applied: the buffer
     // this sample may start filling is one of them
@@ -242,8 +246,9 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
     // this sample (burst_dev.h dly_pre)
     const int d1r = d1_p + 1 == B_D1 ? 0 : d1_p + 1;
     const int p1r = pd1_p + 1 == B_PD1 ? 0 : pd1_p + 1, p2r = pd2_p + 1 == B_PD2 ? 0 : pd2_p + 1;
-    const double2 a = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
-    const double agc_old = S.agc[(size_t)agc_p * C + c];
+    const double2 a = a_n;
+    const double agc_old = agc_n;
+    a_n = S.ana[(size_t)((n + 1) & (ANA_LEN - 1)) * C + c];  // past the Hilbert stage's output: unused
     const double2 cvd = S.d1[(size_t)d1r * C + c];  // d1.update_dont_touch(cval)
     const DlyPre2 btp = dly_pre2(btr, C, dl_bt, dBT);
     const double2 ma_old = S.ma1[(size_t)ma1_p * C + c];
@@ -257,6 +262,7 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
       agc_sum = agc_sum + fabs(av);
       S.agc[(size_t)agc_p * C + c] = fabs(av);
       agc_p = agc_p + 1 == B_AGC ? 0 : agc_p + 1;
+      agc_n = S.agc[(size_t)agc_p * C + c];  // written B_AGC samples ago
       double g = 1.414213562 / fmax(agc_sum / ((double)B_AGC), 0.000001);
       g = fmax(g, 0.000001);
       cr *= g;

@@ -117,6 +117,10 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
   double2 *btd = reinterpret_cast<double2 *>(S.dl[0]) + c;
   double *madiff = S.dl[1] + c;
   long long n = n0;
+  // the analytic sample and the AGC slot it replaces are loaded one sample
+  // ahead: the sample's whole chain starts from them
+  double2 a_n = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
+  double agc_n = S.agc[(size_t)agc_p * C + c];
   while (n < end) {
     if (chk_n - chk_done >= TRI_SLOTS) break;  // every slot holds a check not yet applied
     // every ring slot this sample reads, loaded before any of its stores so
@@ -126,8 +130,9 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
     const int bto = btd_p + 1 == M_BTD ? 0 : btd_p + 1, btn = bto + 1 == M_BTD ? 0 : bto + 1;
     const int mdo = madiff_p + 1 == M_MADIFF ? 0 : madiff_p + 1, mdn = mdo + 1 == M_MADIFF ? 0 : mdo + 1;
     const int p1r = pd1_p + 1 == M_PD1 ? 0 : pd1_p + 1, p2r = pd2_p + 1 == M_PD2 ? 0 : pd2_p + 1;
-    const double2 a = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
-    const double agc_old = S.agc[(size_t)agc_p * C + c];
+    const double2 a = a_n;
+    const double agc_old = agc_n;
+    a_n = S.ana[(size_t)((n + 1) & (ANA_LEN - 1)) * C + c];  // past the Hilbert stage's output: unused
     const double2 cvd = S.d1[(size_t)d1r * C + c];  // d1.update_dont_touch(cval)
     const double2 bt_old = btd[(size_t)bto * C], bt_new = btd[(size_t)btn * C];
     const double2 ma_old = S.ma1[(size_t)ma1_p * C + c];
@@ -141,6 +146,7 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
       agc_sum = agc_sum + fabs(av);
       S.agc[(size_t)agc_p * C + c] = fabs(av);
       agc_p = agc_p + 1 == B_AGC ? 0 : agc_p + 1;
+      agc_n = S.agc[(size_t)agc_p * C + c];  // written B_AGC samples ago
       double g = 1.414213562 / fmax(agc_sum / ((double)B_AGC), 0.000001);
       g = fmax(g, 0.000001);
       cr *= g;
