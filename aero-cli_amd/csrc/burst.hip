@@ -433,8 +433,17 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   int16_t *soft = S.soft + (size_t)c * B_SOFT_RING;
   const long long *chunks = S.chunks + (size_t)c * CHUNK_RING;
   const double PT = 0.4 * WTSIZE;  // IfHavePassedPoint(ee), ee = 0.4
-  const DlyRef dS = dref(T, BDL_S), d41 = dref(T, BDL_41), d42 = dref(T, BDL_42), d8 = dref(T, BDL_8);
-  const DlyRef dA1 = dref(T, BDL_A1);
+  // the short delays in registers (burst_dev.h dly_reg); their weights are
+  // the same for every write pointer
+  double hS[BDL_N_S], h41[BDL_N_41], h42[BDL_N_42], h8[BDL_N_8], hA1[BDL_N_A1];
+  dly_regs_load(hS, S.dl[BDL_S] + c, C, dl_s);
+  dly_regs_load(h41, S.dl[BDL_41] + c, C, dl_41);
+  dly_regs_load(h42, S.dl[BDL_42] + c, C, dl_42);
+  dly_regs_load(h8, S.dl[BDL_8] + c, C, dl_8);
+  dly_regs_load(hA1, S.dl[BDL_A1] + c, C, dl_a1);
+  const double wS = T.dw[BDL_S][0], oS = T.domw[BDL_S][0], w41 = T.dw[BDL_41][0], o41 = T.domw[BDL_41][0];
+  const double w42 = T.dw[BDL_42][0], o42 = T.domw[BDL_42][0], w8 = T.dw[BDL_8][0], o8 = T.domw[BDL_8][0];
+  const double wA1 = T.dw[BDL_A1][0], oA1 = T.domw[BDL_A1][0];
 
   long long n = n0;
   // the loads a sample's FIR and AGC2 need are issued one sample ahead (their
@@ -506,11 +515,6 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     // ---- part B (:450-702); its ring and weight reads first (a1's whatever
     // the symbol-tone window says: a read changes nothing)
     const double agc2_old = agc2_n;
-    const DlyPre pS = dly_pre(S.dl[BDL_S] + c, C, dl_s, dS);
-    const DlyPre p41 = dly_pre(S.dl[BDL_41] + c, C, dl_41, d41);
-    const DlyPre p42 = dly_pre(S.dl[BDL_42] + c, C, dl_42, d42);
-    const DlyPre p8 = dly_pre(S.dl[BDL_8] + c, C, dl_8, d8);
-    const DlyPre pA1 = dly_pre(S.dl[BDL_A1] + c, C, dl_a1, dA1);
     double s2r, s2i;
     {
       // the taps are reloaded (scalar loads) every sample rather than held
@@ -619,7 +623,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       str_i = ni;
       ave_r = ave_r * 0.95 + 0.05 * str_r;
       ave_i = ave_i * 0.95 + 0.05 * str_i;
-      const double spi2 = dly_commit(S.dl[BDL_A1] + c, C, dl_a1, pA1, spr);
+      const double spi2 = dly_reg(hA1, wA1, oA1, spr);
       const double2 qv = T.cis[b_cis_index(q_ptr)];
       const double er_r = qv.x * spr - qv.y * (-spi2), er_i = qv.x * (-spi2) + qv.y * spr;
       double st_err = aero_atan2(er_i, er_r);
@@ -658,9 +662,9 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     }
     BSTAMP(5);
     {  // symbol timing (:482-496)
-      const double st_diff = dly_commit(S.dl[BDL_S] + c, C, dl_s, pS, abval * abval) - (abval * abval);
-      const double st_d1out = dly_commit(S.dl[BDL_41] + c, C, dl_41, p41, st_diff);
-      const double st_d2out = dly_commit(S.dl[BDL_42] + c, C, dl_42, p42, st_d1out);
+      const double st_diff = dly_reg(hS, wS, oS, abval * abval) - (abval * abval);
+      const double st_d1out = dly_reg(h41, w41, o41, st_diff);
+      const double st_d2out = dly_reg(h42, w42, o42, st_d1out);
       double st_eta = (st_d2out - st_diff) * st_d1out;
       {  // st_iir_resonator.update(st_eta)
         double y = 0;
@@ -675,7 +679,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         sry1 = y;
         if (cntr > SPS * (128 + 128)) st_eta = y;
       }
-      const double m1r = st_eta, m1i = -dly_commit(S.dl[BDL_8] + c, C, dl_8, p8, st_eta);
+      const double m1r = st_eta, m1i = -dly_reg(h8, w8, o8, st_eta);
       const double2 so = so_n;
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
       const double st_angle_error = aero_atan2(oim, ore);
@@ -821,11 +825,16 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   ds[BD_LASTMSE * C] = lastmse;
   ds[BD_MSEMA_SUM * C] = msema_sum;
   is[BI_AGC2_P * C] = agc2_p;
-  is[(BI_DL_P0 + BDL_S) * C] = dl_s;
-  is[(BI_DL_P0 + BDL_41) * C] = dl_41;
-  is[(BI_DL_P0 + BDL_42) * C] = dl_42;
-  is[(BI_DL_P0 + BDL_8) * C] = dl_8;
-  is[(BI_DL_P0 + BDL_A1) * C] = dl_a1;
+  dly_regs_store(hS, S.dl[BDL_S] + c, C);
+  dly_regs_store(h41, S.dl[BDL_41] + c, C);
+  dly_regs_store(h42, S.dl[BDL_42] + c, C);
+  dly_regs_store(h8, S.dl[BDL_8] + c, C);
+  dly_regs_store(hA1, S.dl[BDL_A1] + c, C);
+  is[(BI_DL_P0 + BDL_S) * C] = 0;
+  is[(BI_DL_P0 + BDL_41) * C] = 0;
+  is[(BI_DL_P0 + BDL_42) * C] = 0;
+  is[(BI_DL_P0 + BDL_8) * C] = 0;
+  is[(BI_DL_P0 + BDL_A1) * C] = 0;
   is[BI_MSEMA_P * C] = msema_p;
   is[BI_STARTSTOP * C] = startstop;
   is[BI_CNTR * C] = cntr;

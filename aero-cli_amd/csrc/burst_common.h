@@ -50,6 +50,10 @@ constexpr int TRI_GRID = 1024;   // trident workgroups (each loops over the pass
 // Delay<T> instances (ring size, fractional delay): delays(1), delayt41/42(T/4),
 // delayt8(T/8), a1(T/2), bt_d1(T, complex), bt_ma_diff(128 T)
 enum BurstDelay { BDL_S = 0, BDL_41, BDL_42, BDL_8, BDL_A1, BDL_BT, BDL_MADIFF, BDL_COUNT };
+// ring sizes ceil(delay) + 1 of the part-B delays the demodulator keeps in
+// registers (delays 1, SPS/4, SPS/4, SPS/8, SPS/2 with SPS = 2 * 48000 /
+// 10500; burst_engine.hip checks them against the host tables)
+constexpr int BDL_N_S = 2, BDL_N_41 = 4, BDL_N_42 = 4, BDL_N_8 = 3, BDL_N_A1 = 6;
 
 // double state fields
 enum BDS : int {

@@ -132,6 +132,32 @@ __device__ __forceinline__ double dly_commit(double *ring, int C, int &p, const 
   const double newer = r.newer_is_sig ? sig : r.newer;
   return (r.w * newer + r.om * r.older);
 }
+// The demodulator's short fractional delays (sizes 2..6) held in registers,
+// h[i] = the value written i updates ago (h[0] the newest): the update
+// shifts and returns w * h[N-2] + om * h[N-1], exactly dly_commit's
+// w * newer + om * older (older = the slot after the write pointer, i.e.
+// N-1 updates old; newer = N-2 updates old, the value just written when
+// N == 2).  The weights are the same for every write pointer (checked on
+// the host, burst_engine.hip).  dly_regs_load / dly_regs_store convert
+// from / to the ring [N][C] with write pointer p (stored back with p = 0).
+template <int N>
+__device__ __forceinline__ double dly_reg(double (&h)[N], double w, double om, double sig) {
+#pragma unroll
+  for (int i = N - 1; i > 0; --i) h[i] = h[i - 1];
+  h[0] = sig;
+  return (w * h[N - 2] + om * h[N - 1]);
+}
+template <int N>
+__device__ __forceinline__ void dly_regs_load(double (&h)[N], const double *ring, int C, int p) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) h[i] = ring[(size_t)(((p - 1 - i) % N + N) % N) * C];
+}
+template <int N>
+__device__ __forceinline__ void dly_regs_store(const double (&h)[N], double *ring, int C) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) ring[(size_t)(N - 1 - i) * C] = h[i];
+}
+
 struct DlyPre2 {
   double w, om;
   double2 older, newer;

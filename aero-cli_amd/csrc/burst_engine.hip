@@ -484,6 +484,14 @@ int burst_group_create(int device, int flags, int max_channels, int kind, BurstG
     for (int q = 0; q < size; q++)
       if (io[q] != (q + 1) % size) return AERO_E_INVALID;
     if (k == BDL_BT && size <= 2) return AERO_E_INVALID;  // dly_pre2 has no newer-is-sig case
+    // the part-B delays live in registers (burst.hip): their sizes are
+    // compile-time and their weights must not depend on the write pointer
+    const int reg_n[BDL_COUNT] = {BDL_N_S, BDL_N_41, BDL_N_42, BDL_N_8, BDL_N_A1, 0, 0};
+    if (reg_n[k]) {
+      if (size != reg_n[k]) return AERO_E_INVALID;
+      for (int q = 1; q < size; q++)
+        if (w[q] != w[0] || omw[q] != omw[0]) return AERO_E_INVALID;
+    }
     g->T.dsize[k] = size;
     if (int rc = h2d(g->T.dw[k], w)) return rc;
     if (int rc = h2d(g->T.domw[k], omw)) return rc;
