@@ -34,6 +34,10 @@ MODES = {
     'oqpsk10500': dict(bitrate=10500, hop=4096, fs=48000, bytes=18.22, timing='demod',
                        metric='Msamples/s demod+Viterbi, 10500bps OQPSK, 1/2/4/8 GPU; ACARS frames bit-exact vs ref',
                        cpu_seconds=240.0, config='C2', flops=1300.0, nfft_log2=14,
+                       # the coarse kernel's own algorithmic bytes per channel-hop: the
+                       # 16384-entry uint32 snapshot ring read once, the y history of
+                       # bins 2815..13568 (coarse.hip CoarseK<OQPSK>) read and written
+                       coarse_hop_bytes=16384 * 4 + 2 * (13568 - 2815 + 1) * 8,
                        kernels={'demod': 'demod_oqpsk_kernel', 'coarse': 'coarse_kernel', 'frame': 'frame_kernel',
                                 'viterbi': 'viterbi_kernel'}),
     # 2 B int16 in + 0.05 B soft bits out
@@ -760,15 +764,25 @@ def main():
     if rank == 0:
         value = samples / elapsed / 1e6
         # roofline of the dominant kernel (the most device time per step):
-        # the path's algorithmic bytes per step (bytes per
-        # input sample x samples of a step) over that kernel's summed time
-        # per step; the whole step's fraction beside it
+        # that kernel's algorithmic bytes per step over its summed time per
+        # step.  The demodulator carries the path's bytes (SURVEY §8(d):
+        # bytes per input sample x samples of a step); the coarse kernel its
+        # own (snapshot ring + y history per channel-hop, one hop per channel
+        # per launch).  The path figure over the demodulator and the whole
+        # step are reported beside it.
         steps = max(a.steps, 1)
         dom = max(kt, key=lambda k: kt[k][0])
         dom_ms = kt[dom][0] / steps
-        step_bytes = M['bytes'] * C * HOP
+        path_bytes = M['bytes'] * C * HOP
+        step_bytes = path_bytes
+        unit = {'bytes_per_sample': M['bytes']}
+        if dom == 'coarse' and 'coarse_hop_bytes' in M:
+            step_bytes = M['coarse_hop_bytes'] * C * (kt[dom][1] / steps)
+            unit = {'bytes_per_channel_hop': M['coarse_hop_bytes']}
         achieved = step_bytes / (dom_ms / 1e3) / 1e9
-        step_achieved = step_bytes / (elapsed / steps) / 1e9
+        step_achieved = path_bytes / (elapsed / steps) / 1e9
+        path_kernel = 'demod' if 'demod' in kt else dom
+        path_ms = kt[path_kernel][0] / steps
         traffic, traffic_src = pmc_traffic(a.pmc or os.path.join(ROOT, 'profiles', 'pmc_%s.json' % a.mode),
                                            a.mode, C, M['kernels'][dom])
         total_ms = sum(v[0] for v in kt.values()) / steps
@@ -800,13 +814,19 @@ def main():
                                        FS, HOP)),
                        'channels_per_gpu': C, 'total_channels': C * world, 'hop_samples': HOP,
                        'parallelism': 'channel-sharded x%d' % world},
-            'roofline': {'bound': 'hbm', 'kernel': M['kernels'][dom], 'achieved': round(achieved, 2),
-                         'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
-                         'traffic': traffic, 'traffic_source': traffic_src, 'bytes_per_sample': M['bytes'],
-                         'bytes_per_step': int(step_bytes), 'kernel_ms_per_step': round(dom_ms, 3),
-                         'launches_per_step': round(kt[dom][1] / steps, 2),
-                         'step': {'achieved': round(step_achieved, 2), 'frac': round(step_achieved / HBM_PEAK_GBS, 5),
-                                  'ms_per_step': round(elapsed / steps * 1e3, 3)}},
+            'roofline': dict({'bound': 'hbm', 'kernel': M['kernels'][dom], 'achieved': round(achieved, 2),
+                              'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
+                              'traffic': traffic, 'traffic_source': traffic_src},
+                             **unit, **{
+                              'bytes_per_step': int(step_bytes), 'kernel_ms_per_step': round(dom_ms, 3),
+                              'launches_per_step': round(kt[dom][1] / steps, 2),
+                              'path': {'kernel': M['kernels'][path_kernel], 'bytes_per_sample': M['bytes'],
+                                       'bytes_per_step': int(path_bytes),
+                                       'achieved': round(path_bytes / (path_ms / 1e3) / 1e9, 2),
+                                       'frac': round(path_bytes / (path_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)},
+                              'step': {'achieved': round(step_achieved, 2),
+                                       'frac': round(step_achieved / HBM_PEAK_GBS, 5),
+                                       'ms_per_step': round(elapsed / steps * 1e3, 3)}}),
             'kernels': kernels,
             # SURVEY §8(d) / BASELINE.md: the path is FP64-VALU bound, so the whole-path FP64
             # rate (algorithmic flop per input sample x samples/s) is reported beside the HBM one
