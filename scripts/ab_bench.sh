@@ -11,5 +11,5 @@ for v in $VARS; do
   if [ "$v" = base ]; then so=$R/aero-cli_amd/libaero_engine.so; else so=$R/aero-cli_amd/libaero_engine_$v.so; fi
   # a timing-only variant may decode nothing (bench then exits 1): keep its line
   AERO_ENGINE_SO=$so timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline "$@" > $OUT/$v.log 2>&1 || [ $? -eq 1 ]
-  echo "$v $(tail -1 $OUT/$v.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["kernel_ms_per_step"])')"
+  echo "$v $(tail -1 $OUT/$v.log | python3 $R/scripts/ab_line.py)"
 done
