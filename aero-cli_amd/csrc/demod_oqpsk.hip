@@ -400,8 +400,10 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       asm volatile("" : "+v"(cl));
       double *marg = S.marg + (size_t)cl * MARG_LEN;
       double2 *dtb = S.dt + (size_t)cl * DT_LEN;
-      double *pmb = S.pm + (size_t)cl * MSE_LEN;
-      double *msb = S.ms + (size_t)cl * MSE_LEN;
+      // MSEcalc's two moving averages advance together (pm_p == ms_p at
+      // every event), so their slots share one 16-byte entry: one line per
+      // event instead of two
+      double2 *pmsb = reinterpret_cast<double2 *>(S.pm) + (size_t)cl * MSE_LEN;
       int marg_p = s_pi[PI_MARG_P][pair], dt_p = s_pi[PI_DT_P][pair];
       int pm_p = s_pi[PI_PM_P][pair], ms_p = s_pi[PI_MS_P][pair];
       const double pr = ev_pr, pi = ev_pi;
@@ -410,8 +412,8 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       const int dt_rp = (dt_p + 1) % DT_LEN;
       const double marg_old = marg[marg_p];
       const double2 dv = dtb[dt_rp];
-      const double pm_old = pmb[pm_p];
-      const double ms_old = msb[ms_p];
+      const double2 pms_old = pmsb[pm_p];
+      const double pm_old = pms_old.x, ms_old = pms_old.y;
       double ctx1 = s_pd[PD_CTX1][pair], ctx2 = s_pd[PD_CTX2][pair];
       double cty1 = s_pd[PD_CTY1][pair], cty2 = s_pd[PD_CTY2][pair];
       double marg_sum = s_pd[PD_MARG_SUM][pair], pm_sum = s_pd[PD_PM_SUM][pair];
@@ -463,7 +465,7 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
         const double av = DM_HYPOT(qr, qi);
         pm_sum = pm_sum - pm_old;
         pm_sum = pm_sum + fabs(av);
-        pmb[pm_p] = fabs(av);
+        const int pms_slot = pm_p;
         pm_p++;
         pm_p %= MSE_LEN;
         double mu = DM_DIVC(pm_sum, ((double)MSE_LEN));
@@ -473,7 +475,7 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
         const double v = (tda * tda) + (tdb * tdb);
         ms_sum = ms_sum - ms_old;
         ms_sum = ms_sum + fabs(v);
-        msb[ms_p] = fabs(v);
+        pmsb[pms_slot] = make_double2(fabs(av), fabs(v));
         ms_p++;
         ms_p %= MSE_LEN;
         mse = DM_DIVC(ms_sum, ((double)MSE_LEN));

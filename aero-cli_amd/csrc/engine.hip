@@ -332,8 +332,9 @@ size_t layout(DevState &S, DevTables &T, int mode, int C, int flags, char *base)
   S.d8 = carve<double>(p, msk ? (size_t)g.d8_len * C : 1);
   S.marg = carve<double>(p, (size_t)g.marg_len * C);
   S.dt = carve<double2>(p, (size_t)g.dt_len * C);
-  S.pm = carve<double>(p, msk ? 1 : (size_t)g.ms_len * C);
-  S.ms = carve<double>(p, (size_t)g.ms_len * C);
+  // OQPSK: pm holds MSEcalc's (pm, ms) pairs, [C][ms_len] double2 (demod_oqpsk.hip); MSK: ms = msema
+  S.pm = carve<double>(p, msk ? 1 : (size_t)2 * g.ms_len * C);
+  S.ms = carve<double>(p, msk ? (size_t)g.ms_len * C : 1);
   S.pcm = carve<int16_t>(p, (size_t)PCM_CAP * C);
   S.pcm_cap = PCM_CAP;
   S.cring = carve<uint32_t>(p, (size_t)g.nfft * C);

@@ -143,7 +143,7 @@ struct DevState {
   double *d8;              // MSK delayt8 ring [d8_len][C] (time-major)
   double *marg;            // [C][marg_len]
   double2 *dt;             // [C][dt_len]
-  double *pm, *ms;         // [C][ms_len] each (MSK: ms = msema)
+  double *pm, *ms;         // OQPSK: pm = [C][ms_len] (pm, ms) double2 pairs; MSK: ms = msema [C][ms_len]
   int16_t *pcm;            // [PCM_CAP][C] input ring (time-major)
   long long pcm_cap;       // power of 2
   uint32_t *cring;         // [C][nfft] coarse ring: cis index | pcm << 16 (demod-written)

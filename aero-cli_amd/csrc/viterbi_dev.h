@@ -201,11 +201,11 @@ __device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nso
     }
   };
   // the soft pairs of the next 64 steps: lane l holds step i0 + l's pair
-  // (a | b << 8); a step takes its pair with one v_readlane, so no LDS read
+  // (a | b << 16); a step takes its pair with one v_readlane, so no LDS read
   // sits on the step's dependency chain
   auto pairs = [&](int i0) -> uint32_t {
     const int st = i0 + lane;
-    return st < sets ? (uint32_t)sbuf[2 * st] | ((uint32_t)sbuf[2 * st + 1] << 8) : 0u;
+    return st < sets ? (uint32_t)sbuf[2 * st] | ((uint32_t)sbuf[2 * st + 1] << 16) : 0u;
   };
   // Steps before the restricted tail (every state active) in runs that no
   // event interrupts: a run ends where the column index leaves its register
@@ -222,6 +222,8 @@ __device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nso
   const int tail0 = sets - 6 > 6 ? sets - 6 : 6;
   {
     const int msa = (tab_lo & 1) ? 1 : -1, msb = (tab_lo & 2) ? 1 : -1;  // -sa, -sb
+    typedef short v2s __attribute__((ext_vector_type(2)));
+    const v2s coef = {(short)msa, (short)msb};
     const int nbase = -(((tab_lo & 1) ? 255 : 0) + ((tab_lo & 2) ? 255 : 0));
     const int src0 = (s >> 1) << 2, src1 = ((s >> 1) | 32) << 2;
     int i = 6;
@@ -241,9 +243,10 @@ __device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nso
         const int col0 = idx & 63;
         for (int k = 0; k < run; ++k) {
           const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane((int)pv, pk + k);
-          const int ca = (int)(ab & 255u), cb = (int)(ab >> 8);
           const int m0 = __builtin_amdgcn_ds_bpermute(src0, m), m1 = __builtin_amdgcn_ds_bpermute(src1, m);
-          const int nd = nbase + __mul24(msa, ca) + __mul24(msb, cb);  // -soft_dist(tab_lo, ca, cb)
+          // -soft_dist(tab_lo, a, b) = nbase - sa a - sb b as one 16-bit dot
+          // product (v_dot2c_i32_i16, exact integer arithmetic)
+          const int nd = __builtin_amdgcn_sdot2(coef, __builtin_bit_cast(v2s, ab), nbase, false);
           const int e0 = (m0 - nd) & 0xFFFF;
           const int e1 = (m1 + 510 + nd) & 0xFFFF;
           const uint64_t mask = __ballot(e0 > e1);

@@ -103,9 +103,10 @@ def parse():
                          'the GPU box CPU share)')
     ap.add_argument('--cpu-runs', type=int, default=3, help='CPU-baseline repetitions (the median is reported)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--h2d-steps', type=int, default=10,
+    ap.add_argument('--h2d-steps', type=int, default=None,
                     help='continuous modes: steps of the second, H2D-inclusive timed region (int16 blocks pushed '
-                         'from pinned host memory inside it); 0 skips it')
+                         'from pinned host memory inside it; default: as many as --steps, so both regions carry '
+                         'the same pipeline fill and drain); 0 skips it')
     ap.add_argument('--pmc', default=None,
                     help='rocprofv3 PMC summary for the roofline traffic field (default profiles/pmc_<mode>.json; '
                          'used only when it was captured at this mode and channel count)')
@@ -648,7 +649,7 @@ def main():
     preroll = M.get('preroll', PREROLL_HOPS)  # burst channels have no hunter to lock
     pre = preroll + a.warmup  # untimed hops: lock-in pre-roll + warmup
     burst = bool(M.get('burst'))
-    h2d_steps = 0 if burst else max(0, a.h2d_steps)
+    h2d_steps = 0 if burst else max(0, a.steps if a.h2d_steps is None else a.h2d_steps)
     steps_total = pre + a.steps + h2d_steps
     span = steps_total * HOP
     offsets = shard.channel_offsets(C, P, rank)
