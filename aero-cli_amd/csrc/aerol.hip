@@ -283,6 +283,7 @@ __global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, in
   // grid-stride over the jobs of this pass (the job count stays on the device,
   // so the host launches without waiting for the framing kernel)
   const int njobs = *S.njobs;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && S.njobs_host) *S.njobs_host = njobs;
   for (int job = blockIdx.x; job < njobs; job += gridDim.x) {
   __syncthreads();  // LDS of the previous job fully consumed
 #ifdef AERO_X_STAMPS

@@ -247,8 +247,10 @@ struct Group {
     hipEvent_t ev_vit = nullptr;  // this pass's Viterbi done (main stream)
     hipEvent_t ev_framed = nullptr;  // this pass's framing done (main stream)
     bool trace_blocks = false;
-    uint8_t *h_out = nullptr;   // pinned copy of the first `copied` records
-    int *h_n = nullptr;         // pinned copy of the count
+    uint8_t *h_out = nullptr;   // pinned host records, written by the Viterbi kernel
+    int *h_n = nullptr;         // pinned host job count, written by the Viterbi kernel
+    uint8_t *h_out_dev = nullptr;  // the same buffers as the device addresses them
+    int *h_n_dev = nullptr;
     int copied = 0;
     hipEvent_t ev = nullptr;
     bool pending = false;
@@ -628,20 +630,23 @@ int issue_viterbi(Group *e) {
   auto &sl = e->slot[si];
   DevState S2 = e->S;
   S2.njobs = sl.d_n;
-  S2.jobout = sl.d_out;
   S2.jobs = sl.d_jobs;
+  // The kernel writes the job records and their count straight into the
+  // slot's pinned host buffers (3.6 MB per pass at the bench config, over
+  // PCIe while it decodes): no device-to-host copy is queued.  A queued copy
+  // waiting for this kernel held back the next push's host-to-device DMA
+  // until the whole pass had finished (copies of the process run in order),
+  // which serialised a host-pushed stream with the GPU work.
+  S2.jobout = sl.h_out_dev;
+  S2.njobs_host = sl.h_n_dev;
   hipEvent_t a, b;
   ev_begin(e, "viterbi", a, b);
   launch_viterbi(e->st, e->mode, S2, e->T, e->nch, sl.trace_blocks ? 1 : 0);
   ev_end(e, b);
   HIPCHK(hipEventRecord(sl.ev_vit, e->st));
-  HIPCHK(hipStreamWaitEvent(e->st_vit, sl.ev_vit, 0));
   HIPCHK(hipGetLastError());
-  // async hand-off: the count plus the records the job count is likely to need
-  sl.copied = std::min(e->nch, e->max_jobs_seen + e->max_jobs_seen / 4 + 256);
-  HIPCHK(hipMemcpyAsync(sl.h_n, sl.d_n, sizeof(int), hipMemcpyDeviceToHost, e->st_vit));
-  HIPCHK(hipMemcpyAsync(sl.h_out, sl.d_out, (size_t)sl.copied * JOB_OUT, hipMemcpyDeviceToHost, e->st_vit));
-  HIPCHK(hipEventRecord(sl.ev, e->st_vit));
+  sl.copied = e->nch;  // every record is in host memory
+  HIPCHK(hipEventRecord(sl.ev, e->st));
   sl.pending = true;
   e->pending_slots.push_back(si);
   return AERO_OK;
@@ -833,6 +838,8 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
     if (hipMalloc(&sl.d_n, 64) != hipSuccess) return AERO_E_NOMEM;
     if (hipHostMalloc(&sl.h_out, (size_t)JOB_OUT * e->C) != hipSuccess) return AERO_E_NOMEM;
     if (hipHostMalloc(&sl.h_n, 64) != hipSuccess) return AERO_E_NOMEM;
+    HIPCHK(hipHostGetDevicePointer((void **)&sl.h_out_dev, sl.h_out, 0));
+    HIPCHK(hipHostGetDevicePointer((void **)&sl.h_n_dev, sl.h_n, 0));
     if (hipMalloc(&sl.d_jobs, (size_t)16 * e->C) != hipSuccess) return AERO_E_NOMEM;
     HIPCHK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_vit, hipEventDisableTiming));
@@ -1068,7 +1075,10 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
     HIPCHK(copy(e->S.pcm + r0 * e->C + c0, src, n1));
     if (n1 < n) HIPCHK(copy(e->S.pcm + c0, src + n1 * ld, n - n1));
     HIPCHK(hipEventRecord(e->ev_in, e->st_in));
-    HIPCHK(hipEventSynchronize(e->ev_in));  // the caller's buffer is free again
+    {
+      HOST_TIMER(e, "host_push_copy");
+      HIPCHK(hipEventSynchronize(e->ev_in));  // the caller's buffer is free again
+    }
     HIPCHK(hipStreamWaitEvent(e->st, e->ev_in, 0));
     for (int j = 0; j < nch; j++) e->avail[c0 + j] += (long long)n;
   }
@@ -1086,7 +1096,10 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
   // device copy of the counters, from pinned staging (stream-ordered before the next demod)
   const int k = e->next_pin;
   e->next_pin = (k + 1) % Group::NPIN;
-  HIPCHK(hipEventSynchronize(e->pin_ev[k]));
+  {
+    HOST_TIMER(e, "host_push_pin");
+    HIPCHK(hipEventSynchronize(e->pin_ev[k]));
+  }
   memcpy(e->pin_avail[k], e->avail.data() + c0, 8 * (size_t)nch);
   HIPCHK(hipMemcpyAsync(e->S.ls + (size_t)LS_AVAIL * e->C + c0, e->pin_avail[k], 8 * nch, hipMemcpyHostToDevice,
                         e->st));

@@ -161,7 +161,8 @@ struct DevState {
   uint8_t *dl2;            // [C][dl2_len]
   int *jobs;               // [C] job list: channel | (buf << 24)
   int *njobs;              // [1]
-  uint8_t *jobout;         // [C][JOB_OUT]
+  uint8_t *jobout;         // [C][JOB_OUT] (the Viterbi writes it in pinned host memory)
+  int *njobs_host;         // [1] pinned host copy of the job count, written by the Viterbi kernel
   uint8_t *blocks_dbg;     // [C][2500] decoded bits (trace)
 };
 

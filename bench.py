@@ -729,11 +729,20 @@ def main():
         s1 = eng.samples_processed()
         if world > 1:
             dist.barrier()
+        eng.timing_reset()
         t1 = time.perf_counter()
+        tp = [0.0, 0.0, 0.0]  # host seconds in push (incl. the wait for its DMA), run, item drain
         for xh in host_inputs:
+            ta = time.perf_counter()
             eng.push_batch_host(xh.data_ptr(), HOP, C, C)
+            tb = time.perf_counter()
             eng.run()
+            tc = time.perf_counter()
             eng.drain_items()
+            td = time.perf_counter()
+            tp[0] += tb - ta
+            tp[1] += tc - tb
+            tp[2] += td - tc
         eng.sync()
         eng.drain_items()
         torch.cuda.synchronize()
@@ -749,6 +758,10 @@ def main():
         h2d = {'value': round(h_smp / h_el / 1e6, 3), 'unit': 'Msamples/s', 'steps': h2d_steps,
                'ms_per_step': round(h_el / h2d_steps * 1e3, 3),
                'pcie_bytes_per_step': 2 * HOP * C * world,
+               'host_ms_per_step': {k: round(v / h2d_steps * 1e3, 3) for k, v in zip(('push', 'run', 'drain'), tp)},
+               'engine_host_ms_per_step': {k: round(eng.timing(k)[0] / h2d_steps, 3)
+                                           for k in ('host_push', 'host_push_copy', 'host_push_pin', 'host_run',
+                                                     'host_wait_jobs')},
                'note': 'same steps, int16 [hop, channels] blocks pushed from pinned host memory '
                        '(aero_push_pcm_batch, dev=0) inside the timed region'}
         del host_inputs
