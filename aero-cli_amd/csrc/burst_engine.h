@@ -10,6 +10,7 @@
 namespace aero {
 
 struct BurstGroup;
+class HostPool;
 enum BurstKind { BURST_OQPSK = 0, BURST_MSK = 1 };  // 10500 OQPSK / 600-1200 MSK (both bit rates in one group)
 int burst_group_create(int device, int flags, int max_channels, int kind, BurstGroup **out);
 void burst_group_destroy(BurstGroup *g);
@@ -28,5 +29,6 @@ uint64_t burst_stat(const BurstGroup *g, int which);  // 0: R/T tests run, 1: R/
 int burst_dcd_edges(BurstGroup *g, int c, int64_t *edges);  // AeroL datacd changes (waits for the group's work)
 void burst_timing(BurstGroup *g, const char *name, double *ms, long *launches);  // adds to *ms / *launches
 void burst_timing_reset(BurstGroup *g);
+void burst_group_set_pool(BurstGroup *g, HostPool *pool);  // host threads for the R/T tests (the engine's)
 
 }  // namespace aero

@@ -28,6 +28,7 @@
 #include "burst_common.h"
 #include "burst_engine.h"
 #include "engine_common.h"
+#include "host_pool.h"
 #include "tables_host.h"
 
 namespace aero {
@@ -138,6 +139,7 @@ std::vector<uint8_t> pack_bits(const std::vector<int> &bits) {
 
 struct BurstGroup {
   int device = 0, flags = 0, C = 0, nch = 0, kind = BURST_OQPSK;
+  HostPool *hpool = nullptr;  // the engine's host threads (R/T tests by channel)
   std::vector<int> tsu, tblocks;  // MSK: updateMSK's targetSUSize / targetBlocks per channel
   hipStream_t st = nullptr;
   BurstState S{};
@@ -269,9 +271,9 @@ void collect_timing(BurstGroup *g) {
   g->pending_ev.clear();
 }
 
-int run_once(BurstGroup *g, bool trace, bool &progress) {
+// one pass's kernels (asynchronous)
+int launch_pass(BurstGroup *g, bool trace) {
   const int nch = g->nch;
-  progress = false;
   const bool msk = g->kind == BURST_MSK;
   // Hilbert FIR -> front end (runs ahead, records the trident checks it
   // completes) -> the checks' decisions -> the demodulator up to the front
@@ -293,23 +295,87 @@ int run_once(BurstGroup *g, bool trace, bool &progress) {
   else
     timed(g, "burst_frame", [&] { launch_frame_burst(g->st, g->S, nch); });
   timed(g, "burst_viterbi", [&] { launch_rt_viterbi(g->st, g->S, nch * RT_TESTS_PER_PASS); });
+  return AERO_OK;
+}
+
+// waits for the pass, takes its R/T test records and counters, runs the
+// parity traces, and says whether another pass has work
+int finish_pass(BurstGroup *g, bool trace, std::vector<uint8_t> &jobs, int &njobs, bool &progress) {
+  const int nch = g->nch;
   BCHK(hipGetLastError());
-  int njobs = 0;
+  njobs = 0;
   BCHK(hipMemcpyAsync(&njobs, g->S.njobs, sizeof(int), hipMemcpyDeviceToHost, g->st));
   std::vector<long long> ls((size_t)BL_COUNT * g->C);
   BCHK(hipMemcpyAsync(ls.data(), g->S.ls, ls.size() * 8, hipMemcpyDeviceToHost, g->st));
   BCHK(hipStreamSynchronize(g->st));
-  std::vector<uint8_t> jobs((size_t)std::max(njobs, 1) * RT_JOB_OUT);
+  jobs.resize((size_t)std::max(njobs, 1) * RT_JOB_OUT);
   if (njobs > 0)
     BCHK(hipMemcpy(jobs.data(), g->S.jobout, (size_t)njobs * RT_JOB_OUT, hipMemcpyDeviceToHost));
-  // R/T tests in emission order (a channel's tests come from one lane, in order)
-  std::vector<int> bits, deconvol;
+  // traces: committed soft entries (with the start-of-packet markers) and trident records
+  if (g->flags & AERO_F_TRACE_SOFT) {
+    std::vector<int16_t> ring;
+    for (int c = 0; c < nch; c++) {
+      const long long com = ls[(size_t)BL_SCOMMIT * g->C + c];
+      if (com <= g->soft_seen[c]) continue;
+      if (ring.empty()) {
+        ring.resize((size_t)B_SOFT_RING * nch);
+        BCHK(hipMemcpy(ring.data(), g->S.soft, ring.size() * 2, hipMemcpyDeviceToHost));
+      }
+      for (long long k = g->soft_seen[c]; k < com; k++) {
+        const int e = ring[(size_t)c * B_SOFT_RING + (k & (B_SOFT_RING - 1))] & 0x1FF;
+        g->soft_hold[c].push_back(e == B_SOFT_MARK ? (int16_t)-1 : (int16_t)e);
+      }
+      g->soft_seen[c] = com;
+    }
+  }
+  if (g->flags & AERO_F_TRACE_HOPS) {  // trident records of this pass, then the counters restart
+    std::vector<int> hn(nch);
+    BCHK(hipMemcpy(hn.data(), g->S.hop_n, sizeof(int) * nch, hipMemcpyDeviceToHost));
+    std::vector<double> hops;
+    for (int c = 0; c < nch; c++) {
+      if (hn[c] <= 0) continue;
+      if (hn[c] > B_HOP_CAP) return AERO_E_FULL;
+      if (hops.empty()) {
+        hops.resize((size_t)B_HOP_CAP * 6 * nch);
+        BCHK(hipMemcpy(hops.data(), g->S.hops, hops.size() * 8, hipMemcpyDeviceToHost));
+      }
+      g->hop_hold[c].insert(g->hop_hold[c].end(), hops.begin() + (size_t)c * B_HOP_CAP * 6,
+                            hops.begin() + ((size_t)c * B_HOP_CAP + hn[c]) * 6);
+    }
+    BCHK(hipMemset(g->S.hop_n, 0, sizeof(int) * nch));
+  }
+  // more passes while any channel has samples or committed soft bits left
+  long long work = 0;
+  for (int c = 0; c < nch; c++) {
+    work += (g->avail[c] - ls[(size_t)BL_NSAMP * g->C + c]) +
+            (ls[(size_t)BL_SCOMMIT * g->C + c] - ls[(size_t)BL_SCONS * g->C + c]);
+  }
+  progress = work > 0 && (work != g->last_work || njobs > 0);
+  g->last_work = work;
+  return AERO_OK;
+}
+
+
+// the host side of a pass's R/T tests (RTChannelDeleaveFECScram::update /
+// updateMSK: descramble, CRCs, packet assembly, ACARS)
+void process_tests(BurstGroup *g, const std::vector<uint8_t> &jobs, int njobs) {
+  const int nch = g->nch;
+  const bool msk = g->kind == BURST_MSK;
+  // R/T tests in emission order (a channel's tests come from one lane, in
+  // order).  Every piece of state a test touches is its channel's, so the
+  // tests are split over the host pool by channel (c % T == t), each thread
+  // taking its channels' tests in emission order.
+  const int T = (g->hpool && njobs >= 256) ? std::min(g->hpool->size(), std::max(1, njobs / 128)) : 1;
+  std::vector<uint64_t> n_tests(T, 0), n_packets(T, 0);
+  auto tests = [&](int t, int TT) {
+  std::vector<int> deconvol;
   for (int j = 0; j < njobs; j++) {
     const uint8_t *rec = jobs.data() + (size_t)j * RT_JOB_OUT;
     int h[4];
     memcpy(h, rec, 16);
     const int c = h[0], bp = h[1], burst = h[2], nbits = h[3];
-    if (c < 0 || c >= nch || burst == g->ok_burst[c]) continue;  // packet already decoded: the block is FULL
+    if (c < 0 || c >= nch || c % TT != t) continue;
+    if (burst == g->ok_burst[c]) continue;  // packet already decoded: the block is FULL
     deconvol.assign(nbits, 0);
     for (int b = 0; b < nbits; b++) deconvol[b] = ((rec[16 + b / 8] >> (7 - (b % 8))) & 1) ^ g->scr[b];
     enum { OK_R = 3, OK_T = 5, Bad = 0, Test_Failed = 32, Nothing = 8 };
@@ -370,13 +436,13 @@ int run_once(BurstGroup *g, bool trace, bool &progress) {
         if (!info.empty()) info.pop_back();  // infofield.chop(1)
       }
     }
-    g->st_tests++;
+    n_tests[t]++;
     if (g->flags & AERO_F_TRACE_FRAMES) {
       const uint32_t t2[2] = {(uint32_t)bp, (uint32_t)result};
       g->tests_hold[c].insert(g->tests_hold[c].end(), (const uint8_t *)t2, (const uint8_t *)t2 + 8);
     }
     if (result == OK_R || result == OK_T) {
-      g->st_packets++;
+      n_packets[t]++;
       g->ok_burst[c] = burst;
       if (g->flags & AERO_F_TRACE_FRAMES) {
         const uint32_t p2[2] = {(uint32_t)(result == OK_R ? 'R' : 'T'), (uint32_t)info.size()};
@@ -387,48 +453,17 @@ int run_once(BurstGroup *g, bool trace, bool &progress) {
       g->host[c]->rt_packet(result == OK_R, info.data(), (int)info.size(), nsus);
     }
   }
-  // traces: committed soft entries (with the start-of-packet markers) and trident records
-  if (g->flags & AERO_F_TRACE_SOFT) {
-    std::vector<int16_t> ring;
-    for (int c = 0; c < nch; c++) {
-      const long long com = ls[(size_t)BL_SCOMMIT * g->C + c];
-      if (com <= g->soft_seen[c]) continue;
-      if (ring.empty()) {
-        ring.resize((size_t)B_SOFT_RING * nch);
-        BCHK(hipMemcpy(ring.data(), g->S.soft, ring.size() * 2, hipMemcpyDeviceToHost));
-      }
-      for (long long k = g->soft_seen[c]; k < com; k++) {
-        const int e = ring[(size_t)c * B_SOFT_RING + (k & (B_SOFT_RING - 1))] & 0x1FF;
-        g->soft_hold[c].push_back(e == B_SOFT_MARK ? (int16_t)-1 : (int16_t)e);
-      }
-      g->soft_seen[c] = com;
-    }
+  };
+  if (T > 1) {
+    g->hpool->submit(tests, T);
+    g->hpool->wait();
+  } else {
+    tests(0, 1);
   }
-  if (g->flags & AERO_F_TRACE_HOPS) {  // trident records of this pass, then the counters restart
-    std::vector<int> hn(nch);
-    BCHK(hipMemcpy(hn.data(), g->S.hop_n, sizeof(int) * nch, hipMemcpyDeviceToHost));
-    std::vector<double> hops;
-    for (int c = 0; c < nch; c++) {
-      if (hn[c] <= 0) continue;
-      if (hn[c] > B_HOP_CAP) return AERO_E_FULL;
-      if (hops.empty()) {
-        hops.resize((size_t)B_HOP_CAP * 6 * nch);
-        BCHK(hipMemcpy(hops.data(), g->S.hops, hops.size() * 8, hipMemcpyDeviceToHost));
-      }
-      g->hop_hold[c].insert(g->hop_hold[c].end(), hops.begin() + (size_t)c * B_HOP_CAP * 6,
-                            hops.begin() + ((size_t)c * B_HOP_CAP + hn[c]) * 6);
-    }
-    BCHK(hipMemset(g->S.hop_n, 0, sizeof(int) * nch));
+  for (int t = 0; t < T; t++) {
+    g->st_tests += n_tests[t];
+    g->st_packets += n_packets[t];
   }
-  // more passes while any channel has samples or committed soft bits left
-  long long work = 0;
-  for (int c = 0; c < nch; c++) {
-    work += (g->avail[c] - ls[(size_t)BL_NSAMP * g->C + c]) +
-            (ls[(size_t)BL_SCOMMIT * g->C + c] - ls[(size_t)BL_SCONS * g->C + c]);
-  }
-  progress = work > 0 && (work != g->last_work || njobs > 0);
-  g->last_work = work;
-  return AERO_OK;
 }
 
 }  // namespace
@@ -513,6 +548,10 @@ int burst_group_create(int device, int flags, int max_channels, int kind, BurstG
   host_scrambler(g->scr.data());
   *out = g.release();
   return AERO_OK;
+}
+
+void burst_group_set_pool(BurstGroup *g, HostPool *pool) {
+  if (g) g->hpool = pool;
 }
 
 void burst_group_destroy(BurstGroup *g) {
@@ -614,10 +653,22 @@ int burst_run(BurstGroup *g, int flush) {
   if (int rc = flush_init(g)) return rc;
   const bool trace = (g->flags & (AERO_F_TRACE_HOPS | AERO_F_TRACE_SOFT)) != 0;
   g->last_work = -1;
+  std::vector<uint8_t> jobs;
+  int njobs = 0;
+  bool more = false;
+  if (int rc = launch_pass(g, trace)) return rc;
+  if (int rc = finish_pass(g, trace, jobs, njobs, more)) return rc;
   for (int guard = 0; guard < 100000; guard++) {
-    bool more = false;
-    if (int rc = run_once(g, trace, more)) return rc;
+    // the next pass is launched before this pass's R/T tests are handled on
+    // the host (they only touch host state), so that work overlaps the GPU;
+    // parity traces read device state between passes and keep them apart
+    if (more && !trace)
+      if (int rc = launch_pass(g, trace)) return rc;
+    process_tests(g, jobs, njobs);
     if (!more) break;
+    if (trace)
+      if (int rc = launch_pass(g, trace)) return rc;
+    if (int rc = finish_pass(g, trace, jobs, njobs, more)) return rc;
   }
   for (int c = 0; c < g->nch; c++) {
     g->hb_base[c] = (g->avail[c] / HB_SNZ) * HB_SNZ;
