@@ -2300,24 +2300,30 @@ struct PeakDetector {
 
 // QJHilbertFilter on JFastFir (decode/DSP.cpp:730-761, decode/jfft.cpp:322-374,
 // 445-495): 2048-tap analytic-signal kernel, overlap-add in 8192-point blocks
+// QJHilbertFilter::setSize(2048) (decode/DSP.cpp:732-759): the kernel taps
+static std::vector<cpx> hilbert_taps(int N) {
+  std::vector<cpx> k;
+  for (int i = 0; i < N; i++) {
+    if (i == N / 2) {
+      k.push_back(cpx(-1, 0));
+      continue;
+    }
+    if ((i % 2) == 0) {
+      k.push_back(cpx(0, 0));
+      continue;
+    }
+    k.push_back(cpx(0, (2.0 / ((double)N)) / (std::tan(M_PI * (((double)i) / ((double)N) - 0.5)))));
+  }
+  return k;
+}
+
 struct HilbertFir {
   JFFT fft;
   std::vector<cpx> kernel, sigspace, remainder;
   int nfft = 0, sigspace_ptr = 0, signal_non_zero_size = 0, remainder_size = 0;
   HilbertFir() {
     const int N = 2048;
-    std::vector<cpx> k;
-    for (int i = 0; i < N; i++) {
-      if (i == N / 2) {
-        k.push_back(cpx(-1, 0));
-        continue;
-      }
-      if ((i % 2) == 0) {
-        k.push_back(cpx(0, 0));
-        continue;
-      }
-      k.push_back(cpx(0, (2.0 / ((double)N)) / (std::tan(M_PI * (((double)i) / ((double)N) - 0.5)))));
-    }
+    std::vector<cpx> k = hilbert_taps(N);
     const int kernel_non_zero_size = N;
     nfft = 1;
     while (nfft < 4 * kernel_non_zero_size) nfft <<= 1;
@@ -3071,6 +3077,30 @@ void oracle_fft(double *x, int nfft, int inverse) {
   JFFT j;
   j.init(nfft);
   j.fft(reinterpret_cast<cpx *>(x), inverse != 0);
+}
+/* FFTr(n).transform: the burst trident check's real FFT (n reals in, n
+ * complex out, the upper half zeroed as FFTrWrapper's kissfft scaling does) */
+void oracle_fftr(const double *real, double *out, int n) {
+  FFTr f(n);
+  std::vector<double> r(real, real + n);
+  std::vector<cpx> o;
+  f.transform(r, o);
+  memcpy(out, o.data(), sizeof(cpx) * (size_t)n);
+}
+/* HilbertFir: n complex samples through the 2048-tap analytic-signal fast
+ * FIR, one sample at a time; kernel (if not null) receives its 2048
+ * time-domain taps */
+void oracle_hilbert(const double *in, double *out, int n, double *kernel) {
+  HilbertFir h;
+  if (kernel) {
+    const std::vector<cpx> k = hilbert_taps(2048);
+    memcpy(kernel, k.data(), sizeof(cpx) * k.size());
+  }
+  for (int i = 0; i < n; i++) {
+    const cpx y = h.update(cpx(in[2 * i], in[2 * i + 1]));
+    out[2 * i] = y.real();
+    out[2 * i + 1] = y.imag();
+  }
 }
 
 }  // extern "C"
