@@ -5,14 +5,15 @@
  *                   (decode/aerol.cpp:1060-2038): phase-invariant UW search on
  *                   alternating arms, header, block fill; a full 64x78 block
  *                   becomes a Viterbi job (double-buffered per channel).
- *  viterbi_kernel : one wavefront per job.  Deinterleave_ba on load
+ *  viterbi_kernel : one wavefront per pair of jobs.  Deinterleave_ba on load
  *                   (decode/aerol.cpp:594-613), JConvolutionalCodec::
  *                   Decode_Continuous framing (decode/jconvolutionalcodec.cpp:
  *                   146-198) and the libcorrect soft Viterbi (r=1/2, K=7,
  *                   polys {109,79}; restated in oracle/aero_oracle.cpp): lane s
- *                   owns trellis state s, predecessors arrive by ds_bpermute,
- *                   the 64 survivor decisions of a step are one ballot word
- *                   in LDS.  Then DelayLine dl2, AeroLScrambler, LSB-first byte
+ *                   owns trellis state s of both codewords (16-bit metrics
+ *                   packed in one register), predecessors arrive by
+ *                   ds_bpermute, the 64 survivor decisions of a step are one
+ *                   ballot word per codeword in registers.  Then DelayLine dl2, AeroLScrambler, LSB-first byte
  *                   packing and the per-SU CRC-16 (decode/aerol.cpp:1501-1556).
  *
  * Framing never depends on the CRC results: datacd becomes true at the first
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(256) void frame_msk_kernel(DevState S, int nch) {
 
 // ---------------------------------------------------------------- Viterbi
 // BLK = interleaver block (N x 64 soft bits), N = BLK / 64; DL2 = dl2 length + 1.
-// One wave per job, ~5.8 KB of LDS and no per-step barrier
+// One wave per pair of jobs, ~1 KB of LDS and no per-step barrier
 // (viterbi_decode_regs), launched between a coarse hop and a demod launch
 // (engine.hip issue_viterbi).
 #ifdef AERO_X_STAMPS
@@ -273,140 +274,191 @@ void viterbi_read_stamps(unsigned long long *out) {
 #endif
 }
 
+// soft value p of a job's decoder input: the 62 overlap values of the
+// previous block (lane p's ovr), then the block deinterleaved on the fly
+// (deinterleave_ba, decode/aerol.cpp:594-613: position j * 64 + l comes from
+// row (27 l) mod 64, column j), then erasures (128)
+template <int BLK>
+struct BlockSoft {
+  const uint8_t *blk;
+  int ov, ovr;
+  // called by every lane; may_ov (wave-uniform): p may be an overlap position
+  __device__ __forceinline__ int get(int p, bool may_ov) const {
+    const int q = p - ov;
+    int v = 128;
+    if (q >= 0 && q < BLK) v = blk[(((q & 63) * 27) & 63) * (BLK / 64) + (q >> 6)];
+    if (may_ov) {
+      const int o = __builtin_amdgcn_ds_bpermute((p & 63) << 2, ovr);
+      if (q < 0) v = o;
+    }
+    return v;
+  }
+};
+
 template <int BLK, int DL2>
-__global__ __launch_bounds__(64) void viterbi_kernel(DevState S, DevTables T, int trace) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void viterbi_kernel(DevState S, DevTables T, int trace) {
   constexpr int NL = BLK / 64, HALF = BLK / 2;
   constexpr int NW = (62 + BLK + 24) / 2 / 64 + 1;  // 64-bit words of decoded bits
-  __shared__ uint8_t sbuf[62 + BLK + 24 + 2];
   __shared__ uint64_t obits[NW];
   __shared__ uint8_t info[320];
-  // grid-stride over the jobs of this pass (the job count stays on the device,
-  // so the host launches without waiting for the framing kernel)
+  // grid-stride over pairs of this pass's jobs (the job count stays on the
+  // device, so the host launches without waiting for the framing kernel);
+  // the two jobs of a pair decode in one wave (viterbi_decode_regs2) when
+  // they have the same length and different channels, else one after the other
   const int njobs = *S.njobs;
   if (blockIdx.x == 0 && threadIdx.x == 0 && S.njobs_host) *S.njobs_host = njobs;
-  for (int job = blockIdx.x; job < njobs; job += gridDim.x) {
-  __syncthreads();  // LDS of the previous job fully consumed
-#ifdef AERO_X_STAMPS
-  unsigned long long vst_[4] = {0, 0, 0, 0}, vtime_ = __builtin_amdgcn_s_memtime();
-#endif
   const int lane = threadIdx.x;
-  const int4 jd = reinterpret_cast<const int4 *>(S.jobs)[job];
-  const int c = jd.x, buf = jd.y & 1, first = (jd.y >> 1) & 1, reset = (jd.y >> 2) & 1, clear = (jd.y >> 3) & 1;
-  const int scr_pos = jd.z, formatid = jd.w & 0xFF, frame_done = (jd.w >> 8) & 1;
   const int C = S.C;
-  const int ov = first ? 0 : 62;
-  const int nsoft = ov + BLK + 24;
-  // load: overlap + deinterleaved block + 24 erasures
-  if (!first && lane < 62) sbuf[lane] = S.overlap[(size_t)c * 64 + lane];
-  {
-    const uint8_t *blk = S.block + ((size_t)c * 2 + buf) * BLK;
-    const int row = (lane * 27) % 64;  // interleaverowdepermute[lane]
-    for (int j = 0; j < NL; ++j) sbuf[ov + j * 64 + lane] = blk[row * NL + j];
-  }
-  if (lane < 24) sbuf[ov + BLK + lane] = 128;
-  __syncthreads();
-  // keep the last 62 deinterleaved soft values for the next block
-  if (lane < 62) S.overlap[(size_t)c * 64 + lane] = sbuf[ov + BLK - 62 + lane];
-
-  const int sets = nsoft / 2;
-  uint64_t obw;
-  VSTAMP(0);
-  viterbi_decode_regs(sbuf, nsoft, obw, lane);
-  if (lane < NW) obits[lane] = obw;
-  __syncthreads();
-  VSTAMP(1);
-  auto obit = [&](int k) { return (int)((obits[k >> 6] >> (k & 63)) & 1ULL); };
-  // Decode_Continuous: keep decoded bits [25, 25 + BLK/2) clipped to size/2
-  const int nbits = (sets - 25) < HALF ? (sets - 25) : HALF;
-  if (trace) {
-    uint8_t *dbg = S.blocks_dbg + (size_t)c * 2500;
-    if (lane == 0) *reinterpret_cast<int *>(dbg) = nbits;
-    for (int k = lane; k < nbits; k += 64) dbg[4 + k] = (uint8_t)obit(25 + k);
-  }
-  // DelayLine dl2 (aerol.h:464-471): out[q] = old[(p+q+1)%L], new[(p+q)%L] = in[q]
-  // (nbits < DL2: one wrap at most).  Each lane takes the eight bits of its
-  // output bytes: all old values are read (and used) before any new one is
-  // stored, as a neighbour's first read is this lane's last write.
-  static_assert(HALF < DL2, "delay line longer than a block");
-  uint8_t *dlg = S.dl2 + (size_t)c * DL2;
-  const int p0 = S.is[IS_DL2_PTR * C + c];
-  const int nbytes = nbits / 8;
-  constexpr int BPL = (HALF / 8 + 63) / 64;  // output bytes per lane
-  int bytev[BPL];
+  // a job's soft stream: overlap + deinterleaved block + 24 erasures, read by
+  // the decoder straight from the block (no LDS copy); the old overlap is
+  // taken into a register before this block's last 62 values replace it
+  auto source = [&](int job) -> BlockSoft<BLK> {
+    const int4 jd = reinterpret_cast<const int4 *>(S.jobs)[job];
+    const int c = jd.x, buf = jd.y & 1, first = (jd.y >> 1) & 1;
+    BlockSoft<BLK> b;
+    b.blk = S.block + ((size_t)c * 2 + buf) * BLK;
+    b.ov = first ? 0 : 62;
+    b.ovr = (!first && lane < 62) ? S.overlap[(size_t)c * 64 + lane] : 0;
+    if (lane < 62) S.overlap[(size_t)c * 64 + lane] = (uint8_t)b.get(b.ov + BLK - 62 + lane, false);
+    return b;
+  };
+  // Decode_Continuous output, delay line, scrambler, SU CRCs and the job record
+  auto post = [&](int job, int nsoft, uint64_t obw) {
+    const int4 jd = reinterpret_cast<const int4 *>(S.jobs)[job];
+    const int c = jd.x, reset = (jd.y >> 2) & 1, clear = (jd.y >> 3) & 1;
+    const int scr_pos = jd.z, formatid = jd.w & 0xFF, frame_done = (jd.w >> 8) & 1;
+    const int sets = nsoft / 2;
+    __syncthreads();  // the previous post's reads of obits / info are done
+    if (lane < NW) obits[lane] = obw;
+    __syncthreads();
+    auto obit = [&](int k) { return (int)((obits[k >> 6] >> (k & 63)) & 1ULL); };
+    // Decode_Continuous: keep decoded bits [25, 25 + BLK/2) clipped to size/2
+    const int nbits = (sets - 25) < HALF ? (sets - 25) : HALF;
+    if (trace) {
+      uint8_t *dbg = S.blocks_dbg + (size_t)c * 2500;
+      if (lane == 0) *reinterpret_cast<int *>(dbg) = nbits;
+      for (int k = lane; k < nbits; k += 64) dbg[4 + k] = (uint8_t)obit(25 + k);
+    }
+    // DelayLine dl2 (aerol.h:464-471): out[q] = old[(p+q+1)%L], new[(p+q)%L] = in[q]
+    // (nbits < DL2: one wrap at most).  Each lane takes the eight bits of its
+    // output bytes: all old values are read (and used) before any new one is
+    // stored, as a neighbour's first read is this lane's last write.
+    static_assert(HALF < DL2, "delay line longer than a block");
+    uint8_t *dlg = S.dl2 + (size_t)c * DL2;
+    const int p0 = S.is[IS_DL2_PTR * C + c];
+    const int nbytes = nbits / 8;
+    constexpr int BPL = (HALF / 8 + 63) / 64;  // output bytes per lane
+    int bytev[BPL];
 #pragma unroll
-  for (int u = 0; u < BPL; ++u) {
-    const int bb = lane + 64 * u;
-    int v = 0;
-    if (bb < nbytes) {
-      // scrambler + LSB-first packing (aerol.cpp:1506-1520)
-      for (int i = 0; i < 8; ++i) {
-        int r = p0 + 8 * bb + i + 1;
-        r = r >= DL2 ? r - DL2 : r;
-        r = r >= DL2 ? r - DL2 : r;
-        v |= ((dlg[r] ^ T.scr[scr_pos + 8 * bb + i]) & 1) << i;
+    for (int u = 0; u < BPL; ++u) {
+      const int bb = lane + 64 * u;
+      int v = 0;
+      if (bb < nbytes) {
+        // scrambler + LSB-first packing (aerol.cpp:1506-1520)
+        for (int i = 0; i < 8; ++i) {
+          int r = p0 + 8 * bb + i + 1;
+          r = r >= DL2 ? r - DL2 : r;
+          r = r >= DL2 ? r - DL2 : r;
+          v |= ((dlg[r] ^ T.scr[scr_pos + 8 * bb + i]) & 1) << i;
+        }
       }
+      bytev[u] = v;
     }
-    bytev[u] = v;
-  }
 #pragma unroll
-  for (int u = 0; u < BPL; ++u) {
-    const int bb = lane + 64 * u;
-    if (bb < 312) info[bb] = (uint8_t)(bb < nbytes ? bytev[u] : 0);
-  }
-  for (int bb = lane + 64 * BPL; bb < 312; bb += 64) info[bb] = 0;
-  __syncthreads();  // every old delay-line value read before the writes below
-  for (int k = lane; k < nbits; k += 64) {
-    int w = p0 + k;
-    w = w >= DL2 ? w - DL2 : w;
-    dlg[w] = (uint8_t)obit(25 + k);
-  }
-  if (lane == 0) S.is[IS_DL2_PTR * C + c] = (p0 + nbits) % DL2;
-  // per-SU CRC (aerol.cpp:1531-1543); a 600/1200 frame spans 2-3 blocks and
-  // its SUs are checked on the host once the frame's infofield is complete
-  const int nsu = nbytes / 12;
-  bool ok = false;
-  if (lane < nsu && frame_done && BLK == BLOCK) {
-    const uint8_t *su = info + 12 * lane;
-    unsigned crc = 0xFFFF, sum = 0;
-    for (int i = 0; i < 10; ++i) {
-      unsigned mb = su[i];
-      sum += mb;
-      for (int k = 0; k < 8; ++k) {
-        const unsigned bit = mb & 1;
-        mb >>= 1;
-        const unsigned cb = crc & 1;
-        crc >>= 1;
-        if (cb ^ bit) crc ^= 0x8408;
+    for (int u = 0; u < BPL; ++u) {
+      const int bb = lane + 64 * u;
+      if (bb < 312) info[bb] = (uint8_t)(bb < nbytes ? bytev[u] : 0);
+    }
+    for (int bb = lane + 64 * BPL; bb < 312; bb += 64) info[bb] = 0;
+    __syncthreads();  // every old delay-line value read before the writes below
+    for (int k = lane; k < nbits; k += 64) {
+      int w = p0 + k;
+      w = w >= DL2 ? w - DL2 : w;
+      dlg[w] = (uint8_t)obit(25 + k);
+    }
+    if (lane == 0) S.is[IS_DL2_PTR * C + c] = (p0 + nbits) % DL2;
+    // per-SU CRC (aerol.cpp:1531-1543); a 600/1200 frame spans 2-3 blocks and
+    // its SUs are checked on the host once the frame's infofield is complete
+    const int nsu = nbytes / 12;
+    bool ok = false;
+    if (lane < nsu && frame_done && BLK == BLOCK) {
+      const uint8_t *su = info + 12 * lane;
+      unsigned crc = 0xFFFF, sum = 0;
+      for (int i = 0; i < 10; ++i) {
+        unsigned mb = su[i];
+        sum += mb;
+        for (int k = 0; k < 8; ++k) {
+          const unsigned bit = mb & 1;
+          mb >>= 1;
+          const unsigned cb = crc & 1;
+          crc >>= 1;
+          if (cb ^ bit) crc ^= 0x8408;
+        }
       }
+      unsigned calc = (~crc) & 0xFFFF;
+      const unsigned rec = ((unsigned)su[11] << 8) | su[10];
+      if (!rec && calc != rec && sum == 0) calc = 0;
+      ok = calc == rec;
     }
-    unsigned calc = (~crc) & 0xFFFF;
-    const unsigned rec = ((unsigned)su[11] << 8) | su[10];
-    if (!rec && calc != rec && sum == 0) calc = 0;
-    ok = calc == rec;
-  }
-  const unsigned long long okm = __ballot(ok);
-  uint8_t *out = S.jobout + (size_t)job * JOB_OUT;
-  for (int b = lane; b < 312; b += 64) out[b] = info[b];
-  if (lane == 0) {
-    int *o = reinterpret_cast<int *>(out + 312);
-    if (BLK == BLOCK) {
-      o[0] = frame_done ? nbytes : -1;
-      o[1] = (int)(okm & 0x3FFFFFFULL);
-    } else {  // block bytes; bit 8: frame done, bit 9: infofield cleared before this block
-      o[0] = nbytes | (frame_done << 8) | (clear << 9);
-      o[1] = 0;
+    const unsigned long long okm = __ballot(ok);
+    uint8_t *out = S.jobout + (size_t)job * JOB_OUT;
+    for (int b = lane; b < 312; b += 64) out[b] = info[b];
+    if (lane == 0) {
+      int *o = reinterpret_cast<int *>(out + 312);
+      if (BLK == BLOCK) {
+        o[0] = frame_done ? nbytes : -1;
+        o[1] = (int)(okm & 0x3FFFFFFULL);
+      } else {  // block bytes; bit 8: frame done, bit 9: infofield cleared before this block
+        o[0] = nbytes | (frame_done << 8) | (clear << 9);
+        o[1] = 0;
+      }
+      o[2] = formatid;
+      o[3] = c | (reset << 30);
     }
-    o[2] = formatid;
-    o[3] = c | (reset << 30);
-  }
-  VSTAMP(2);
+  };
+  for (int pj = blockIdx.x; 2 * pj < njobs; pj += gridDim.x) {
+    __syncthreads();  // LDS of the previous pair fully consumed
 #ifdef AERO_X_STAMPS
-  if (lane == 0) {
-    for (int k = 0; k < 3; ++k) atomicAdd(&g_vstamps[k], vst_[k]);
-    atomicAdd(&g_vstamps[3], 1ull);
-  }
+    unsigned long long vst_[4] = {0, 0, 0, 0}, vtime_ = __builtin_amdgcn_s_memtime();
 #endif
-  }  // job loop
+    const int jobA = 2 * pj, jobB = 2 * pj + 1;
+    bool paired = false;
+    if (jobB < njobs) {
+      const int4 ja = reinterpret_cast<const int4 *>(S.jobs)[jobA];
+      const int4 jb = reinterpret_cast<const int4 *>(S.jobs)[jobB];
+      // same length (both continue or both start a stream), different channels
+      // (a channel's second block would read the overlap this one writes)
+      paired = ja.x != jb.x && ((ja.y ^ jb.y) & 2) == 0;
+    }
+    if (paired) {
+      const BlockSoft<BLK> sa = source(jobA), sb = source(jobB);
+      const int nsoft = sa.ov + BLK + 24;
+      VSTAMP(0);
+      uint64_t obwA, obwB;
+      viterbi_decode_regs2(sa, sb, nsoft, obwA, obwB, lane);
+      VSTAMP(1);
+      post(jobA, nsoft, obwA);
+      post(jobB, nsoft, obwB);
+      VSTAMP(2);
+    } else {
+      for (int job = jobA; job <= jobB && job < njobs; ++job) {
+        const BlockSoft<BLK> sa = source(job);
+        const int nsoft = sa.ov + BLK + 24;
+        VSTAMP(0);
+        uint64_t obw, unused;
+        viterbi_decode_regs2(sa, sa, nsoft, obw, unused, lane);
+        VSTAMP(1);
+        post(job, nsoft, obw);
+        VSTAMP(2);
+      }
+    }
+#ifdef AERO_X_STAMPS
+    if (lane == 0) {
+      for (int k = 0; k < 3; ++k) atomicAdd(&g_vstamps[k], vst_[k]);
+      atomicAdd(&g_vstamps[3], 1ull);
+    }
+#endif
+  }  // pair loop
 }
 
 void launch_frame(hipStream_t st, int mode, const DevState &S, int nch) {
@@ -423,6 +475,7 @@ void launch_frame(hipStream_t st, int mode, const DevState &S, int nch) {
 // on the device); the grid is capped, blocks stride over the jobs
 void launch_viterbi(hipStream_t st, int mode, const DevState &S, const DevTables &T, int max_jobs, int trace) {
   if (max_jobs <= 0) return;
+  max_jobs = (max_jobs + 1) / 2;  // one block per pair of jobs
   max_jobs = max_jobs < 16384 ? max_jobs : 16384;
   if (mode == MODE_OQPSK)
     hipLaunchKernelGGL((viterbi_kernel<BLOCK, DL2_LEN>), dim3(max_jobs), dim3(64), 0, st, S, T, trace);

@@ -321,3 +321,246 @@ __device__ __forceinline__ void viterbi_decode_regs(const uint8_t *sbuf, int nso
 }
 
 }  // namespace aero
+
+namespace aero {
+
+// Both codewords' tracebacks in one walk (their column schedule is the
+// same): per column two v_readlane per codeword and a few scalar operations,
+// the two path chains independent of each other.  Output bits (bit b
+// descending) collect in one 64-bit scalar word per codeword, merged into
+// lane b >> 6 of obw when the word is complete.  The caller advances outpos
+// and len.
+__device__ __forceinline__ void vit_traceback2(const uint64_t hA0, const uint64_t hA1, const uint64_t hA2,
+                                               const uint64_t hB0, const uint64_t hB1, const uint64_t hB2,
+                                               uint64_t &obwA, uint64_t &obwB, int bpA, int bpB, int mintb,
+                                               int index, int len, int outpos, int lane) {
+  const int nout = len - mintb;
+  int idx = index;
+  int j = 0;
+  int bb = __builtin_amdgcn_readfirstlane(outpos + nout - 1);  // output bit of column j = mintb
+  uint64_t accA = 0, accB = 0;
+  auto flush = [&](int wd) {
+    obwA = lane == wd ? (obwA | accA) : obwA;
+    obwB = lane == wd ? (obwB | accB) : obwB;
+    accA = 0;
+    accB = 0;
+  };
+  while (j < len) {
+    idx = idx == 0 ? HCAP - 1 : idx - 1;
+    int run = (idx & 63) + 1;
+    if (run > len - j) run = len - j;
+    auto walk = [&](const uint64_t hwA, const uint64_t hwB) {
+      for (int k = 0; k < run; ++k, ++j) {
+        const int col = (idx - k) & 63;
+        const uint64_t hvA = readlane64(hwA, col), hvB = readlane64(hwB, col);
+        const int hbA = (int)((hvA >> bpA) & 1ULL), hbB = (int)((hvB >> bpB) & 1ULL);
+        bpA = (bpA >> 1) | (hbA << 5);
+        bpB = (bpB >> 1) | (hbB << 5);
+        if (j >= mintb) {
+          accA |= (uint64_t)hbA << (bb & 63);
+          accB |= (uint64_t)hbB << (bb & 63);
+          if ((bb & 63) == 0) flush(bb >> 6);
+          --bb;
+        }
+      }
+    };
+    const int w = __builtin_amdgcn_readfirstlane(idx >> 6);
+    if (w == 0)
+      walk(hA0, hB0);
+    else if (w == 1)
+      walk(hA1, hB1);
+    else
+      walk(hA2, hB2);
+    idx -= run - 1;
+  }
+  if (((bb + 1) & 63) != 0) flush((bb + 1) >> 6);  // the partly filled last word
+}
+
+// Two codewords of the same length in one wave: lane s holds state s's path
+// metric of codeword A in its low 16 bits and of codeword B in its high 16
+// bits.  The uint16 metric arithmetic of the single-codeword decoder is
+// modulo 2^16, which is exactly what the packed 16-bit VALU operations
+// compute, so one pair of bpermutes, one packed branch metric, two packed
+// adds, a packed minimum and two compares advance both trellises a step; the
+// renormalisation, traceback and output schedule depend only on the step
+// count, so both codewords have their events at the same steps.  Same
+// metrics, ties, renormalisation, history, traceback and tail as
+// viterbi_decode_regs, so each codeword decodes to the same bits.
+// Src::get(p, may_ov) returns soft value p of the codeword (called by every
+// lane; may_ov: wave-uniform, p may fall in the overlap part); the soft
+// pairs of the next 64 steps are fetched one run of 64 ahead, so the
+// decoder needs no LDS.
+template <class Src>
+__device__ __forceinline__ void viterbi_decode_regs2(const Src &srcA, const Src &srcB, int nsoft, uint64_t &obwA,
+                                                     uint64_t &obwB, int lane) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const int sets = nsoft / 2;
+  const int s = lane;
+  const int tab_lo = conv_table(s), tab_hi = conv_table(s | 64);
+  uint64_t hA0 = 0, hA1 = 0, hA2 = 0, hB0 = 0, hB1 = 0, hB2 = 0;
+  obwA = 0;
+  obwB = 0;
+  int mA = 0, mB = 0;
+  for (int i = 0; i < 6 && i < sets; ++i) {
+    const int pa = shfl_idx(mA, s >> 1), pb = shfl_idx(mB, s >> 1);
+    const int aA = srcA.get(2 * i, true), bA = srcA.get(2 * i + 1, true);
+    const int aB = srcB.get(2 * i, true), bB = srcB.get(2 * i + 1, true);
+    if (s < (2 << i)) {
+      mA = (soft_dist(conv_table(s), aA, bA) + pa) & 0xFFFF;
+      mB = (soft_dist(conv_table(s), aB, bB) + pb) & 0xFFFF;
+    }
+  }
+  int index = 0, len = 0, renorm = 0, outpos = 0;  // wave-uniform, shared by both codewords
+  auto search = [&](int m, int skip) -> int {
+    int key = (s % skip == 0) ? ((m << 6) | s) : 0x7FFFFFFF;
+    for (int off = 32; off > 0; off >>= 1) {
+      const int o = __shfl_xor(key, off, 64);
+      key = o < key ? o : key;
+    }
+    return __builtin_amdgcn_readfirstlane(key) & 63;
+  };
+  auto traceback = [&](int bestA, int bestB, int mintb) {
+    vit_traceback2(hA0, hA1, hA2, hB0, hB1, hB2, obwA, obwB, bestA, bestB, mintb, index, len, outpos, lane);
+    const int nout = len - mintb;
+    outpos += nout;
+    len -= nout;
+  };
+  // process(skip) of the single decoder after its counters have advanced
+  auto events = [&](int skip) {
+    if (renorm == RENORM) {
+      renorm = 0;
+      const int bA = search(mA, skip), bB = search(mB, skip);
+      mA = (mA - __builtin_amdgcn_readlane(mA, bA)) & 0xFFFF;
+      mB = (mB - __builtin_amdgcn_readlane(mB, bB)) & 0xFFFF;
+      if (len == HCAP) traceback(bA, bB, MINTB);
+    } else if (len == HCAP) {
+      traceback(search(mA, skip), search(mB, skip), MINTB);
+    }
+  };
+  const int tail0 = sets - 6 > 6 ? sets - 6 : 6;
+  {
+    // branch metric soft_dist(tab_lo, a, b) = c0 + sa a + sb b with sa, sb =
+    // +-1 (0xFFFF modulo 2^16); the s | 64 edge's metric is 510 minus it
+    const unsigned short sa = (tab_lo & 1) ? 0xFFFF : 1, sb = (tab_lo & 2) ? 0xFFFF : 1;
+    const unsigned short c0 = (unsigned short)(((tab_lo & 1) ? 255 : 0) + ((tab_lo & 2) ? 255 : 0));
+    const u16x2 SA = {sa, sa}, SB = {sb, sb}, C0 = {c0, c0}, K510 = {510, 510};
+    const int src0 = (s >> 1) << 2, src1 = ((s >> 1) | 32) << 2;
+    // lane l: step i0 + l's a values (A low, B high) in pa, its b values in pb
+    auto pairs = [&](int i0, uint32_t &pa, uint32_t &pb) {
+      const int st = i0 + lane;
+      const bool ov = 2 * i0 < 64;
+      const uint32_t aA = (uint32_t)srcA.get(2 * st, ov), bA = (uint32_t)srcA.get(2 * st + 1, ov);
+      const uint32_t aB = (uint32_t)srcB.get(2 * st, ov), bB = (uint32_t)srcB.get(2 * st + 1, ov);
+      pa = st < sets ? aA | (aB << 16) : 0u;
+      pb = st < sets ? bA | (bB << 16) : 0u;
+    };
+    uint32_t M = (uint32_t)mA | ((uint32_t)mB << 16);
+    int i = 6;
+    uint32_t pva, pvb, nva, nvb;
+    pairs(6, pva, pvb);
+    pairs(6 + 64, nva, nvb);
+    int pk = 0;
+    while (i < tail0) {
+      const int idx = __builtin_amdgcn_readfirstlane(index);
+      const int w = idx >> 6;
+      int run = (w == 2 ? HCAP : 64 * (w + 1)) - idx;
+      run = min(run, tail0 - i);
+      run = min(run, RENORM - renorm);
+      run = min(run, HCAP - len);
+      run = min(run, 64 - pk);
+      run = __builtin_amdgcn_readfirstlane(run);
+      auto steps = [&](uint64_t &hwA, uint64_t &hwB) {
+        uint32_t loA = (uint32_t)hwA, hiA = (uint32_t)(hwA >> 32);
+        uint32_t loB = (uint32_t)hwB, hiB = (uint32_t)(hwB >> 32);
+        const int col0 = idx & 63;
+        for (int k = 0; k < run; ++k) {
+          const uint32_t ap = (uint32_t)__builtin_amdgcn_readlane((int)pva, pk + k);
+          const uint32_t bp = (uint32_t)__builtin_amdgcn_readlane((int)pvb, pk + k);
+          const uint32_t m0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src0, (int)M);
+          const uint32_t m1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src1, (int)M);
+          const u16x2 d0 = SA * __builtin_bit_cast(u16x2, ap) + (SB * __builtin_bit_cast(u16x2, bp) + C0);
+          u16x2 d1 = K510 - d0;
+          asm volatile("" : "+v"(d1));  // both branch metrics off the metric chain
+          const u16x2 e0 = __builtin_bit_cast(u16x2, m0) + d0, e1 = __builtin_bit_cast(u16x2, m1) + d1;
+          const uint64_t maskA = __ballot(e0.x > e1.x), maskB = __ballot(e0.y > e1.y);
+          M = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(e0, e1));
+          const int col = col0 + k;
+          // the mask SGPRs were just written by VALU compares: the wait
+          // states the v_writelane needs are explicit (see viterbi_decode_regs)
+          asm("s_nop 4\n\t"
+              "v_writelane_b32 %0, %4, m0\n\t"
+              "v_writelane_b32 %1, %5, m0\n\t"
+              "v_writelane_b32 %2, %6, m0\n\t"
+              "v_writelane_b32 %3, %7, m0"
+              : "+v"(loA), "+v"(hiA), "+v"(loB), "+v"(hiB)
+              : "s"((uint32_t)maskA), "s"((uint32_t)(maskA >> 32)), "s"((uint32_t)maskB),
+                "s"((uint32_t)(maskB >> 32)), "{m0}"(col));
+        }
+        hwA = ((uint64_t)hiA << 32) | loA;
+        hwB = ((uint64_t)hiB << 32) | loB;
+      };
+      if (w == 0)
+        steps(hA0, hB0);
+      else if (w == 1)
+        steps(hA1, hB1);
+      else
+        steps(hA2, hB2);
+      i += run;
+      pk += run;
+      index = idx + run == HCAP ? 0 : idx + run;
+      renorm += run;
+      len += run;
+      if (pk == 64) {
+        pva = nva;
+        pvb = nvb;
+        pairs(i + 64, nva, nvb);
+        pk = 0;
+      }
+      if (renorm == RENORM || len == HCAP) {
+        mA = (int)(M & 0xFFFFu);
+        mB = (int)(M >> 16);
+        events(1);
+        M = (uint32_t)mA | ((uint32_t)mB << 16);
+      }
+    }
+    mA = (int)(M & 0xFFFFu);
+    mB = (int)(M >> 16);
+  }
+  for (int i = tail0; i < sets; ++i) {
+    const int aA = srcA.get(2 * i, true), bA = srcA.get(2 * i + 1, true);
+    const int aB = srcB.get(2 * i, true), bB = srcB.get(2 * i + 1, true);
+    const bool tail = i >= sets - 6;
+    const int skip = tail ? (1 << (7 - (sets - i))) : 1;
+    const bool act = (s % skip) == 0;
+    const int w = __builtin_amdgcn_readfirstlane(index >> 6);
+    const bool mine = lane == (index & 63);
+    {
+      const int m0 = shfl_idx(mA, s >> 1), m1 = shfl_idx(mA, (s >> 1) | 32);
+      const int e0 = (m0 + soft_dist(tab_lo, aA, bA)) & 0xFFFF, e1 = (m1 + soft_dist(tab_hi, aA, bA)) & 0xFFFF;
+      const int h = (e0 <= e1) ? 0 : 1;
+      if (act) mA = h ? e1 : e0;
+      const uint64_t mask = __ballot(act && h);
+      hA0 = (mine && w == 0) ? mask : hA0;
+      hA1 = (mine && w == 1) ? mask : hA1;
+      hA2 = (mine && w == 2) ? mask : hA2;
+    }
+    {
+      const int m0 = shfl_idx(mB, s >> 1), m1 = shfl_idx(mB, (s >> 1) | 32);
+      const int e0 = (m0 + soft_dist(tab_lo, aB, bB)) & 0xFFFF, e1 = (m1 + soft_dist(tab_hi, aB, bB)) & 0xFFFF;
+      const int h = (e0 <= e1) ? 0 : 1;
+      if (act) mB = h ? e1 : e0;
+      const uint64_t mask = __ballot(act && h);
+      hB0 = (mine && w == 0) ? mask : hB0;
+      hB1 = (mine && w == 1) ? mask : hB1;
+      hB2 = (mine && w == 2) ? mask : hB2;
+    }
+    index++;
+    if (index == HCAP) index = 0;
+    renorm++;
+    len++;
+    events(skip);
+  }
+  traceback(0, 0, 0);
+}
+
+}  // namespace aero
