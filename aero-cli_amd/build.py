@@ -37,8 +37,13 @@ CXX_SRCS = ['tables_host.cpp', 'acars_host.cpp']
 # libm ports out of the loop into SGPRs, hundreds of them, which then spill
 # (AGPR / VGPR-lane round trips every sample).  Without it they stay
 # rematerialised at their use.
+# The continuous OQPSK demod schedules better with memory clauses kept
+# together (its loop's table gathers and ring loads issue back to back):
+# 14.9 -> 14.6 ms per hop (profiles/r04/ab/round3c/ab_sched_*.log; max-ilp
+# 14.8, and both strategies slow the coarse kernel, which keeps the default).
 FILE_FLAGS = {'burst.hip': ['-mllvm', '-disable-machine-licm'],
-              'burst_msk.hip': ['-mllvm', '-disable-machine-licm']}
+              'burst_msk.hip': ['-mllvm', '-disable-machine-licm'],
+              'demod_oqpsk.hip': ['-mllvm', '--amdgpu-sched-strategy=max-memory-clause']}
 
 
 def _run(cmd):
