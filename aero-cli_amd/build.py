@@ -26,7 +26,7 @@ ARCH = os.environ.get('AERO_OFFLOAD_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', shutil.which('hipcc') or '/opt/rocm/bin/hipcc')
 # bit-exactness: no FP contraction, no fast math, anywhere on the product path
 FP = ['-ffp-contract=off', '-fno-fast-math']
-HIP_FLAGS = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH, '-munsafe-fp-atomics'] + FP
+HIP_FLAGS = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH] + FP
 CXX_FLAGS = ['-O2', '-std=c++17', '-fPIC', '-Wall'] + FP
 
 HIP_SRCS = ['demod_oqpsk.hip', 'demod_msk.hip', 'coarse.hip', 'aerol.hip', 'engine.hip', 'chan.hip', 'burst.hip', 'burst_msk.hip',

@@ -777,22 +777,27 @@ def main():
         stats = {k: int(t[2 + i]) for i, k in enumerate(keys)}
     if rank == 0:
         value = samples / elapsed / 1e6
-        # roofline of the dominant kernel (the most device time per step):
-        # that kernel's algorithmic bytes per step over its summed time per
-        # step.  The demodulator carries the path's bytes (SURVEY §8(d):
-        # bytes per input sample x samples of a step); the coarse kernel its
-        # own (snapshot ring + y history per channel-hop, one hop per channel
-        # per launch).  The path figure over the demodulator and the whole
-        # step are reported beside it.
+        # roofline of the dominant kernel (the most device time per step) on
+        # the SURVEY.md §8(d) / BASELINE.md basis: the path's algorithmic bytes
+        # (bytes per input sample x the samples one step processes) over that
+        # kernel's summed device time per step.  The coarse kernel's own
+        # algorithmic bytes (snapshot ring + y history per channel-hop) are
+        # reported beside it as roofline.kernel_traffic, the demodulator's
+        # figure as roofline.path and the whole step as roofline.step.
         steps = max(a.steps, 1)
         dom = max(kt, key=lambda k: kt[k][0])
         dom_ms = kt[dom][0] / steps
         path_bytes = M['bytes'] * C * HOP
         step_bytes = path_bytes
-        unit = {'bytes_per_sample': M['bytes']}
+        unit = {'bytes_per_sample': M['bytes'], 'samples_per_step': C * HOP}
+        kernel_traffic = None
         if dom == 'coarse' and 'coarse_hop_bytes' in M:
-            step_bytes = M['coarse_hop_bytes'] * C * (kt[dom][1] / steps)
-            unit = {'bytes_per_channel_hop': M['coarse_hop_bytes']}
+            kb = M['coarse_hop_bytes'] * C * (kt[dom][1] / steps)
+            kernel_traffic = {'bytes_per_channel_hop': M['coarse_hop_bytes'], 'bytes_per_step': int(kb),
+                              'achieved': round(kb / (dom_ms / 1e3) / 1e9, 2),
+                              'frac': round(kb / (dom_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
+                              'note': "the coarse kernel's own algorithmic bytes: 16384-entry uint32 snapshot "
+                                      'ring read + y history of the searched bins read and written'}
         achieved = step_bytes / (dom_ms / 1e3) / 1e9
         step_achieved = path_bytes / (elapsed / steps) / 1e9
         path_kernel = 'demod' if 'demod' in kt else dom
@@ -831,7 +836,7 @@ def main():
             'roofline': dict({'bound': 'hbm', 'kernel': M['kernels'][dom], 'achieved': round(achieved, 2),
                               'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
                               'traffic': traffic, 'traffic_source': traffic_src},
-                             **unit, **{
+                             **unit, **{'kernel_traffic': kernel_traffic,
                               'bytes_per_step': int(step_bytes), 'kernel_ms_per_step': round(dom_ms, 3),
                               'launches_per_step': round(kt[dom][1] / steps, 2),
                               'path': {'kernel': M['kernels'][path_kernel], 'bytes_per_sample': M['bytes'],
