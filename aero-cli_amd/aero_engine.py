@@ -102,6 +102,7 @@ _SIGS = {
                                           ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
     'aero_pop_hops': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                      ctypes.POINTER(ctypes.c_size_t)]),
+    'aero_trace_select': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     'aero_pop_pt': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                    ctypes.POINTER(ctypes.c_size_t)]),
     'aero_pop_blocks': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
@@ -283,6 +284,12 @@ class Engine:
         """ptr: HIP device pointer of int16 [n, ld] (e.g. torch tensor.data_ptr())."""
         _check(self.lib.aero_push_pcm_batch(self.h, ctypes.c_void_p(ptr), n, ld, nch, 1), 'aero_push_pcm_batch')
 
+    def trace_select(self, channels):
+        """Keeps traces (soft bits, hops, pt, blocks, frames) of these
+        continuous channels only; [] keeps every channel's again."""
+        arr = (ctypes.c_int * max(1, len(channels)))(*[int(c) for c in channels])
+        _check(self.lib.aero_trace_select(self.h, arr, len(channels)), 'aero_trace_select')
+
     def run(self):
         _check(self.lib.aero_run(self.h), 'aero_run')
 
@@ -348,9 +355,10 @@ class Engine:
             if n.value < 64:
                 return out
 
-    def drain_items(self, lines=False, cap=4096):
+    def drain_items(self, lines=False, cap=4096, keep=None):
         """Pops the items of every channel (aero_pop_items_all).  Returns the
-        count, or (channel, canonical line) pairs with lines=True."""
+        count, or (channel, canonical line) pairs with lines=True (only the
+        channels in the set `keep`, when given)."""
         if getattr(self, '_drain_cap', 0) != cap:
             self._drain_buf = ((AcarsItem * cap)(), (ctypes.c_int * cap)())
             self._drain_cap = cap
@@ -361,7 +369,7 @@ class Engine:
             _check(self.lib.aero_pop_items_all(self.h, arr, chs, cap, ctypes.byref(n)), 'aero_pop_items_all')
             total += n.value
             if lines:
-                out.extend((chs[i], item_line(arr[i])) for i in range(n.value))
+                out.extend((chs[i], item_line(arr[i])) for i in range(n.value) if keep is None or chs[i] in keep)
             if n.value < cap:
                 return out if lines else total
 

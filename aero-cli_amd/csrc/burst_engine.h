@@ -25,7 +25,7 @@ int burst_pop_tests(BurstGroup *g, int c, uint8_t *dst, size_t cap, size_t *n);
 int burst_pop_packets(BurstGroup *g, int c, uint8_t *dst, size_t cap, size_t *n);
 std::vector<aero_acars_item> &burst_items(BurstGroup *g, int c);
 uint64_t burst_processed(const BurstGroup *g);
-uint64_t burst_stat(const BurstGroup *g, int which);  // 0: R/T tests run, 1: R/T packets decoded
+uint64_t burst_stat(const BurstGroup *g, int which);  // 0: R/T tests run, 1: R/T packets decoded, 2: most tests of one pass
 int burst_dcd_edges(BurstGroup *g, int c, int64_t *edges);  // AeroL datacd changes (waits for the group's work)
 void burst_timing(BurstGroup *g, const char *name, double *ms, long *launches);  // adds to *ms / *launches
 void burst_timing_reset(BurstGroup *g);

@@ -158,6 +158,7 @@ struct BurstGroup {
   size_t scratch_cap = 0;
   uint64_t processed = 0;
   uint64_t st_tests = 0, st_packets = 0;  // aero_stat "rt_tests" / "rt_packets"
+  uint64_t st_pass_max = 0;               // aero_stat "rt_pass_max": most R/T tests of one pass
   // AERO_F_TIMING: HIP-event milliseconds and launches per kernel name
   std::map<std::string, std::pair<double, long>> timing;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending_ev;
@@ -366,6 +367,7 @@ void process_tests(BurstGroup *g, const std::vector<uint8_t> &jobs, int njobs) {
   // tests are split over the host pool by channel (c % T == t), each thread
   // taking its channels' tests in emission order.
   const int T = (g->hpool && njobs >= 256) ? std::min(g->hpool->size(), std::max(1, njobs / 128)) : 1;
+  g->st_pass_max = std::max<uint64_t>(g->st_pass_max, (uint64_t)std::max(njobs, 0));
   std::vector<uint64_t> n_tests(T, 0), n_packets(T, 0);
   auto tests = [&](int t, int TT) {
   std::vector<int> deconvol;
@@ -805,7 +807,10 @@ int burst_dcd_edges(BurstGroup *g, int c, int64_t *edges) {
   return AERO_OK;
 }
 
-uint64_t burst_stat(const BurstGroup *g, int which) { return !g ? 0 : (which ? g->st_packets : g->st_tests); }
+uint64_t burst_stat(const BurstGroup *g, int which) {
+  if (!g) return 0;
+  return which == 2 ? g->st_pass_max : (which ? g->st_packets : g->st_tests);
+}
 void burst_timing(BurstGroup *g, const char *name, double *ms, long *launches) {
   if (!g) return;
   collect_timing(g);

@@ -169,27 +169,35 @@ struct Group {
   std::vector<std::vector<double>> hop_hold, pt_hold;
   std::vector<std::vector<uint8_t>> blk_hold, frame_hold;
   std::vector<long long> soft_seen;
+  // aero_trace_select: host-side trace collection for these local channels
+  // only (empty: every channel)
+  bool trace_some = false;
+  std::vector<int> trace_list;
+  std::vector<uint8_t> trace_mask;
+  bool traced(int c) const { return !trace_some || trace_mask[c]; }
   // scratch
   int16_t *d_scratch = nullptr;
   size_t scratch_cap = 0;
   std::vector<uint8_t> h_dbg;
-  // Asynchronous frame hand-off.  A pass that demodulates writes its Viterbi
-  // job records into one of NSLOT device slots; the records and the job count
-  // go back by an async copy into pinned memory, and the host SU/ACARS work
-  // for them starts once that copy's event has completed, while the GPU runs
-  // on.  aero_run therefore never waits for the GPU.
+  // Asynchronous frame hand-off.  A pass that demodulates lists its Viterbi
+  // jobs in one of NSLOT slots; the Viterbi kernel writes the job records and
+  // the job count straight into the slot's mapped pinned host buffers, and
+  // the host SU/ACARS work for them starts once the slot's event (recorded
+  // after that kernel) has completed, while the GPU runs on.  aero_run
+  // therefore never waits for the GPU.
   struct JobSlot {
-    uint8_t *d_out = nullptr;   // [C][JOB_OUT] (device)
     int *d_n = nullptr;         // job count (device)
     int *d_jobs = nullptr;      // [C] int4 job list of this pass (device)
     hipEvent_t ev_vit = nullptr;  // this pass's Viterbi done (main stream)
     hipEvent_t ev_framed = nullptr;  // this pass's framing done (main stream)
     bool trace_blocks = false;
-    uint8_t *h_out = nullptr;   // pinned host records, written by the Viterbi kernel
-    int *h_n = nullptr;         // pinned host job count, written by the Viterbi kernel
+    // mapped pinned host records and job count, written by the Viterbi kernel
+    // (system-scope stores); the host reads them only after `ev`, which the
+    // main stream records after that kernel
+    uint8_t *h_out = nullptr;
+    int *h_n = nullptr;
     uint8_t *h_out_dev = nullptr;  // the same buffers as the device addresses them
     int *h_n_dev = nullptr;
-    int copied = 0;
     hipEvent_t ev = nullptr;
     bool pending = false;
   };
@@ -213,9 +221,6 @@ struct Group {
   hipStream_t st_in = nullptr;
   std::deque<std::pair<long long, hipEvent_t>> consumed;
   std::vector<hipEvent_t> ev_free;
-  // the job records' copy back to the host runs on its own stream, beside
-  // the next pass's kernels
-  hipStream_t st_vit = nullptr;
   int vit_pending = -1;          // slot whose Viterbi launch is deferred
   hipEvent_t ev_in = nullptr;
   // aero_chan_feed job tables (pinned -> device, reused once their event completed)
@@ -408,16 +413,19 @@ int process_slot(Group *e, int si) {
   HOST_TIMER(e, "host_frames");
   e->hpool->wait();  // previous slot's frames first (per-channel order)
   e->h_jobs_task.resize((size_t)std::max(njobs, 1) * JOB_OUT);
-  if (njobs > 0) memcpy(e->h_jobs_task.data(), sl.h_out, (size_t)std::min(njobs, sl.copied) * JOB_OUT);
-  if (njobs > sl.copied)  // more jobs than the async copy covered: the slot's device records are intact
-    HIPCHK(hipMemcpy(e->h_jobs_task.data() + (size_t)sl.copied * JOB_OUT, sl.d_out + (size_t)sl.copied * JOB_OUT,
-                     (size_t)(njobs - sl.copied) * JOB_OUT, hipMemcpyDeviceToHost));
+  if (njobs > 0) memcpy(e->h_jobs_task.data(), sl.h_out, (size_t)njobs * JOB_OUT);
   sl.pending = false;
   const bool blocks = (e->flags & AERO_F_TRACE_BLOCKS) != 0;
   if (blocks) {
     // traces run synchronously (run_group waited for this slot): blocks_dbg is this pass's
     e->h_dbg_task.resize((size_t)2500 * C);
-    HIPCHK(hipMemcpy(e->h_dbg_task.data(), e->S.blocks_dbg, e->h_dbg_task.size(), hipMemcpyDeviceToHost));
+    if (!e->trace_some) {
+      HIPCHK(hipMemcpy(e->h_dbg_task.data(), e->S.blocks_dbg, e->h_dbg_task.size(), hipMemcpyDeviceToHost));
+    } else {
+      for (int c : e->trace_list)
+        HIPCHK(hipMemcpy(e->h_dbg_task.data() + (size_t)c * 2500, e->S.blocks_dbg + (size_t)c * 2500, 2500,
+                         hipMemcpyDeviceToHost));
+    }
   }
   if (njobs <= 0) return AERO_OK;
   e->st_jobs += (uint64_t)njobs;
@@ -434,7 +442,7 @@ int process_slot(Group *e, int si) {
       const int c = meta[3] & 0x3FFFFFFF;
       const int reset = (meta[3] >> 30) & 1;
       if (c < 0 || c >= nch || c % T != t) continue;
-      if (blocks) {
+      if (blocks && e->traced(c)) {
         const uint8_t *d = e->h_dbg_task.data() + (size_t)c * 2500;
         int nb;
         memcpy(&nb, d, 4);
@@ -467,7 +475,7 @@ int process_slot(Group *e, int si) {
         frames++;
         su_ok += (uint64_t)__builtin_popcount(mask);
         e->host[c]->frame(info, flen, mask, meta[2]);
-        if (e->flags & AERO_F_TRACE_FRAMES) {
+        if ((e->flags & AERO_F_TRACE_FRAMES) && e->traced(c)) {
           uint8_t rec[320] = {0};
           memcpy(rec, info, flen);
           const uint32_t L = (uint32_t)flen, M = mask;
@@ -507,30 +515,48 @@ void host_wait(aero_engine *e) {
 
 int collect_traces(Group *e) {
   const int C = e->C, nch = e->nch;
+  // the channels whose traces are kept (aero_trace_select), and whether
+  // their rows are copied one by one (a few channels of a large group)
+  std::vector<int> sel;
+  if (!e->trace_some) {
+    sel.resize(nch);
+    for (int c = 0; c < nch; c++) sel[c] = c;
+  } else {
+    sel = e->trace_list;
+  }
+  const bool rows = e->trace_some;
   std::vector<int> hn(nch);
   if (e->flags & AERO_F_TRACE_HOPS) HIPCHK(hipMemcpy(hn.data(), e->S.hop_n, sizeof(int) * nch, hipMemcpyDeviceToHost));
   bool anyhop = false;
   for (int c = 0; c < nch; c++) anyhop |= hn[c] > 0;
   if (anyhop) {
-    std::vector<double> h((size_t)HOP_CAP * 6 * nch);
-    HIPCHK(hipMemcpy(h.data(), e->S.hops, h.size() * 8, hipMemcpyDeviceToHost));
-    for (int c = 0; c < nch; c++) {
+    const size_t rec = (size_t)HOP_CAP * 6;
+    std::vector<double> h(rec * (rows ? 1 : nch));
+    if (!rows) HIPCHK(hipMemcpy(h.data(), e->S.hops, h.size() * 8, hipMemcpyDeviceToHost));
+    for (int c : sel) {
       const int n = std::min(hn[c], HOP_CAP);
-      e->hop_hold[c].insert(e->hop_hold[c].end(), h.begin() + (size_t)c * HOP_CAP * 6,
-                            h.begin() + ((size_t)c * HOP_CAP + n) * 6);
+      if (n <= 0) continue;
+      const double *src = h.data() + (rows ? 0 : (size_t)c * rec);
+      if (rows) HIPCHK(hipMemcpy(h.data(), e->S.hops + (size_t)c * rec, (size_t)n * 6 * 8, hipMemcpyDeviceToHost));
+      e->hop_hold[c].insert(e->hop_hold[c].end(), src, src + (size_t)n * 6);
     }
     HIPCHK(hipMemset(e->S.hop_n, 0, sizeof(int) * nch));
   }
   if (e->flags & AERO_F_TRACE_PT) {
     std::vector<long long> pn(nch);
     HIPCHK(hipMemcpy(pn.data(), e->S.ls + (size_t)LS_PT_N * C, 8 * nch, hipMemcpyDeviceToHost));
-    std::vector<double2> pts((size_t)PT_CAP * nch);
-    HIPCHK(hipMemcpy(pts.data(), e->S.pt, pts.size() * sizeof(double2), hipMemcpyDeviceToHost));
-    for (int c = 0; c < nch; c++) {
+    std::vector<double2> pts((size_t)PT_CAP * (rows ? 1 : nch));
+    if (!rows) HIPCHK(hipMemcpy(pts.data(), e->S.pt, pts.size() * sizeof(double2), hipMemcpyDeviceToHost));
+    for (int c : sel) {
       if (pn[c] > PT_CAP) return AERO_E_FULL;
+      if (pn[c] <= 0) continue;
+      const double2 *src = pts.data() + (rows ? 0 : (size_t)c * PT_CAP);
+      if (rows)
+        HIPCHK(hipMemcpy(pts.data(), e->S.pt + (size_t)c * PT_CAP, (size_t)pn[c] * sizeof(double2),
+                         hipMemcpyDeviceToHost));
       for (long long k = 0; k < pn[c]; k++) {
-        e->pt_hold[c].push_back(pts[(size_t)c * PT_CAP + k].x);
-        e->pt_hold[c].push_back(pts[(size_t)c * PT_CAP + k].y);
+        e->pt_hold[c].push_back(src[k].x);
+        e->pt_hold[c].push_back(src[k].y);
       }
     }
     HIPCHK(hipMemset(e->S.ls + (size_t)LS_PT_N * C, 0, 8 * nch));
@@ -540,15 +566,22 @@ int collect_traces(Group *e) {
   std::vector<long long> sp(nch);
   HIPCHK(hipMemcpy(sp.data(), e->S.ls + (size_t)LS_SOFT_P * C, 8 * nch, hipMemcpyDeviceToHost));
   std::vector<uint8_t> ring;
-  for (int c = 0; c < nch; c++) {
+  for (int c : sel) {
     const long long emitted = sp[c] - sp[c] % e->g.soft_group;
     if (emitted > e->soft_seen[c]) {
-      if (ring.empty()) {
-        ring.resize((size_t)SOFT_RING * nch);
-        HIPCHK(hipMemcpy(ring.data(), e->S.soft, ring.size(), hipMemcpyDeviceToHost));
+      const uint8_t *r;
+      if (rows) {
+        ring.resize(SOFT_RING);
+        HIPCHK(hipMemcpy(ring.data(), e->S.soft + (size_t)c * SOFT_RING, SOFT_RING, hipMemcpyDeviceToHost));
+        r = ring.data();
+      } else {
+        if (ring.empty()) {
+          ring.resize((size_t)SOFT_RING * nch);
+          HIPCHK(hipMemcpy(ring.data(), e->S.soft, ring.size(), hipMemcpyDeviceToHost));
+        }
+        r = ring.data() + (size_t)c * SOFT_RING;
       }
-      for (long long k = e->soft_seen[c]; k < emitted; k++)
-        e->soft_hold[c].push_back(ring[(size_t)c * SOFT_RING + (k & (SOFT_RING - 1))]);
+      for (long long k = e->soft_seen[c]; k < emitted; k++) e->soft_hold[c].push_back(r[k & (SOFT_RING - 1)]);
       e->soft_seen[c] = emitted;
     }
   }
@@ -559,8 +592,8 @@ int collect_traces(Group *e) {
 // coarse hop and demod launch, with the whole GPU to itself.  (Measured, see
 // beside the demod its waves take issue and LDS cycles from the
 // latency-bound demod waves, which then lose as much time as the Viterbi
-// takes; beside the coarse FFT there is no room.)  Its job records go back to
-// the host on a side stream.
+// takes; beside the coarse FFT there is no room.)  Its job records go to the
+// host through mapped pinned memory the kernel writes itself.
 int issue_viterbi(Group *e) {
   const int si = e->vit_pending;
   if (si < 0) return AERO_OK;
@@ -583,7 +616,6 @@ int issue_viterbi(Group *e) {
   ev_end(e, b);
   HIPCHK(hipEventRecord(sl.ev_vit, e->st));
   HIPCHK(hipGetLastError());
-  sl.copied = e->nch;  // every record is in host memory
   HIPCHK(hipEventRecord(sl.ev, e->st));
   sl.pending = true;
   e->pending_slots.push_back(si);
@@ -668,7 +700,7 @@ int run_group(Group *e, int flush) {
     }
     DevState S2 = e->S;
     S2.njobs = sl.d_n;
-    S2.jobout = sl.d_out;
+    S2.jobout = nullptr;  // framing lists jobs only; the Viterbi writes the records
     S2.jobs = sl.d_jobs;
     HIPCHK(hipMemsetAsync(sl.d_n, 0, sizeof(int), e->st));
     {
@@ -704,7 +736,6 @@ int drain_group(Group *e) {
   // the GPU's remaining passes
   if (int rc = poll_slots(e, true)) return rc;
   HIPCHK(hipStreamSynchronize(e->st));
-  HIPCHK(hipStreamSynchronize(e->st_vit));
   if (int rc = poll_slots(e, true)) return rc;
   if (e->flags & (AERO_F_TRACE_PT | AERO_F_TRACE_SOFT | AERO_F_TRACE_HOPS))
     if (int rc = collect_traces(e)) return rc;
@@ -772,10 +803,13 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
   layout(e->S, e->T, mode, e->C, e->flags, reinterpret_cast<char *>(e->pool));
   HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
   for (auto &sl : e->slot) {
-    if (hipMalloc(&sl.d_out, (size_t)JOB_OUT * e->C) != hipSuccess) return AERO_E_NOMEM;
     if (hipMalloc(&sl.d_n, 64) != hipSuccess) return AERO_E_NOMEM;
-    if (hipHostMalloc(&sl.h_out, (size_t)JOB_OUT * e->C) != hipSuccess) return AERO_E_NOMEM;
-    if (hipHostMalloc(&sl.h_n, 64) != hipSuccess) return AERO_E_NOMEM;
+    // kernel-written zero-copy buffers: mapped (a device address for the
+    // Viterbi kernel) and coherent (its system-scope stores reach host memory
+    // without a cache flush); read by the host after the slot's event
+    if (hipHostMalloc(&sl.h_out, (size_t)JOB_OUT * e->C, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return AERO_E_NOMEM;
+    if (hipHostMalloc(&sl.h_n, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return AERO_E_NOMEM;
     HIPCHK(hipHostGetDevicePointer((void **)&sl.h_out_dev, sl.h_out, 0));
     HIPCHK(hipHostGetDevicePointer((void **)&sl.h_n_dev, sl.h_n, 0));
     if (hipMalloc(&sl.d_jobs, (size_t)16 * e->C) != hipSuccess) return AERO_E_NOMEM;
@@ -783,7 +817,6 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
     HIPCHK(hipEventCreateWithFlags(&sl.ev_vit, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_framed, hipEventDisableTiming));
   }
-  HIPCHK(hipStreamCreateWithFlags(&e->st_vit, hipStreamNonBlocking));
   for (int k = 0; k < Group::NPIN; k++) {
     if (hipHostMalloc(&e->pin_avail[k], sizeof(long long) * e->C) != hipSuccess) return AERO_E_NOMEM;
     HIPCHK(hipEventCreateWithFlags(&e->pin_ev[k], hipEventDisableTiming));
@@ -856,10 +889,8 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
 void group_destroy(Group *e) {
   if (!e) return;
   if (e->st) hipStreamSynchronize(e->st);
-  if (e->st_vit) hipStreamSynchronize(e->st_vit);
   ev_collect(e);
   for (auto &sl : e->slot) {
-    if (sl.d_out) (void)hipFree(sl.d_out);
     if (sl.d_n) (void)hipFree(sl.d_n);
     if (sl.d_jobs) (void)hipFree(sl.d_jobs);
     if (sl.ev_vit) (void)hipEventDestroy(sl.ev_vit);
@@ -888,7 +919,6 @@ void group_destroy(Group *e) {
   if (e->st_in) (void)hipStreamDestroy(e->st_in);
   if (e->d_scratch) (void)hipFree(e->d_scratch);
   if (e->pool) (void)hipFree(e->pool);
-  if (e->st_vit) (void)hipStreamDestroy(e->st_vit);
   if (e->st) (void)hipStreamDestroy(e->st);
 }
 
@@ -937,9 +967,10 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
   HOST_TIMER(e, "host_push");
   if (dev)
     if (int rc = check_dev_ptr(src)) return rc;
-  // pinned host input goes straight into the PCM ring rows (one 2-D DMA on
-  // the input stream, overlapping the kernels already queued), as a device
-  // source does; pageable input is staged
+  // pinned host input goes straight into the PCM ring rows (a DMA on the
+  // input stream, overlapping the kernels already queued: one 1-D copy when
+  // the batch is whole ring rows, a 2-D copy otherwise), as a device source
+  // does; pageable input is staged
   const bool pinned = !dev && nch >= 64 && is_pinned_host(src);
   const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   if (pinned) dev = true;
@@ -1169,9 +1200,10 @@ int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) 
     else
       return AERO_E_INVALID;
     HIPCHK(hipSetDevice(e->device));
-    if (!e->burst[kind])
+    if (!e->burst[kind]) {
       if (int rc = burst_group_create(e->device, e->flags, e->max_channels, kind, &e->burst[kind])) return rc;
       burst_group_set_pool(e->burst[kind], e->hpool.get());
+    }
     int local;
     if (int rc = burst_open(e->burst[kind], (int)cfg->bitrate, cfg->disable_reassembly != 0, &local)) return rc;
     *ch_out = (int)e->chmap.size();
@@ -1290,6 +1322,28 @@ int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld,
     int rc = push_common(g, pcm + off * ld, piece, ld, nch, 0, dev != 0);
     if (rc) return rc;
     off += piece;
+  }
+  return AERO_OK;
+}
+
+int aero_trace_select(aero_engine *e, const int *ch, int n) {
+  if (!e || n < 0 || (n && !ch)) return AERO_E_INVALID;
+  for (int i = 0; i < n; i++) {
+    int c;
+    if (!route(e, ch[i], c)) return AERO_E_INVALID;
+  }
+  host_wait(e);
+  for (auto &g : e->groups) {
+    if (!g) continue;
+    g->trace_some = n > 0;  // a group with none of the channels keeps none
+    g->trace_list.clear();
+    g->trace_mask.assign(g->C, 0);
+  }
+  for (int i = 0; i < n; i++) {
+    int c;
+    Group *g = route(e, ch[i], c);
+    if (!g->trace_mask[c]) g->trace_list.push_back(c);
+    g->trace_mask[c] = 1;
   }
   return AERO_OK;
 }
@@ -1446,8 +1500,13 @@ int aero_stat(aero_engine *e, const char *name, uint64_t *value) {
   host_wait(e);  // counters of frames the host workers are still handling
   uint64_t v = 0;
   const std::string n(name);
-  if (n != "rt_tests" && n != "rt_packets" && n != "viterbi_jobs" && n != "frames" && n != "su_crc_ok")
+  if (n != "rt_tests" && n != "rt_packets" && n != "rt_pass_max" && n != "viterbi_jobs" && n != "frames" &&
+      n != "su_crc_ok")
     return AERO_E_INVALID;
+  if (n == "rt_pass_max") {
+    *value = std::max(burst_stat(e->burst[0], 2), burst_stat(e->burst[1], 2));
+    return AERO_OK;
+  }
   if (n == "rt_tests" || n == "rt_packets") {
     *value = burst_stat(e->burst[0], n == "rt_packets") + burst_stat(e->burst[1], n == "rt_packets");
     return AERO_OK;

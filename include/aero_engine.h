@@ -133,6 +133,11 @@ int aero_pop_items_all(aero_engine *e, aero_acars_item *dst, int *ch, size_t cap
  * frames: 320 bytes per completed frame (312 infofield, u32 len, u32 crc mask);
  * needs AERO_F_TRACE_FRAMES. */
 int aero_pop_hops(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n);
+/* Limits the trace collection of continuous channels (soft bits, hops, pt,
+ * blocks, frames) to the n channels in ch (n = 0: every channel again), so
+ * a parity test can sample a few channels of a full-size batch.  Test
+ * support; no reference counterpart. */
+int aero_trace_select(aero_engine *e, const int *ch, int n);
 int aero_pop_pt(aero_engine *e, int ch, double *dst, size_t cap_records, size_t *n);
 int aero_pop_blocks(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
 int aero_pop_frames(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
@@ -155,7 +160,9 @@ void aero_timing_reset(aero_engine *e);
  * the GPU Viterbi decoded and handed back), "frames" (frames delivered to
  * the SU/ACARS host), "su_crc_ok" (SUs whose CRC-16 checked); burst
  * channels: "rt_tests" (RTChannelDeleaveFECScram decodes run),
- * "rt_packets" (R/T packets that passed their CRCs).  Joins the
+ * "rt_packets" (R/T packets that passed their CRCs), "rt_pass_max" (the most
+ * R/T tests one pass handed to the host; from 256 on they are split over the
+ * host threads).  Joins the
  * asynchronous host frame work first.  AERO_E_INVALID for another name. */
 int aero_stat(aero_engine *e, const char *name, uint64_t *value);
 
