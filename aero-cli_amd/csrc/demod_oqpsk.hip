@@ -25,31 +25,20 @@
 
 namespace aero {
 
-// Timing experiments only (never in the product build): AERO_X_OCML swaps
-// the bit-exact libm for the device ocml one, AERO_X_DIVMUL turns divisions
-// by constants into multiplications, to price those parts of the loop.
-#if defined(AERO_X_OCML) || defined(AERO_X_OCML_HYPOT)
+// Timing experiment only (never in the product build): AERO_X_OCML swaps the
+// bit-exact libm for the device ocml one, to price exactness.
+#ifdef AERO_X_OCML
 #define DM_HYPOT ::hypot
-#else
-#define DM_HYPOT aero_hypot
-#endif
-#if defined(AERO_X_OCML) || defined(AERO_X_OCML_ATAN2)
 #define DM_ATAN2 ::atan2
-#else
-#define DM_ATAN2 aero_atan2
-#endif
-#if defined(AERO_X_OCML) || defined(AERO_X_OCML_EVENT)
 #define DM_TANH ::tanh
 #define DM_SINCOS(x, s, c) ::sincos(x, &(s), &(c))
 #else
+#define DM_HYPOT aero_hypot
+#define DM_ATAN2 aero_atan2
 #define DM_TANH aero_tanh
 #define DM_SINCOS(x, s, c) aero_sincos(x, s, c)
 #endif
-#ifdef AERO_X_DIVMUL
-#define DM_DIVC(a, c) ((a) * (1.0 / (c)))
-#else
 #define DM_DIVC(a, c) ((a) / (c))
-#endif
 
 // AERO_X_STAMPS (diagnostic build only): s_memtime cycle totals per loop
 // section of wave 0 of workgroup 0, with scheduling barriers at the stamps
@@ -132,115 +121,270 @@ __device__ __forceinline__ int qround(double d) {  // qRound (Qt 5.9 qglobal.h:5
 }
 
 // carrier-step state kept in LDS (read and written once per carrier event,
-// i.e. once per ~9 samples): keeping it out of VGPRs leaves the per-sample
-// path room for the 55 FIR partial sums without spilling
+// i.e. once per ~9 samples)
 enum { PD_CTX1, PD_CTX2, PD_CTY1, PD_CTY2, PD_MARG_SUM, PD_PM_SUM, PD_MS_SUM, PD_MSE, PD_PTD_RE, PD_PTD_IM,
        PD_M2_FREQ, PD_N };
 enum { PI_MARG_P, PI_DT_P, PI_PM_P, PI_MS_P, PI_N };
 enum { PL_SOFTP, PL_PTN, PL_N };
 
-constexpr int DEMOD_BLOCK = 256;  // channels (= lanes) per workgroup
+constexpr int DEMOD_BLOCK = 256;  // channels per workgroup
+// Two waves per channel group: waves 0-3 run the per-sample chain of the
+// block's 256 channels, waves 4-7 the RRC partial-sum update of the same
+// channels (wave w + 4 serves wave w; the dispatcher places them on the same
+// SIMD, tools/wave_place.hip)
+constexpr int DEMOD_THREADS = 2 * DEMOD_BLOCK;
 // coarse-ring entries staged per channel before one 32-byte write
 constexpr int RING_GROUP = 8;
+// chain -> FIR sequence word: iterations published, | CSEQ_DONE at the end
+constexpr int CSEQ_DONE = 1 << 30;
+// a wait that never ends (a broken hand-off) gives up after ~2^24 polls
+// (about a second) instead of hanging the GPU; the parity tests then fail
+constexpr int SPIN_LIMIT = 1 << 24;
+
+// LDS ordering between the two waves of a pair: every LDS access issued
+// before this has completed (the workgroup-scope release of the AMDGPU memory
+// model, without the wait for outstanding global stores a release fence
+// would add)
+__device__ __forceinline__ void lds_release() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ int lds_load(const int *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// the LDS reads after a poll must not be hoisted above it (compiler barrier;
+// the hardware returns a wave's LDS reads in order)
+__device__ __forceinline__ void lds_acquire() { asm volatile("" ::: "memory"); }
+__device__ __forceinline__ void lds_store(int *p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+constexpr int FIR_LDS_IM = (NTAPS - 1) / 2, FIR_LDS_RE = 21;
+
+struct DemodShared {
+  uint32_t ring[RING_GROUP][DEMOD_BLOCK];
+  double pd[PD_N][DEMOD_BLOCK];
+  long long pl[PL_N][DEMOD_BLOCK];
+  int pi[PI_N][DEMOD_BLOCK];
+  // chain -> FIR: the mixed sample of chain iteration it (slot it & 1) and
+  // the lanes that produced one; FIR -> chain: R_53 after iteration it
+  double2 x[2][DEMOD_BLOCK];
+  double2 r53[2][DEMOD_BLOCK];
+  unsigned long long mask[2][4];
+  int cseq[4], fseq[4];
+  // the FIR wave's oldest partial sums: imaginary R_0..R_26 and real
+  // R_0..R_20 (the other 60 are registers; all 108 would leave the wave no
+  // room below the 256 VGPRs of two waves per SIMD)
+  double qil[FIR_LDS_IM][DEMOD_BLOCK];
+  double qrl[FIR_LDS_RE][DEMOD_BLOCK];
+};
+
+// dst += a (dst = a + b) for the lanes in m only, the rest keep dst: one
+// EXEC-masked VALU op.  In C++ this is a divergent branch, and for values
+// carried around the FIR loop the register allocator then keeps a second
+// copy of every partial sum (the then- and bypass-values of the join), which
+// does not fit; here the partial sum is updated in place.
+__device__ __forceinline__ void add_masked(double &dst, double a, double b, unsigned long long m) {
+  unsigned long long sv;
+  asm volatile(
+      "s_and_saveexec_b64 %0, %4\n\t"
+      "v_add_f64 %1, %2, %3\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(sv), "+v"(dst)
+      : "v"(a), "v"(b), "s"(m)
+      : "scc");
+}
+
+// The RRC (FIR::FIRUpdateAndProcess, decode/DSP.cpp:290-304) in transposed
+// form, R_j(n) = R_{j-1}(n-1) + h[j] x(n), j = 0..54: the filter output used
+// at sample n is R_54(n-1), so only R_54's update is on the chain.  This wave
+// holds R_0..R_53 of its 64 channels (real R_21..R_53 and imaginary
+// R_27..R_53 in registers, the older ones in LDS) and, per chain iteration,
+// takes the mixed samples the chain wave published, forms R_53 first and
+// hands it back (the chain forms R_54 = R_53 + h[54] x itself), then updates
+// the rest while the chain runs on.  h[j] == h[54 - j] bit for bit
+// (host-checked), so the slots of a tap pair share one product; the
+// additions are the reference's, term for term.  Lanes whose chain lane
+// produced no sample in an iteration (waiting for their carrier event) keep
+// their sums.
+__device__ __forceinline__ void demod_fir_wave(const DevState &S, DemodShared &sh, int c, int pair, int wv,
+                                               bool valid) {
+  const int C = S.C;
+  constexpr int NL = (NTAPS - 1) / 2;  // tap pairs k = 0..26, centre 27
+  constexpr int NRL = FIR_LDS_RE, NIL = FIR_LDS_IM;
+  // q[j]: R_j real (j >= NRL used); qi[j]: R_j imaginary (j >= NIL used)
+  double q[NTAPS - 1], qi[NTAPS - 1];
+  {
+    // a lane past the last channel loads channel 0's sums (never used or stored)
+    const double *fir = S.fir + (valid ? c : 0);
+#pragma unroll
+    for (int j = 0; j < NRL; ++j) sh.qrl[j][pair] = fir[(size_t)j * C];
+#pragma unroll
+    for (int j = NRL; j < NTAPS - 1; ++j) q[j] = fir[(size_t)j * C];
+#pragma unroll
+    for (int j = 0; j < NIL; ++j) sh.qil[j][pair] = fir[(size_t)(NTAPS + j) * C];
+#pragma unroll
+    for (int j = NIL; j < NTAPS - 1; ++j) qi[j] = fir[(size_t)(NTAPS + j) * C];
+  }
+  const unsigned long long vmask = __ballot(valid);
+  for (int it = 0;; ++it) {
+    int cs;
+    for (int spin = 0;; ++spin) {
+      cs = __builtin_amdgcn_readfirstlane(lds_load(&sh.cseq[wv]));
+      if ((cs & (CSEQ_DONE - 1)) > it || (cs & CSEQ_DONE)) break;
+      if (spin > SPIN_LIMIT) {
+        cs = CSEQ_DONE;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if ((cs & (CSEQ_DONE - 1)) <= it) break;  // the chain has finished and every iteration is handled
+    lds_acquire();
+    const int par = it & 1;
+    const unsigned long long mv = sh.mask[par][wv];
+    const unsigned long long m =
+        (((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(mv >> 32)) << 32) |
+         (unsigned)__builtin_amdgcn_readfirstlane((unsigned)mv)) & vmask;
+    const double2 xv = sh.x[par][pair];
+    const double cv = xv.x, cvi = xv.y;
+    const double t1 = c_taps[1];
+    const double pr1 = t1 * cv, pi1 = t1 * cvi;
+    // R_53 first, for the chain
+    add_masked(q[NTAPS - 2], q[NTAPS - 3], pr1, m);
+    add_masked(qi[NTAPS - 2], qi[NTAPS - 3], pi1, m);
+    sh.r53[par][pair] = make_double2(q[NTAPS - 2], qi[NTAPS - 2]);
+    lds_release();
+    lds_store(&sh.fseq[wv], it + 1);
+    const bool act = (m >> (pair & 63)) & 1;
+    // slot 54 - k and slot k share h[k] x (k = 0..26), then the centre;
+    // slot 54 is the chain's, slot 53 was formed above.  The lower slots run
+    // oldest-first, each taking the previous slot's value before this sample
+    // (prev), so the LDS ones are read once and written once.
+    double prev_re = 0.0, prev_im = 0.0;
+#pragma unroll
+    for (int k = 0; k <= NL; ++k) {
+      const double t = c_taps[k];
+      const double pr = k == 1 ? pr1 : t * cv, pim = k == 1 ? pi1 : t * cvi;
+      if (k >= 2 && k < NL) {  // upper slot 54 - k (registers)
+        add_masked(q[NTAPS - 1 - k], q[NTAPS - 2 - k], pr, m);
+        add_masked(qi[NTAPS - 1 - k], qi[NTAPS - 2 - k], pim, m);
+      }
+      // lower slot k (the centre, k = 27, too)
+      if (k < NRL) {
+        const double old = sh.qrl[k][pair];
+        const double nv = prev_re + pr;
+        sh.qrl[k][pair] = act ? nv : old;
+        prev_re = old;
+      } else {
+        const double old = q[k];
+        add_masked(q[k], prev_re, pr, m);
+        prev_re = old;
+      }
+      if (k < NIL) {
+        const double old = sh.qil[k][pair];
+        const double nv = prev_im + pim;
+        sh.qil[k][pair] = act ? nv : old;
+        prev_im = old;
+      } else {
+        const double old = qi[k];
+        add_masked(qi[k], prev_im, pim, m);
+        prev_im = old;
+      }
+    }
+  }
+  if (!valid) return;
+  int cl = c;
+  asm volatile("" : "+v"(cl));
+  double *fir = S.fir + cl;
+#pragma unroll
+  for (int j = 0; j < NRL; ++j) fir[(size_t)j * C] = sh.qrl[j][pair];
+#pragma unroll
+  for (int j = NRL; j < NTAPS - 1; ++j) fir[(size_t)j * C] = q[j];
+#pragma unroll
+  for (int j = 0; j < NIL; ++j) fir[(size_t)(NTAPS + j) * C] = sh.qil[j][pair];
+#pragma unroll
+  for (int j = NIL; j < NTAPS - 1; ++j) fir[(size_t)(NTAPS + j) * C] = qi[j];
+}
 
 template <bool TRACE>
-__global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, DevTables T, int nch, int flush) {
-  // LDS (38 KB per 256-channel block): the coarse-ring staging area (entries
-  // of 8 consecutive samples leave as one 32-byte write per channel instead
-  // of eight 4-byte ones) and the carrier-step state.  The RRC taps are
-  // scalar constant-memory loads.
-// the first QIM_LDS imaginary partial sums live in LDS, the rest in
-// registers (0: all in registers; 55: all in LDS, the round-2 layout)
-#ifndef QIM_LDS
-#define QIM_LDS 0
-#endif
-  __shared__ double s_qim[QIM_LDS > 0 ? QIM_LDS : 1][DEMOD_BLOCK];
-#define QIM(j) (*((j) < QIM_LDS ? &s_qim[(j) < QIM_LDS ? (j) : 0][pair] : &qi[j]))
-  __shared__ uint32_t s_ring[RING_GROUP][DEMOD_BLOCK];
-  __shared__ double s_pd[PD_N][DEMOD_BLOCK];
-  __shared__ long long s_pl[PL_N][DEMOD_BLOCK];
-  __shared__ int s_pi[PI_N][DEMOD_BLOCK];
-  const int c = blockIdx.x * DEMOD_BLOCK + threadIdx.x;
-  const int pair = threadIdx.x;  // this channel's LDS column
-  if (c >= nch) return;
+__device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTables &T, DemodShared &sh, int c,
+                                                 int pair, int wv, bool valid, int flush) {
   const int C = S.C;
-
   // sample counters relative to n0 (a launch covers at most one hop)
-  const long long n0 = S.ls[LS_NSAMP * C + c];
-  const long long avail = S.ls[LS_AVAIL * C + c];
-  const long long filled0 = S.ls[LS_FILLED * C + c];
-  const int hops_done = S.is[IS_HOPS_DONE * C + c];
-  const long long boundary = (long long)HOP * (hops_done + 1) - 1;
-  long long end = avail < boundary ? avail : boundary;
-  if (!flush && avail <= boundary) end = n0;  // wait for a whole segment + the hop's ring entry
-  const int capm = S.pcm_cap - 1;
-  const int pb = (int)(n0 & capm);          // PCM ring row of sample n0
-  const int rb = (int)(n0 & (NFFT - 1));    // coarse-ring slot of sample n0
-  const int ia = (int)(avail - n0);         // pushed samples beyond n0 (<= ring size)
-  const int ie = (int)(end - n0);
-  int ifl = (int)(filled0 - n0);            // coarse-ring entries written: samples < n0 + ifl
-
-  double mc_ptr = S.ds[DS_MC_PTR * C + c], mc_step = S.ds[DS_MC_STEP * C + c];
-  // coarse-ring catch-up (entry of sample n0 not yet written)
-  if (ifl == 0 && ia > 0) {
-    const int16_t x = S.pcm[(size_t)pb * C + c];
-    S.cring[(size_t)c * NFFT + rb] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
-    ifl = 1;
+  long long n0 = 0;
+  int pb = 0, rb = 0, ia = 0, ie = 0, ifl = 0, capm = S.pcm_cap - 1;
+  double mc_ptr = 0.0, mc_step = 0.0;
+  if (valid) {
+    n0 = S.ls[LS_NSAMP * C + c];
+    const long long avail = S.ls[LS_AVAIL * C + c];
+    const long long filled0 = S.ls[LS_FILLED * C + c];
+    const int hops_done = S.is[IS_HOPS_DONE * C + c];
+    const long long boundary = (long long)HOP * (hops_done + 1) - 1;
+    long long end = avail < boundary ? avail : boundary;
+    if (!flush && avail <= boundary) end = n0;  // wait for a whole segment + the hop's ring entry
+    pb = (int)(n0 & capm);          // PCM ring row of sample n0
+    rb = (int)(n0 & (NFFT - 1));    // coarse-ring slot of sample n0
+    ia = (int)(avail - n0);         // pushed samples beyond n0 (<= ring size)
+    ie = (int)(end - n0);
+    ifl = (int)(filled0 - n0);      // coarse-ring entries written: samples < n0 + ifl
+    mc_ptr = S.ds[DS_MC_PTR * C + c];
+    mc_step = S.ds[DS_MC_STEP * C + c];
+    // coarse-ring catch-up (entry of sample n0 not yet written)
+    if (ifl == 0 && ia > 0) {
+      const int16_t x = S.pcm[(size_t)pb * C + c];
+      S.cring[(size_t)c * NFFT + rb] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
+      ifl = 1;
+    }
+    if (ie <= 0) {
+      S.ls[LS_FILLED * C + c] = n0 + ifl;
+      ie = 0;
+    }
   }
-  if (ie <= 0) {
-    S.ls[LS_FILLED * C + c] = n0 + ifl;
-    return;
-  }
-
-  double m2_ptr = S.ds[DS_M2_PTR * C + c], m2_step = S.ds[DS_M2_STEP * C + c];
-  double so_ptr = S.ds[DS_SO_PTR * C + c], so_last = S.ds[DS_SO_LAST * C + c];
-  double so_step = S.ds[DS_SO_STEP * C + c], so_freq = S.ds[DS_SO_FREQ * C + c];
-  double agc_sum = S.ds[DS_AGC_SUM * C + c];
-  double d1[2], d41[4], d42[4], d8[3];
+  const bool work = ie > 0;
+  double m2_ptr = 0, m2_step = 0, so_ptr = 0, so_last = 0, so_step = 0, so_freq = 0, agc_sum = 0;
+  double d1[2] = {0, 0}, d41[4] = {0, 0, 0, 0}, d42[4] = {0, 0, 0, 0}, d8[3] = {0, 0, 0};
+  double srx1 = 0, srx2 = 0, sry1 = 0, sry2 = 0, s2l_re = 0, s2l_im = 0;
+  double q54 = 0, q54i = 0;  // R_54: the filter output of the next sample
+  int agc_ptr = 0, yui = 0, s2l_init = 0;
+  int16_t pcm_next = 0, pcm_next2 = 0;
+  double agc_next = 0;
+  if (work) {
+    m2_ptr = S.ds[DS_M2_PTR * C + c], m2_step = S.ds[DS_M2_STEP * C + c];
+    so_ptr = S.ds[DS_SO_PTR * C + c], so_last = S.ds[DS_SO_LAST * C + c];
+    so_step = S.ds[DS_SO_STEP * C + c], so_freq = S.ds[DS_SO_FREQ * C + c];
+    agc_sum = S.ds[DS_AGC_SUM * C + c];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) d1[k] = S.ds[(DS_D1_0 + k) * C + c];
+    for (int k = 0; k < 2; ++k) d1[k] = S.ds[(DS_D1_0 + k) * C + c];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) d41[k] = S.ds[(DS_D41_0 + k) * C + c];
+    for (int k = 0; k < 4; ++k) d41[k] = S.ds[(DS_D41_0 + k) * C + c];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) d42[k] = S.ds[(DS_D42_0 + k) * C + c];
+    for (int k = 0; k < 4; ++k) d42[k] = S.ds[(DS_D42_0 + k) * C + c];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) d8[k] = S.ds[(DS_D8_0 + k) * C + c];
-  double srx1 = S.ds[DS_SR_X1 * C + c], srx2 = S.ds[DS_SR_X2 * C + c];
-  double sry1 = S.ds[DS_SR_Y1 * C + c], sry2 = S.ds[DS_SR_Y2 * C + c];
-  double s2l_re = S.ds[DS_S2L_RE * C + c], s2l_im = S.ds[DS_S2L_IM * C + c];
-  int agc_ptr = S.is[IS_AGC_PTR * C + c];
-  int yui = S.is[IS_YUI * C + c], s2l_init = S.is[IS_S2L_INIT * C + c];
-  {  // carrier-step state -> LDS
+    for (int k = 0; k < 3; ++k) d8[k] = S.ds[(DS_D8_0 + k) * C + c];
+    srx1 = S.ds[DS_SR_X1 * C + c], srx2 = S.ds[DS_SR_X2 * C + c];
+    sry1 = S.ds[DS_SR_Y1 * C + c], sry2 = S.ds[DS_SR_Y2 * C + c];
+    s2l_re = S.ds[DS_S2L_RE * C + c], s2l_im = S.ds[DS_S2L_IM * C + c];
+    agc_ptr = S.is[IS_AGC_PTR * C + c];
+    yui = S.is[IS_YUI * C + c], s2l_init = S.is[IS_S2L_INIT * C + c];
     static constexpr int pd_src[PD_N] = {DS_CT_X1, DS_CT_X2, DS_CT_Y1, DS_CT_Y2, DS_MARG_SUM, DS_PM_SUM,
                                          DS_MS_SUM, DS_MSE, DS_PTD_RE, DS_PTD_IM, DS_M2_FREQ};
     static constexpr int pi_src[PI_N] = {IS_MARG_P, IS_DT_P, IS_PM_P, IS_MS_P};
 #pragma unroll
-    for (int k = 0; k < PD_N; ++k) s_pd[k][pair] = S.ds[pd_src[k] * C + c];
+    for (int k = 0; k < PD_N; ++k) sh.pd[k][pair] = S.ds[pd_src[k] * C + c];
 #pragma unroll
-    for (int k = 0; k < PI_N; ++k) s_pi[k][pair] = S.is[pi_src[k] * C + c];
-    s_pl[PL_SOFTP][pair] = S.ls[LS_SOFT_P * C + c];
-    s_pl[PL_PTN][pair] = TRACE ? S.ls[LS_PT_N * C + c] : 0;
+    for (int k = 0; k < PI_N; ++k) sh.pi[k][pair] = S.is[pi_src[k] * C + c];
+    sh.pl[PL_SOFTP][pair] = S.ls[LS_SOFT_P * C + c];
+    sh.pl[PL_PTN][pair] = TRACE ? S.ls[LS_PT_N * C + c] : 0;
+    q54 = S.fir[(size_t)(NTAPS - 1) * C + c];
+    q54i = S.fir[(size_t)(2 * NTAPS - 1) * C + c];
+    // R_53 before the first sample: the slot chain iteration 0 reads
+    sh.r53[1][pair] = make_double2(S.fir[(size_t)(NTAPS - 2) * C + c], S.fir[(size_t)(2 * NTAPS - 2) * C + c]);
+    // sample n0+i's AGC ring slot is loaded one sample ahead, its PCM word two
+    // samples ahead: the coarse-ring entry staged during sample i holds sample
+    // i+1's PCM word, which one sample ahead would be waited for at once
+    pcm_next = S.pcm[(size_t)pb * C + c];
+    pcm_next2 = S.pcm[(size_t)((pb + 1) & capm) * C + c];
+    agc_next = S.agc[(size_t)agc_ptr * C + c];
   }
-
-  // transposed RRC partial sums R_j(n-1), j = 0..54, real and imaginary, in
-  // registers (110 doubles of the 512-register budget of the one wave per
-  // SIMD; as LDS the imaginary part cost two LDS round trips per tap and
-  // sample)
-  double q[NTAPS];
-  double qi[NTAPS];
-#pragma unroll
-  for (int j = 0; j < NTAPS; ++j) q[j] = S.fir[(size_t)j * C + c];
-#pragma unroll
-  for (int j = 0; j < NTAPS; ++j) QIM(j) = S.fir[(size_t)(NTAPS + j) * C + c];
-
   const double PT = 0.4 * WTSIZE;  // IfHavePassedPoint(ee) with ee = 0.4 (oqpskdemodulator.cpp:225)
 
-  // sample n0+i's AGC ring slot is loaded one sample ahead, its PCM word two
-  // samples ahead: the coarse-ring entry staged during sample i holds sample
-  // i+1's PCM word, which one sample ahead would be waited for at once
-  int16_t pcm_next = S.pcm[(size_t)pb * C + c];
-  int16_t pcm_next2 = S.pcm[(size_t)((pb + 1) & capm) * C + c];
-  double agc_next = S.agc[(size_t)agc_ptr * C + c];
   // Event-aligned iteration.  The carrier/MSE/soft-bit step runs at every
   // second sample instant (one channel in ~9 samples), but in lockstep
   // sample order some lane of a wave has one at almost every sample, so the
@@ -248,14 +392,16 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
   // own samples until its next carrier event (inner loop), and the carrier
   // step then runs once for all lanes together.  Per lane the operations and
   // their order are exactly the reference's; only the interleaving of
-  // different channels changes.
-  int i = 0;
+  // different channels changes.  Every inner iteration hands the active
+  // lanes' mixed samples to the FIR wave (`it` counts the wave's iterations).
+  int i = 0, it = 0, spin_left = SPIN_LIMIT;
   double ev_pr = 0.0, ev_pi = 0.0;
 #ifdef AERO_X_STAMPS
   unsigned long long xstamp_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, xtime_ = __builtin_amdgcn_s_memtime();
 #endif
   while (i < ie) {
     bool pend = false;
+    it = __builtin_amdgcn_readfirstlane(lds_load(&sh.cseq[wv]));
     do {
       XSTAMP(0);  // loop control
       const int16_t xs = pcm_next;
@@ -272,32 +418,35 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       const double dval = ((double)xs) / 32768.0;
       // mix (oqpskdemodulator.cpp:390): cval = CIS * dval, componentwise
       const double cv = cm.x * dval, cvi = cm.y * dval;
-      // rrc (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
-      double s2r = q[NTAPS - 1], s2i = QIM(NTAPS - 1);
+      // hand x(n) to the FIR wave (its slot was read: the FIR wave passed
+      // iteration it - 2 before this wave's wait in iteration it - 1)
       {
-        // R_j(n) = R_{j-1}(n-1) + h[j] x(n) with h[j] == h[54 - j] bit for bit
-        // (host-checked): the slots of a tap pair share one product, so the
-        // taps run outside-in (slots 54 - k and k for k = 0..26, then the
-        // centre), with the old value of slot k kept for slot k + 1.  Taps are
-        // uniform scalar loads from constant memory.
-        double prev_re = 0.0, prev_im = 0.0;  // slot k - 1 before this sample
-#pragma unroll
-        for (int k = 0; k < (NTAPS - 1) / 2; ++k) {
-          const double t = c_taps[k];
-          const double pr = t * cv, pim = t * cvi;
-          const double old_re = q[k], old_im = QIM(k);
-          q[NTAPS - 1 - k] = q[NTAPS - 2 - k] + pr;
-          QIM(NTAPS - 1 - k) = QIM(NTAPS - 2 - k) + pim;
-          q[k] = prev_re + pr;
-          QIM(k) = prev_im + pim;
-          prev_re = old_re;
-          prev_im = old_im;
-          if (QIM_LDS > 0 && (k & 7) == 7) asm volatile("" : : : "memory");
-        }
-        const double tc = c_taps[(NTAPS - 1) / 2];
-        q[(NTAPS - 1) / 2] = prev_re + tc * cv;
-        QIM((NTAPS - 1) / 2) = prev_im + tc * cvi;
+        const int par = it & 1;
+        sh.x[par][pair] = make_double2(cv, cvi);
+        sh.mask[par][wv] = __builtin_amdgcn_read_exec();
+        lds_release();
+        lds_store(&sh.cseq[wv], it + 1);
       }
+      // rrc output of this sample: R_54(n-1); then R_54(n) = R_53(n-1) + h[54] x(n)
+      // with R_53(n-1) from the FIR wave's iteration it - 1
+      double s2r = q54, s2i = q54i;
+      {
+        if (it > 0) {
+          for (int spin = 0; __builtin_amdgcn_readfirstlane(lds_load(&sh.fseq[wv])) < it; ++spin) {
+            if (spin > spin_left) {  // broken hand-off: stop waiting for good
+              spin_left = 0;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          lds_acquire();
+        }
+        const double2 r53 = sh.r53[(it & 1) ^ 1][pair];
+        const double t0 = c_taps[0];
+        q54 = r53.x + t0 * cv;
+        q54i = r53.y + t0 * cvi;
+      }
+      it = __builtin_amdgcn_readfirstlane(it + 1);
       // AGC (DSP.cpp:371-380) on |sig2| (oqpskdemodulator.cpp:399-405)
       const double dab = sqrt(s2r * s2r + s2i * s2i);
       {
@@ -312,7 +461,7 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
         s2i *= g;
       }
       // clipping (:408-410)
-      XSTAMP(1);  // loads, FIR update, AGC
+      XSTAMP(1);  // loads, FIR hand-off, AGC
       const double ab = DM_HYPOT(s2r, s2i);
       if (ab > 2.84) {
         const double k = 2.84 / ab;
@@ -353,8 +502,8 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
         yui++;
         yui %= 2;
         if (!yui) {
-          s_pd[PD_PTD_RE][pair] = pr;
-          s_pd[PD_PTD_IM][pair] = pi;
+          sh.pd[PD_PTD_RE][pair] = pr;
+          sh.pd[PD_PTD_IM][pair] = pi;
         } else {
           ev_pr = pr;
           ev_pi = pi;
@@ -371,16 +520,16 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
         const int m = rb + i + 1;  // ring slot before masking
         const int k = m & (RING_GROUP - 1);
         {
-          s_ring[k][pair] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)pcm_next << 16);
+          sh.ring[k][pair] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)pcm_next << 16);
           if (k == RING_GROUP - 1) {
             uint32_t *dst = S.cring + (size_t)c * NFFT + ((m - (RING_GROUP - 1)) & (NFFT - 1));
             if (i + 1 - (RING_GROUP - 1) >= 1) {  // the whole group was staged by this launch
 #pragma unroll
               for (int q4 = 0; q4 < RING_GROUP / 4; ++q4)
-                reinterpret_cast<uint4 *>(dst)[q4] = make_uint4(s_ring[4 * q4][pair], s_ring[4 * q4 + 1][pair],
-                                                                s_ring[4 * q4 + 2][pair], s_ring[4 * q4 + 3][pair]);
+                reinterpret_cast<uint4 *>(dst)[q4] = make_uint4(sh.ring[4 * q4][pair], sh.ring[4 * q4 + 1][pair],
+                                                                sh.ring[4 * q4 + 2][pair], sh.ring[4 * q4 + 3][pair]);
             } else {
-              for (int j = (RING_GROUP - 1) - i; j < RING_GROUP; ++j) dst[j] = s_ring[j][pair];
+              for (int j = (RING_GROUP - 1) - i; j < RING_GROUP; ++j) dst[j] = sh.ring[j][pair];
             }
           }
         }
@@ -404,8 +553,8 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       // every event), so their slots share one 16-byte entry: one line per
       // event instead of two
       double2 *pmsb = reinterpret_cast<double2 *>(S.pm) + (size_t)cl * MSE_LEN;
-      int marg_p = s_pi[PI_MARG_P][pair], dt_p = s_pi[PI_DT_P][pair];
-      int pm_p = s_pi[PI_PM_P][pair], ms_p = s_pi[PI_MS_P][pair];
+      int marg_p = sh.pi[PI_MARG_P][pair], dt_p = sh.pi[PI_DT_P][pair];
+      int pm_p = sh.pi[PI_PM_P][pair], ms_p = sh.pi[PI_MS_P][pair];
       const double pr = ev_pr, pi = ev_pi;
       // the four moving-average rings of this symbol, loaded together
       // before any ring store so their latencies overlap
@@ -414,12 +563,12 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       const double2 dv = dtb[dt_rp];
       const double2 pms_old = pmsb[pm_p];
       const double pm_old = pms_old.x, ms_old = pms_old.y;
-      double ctx1 = s_pd[PD_CTX1][pair], ctx2 = s_pd[PD_CTX2][pair];
-      double cty1 = s_pd[PD_CTY1][pair], cty2 = s_pd[PD_CTY2][pair];
-      double marg_sum = s_pd[PD_MARG_SUM][pair], pm_sum = s_pd[PD_PM_SUM][pair];
-      double ms_sum = s_pd[PD_MS_SUM][pair], mse;
-      const double ptd_re = s_pd[PD_PTD_RE][pair], ptd_im = s_pd[PD_PTD_IM][pair];
-      double m2_freq = s_pd[PD_M2_FREQ][pair];
+      double ctx1 = sh.pd[PD_CTX1][pair], ctx2 = sh.pd[PD_CTX2][pair];
+      double cty1 = sh.pd[PD_CTY1][pair], cty2 = sh.pd[PD_CTY2][pair];
+      double marg_sum = sh.pd[PD_MARG_SUM][pair], pm_sum = sh.pd[PD_PM_SUM][pair];
+      double ms_sum = sh.pd[PD_MS_SUM][pair], mse;
+      const double ptd_re = sh.pd[PD_PTD_RE][pair], ptd_im = sh.pd[PD_PTD_IM][pair];
+      double m2_freq = sh.pd[PD_M2_FREQ][pair];
       double qr = pr, qi = ptd_im;  // pt_qpsk
       // carrier tracking (:456-470)
       const double ct_xt = DM_TANH(pi) * pr;
@@ -456,9 +605,9 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
       qr = rr;
       qi = ri;
       if (TRACE) {
-        const long long ptn = s_pl[PL_PTN][pair];
+        const long long ptn = sh.pl[PL_PTN][pair];
         if (ptn < S.pt_cap) S.pt[(size_t)cl * S.pt_cap + ptn] = make_double2(qr, qi);
-        s_pl[PL_PTN][pair] = ptn + 1;
+        sh.pl[PL_PTN][pair] = ptn + 1;
       }
       // MSEcalc::Update (DSP.cpp:449-461)
       {
@@ -487,72 +636,72 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
         int rbit = qround(0.75 * qr * 127.0 + 128.0);
         if (rbit > 255) rbit = 255;
         if (rbit < 0) rbit = 0;
-        const long long softp = s_pl[PL_SOFTP][pair];
+        const long long softp = sh.pl[PL_SOFTP][pair];
         {
           uint8_t *soft = S.soft + (size_t)cl * SOFT_RING;
           soft[softp & (SOFT_RING - 1)] = (uint8_t)ibit;
           soft[(softp + 1) & (SOFT_RING - 1)] = (uint8_t)rbit;
         }
-        s_pl[PL_SOFTP][pair] = softp + 2;
+        sh.pl[PL_SOFTP][pair] = softp + 2;
       }
-      s_pd[PD_CTX1][pair] = ctx1;
-      s_pd[PD_CTX2][pair] = ctx2;
-      s_pd[PD_CTY1][pair] = cty1;
-      s_pd[PD_CTY2][pair] = cty2;
-      s_pd[PD_MARG_SUM][pair] = marg_sum;
-      s_pd[PD_PM_SUM][pair] = pm_sum;
-      s_pd[PD_MS_SUM][pair] = ms_sum;
-      s_pd[PD_MSE][pair] = mse;
-      s_pd[PD_M2_FREQ][pair] = m2_freq;
-      s_pi[PI_MARG_P][pair] = marg_p;
-      s_pi[PI_DT_P][pair] = dt_p;
-      s_pi[PI_PM_P][pair] = pm_p;
-      s_pi[PI_MS_P][pair] = ms_p;
+      sh.pd[PD_CTX1][pair] = ctx1;
+      sh.pd[PD_CTX2][pair] = ctx2;
+      sh.pd[PD_CTY1][pair] = cty1;
+      sh.pd[PD_CTY2][pair] = cty2;
+      sh.pd[PD_MARG_SUM][pair] = marg_sum;
+      sh.pd[PD_PM_SUM][pair] = pm_sum;
+      sh.pd[PD_MS_SUM][pair] = ms_sum;
+      sh.pd[PD_MSE][pair] = mse;
+      sh.pd[PD_M2_FREQ][pair] = m2_freq;
+      sh.pi[PI_MARG_P][pair] = marg_p;
+      sh.pi[PI_DT_P][pair] = dt_p;
+      sh.pi[PI_PM_P][pair] = pm_p;
+      sh.pi[PI_MS_P][pair] = ms_p;
       nco_next(m2_ptr, m2_step);
       ++i;
     }
     XSTAMP(5);  // carrier event step
   }
+  // every lane of the wave passes here: the FIR wave may stop once it has
+  // handled the iterations published so far
+  lds_release();
+  lds_store(&sh.cseq[wv], lds_load(&sh.cseq[wv]) | CSEQ_DONE);
 #ifdef AERO_X_STAMPS
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     for (int k = 0; k < 6; ++k) g_stamps[k] += xstamp_[k];
     g_stamps[6] += (unsigned long long)i;  // samples
   }
 #endif
+  if (!work) return;
   // staged entries of an unfinished 16-sample group
   if (ifl - 1 >= 1 && ((rb + ifl - 1) & (RING_GROUP - 1)) != RING_GROUP - 1) {
     const int last = ifl - 1;                                // relative sample of the last staged entry
     const int g0 = last - ((rb + last) & (RING_GROUP - 1));  // relative sample of its group's slot 0
     uint32_t *dst = S.cring + (size_t)c * NFFT + ((rb + g0) & (NFFT - 1));
-    for (int j = (g0 >= 1 ? 0 : 1 - g0); j <= last - g0; ++j) dst[j] = s_ring[j][pair];
+    for (int j = (g0 >= 1 ? 0 : 1 - g0); j <= last - g0; ++j) dst[j] = sh.ring[j][pair];
   }
 
   // epilogue addresses are recomputed from a laundered channel index so the
-  // compiler cannot keep ~110 prologue addresses live across the sample loop
+  // compiler cannot keep the prologue addresses live across the sample loop
   int cl = c;
   asm volatile("" : "+v"(cl));
-  {
-    double *fir = S.fir + cl;
-#pragma unroll
-    for (int j = 0; j < NTAPS; ++j) fir[(size_t)j * C] = q[j];
-#pragma unroll
-    for (int j = 0; j < NTAPS; ++j) fir[(size_t)(NTAPS + j) * C] = QIM(j);
-  }
+  S.fir[(size_t)(NTAPS - 1) * C + cl] = q54;
+  S.fir[(size_t)(2 * NTAPS - 1) * C + cl] = q54i;
   double *ds = S.ds + cl;
   int *is = S.is + cl;
   long long *ls = S.ls + cl;
   ls[LS_NSAMP * C] = n0 + i;
   ls[LS_FILLED * C] = n0 + ifl;
-  ls[LS_SOFT_P * C] = s_pl[PL_SOFTP][pair];
-  if (TRACE) ls[LS_PT_N * C] = s_pl[PL_PTN][pair];
+  ls[LS_SOFT_P * C] = sh.pl[PL_SOFTP][pair];
+  if (TRACE) ls[LS_PT_N * C] = sh.pl[PL_PTN][pair];
   {
     static constexpr int pd_dst[PD_N] = {DS_CT_X1, DS_CT_X2, DS_CT_Y1, DS_CT_Y2, DS_MARG_SUM, DS_PM_SUM,
                                          DS_MS_SUM, DS_MSE, DS_PTD_RE, DS_PTD_IM, DS_M2_FREQ};
     static constexpr int pi_dst[PI_N] = {IS_MARG_P, IS_DT_P, IS_PM_P, IS_MS_P};
 #pragma unroll
-    for (int k = 0; k < PD_N; ++k) ds[pd_dst[k] * C] = s_pd[k][pair];
+    for (int k = 0; k < PD_N; ++k) ds[pd_dst[k] * C] = sh.pd[k][pair];
 #pragma unroll
-    for (int k = 0; k < PI_N; ++k) is[pi_dst[k] * C] = s_pi[k][pair];
+    for (int k = 0; k < PI_N; ++k) is[pi_dst[k] * C] = sh.pi[k][pair];
   }
   ds[DS_M2_PTR * C] = m2_ptr;
   ds[DS_M2_STEP * C] = m2_step;
@@ -582,8 +731,31 @@ __global__ __launch_bounds__(DEMOD_BLOCK) void demod_oqpsk_kernel(DevState S, De
   is[IS_S2L_INIT * C] = s2l_init;
 }
 
+// One workgroup = 256 channels, two waves per 64 channels (chain + FIR).
+// Segment contract: a launch advances every channel from nsamp up to (but
+// excluding) its next coarse-estimate hop sample, or to the pushed end; it
+// also writes the coarse-ring entry of the sample after each processed one
+// (ring fill precedes the hop that uses it, oqpskdemodulator.cpp:351-369).
+template <bool TRACE>
+__global__ __launch_bounds__(DEMOD_THREADS) void demod_oqpsk_kernel(DevState S, DevTables T, int nch, int flush) {
+  __shared__ DemodShared sh;
+  const int pair = threadIdx.x & (DEMOD_BLOCK - 1);  // this channel's LDS column
+  const int wv = pair >> 6;                          // channel wave of the block
+  const int c = blockIdx.x * DEMOD_BLOCK + pair;
+  const bool valid = c < nch;
+  if (threadIdx.x < 4) {
+    sh.cseq[threadIdx.x] = 0;
+    sh.fseq[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x >= DEMOD_BLOCK)
+    demod_fir_wave(S, sh, c, pair, wv, valid);
+  else
+    demod_chain_wave<TRACE>(S, T, sh, c, pair, wv, valid, flush);
+}
+
 void launch_demod(hipStream_t st, const DevState &S, const DevTables &T, int nch, int flush, bool trace) {
-  dim3 grid((nch + DEMOD_BLOCK - 1) / DEMOD_BLOCK), block(DEMOD_BLOCK);
+  dim3 grid((nch + DEMOD_BLOCK - 1) / DEMOD_BLOCK), block(DEMOD_THREADS);
   if (trace)
     hipLaunchKernelGGL(demod_oqpsk_kernel<true>, grid, block, 0, st, S, T, nch, flush);
   else
