@@ -463,9 +463,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void vi
 
 void launch_frame(hipStream_t st, int mode, const DevState &S, int nch) {
   const dim3 g((nch + 255) / 256), b(256);
+  // MSK framing depends on the AeroL bit rate only
   if (mode == MODE_OQPSK)
     hipLaunchKernelGGL(frame_kernel, g, b, 0, st, S, nch);
-  else if (mode == MODE_MSK600)
+  else if (msk_bitrate(mode) == 600)
     hipLaunchKernelGGL(frame_msk_kernel<MODE_MSK600>, g, b, 0, st, S, nch);
   else
     hipLaunchKernelGGL(frame_msk_kernel<MODE_MSK1200>, g, b, 0, st, S, nch);
@@ -479,7 +480,7 @@ void launch_viterbi(hipStream_t st, int mode, const DevState &S, const DevTables
   max_jobs = max_jobs < 16384 ? max_jobs : 16384;
   if (mode == MODE_OQPSK)
     hipLaunchKernelGGL((viterbi_kernel<BLOCK, DL2_LEN>), dim3(max_jobs), dim3(64), 0, st, S, T, trace);
-  else if (mode == MODE_MSK600)
+  else if (msk_bitrate(mode) == 600)
     hipLaunchKernelGGL((viterbi_kernel<6 * 64, MSK_DL2_LEN>), dim3(max_jobs), dim3(64), 0, st, S, T, trace);
   else
     hipLaunchKernelGGL((viterbi_kernel<9 * 64, MSK_DL2_LEN>), dim3(max_jobs), dim3(64), 0, st, S, T, trace);

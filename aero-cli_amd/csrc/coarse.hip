@@ -43,17 +43,32 @@ struct CoarseK<MODE_OQPSK> {
   static constexpr int YLO = 2815, YHI = 13568;
   static constexpr double FS = 48000.0;
 };
+// MSK at Fs (setSettings(13, 900, 600, Fs)): hzperbin = Fs / 8192; startbin
+// round(900 / hzperbin), stopbin nfft - startbin, the fold search over
+// [round(-900 / hzperbin + 4096), round(900 / hzperbin + 4096)) with
+// expectedpeakbin round(600 / (2 hzperbin)); y kept over MSK_YLO..MSK_YHI
+template <int FS>
+struct MskCoarseBins;
 template <>
-struct CoarseK<MODE_MSK600> {
-  static constexpr int LOG2N = 13, HOPN = 2048, START = 614, STOP = 7578, ILO = 3482, IHI = 4710, EPB = 205;
-  static constexpr int YLO = 3276, YHI = 4915;
-  static constexpr double FS = 12000.0;
+struct MskCoarseBins<12000> {
+  static constexpr int START = 614, STOP = 7578, ILO = 3482, IHI = 4710, EPB = 205;
 };
 template <>
-struct CoarseK<MODE_MSK1200> {
-  static constexpr int LOG2N = 13, HOPN = 2048, START = 307, STOP = 7885, ILO = 3789, IHI = 4403, EPB = 102;
-  static constexpr int YLO = 3686, YHI = 4505;
-  static constexpr double FS = 24000.0;
+struct MskCoarseBins<24000> {
+  static constexpr int START = 307, STOP = 7885, ILO = 3789, IHI = 4403, EPB = 102;
+};
+template <>
+struct MskCoarseBins<48000> {
+  static constexpr int START = 154, STOP = 8038, ILO = 3942, IHI = 4250, EPB = 51;
+};
+template <int M>
+struct CoarseK {
+  using B = MskCoarseBins<msk_fs(M)>;
+  static constexpr int LOG2N = 13, HOPN = 2048, START = B::START, STOP = B::STOP, ILO = B::ILO, IHI = B::IHI,
+                       EPB = B::EPB;
+  static constexpr int YLO = MSK_YLO, YHI = MSK_YHI;
+  static_assert(ILO - EPB - 1 >= YLO && IHI - 1 + EPB + 1 <= YHI, "fold search inside the kept y bins");
+  static constexpr double FS = (double)msk_fs(M);
 };
 
 __device__ __forceinline__ void set_freq1(double &freq, double &step, double f, double fs) {  // SetFreq (DSP.cpp:163-168)
@@ -418,12 +433,21 @@ void coarse_read_stamps(unsigned long long *out) {
 }
 
 void launch_coarse(hipStream_t st, int mode, const DevState &S, const DevTables &T, int nch) {
-  if (mode == MODE_OQPSK)
-    hipLaunchKernelGGL(coarse_kernel<MODE_OQPSK>, dim3(nch), dim3(1024), 0, st, S, T, nch);
-  else if (mode == MODE_MSK600)
-    hipLaunchKernelGGL(coarse_kernel<MODE_MSK600>, dim3(nch), dim3(512), 0, st, S, T, nch);
-  else
-    hipLaunchKernelGGL(coarse_kernel<MODE_MSK1200>, dim3(nch), dim3(512), 0, st, S, T, nch);
+  switch (mode) {
+    case MODE_OQPSK: hipLaunchKernelGGL(coarse_kernel<MODE_OQPSK>, dim3(nch), dim3(1024), 0, st, S, T, nch); break;
+    case MODE_MSK600: hipLaunchKernelGGL(coarse_kernel<MODE_MSK600>, dim3(nch), dim3(512), 0, st, S, T, nch); break;
+    case MODE_MSK1200: hipLaunchKernelGGL(coarse_kernel<MODE_MSK1200>, dim3(nch), dim3(512), 0, st, S, T, nch); break;
+    case MODE_MSK600_24K:
+      hipLaunchKernelGGL(coarse_kernel<MODE_MSK600_24K>, dim3(nch), dim3(512), 0, st, S, T, nch);
+      break;
+    case MODE_MSK600_48K:
+      hipLaunchKernelGGL(coarse_kernel<MODE_MSK600_48K>, dim3(nch), dim3(512), 0, st, S, T, nch);
+      break;
+    case MODE_MSK1200_12K:
+      hipLaunchKernelGGL(coarse_kernel<MODE_MSK1200_12K>, dim3(nch), dim3(512), 0, st, S, T, nch);
+      break;
+    default: hipLaunchKernelGGL(coarse_kernel<MODE_MSK1200_48K>, dim3(nch), dim3(512), 0, st, S, T, nch); break;
+  }
 }
 
 }  // namespace aero

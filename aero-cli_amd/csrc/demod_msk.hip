@@ -2,7 +2,8 @@
  * demod_msk.hip — batched continuous MSK demodulator (600 / 1200 bps) for
  * gfx950: MskDemodulator::writeData (decode/mskdemodulator.cpp:252-428) as
  * aero-decode configures it (decode/decode.cpp:142-150: Fs 12000 / 24000,
- * fb stays 600, freq_center 0, AFC on, dcd never set).
+ * fb stays 600, freq_center 0, AFC on, dcd never set), and at 48 kHz after a
+ * rate change (mskdemodulator.cpp:473-481; one kernel per Fs, MskK).
  *
  * One VFO channel per lane, thousands side by side, the same structure as
  * demod_oqpsk.hip:
@@ -28,8 +29,6 @@
 
 namespace aero {
 
-__constant__ double c_msk_sr_b[3];  // st resonator, 12 kHz design (mskdemodulator.cpp:191-203)
-__constant__ double c_msk_sr_a[3];
 __constant__ double c_msk_d8w[2];   // delayt8 weights {weighting, 1 - weighting} (pointer-independent, host-checked)
 
 namespace {
@@ -78,11 +77,13 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   constexpr int DTL = SPS / 2 + 1;       // dt.setLength(SPS / 2)
   constexpr int MARG = SPS;              // marg = MovingAverage(SPS)
   constexpr double FS = (double)K::FS;
-  // imaginary matched-filter partial sums: registers for 600 bps (40 taps,
-  // ~400 of the 512 registers with the real ones), LDS for 1200 bps (80 taps
-  // would not fit)
+  // imaginary matched-filter partial sums: registers at 12 kHz (40 taps,
+  // ~400 of the 512 registers with the real ones), LDS at 24 / 48 kHz (80 /
+  // 160 taps would not fit); at 48 kHz the oldest 100 real ones are LDS too
   constexpr bool QREG = NT <= 40;
+  constexpr int NRL = NT > 80 ? NT - 60 : 0;  // real partial sums 0..NRL-1 in LDS
   __shared__ double s_qim[QREG ? 1 : NT][WG];
+  __shared__ double s_qre[NRL > 0 ? NRL : 1][WG];
   __shared__ double s_taps[NT];
   {
     const int l = threadIdx.x;
@@ -128,10 +129,11 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   double marg_sum = S.ds[DS_MARG_SUM * C + c], ms_sum = S.ds[DS_MS_SUM * C + c];
   double mse = S.ds[DS_MSE * C + c], diff_last = S.ds[DS_DIFF_LAST * C + c];
   long long ev = S.ls[LS_EVENTS * C + c];
+  const int ms_off = S.is[IS_MS_OFF * C + c];  // msema's slot offset (see IS_MS_OFF)
   long long softp = S.ls[LS_SOFT_P * C + c];
   long long ptn = S.ls[LS_PT_N * C + c];
 
-  double q[NT];
+  double qr[NT - NRL];
   double qi[QREG ? NT : 1];
   auto QI = [&](int j) -> double & {
     if constexpr (QREG)
@@ -139,12 +141,18 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
     else
       return s_qim[j][lane];
   };
+  auto Q = [&](int j) -> double & {
+    if (j < NRL)
+      return s_qre[j < NRL ? j : 0][lane];
+    else
+      return qr[j - NRL];
+  };
 #pragma unroll
-  for (int j = 0; j < NT; ++j) q[j] = S.fir[(size_t)j * C + c];
+  for (int j = 0; j < NT; ++j) Q(j) = S.fir[(size_t)j * C + c];
 #pragma unroll
   for (int j = 0; j < NT; ++j) QI(j) = S.fir[(size_t)(NT + j) * C + c];
 
-  const double PT = 0.0125 * WTSIZE;  // IfHavePassedPoint(ee), ee = 0.0125 (mskdemodulator.cpp:203)
+  const double PT = K::EE * WTSIZE;  // IfHavePassedPoint(ee) (mskdemodulator.cpp:177-203)
   const double d8w = c_msk_d8w[0], d8omw = c_msk_d8w[1];
 
   int i = 0;
@@ -173,10 +181,13 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       const double2 cm = T.cis[cis_index(m2_ptr)];
       const double cv = cm.x * dval, cvi = cm.y * dval;  // mixer2.WTCISValue() * dval
       // matched filter: FIRUpdateAndProcess reads the 2*SPS samples before the newest
-      double s2r = q[NT - 1], s2i = QI(NT - 1);
+      double s2r = Q(NT - 1), s2i = QI(NT - 1);
 #pragma unroll
-      for (int j = NT - 1; j >= 1; --j) q[j] = q[j - 1] + s_taps[j] * cv;
-      q[0] = 0.0 + s_taps[0] * cv;
+      for (int j = NT - 1; j >= 1; --j) {
+        Q(j) = Q(j - 1) + s_taps[j] * cv;
+        if (NRL > 0 && j < NRL && (j & 7) == 0) asm volatile("" : : : "memory");
+      }
+      Q(0) = 0.0 + s_taps[0] * cv;
 #pragma unroll
       for (int j = NT - 1; j >= 1; --j) {
         QI(j) = QI(j - 1) + s_taps[j] * cvi;
@@ -211,11 +222,11 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       {
         const double sig = aero_hypot(s2r, pdi);
         double y = 0;
-        y += srx2 * c_msk_sr_b[2];
-        y += srx1 * c_msk_sr_b[1];
-        y += sig * c_msk_sr_b[0];
-        y -= sry2 * c_msk_sr_a[2];
-        y -= sry1 * c_msk_sr_a[1];
+        y += srx2 * K::SR_B2;
+        y += srx1 * 0.0;
+        y += sig * K::SR_B0;
+        y -= sry2 * K::SR_A2;
+        y -= sry1 * K::SR_A1;
         srx2 = srx1;
         srx1 = sig;
         sry2 = sry1;
@@ -330,7 +341,7 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
         const double tdb = (fabs((pi) * 0.75) - 1.0);
         const double v = (tda * tda) + (tdb * tdb);
         double *mb = S.ms + (size_t)cl * MSK_MSEMA;
-        const int p = (int)(ev % MSK_MSEMA);
+        const int p = (int)((ev + ms_off) % MSK_MSEMA);
         ms_sum = ms_sum - mb[p];
         ms_sum = ms_sum + fabs(v);
         mb[p] = fabs(v);
@@ -362,7 +373,7 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   {
     double *fir = S.fir + cl;
 #pragma unroll
-    for (int j = 0; j < NT; ++j) fir[(size_t)j * C] = q[j];
+    for (int j = 0; j < NT; ++j) fir[(size_t)j * C] = Q(j);
 #pragma unroll
     for (int j = 0; j < NT; ++j) fir[(size_t)(NT + j) * C] = QI(j);
   }
@@ -391,19 +402,24 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   ds[DS_DIFF_LAST * C] = diff_last;
 }
 
+template <int M>
+static void launch_msk_mode(hipStream_t st, const DevState &S, const DevTables &T, int nch, int flush) {
+  constexpr int WG = MskK<M>::WG;
+  hipLaunchKernelGGL(demod_msk_kernel<M>, dim3((nch + WG - 1) / WG), dim3(WG), 0, st, S, T, nch, flush);
+}
+
 void launch_demod_msk(hipStream_t st, int mode, const DevState &S, const DevTables &T, int nch, int flush) {
-  if (mode == MODE_MSK600) {
-    constexpr int WG = MskK<MODE_MSK600>::WG;
-    hipLaunchKernelGGL(demod_msk_kernel<MODE_MSK600>, dim3((nch + WG - 1) / WG), dim3(WG), 0, st, S, T, nch, flush);
-  } else {
-    constexpr int WG = MskK<MODE_MSK1200>::WG;
-    hipLaunchKernelGGL(demod_msk_kernel<MODE_MSK1200>, dim3((nch + WG - 1) / WG), dim3(WG), 0, st, S, T, nch, flush);
+  switch (mode) {
+    case MODE_MSK600: return launch_msk_mode<MODE_MSK600>(st, S, T, nch, flush);
+    case MODE_MSK1200: return launch_msk_mode<MODE_MSK1200>(st, S, T, nch, flush);
+    case MODE_MSK600_24K: return launch_msk_mode<MODE_MSK600_24K>(st, S, T, nch, flush);
+    case MODE_MSK600_48K: return launch_msk_mode<MODE_MSK600_48K>(st, S, T, nch, flush);
+    case MODE_MSK1200_12K: return launch_msk_mode<MODE_MSK1200_12K>(st, S, T, nch, flush);
+    default: return launch_msk_mode<MODE_MSK1200_48K>(st, S, T, nch, flush);
   }
 }
 
-void upload_msk_constants(const double *sr_b, const double *sr_a, const double *d8w) {
-  hipMemcpyToSymbol(HIP_SYMBOL(c_msk_sr_b), sr_b, sizeof(double) * 3);
-  hipMemcpyToSymbol(HIP_SYMBOL(c_msk_sr_a), sr_a, sizeof(double) * 3);
+void upload_msk_constants(const double *d8w) {
   hipMemcpyToSymbol(HIP_SYMBOL(c_msk_d8w), d8w, sizeof(double) * 2);
 }
 

@@ -45,7 +45,7 @@ void launch_demod(hipStream_t, const DevState &, const DevTables &, int, int, bo
 void upload_demod_constants(const double *, const DelayDesc *, const double *, const double *, const double *,
                             const double *);
 void launch_demod_msk(hipStream_t, int, const DevState &, const DevTables &, int, int);
-void upload_msk_constants(const double *, const double *, const double *);
+void upload_msk_constants(const double *);
 void demod_read_stamps(unsigned long long *);
 void coarse_read_stamps(unsigned long long *);
 void viterbi_read_stamps(unsigned long long *);
@@ -152,7 +152,7 @@ struct Group {
   int mode = MODE_OQPSK;
   ModeGeom g{};
   int device = 0, flags = 0, C = 0, nch = 0;
-  const char *tag = "";  // timing-name prefix ("" for OQPSK, "msk600_", "msk1200_")
+  const char *tag = "";  // timing-name prefix ("" for OQPSK, "msk600_", "msk1200_", "msk600_48k_", ...)
   hipStream_t st = nullptr;
   DevState S{};
   DevTables T{};
@@ -169,6 +169,9 @@ struct Group {
   std::vector<std::vector<double>> hop_hold, pt_hold;
   std::vector<std::vector<uint8_t>> blk_hold, frame_hold;
   std::vector<long long> soft_seen;
+  // samples the channel demodulated before it moved into this group (an MSK
+  // rate change): hop records count from the channel's first sample
+  std::vector<long long> hop_base;
   // aero_trace_select: host-side trace collection for these local channels
   // only (empty: every channel)
   bool trace_some = false;
@@ -538,7 +541,11 @@ int collect_traces(Group *e) {
       if (n <= 0) continue;
       const double *src = h.data() + (rows ? 0 : (size_t)c * rec);
       if (rows) HIPCHK(hipMemcpy(h.data(), e->S.hops + (size_t)c * rec, (size_t)n * 6 * 8, hipMemcpyDeviceToHost));
-      e->hop_hold[c].insert(e->hop_hold[c].end(), src, src + (size_t)n * 6);
+      auto &hh = e->hop_hold[c];
+      const size_t at = hh.size();
+      hh.insert(hh.end(), src, src + (size_t)n * 6);
+      if (e->hop_base[c])
+        for (size_t r = at; r < hh.size(); r += 6) hh[r] += (double)e->hop_base[c];
     }
     HIPCHK(hipMemset(e->S.hop_n, 0, sizeof(int) * nch));
   }
@@ -792,7 +799,9 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
   e->device = E->device;
   e->flags = E->flags;
   e->hpool = E->hpool.get();
-  e->tag = mode == MODE_OQPSK ? "" : (mode == MODE_MSK600 ? "msk600_" : "msk1200_");
+  static const char *const tags[MODE_COUNT] = {"", "msk600_", "msk1200_", "msk600_24k_", "msk600_48k_",
+                                                "msk1200_12k_", "msk1200_48k_"};
+  e->tag = tags[mode];
   e->C = (E->max_channels + 63) & ~63;
   DevState S{};
   DevTables T{};
@@ -875,9 +884,7 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
     if (!host_delay_uniform(sps / 2.0, size, age_old, age_new, w, omw)) return AERO_E_INVALID;
     if (size != e->g.d8_len || age_old != sps / 2 || age_new != sps / 2 - 1) return AERO_E_INVALID;
     const double d8w[2] = {w, omw};
-    const double sr_b[3] = {5.233248111921052e-04, 0, -5.233248111921052e-04};
-    const double sr_a[3] = {1, -1.974342917561558, 0.998953350377616};
-    upload_msk_constants(sr_b, sr_a, d8w);
+    upload_msk_constants(d8w);  // the st resonator design is per Fs (MskK)
   }
   HIPCHK(hipMemcpy((void *)e->T.taps, taps.data(), sizeof(double) * 128, hipMemcpyHostToDevice));
   HIPCHK(hipGetLastError());
@@ -1134,6 +1141,157 @@ int feed_group(Group *e, const std::vector<std::pair<int, std::pair<const int16_
 
 }  // namespace
 
+namespace {
+
+// A new local channel of the group of `mode` (created on first use) for
+// engine channel gc; its device state is initialised by flush_pending_init
+int group_add_channel(aero_engine *e, int mode, const aero_channel_cfg &cfg, int gc, int *local) {
+  if (!e->groups[mode])
+    if (int rc = group_create(e, mode, e->groups[mode])) return rc;
+  Group *g = e->groups[mode].get();
+  if (g->nch >= g->C) return AERO_E_FULL;
+  const int c = g->nch;
+  g->nch++;
+  g->cfg.push_back(cfg);
+  g->gch.push_back(gc);
+  g->avail.push_back(0);
+  g->nsamp.push_back(0);
+  g->hops.push_back(0);
+  g->host.emplace_back(new PChannelHost(cfg.disable_reassembly != 0));
+  g->infofield.emplace_back();
+  g->soft_hold.emplace_back();
+  g->hop_hold.emplace_back();
+  g->pt_hold.emplace_back();
+  g->blk_hold.emplace_back();
+  g->frame_hold.emplace_back();
+  g->soft_seen.push_back(0);
+  g->hop_base.push_back(0);
+  if (g->trace_some) g->trace_mask.resize(g->C, 0);
+  *local = c;
+  return AERO_OK;
+}
+
+// MskDemodulator::dataReceived at another sample rate (decode/mskdemodulator.cpp
+// :473-481): setSettings(last_applied_settings with the new Fs) (:94-218) is
+// applied to the channel's state, and the channel moves to the group of the
+// new rate.  All of its samples so far are demodulated and decoded first (a
+// flush of the old group: continuous channels are chunk-invariant, so the
+// other channels' outputs do not change).  What setSettings keeps and what
+// it resets:
+//   kept: mixer_center / mixer2 / st_osc phase pointers, the coarse ring's
+//     contents (its pointer restarts), the coarse y history and emptying
+//     countdown, msema (created by the ctor only), DiffDecode, the soft bits
+//     not yet framed, AeroL, SignalHunter;
+//   resized, contents kept: dt (SPS/2 + 1) and delayedsmpl (SPS + 1)
+//     (DelayThing::setLength, QVector::resize), pointers restart;
+//   reset: frequencies (mixer_center and mixer2 to freq_center 0, st_osc to
+//     fb/2 at the new Fs), matched filters, AGC, marg, delayt8, the st
+//     resonator (its design follows Fs), mse = 10.
+int msk_migrate(aero_engine *e, int ch, uint32_t fs) {
+  const int from = e->chmap[ch].first, c = e->chmap[ch].second;
+  Group *g = e->groups[from].get();
+  const int to = msk_mode(msk_bitrate(from), (int)fs);
+  if (to < 0) return AERO_E_RATE;
+  HIPCHK(hipSetDevice(e->device));
+  if (int rc = flush_pending_init(g)) return rc;
+  if (int rc = run_group(g, 1)) return rc;
+  if (int rc = drain_group(g)) return rc;
+  host_wait(e);
+  aero_channel_cfg cfg = g->cfg[c];
+  cfg.fs = fs;
+  int c2;
+  if (int rc = group_add_channel(e, to, cfg, ch, &c2)) return rc;
+  Group *h = e->groups[to].get();
+  if (int rc = flush_pending_init(h)) return rc;
+  const int C = g->C, C2 = h->C;
+  // scalar state: read the old channel's fields, apply setSettings, write
+  std::vector<double> ds(DS_COUNT);
+  std::vector<int> is(IS_COUNT);
+  std::vector<long long> ls(LS_COUNT);
+  HIPCHK(hipMemcpy2D(ds.data(), 8, g->S.ds + c, (size_t)8 * C, 8, DS_COUNT, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy2D(is.data(), 4, g->S.is + c, (size_t)4 * C, 4, IS_COUNT, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy2D(ls.data(), 8, g->S.ls + c, (size_t)8 * C, 8, LS_COUNT, hipMemcpyDeviceToHost));
+  const long long n_old = ls[LS_NSAMP], ev_old = ls[LS_EVENTS], zb = ls[LS_ZERO_BEFORE];
+  ds[DS_M2_FREQ] = 0;
+  ds[DS_M2_STEP] = 0;
+  ds[DS_MC_FREQ] = 0;
+  ds[DS_MC_STEP] = 0;
+  ds[DS_SO_FREQ] = 300;  // st_osc.SetFreq(fb / 2, Fs)
+  ds[DS_SO_STEP] = (300.0) * ((double)WTSIZE) / ((float)h->g.fs);
+  ds[DS_AGC_SUM] = 0;
+  ds[DS_SR_X1] = ds[DS_SR_X2] = ds[DS_SR_Y1] = ds[DS_SR_Y2] = 0;
+  ds[DS_MARG_SUM] = 0;
+  ds[DS_MSE] = 10.0;
+  is[IS_HOPS_DONE] = 0;
+  is[IS_MS_OFF] = (int)((is[IS_MS_OFF] + ev_old) % MSK_MSEMA);
+  ls[LS_NSAMP] = ls[LS_AVAIL] = ls[LS_FILLED] = ls[LS_ZERO_BEFORE] = 0;
+  ls[LS_PT_N] = 0;
+  ls[LS_EVENTS] = 0;
+  HIPCHK(hipMemcpy2D(h->S.ds + c2, (size_t)8 * C2, ds.data(), 8, 8, DS_COUNT, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy2D(h->S.is + c2, (size_t)4 * C2, is.data(), 4, 4, IS_COUNT, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy2D(h->S.ls + c2, (size_t)8 * C2, ls.data(), 8, 8, LS_COUNT, hipMemcpyHostToDevice));
+  // rows that carry over (same sizes in both groups)
+  HIPCHK(hipMemcpy(h->S.soft + (size_t)c2 * SOFT_RING, g->S.soft + (size_t)c * SOFT_RING, SOFT_RING,
+                   hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(h->S.block + (size_t)c2 * 2 * h->g.block, g->S.block + (size_t)c * 2 * g->g.block,
+                   (size_t)2 * g->g.block, hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(h->S.overlap + (size_t)c2 * 64, g->S.overlap + (size_t)c * 64, 64, hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(h->S.dl2 + (size_t)c2 * h->g.dl2_len, g->S.dl2 + (size_t)c * g->g.dl2_len, g->g.dl2_len,
+                   hipMemcpyDeviceToDevice));
+  const size_t ylen = (size_t)(g->g.y_hi - g->g.y_lo + 1);
+  HIPCHK(hipMemcpy(h->S.y + c2 * ylen, g->S.y + c * ylen, ylen * 8, hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(h->S.ms + (size_t)c2 * MSK_MSEMA, g->S.ms + (size_t)c * MSK_MSEMA, (size_t)8 * MSK_MSEMA,
+                   hipMemcpyDeviceToDevice));
+  // dt and delayedsmpl resized with their contents (QVector index = ring slot)
+  const int dtn = std::min(g->g.dt_len, h->g.dt_len), dsn = std::min(g->g.dsm_len, h->g.dsm_len);
+  HIPCHK(hipMemcpy(h->S.dt + (size_t)c2 * h->g.dt_len, g->S.dt + (size_t)c * g->g.dt_len, (size_t)16 * dtn,
+                   hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy2D(h->S.dsm + c2, (size_t)16 * C2, g->S.dsm + c, (size_t)16 * C, 16, dsn, hipMemcpyDeviceToDevice));
+  // the coarse ring: slot = sample index mod nfft on both sides; entries of
+  // samples the AFC zeroed (below zero_before) are written as zeros
+  {
+    const int nf = g->g.nfft;
+    std::vector<uint32_t> ring(nf);
+    HIPCHK(hipMemcpy(ring.data(), g->S.cring + (size_t)c * nf, (size_t)4 * nf, hipMemcpyDeviceToHost));
+    for (int j = 0; j < nf; j++) {
+      const long long smp = (n_old - 1) - (((n_old - 1 - j) % nf + nf) % nf);  // last sample in slot j
+      if (smp < zb) ring[j] = 0;  // CIS[0] x 0: the zero a cleared bbcycbuff holds
+    }
+    HIPCHK(hipMemcpy(h->S.cring + (size_t)c2 * nf, ring.data(), (size_t)4 * nf, hipMemcpyHostToDevice));
+  }
+  // host state moves with the channel
+  h->host[c2] = std::move(g->host[c]);
+  g->host[c].reset(new PChannelHost(cfg.disable_reassembly != 0));
+  std::swap(h->infofield[c2], g->infofield[c]);
+  std::swap(h->soft_hold[c2], g->soft_hold[c]);
+  std::swap(h->hop_hold[c2], g->hop_hold[c]);
+  std::swap(h->pt_hold[c2], g->pt_hold[c]);
+  std::swap(h->blk_hold[c2], g->blk_hold[c]);
+  std::swap(h->frame_hold[c2], g->frame_hold[c]);
+  h->soft_seen[c2] = g->soft_seen[c];
+  h->hop_base[c2] = g->hop_base[c] + n_old;
+  if (g->trace_some && g->trace_mask[c]) {
+    h->trace_some = true;
+    h->trace_mask.resize(h->C, 0);
+    h->trace_mask[c2] = 1;
+    h->trace_list.push_back(c2);
+  }
+  e->chmap[ch] = {to, c2};
+  return AERO_OK;
+}
+
+// the group and local index of a continuous channel for a message at rate fs:
+// an MSK channel whose group runs at another rate moves first
+Group *route_rate(aero_engine *e, int ch, uint32_t fs, int &local, int &rc) {
+  rc = AERO_OK;
+  Group *g = route(e, ch, local);
+  if (!g || g->mode == MODE_OQPSK || fs == (uint32_t)g->g.fs) return g;  // OQPSK only logs it (:626-628)
+  if ((rc = msk_migrate(e, ch, fs))) return nullptr;
+  return route(e, ch, local);
+}
+
+}  // namespace
+
 extern "C" {
 
 const char *aero_strerror(int rc) {
@@ -1213,34 +1371,15 @@ int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) 
   int mode;
   if (cfg->bitrate == 10500 && cfg->fs == 48000)
     mode = MODE_OQPSK;
-  else if (cfg->bitrate == 600 && cfg->fs == 12000)  // decode/decode.cpp:145
-    mode = MODE_MSK600;
-  else if (cfg->bitrate == 1200 && cfg->fs == 24000)
-    mode = MODE_MSK1200;
+  else if (cfg->bitrate == 600 || cfg->bitrate == 1200)  // 12 / 24 kHz as decode/decode.cpp:145, or 48 kHz
+    mode = msk_mode(cfg->bitrate, (int)cfg->fs);
   else
-    return AERO_E_INVALID;  // decode/decode.h:42 validBitRates, with their rates
+    mode = -1;
+  if (mode < 0) return AERO_E_INVALID;  // decode/decode.h:42 validBitRates, with their rates
   HIPCHK(hipSetDevice(e->device));
-  if (!e->groups[mode]) {
-    if (int rc = group_create(e, mode, e->groups[mode])) return rc;
-  }
-  Group *g = e->groups[mode].get();
-  if (g->nch >= g->C) return AERO_E_FULL;
   host_wait(e);  // the host task indexes the per-channel tables
-  const int c = g->nch;
-  g->nch++;  // device state initialised by flush_pending_init before the next push/run
-  g->cfg.push_back(*cfg);
-  g->gch.push_back((int)e->chmap.size());
-  g->avail.push_back(0);
-  g->nsamp.push_back(0);
-  g->hops.push_back(0);
-  g->host.emplace_back(new PChannelHost(cfg->disable_reassembly != 0));
-  g->infofield.emplace_back();
-  g->soft_hold.emplace_back();
-  g->hop_hold.emplace_back();
-  g->pt_hold.emplace_back();
-  g->blk_hold.emplace_back();
-  g->frame_hold.emplace_back();
-  g->soft_seen.push_back(0);
+  int c;
+  if (int rc = group_add_channel(e, mode, *cfg, (int)e->chmap.size(), &c)) return rc;
   *ch_out = (int)e->chmap.size();
   e->chmap.push_back({mode, c});
   return AERO_OK;
@@ -1263,13 +1402,14 @@ int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t
   BurstGroup *bg;
   const int b = route_burst(e, ch, &bg);
   if (b >= 0) return (pcm || !n) ? push_burst(e, bg, b, pcm, n, false) : AERO_E_INVALID;  // rate only logged (:626-628)
-  int c;
-  Group *g = route(e, ch, c);
-  if (!g || (!pcm && n)) return AERO_E_INVALID;
+  if (!pcm && n) return AERO_E_INVALID;
   // OQPSK only logs a rate mismatch (oqpskdemodulator.cpp:626-628); the MSK
-  // demodulator would re-apply its settings at the new rate
-  // (mskdemodulator.cpp:472-480), which this engine does not support
-  if (g->mode != MODE_OQPSK && fs != (uint32_t)g->g.fs) return AERO_E_RATE;
+  // demodulator re-applies its settings at the new rate (mskdemodulator.cpp
+  // :473-481): the channel moves to that rate's group (msk_migrate)
+  int c, rc;
+  Group *g = route_rate(e, ch, fs, c, rc);
+  if (rc) return rc;
+  if (!g) return AERO_E_INVALID;
   if (!n) return AERO_OK;
   HIPCHK(hipSetDevice(e->device));
   // split so one piece never exceeds the ring
@@ -1287,10 +1427,11 @@ int aero_push_pcm_dev(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint
   BurstGroup *bg;
   const int b = route_burst(e, ch, &bg);
   if (b >= 0) return (pcm || !n) ? push_burst(e, bg, b, pcm, n, true) : AERO_E_INVALID;
-  int c;
-  Group *g = route(e, ch, c);
-  if (!g || (!pcm && n)) return AERO_E_INVALID;
-  if (g->mode != MODE_OQPSK && fs != (uint32_t)g->g.fs) return AERO_E_RATE;
+  if (!pcm && n) return AERO_E_INVALID;
+  int c, rc;
+  Group *g = route_rate(e, ch, fs, c, rc);
+  if (rc) return rc;
+  if (!g) return AERO_E_INVALID;
   if (!n) return AERO_OK;
   HIPCHK(hipSetDevice(e->device));
   size_t off = 0;
@@ -1641,10 +1782,10 @@ int aero_engine_feed_dev(aero_engine *e, int nitems, const int *ch, const int16_
       if (int rc = push_burst(e, bg, b, src[i], n[i], true)) return rc;
       continue;
     }
-    int c;
-    Group *g = route(e, ch[i], c);
+    int c, rc;
+    Group *g = route_rate(e, ch[i], fs[i], c, rc);
+    if (rc) return rc;
     if (!g || !src[i]) return AERO_E_INVALID;
-    if (g->mode != MODE_OQPSK && fs[i] != (uint32_t)g->g.fs) return AERO_E_RATE;
     per[g->mode].push_back({c, {src[i], n[i]}});
   }
   for (int m = 0; m < MODE_COUNT; m++)

@@ -33,26 +33,65 @@ constexpr int DL2_LEN = 4987;         // DelayLine setLength(4992-6) (aerol.cpp:
 constexpr int VIT_MAX = 5078;         // 62 overlap + 4992 + 24 pad
 constexpr int JOB_OUT = 328;          // 312 infofield + len + mask + formatid + channel
 
-// channel kinds (one engine group per kind; aero_channel_cfg.bitrate)
-enum Mode : int { MODE_OQPSK = 0, MODE_MSK600 = 1, MODE_MSK1200 = 2, MODE_COUNT = 3 };
+// channel kinds, one engine group per kind: 10500-bps OQPSK, and continuous
+// MSK per (demodulator sample rate, AeroL bit rate).  aero-decode configures
+// 600 bps at 12 kHz and 1200 bps at 24 kHz (decode/decode.cpp:142-150); a
+// message at another rate re-applies the MSK settings at that rate
+// (MskDemodulator::dataReceived, decode/mskdemodulator.cpp:473-481, settings
+// :94-218) and the channel moves to the group of that rate (engine.hip
+// msk_migrate).  Supported MSK rates: 12000, 24000, 48000 (the VFO rates
+// aero-publish produces by default, publish/publisher.cpp:164-176).
+enum Mode : int {
+  MODE_OQPSK = 0,
+  MODE_MSK600 = 1,       // 600 bps, 12 kHz
+  MODE_MSK1200 = 2,      // 1200 bps, 24 kHz
+  MODE_MSK600_24K = 3,
+  MODE_MSK600_48K = 4,
+  MODE_MSK1200_12K = 5,
+  MODE_MSK1200_48K = 6,
+  MODE_COUNT = 7
+};
+constexpr int msk_fs(int m) {
+  return (m == MODE_MSK600 || m == MODE_MSK1200_12K) ? 12000
+                                                      : ((m == MODE_MSK1200 || m == MODE_MSK600_24K) ? 24000 : 48000);
+}
+constexpr int msk_bitrate(int m) {
+  return (m == MODE_MSK600 || m == MODE_MSK600_24K || m == MODE_MSK600_48K) ? 600 : 1200;
+}
+// the MSK group of (AeroL bit rate, sample rate), or -1 for an unsupported rate
+inline int msk_mode(int bitrate, int fs) {
+  for (int m = MODE_MSK600; m < MODE_COUNT; ++m)
+    if (msk_bitrate(m) == bitrate && msk_fs(m) == fs) return m;
+  return -1;
+}
 
 // continuous MSK (MskDemodulator as Decoder configures it, decode/decode.cpp:142-150,
-// decode/mskdemodulator.cpp:94-218): fb stays 600, Fs 12000 / 24000
+// decode/mskdemodulator.cpp:94-218): fb stays 600 whatever the bit rate, so the
+// demodulator depends on Fs only (SPS = Fs / 600, matched filter 2 SPS taps,
+// AGC(1, Fs), the st resonator design and IfHavePassedPoint point chosen by
+// Fs, :177-203); the AeroL framing on the bit rate
 template <int M>
-struct MskK;
-template <>
-struct MskK<MODE_MSK600> {
-  static constexpr int FS = 12000, SPS = 20, BITRATE = 600, LEAVER = 6, WG = 256;
-};
-template <>
-struct MskK<MODE_MSK1200> {
-  static constexpr int FS = 24000, SPS = 40, BITRATE = 1200, LEAVER = 9, WG = 128;
+struct MskK {
+  static constexpr int FS = msk_fs(M), SPS = FS / 600, BITRATE = msk_bitrate(M), LEAVER = BITRATE == 600 ? 6 : 9,
+                       WG = SPS == 20 ? 256 : (SPS == 40 ? 128 : 64);
+  static constexpr bool F48 = FS == 48000;  // "300hz / 4hz / 48000" design, else "300hz / 4hz / 12000"
+  static constexpr double SR_B0 = F48 ? 1.308825621597620e-04 : 5.233248111921052e-04;
+  static constexpr double SR_B2 = -SR_B0;
+  static constexpr double SR_A1 = F48 ? -1.998196509168551 : -1.974342917561558;
+  static constexpr double SR_A2 = F48 ? 0.999738234875681 : 0.998953350377616;
+  static constexpr double EE = F48 ? 0.025 : 0.0125;
 };
 constexpr int MSK_NFFT = 8192;          // coarsefreqest_fft_power 13 (mskdemodulator.h:26)
 constexpr int MSK_HOP = 2048;           // 75 % overlap (mskdemodulator.cpp:289-291)
 constexpr int MSK_MSEMA = 600;          // msema = MovingAverage(600) (mskdemodulator.cpp:57)
 constexpr int MSK_BLOCK_MAX = 9 * 64;   // 576
 constexpr int MSK_DL2_LEN = 571;        // dl2.setLength(576 - 6) (aerol.cpp:979,988)
+// y[] bins every MSK group keeps: the fold search at 12 kHz reads
+// round(+-lockingbw/hzperbin + nfft/2) +- (expectedpeakbin + 1), and the
+// ranges at 24 and 48 kHz lie inside it, so a channel that changes rate finds
+// the history it needs (the reference keeps y over a rate change,
+// coarsefreqestimate.cpp:39-76 only resizes it)
+constexpr int MSK_YLO = 3276, MSK_YHI = 4915;
 
 // per-mode geometry shared by the host layout and the kernels
 struct ModeGeom {
@@ -61,9 +100,9 @@ struct ModeGeom {
 };
 inline ModeGeom mode_geom(int m) {
   if (m == MODE_OQPSK) return {48000, 16384, 4096, 192000, 55, 800, 401, 400, 0, 0, 4992, 78, 4987, 2815, 13568, 32};
-  // MSK: y[] bins the fold search reads: round(+-lockingbw/hzperbin + nfft/2) +- (expectedpeakbin + 1)
-  if (m == MODE_MSK600) return {12000, 8192, 2048, 12000, 40, 20, 11, 600, 21, 11, 384, 6, 571, 3276, 4915, 12};
-  return {24000, 8192, 2048, 24000, 80, 40, 21, 600, 41, 21, 576, 9, 571, 3686, 4505, 12};
+  const int fs = msk_fs(m), sps = fs / 600, leaver = msk_bitrate(m) == 600 ? 6 : 9;
+  return {fs,      MSK_NFFT,   MSK_HOP,     fs,          2 * sps, sps,     sps / 2 + 1, MSK_MSEMA,
+          sps + 1, sps / 2 + 1, leaver * 64, leaver, MSK_DL2_LEN, MSK_YLO, MSK_YHI, 12};
 }
 
 // double state fields
@@ -105,6 +144,9 @@ enum IS : int {
   // decoder status events (decode/decode.cpp:429-439): DataCarrierDetect
   // changes as SignalHunter::handleDcd sees them, newFreqCenter emissions
   IS_DCD_EDGES, IS_HUNT_STEPS,
+  // MSK: msema's slot offset (its pointer keeps running over a rate change
+  // while marg and dt restart with the event counter)
+  IS_MS_OFF,
   IS_COUNT
 };
 

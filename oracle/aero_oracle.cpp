@@ -2011,13 +2011,21 @@ struct Msk {
     dt.setLength(40);
     coarse.setSettings(13, 500, 125, 8000);   // CoarseFreqEstimate ctor defaults
     coarse.setSettings(14, 900, 600, 48000);  // mskdemodulator.cpp:70
-    // setSettings (mskdemodulator.cpp:94-218)
-    Fs = bitrate == 600 ? 12000 : 24000;
+    setSettings(bitrate == 600 ? 12000 : 24000);  // decode/decode.cpp:145
+    hunter.setParams(0, 6000, 900);  // decode/decode.cpp:193
+  }
+
+  // setSettings (mskdemodulator.cpp:94-218) with the Decoder's settings
+  // (freq_center 0, lockingbw 900, fb 600, fft power 13) at sample rate _Fs:
+  // at construction, and again from dataReceived when a message arrives at
+  // another rate (:473-481)
+  void setSettings(double _Fs) {
+    Fs = _Fs;
     double freq_center = 0;
     if (freq_center > ((Fs / 2.0) - (lockingbw / 2.0))) freq_center = ((Fs / 2.0) - (lockingbw / 2.0));
     SamplesPerSymbol = int(Fs / fb);
     bbnfft = 8192;
-    bbcycbuff.assign(bbnfft, cpx(0, 0));
+    bbcycbuff.resize(bbnfft, cpx(0, 0));  // QVector::resize keeps the contents
     bbcycbuff_ptr = 0;
     coarse.setSettings(13, lockingbw, fb, Fs);
     mixer_center.SetFreq(freq_center, (int)Fs);
@@ -2030,21 +2038,31 @@ struct Msk {
     fir_im.init(mf);
     agc.init(1, Fs);
     mse = 10.0;
-    // fb < 1200 and Fs != 48000 for both bit rates: the 12 kHz design (:191-203)
-    st_iir_resonator.a[0] = 1;
-    st_iir_resonator.a[1] = -1.974342917561558;
-    st_iir_resonator.a[2] = 0.998953350377616;
-    st_iir_resonator.b[0] = 5.233248111921052e-04;
-    st_iir_resonator.b[1] = 0;
-    st_iir_resonator.b[2] = -5.233248111921052e-04;
-    ee = 0.0125;
+    // fb < 1200 (it stays 600): the 48 kHz design at Fs 48000, else the 12 kHz
+    // one (:177-203)
+    if (Fs == 48000) {
+      st_iir_resonator.a[0] = 1;
+      st_iir_resonator.a[1] = -1.998196509168551;
+      st_iir_resonator.a[2] = 0.999738234875681;
+      st_iir_resonator.b[0] = 1.308825621597620e-04;
+      st_iir_resonator.b[1] = 0;
+      st_iir_resonator.b[2] = -1.308825621597620e-04;
+      ee = 0.025;
+    } else {
+      st_iir_resonator.a[0] = 1;
+      st_iir_resonator.a[1] = -1.974342917561558;
+      st_iir_resonator.a[2] = 0.998953350377616;
+      st_iir_resonator.b[0] = 5.233248111921052e-04;
+      st_iir_resonator.b[1] = 0;
+      st_iir_resonator.b[2] = -5.233248111921052e-04;
+      ee = 0.0125;
+    }
     correctionfactor = 1.0;
     st_iir_resonator.init();
     marg = MovingAverage(SamplesPerSymbol);
     dt.setLength(SamplesPerSymbol / 2);
     delayedsmpl.setLength(SamplesPerSymbol);
     delayt8.setdelay((SamplesPerSymbol) / 2.0);
-    hunter.setParams(0, 6000, 900);  // decode/decode.cpp:193
   }
 
   void CenterFreqChangedSlot(double freq_center) {  // mskdemodulator.cpp:220-240
@@ -2989,6 +3007,13 @@ oracle_chan *oracle_create(int bitrate, int flags) {
   return c;
 }
 void oracle_destroy(oracle_chan *c) { delete c; }
+// Decoder::audioReceived -> dataReceived(audio, sampleRate): an MSK channel
+// re-applies its settings at a new rate (decode/mskdemodulator.cpp:473-481);
+// OQPSK and the burst demodulators only log a mismatch
+int oracle_push_rate(oracle_chan *c, const int16_t *pcm, size_t n, int fs) {
+  if (c->msk && fs > 0 && (double)fs != c->msk->Fs) c->msk->setSettings((double)fs);
+  return oracle_push(c, pcm, n);
+}
 int oracle_push(oracle_chan *c, const int16_t *pcm, size_t n) {
   if (!n) return 0;
   if (c->oq)

@@ -34,6 +34,9 @@ void oracle_destroy(oracle_chan *c);
 /* One call == one ZMQ message == OqpskDemodulator::dataReceived
  * (decode/oqpskdemodulator.cpp:624-630). */
 int oracle_push(oracle_chan *c, const int16_t *pcm, size_t n);
+/* the same with the message's sample rate (Decoder::audioReceived): an MSK
+ * channel re-applies its settings at a new rate (mskdemodulator.cpp:473-481) */
+int oracle_push_rate(oracle_chan *c, const int16_t *pcm, size_t n, int fs);
 
 /* Soft bits delivered to AeroL (groups of 32, decode/oqpskdemodulator.cpp:534-540). */
 size_t oracle_softbits(const oracle_chan *c, uint8_t *dst, size_t cap);

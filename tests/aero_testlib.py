@@ -58,16 +58,16 @@ def synth(seconds=10.0, seed=0xAE20, carrier=12037.5, ebn0=12.0, amplitude=0.25,
 
 
 def synth_msk(seconds=10.0, bitrate=600, seed=0xAE40, carrier=1800.0, ebn0=12.0, amplitude=0.25, phase0=0.3,
-              msg_rate=0.6, lead_in=500, baud=None, return_frames=False):
+              msg_rate=0.6, lead_in=500, baud=None, return_frames=False, fs=None):
     """int16 PCM of a 600/1200-bps MSK P-channel at 12/24 kHz (SURVEY.md §8(d)
-    C3 input) + the transmitted 72-byte information fields per frame.  `baud`
-    (default = bitrate) is the modulation rate; the frame layout follows
-    `bitrate`."""
+    C3 input; `fs` overrides the rate) + the transmitted 72-byte information
+    fields per frame.  `baud` (default = bitrate) is the modulation rate; the
+    frame layout follows `bitrate`."""
     global _synth
     if _synth is None:
         _synth = ctypes.CDLL(SYNTH_SO)
     _synth.aero_synth_msk.restype = ctypes.c_size_t
-    fs = 12000.0 if bitrate == 600 else 24000.0
+    fs = float(fs) if fs else (12000.0 if bitrate == 600 else 24000.0)
     n = int(fs * seconds)
     pcm = np.zeros(n, dtype=np.int16)
     maxf = int(seconds * (baud or bitrate) / 1200) + 8
@@ -148,6 +148,7 @@ class Oracle:
             L.oracle_create.argtypes = [ctypes.c_int, ctypes.c_int]
             L.oracle_destroy.argtypes = [ctypes.c_void_p]
             L.oracle_push.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+            L.oracle_push_rate.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
             for f in ('oracle_softbits', 'oracle_blocks', 'oracle_frames', 'oracle_items'):
                 getattr(L, f).restype = ctypes.c_size_t
                 getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
@@ -188,13 +189,18 @@ class Oracle:
             self.L.oracle_destroy(self.h)
             self.h = None
 
-    def push(self, pcm):
+    def push(self, pcm, fs=None):
+        """One message; with `fs` the message's sample rate (an MSK channel
+        re-applies its settings when it changes)."""
         pcm = np.ascontiguousarray(pcm, dtype=np.int16)
-        self.L.oracle_push(self.h, pcm.ctypes.data, pcm.size)
+        if fs is None:
+            self.L.oracle_push(self.h, pcm.ctypes.data, pcm.size)
+        else:
+            self.L.oracle_push_rate(self.h, pcm.ctypes.data, pcm.size, int(fs))
 
-    def push_chunked(self, pcm, chunk=12000):
+    def push_chunked(self, pcm, chunk=12000, fs=None):
         for i in range(0, len(pcm), chunk):
-            self.push(pcm[i:i + chunk])
+            self.push(pcm[i:i + chunk], fs)
 
     def _get(self, fn, dtype, rec=1):
         n = fn(self.h, None, 0)

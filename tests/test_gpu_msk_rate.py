@@ -1,0 +1,80 @@
+"""MSK rate change at the boundary: MskDemodulator::dataReceived re-applies
+setSettings at a message's sample rate when it differs from the current one
+(decode/mskdemodulator.cpp:473-481, settings :94-218), so a 600-bps VFO that
+aero-publish emits at an explicit INI out_rate (publish/publisher.cpp:160-176)
+still decodes.  The engine moves such a channel to the group of the new rate
+with the state setSettings keeps (engine.hip msk_migrate); the oracle
+re-applies setSettings (oracle_push_rate).  Soft bits, hop records (f64
+bitwise, sample index counted from the channel's first sample), frames and
+ACARS items must equal the oracle's, for rate sequences through 12, 24 and 48
+kHz and with channels that keep their rate beside them."""
+import numpy as np
+import pytest
+
+import aero_testlib as tl
+
+pytestmark = pytest.mark.gpu
+
+# (bitrate, [(fs, seconds, seed, carrier Hz, Eb/N0 dB)], message seconds)
+CHANNELS = [
+    (600, [(12000, 12.0, 0xE100, 1800.0, 14.0), (48000, 6.0, 0xE101, 1800.0, 14.0),
+           (24000, 30.0, 0xE102, 1800.0, 14.0)], 0.25),
+    (600, [(12000, 24.0, 0xE110, 1500.0, 12.0)], 0.25),                       # stays at 12 kHz
+    (1200, [(24000, 10.0, 0xE120, 1800.0, 14.0), (12000, 24.0, 0xE121, 1800.0, 14.0)], 0.5),
+    (1200, [(24000, 6.0, 0xE130, 2100.0, 14.0), (48000, 6.0, 0xE131, 2100.0, 14.0),
+            (24000, 12.0, 0xE132, 2100.0, 14.0)], 0.125),
+]
+
+
+def _messages(bitrate, segs, msg_s):
+    out = []
+    for fs, sec, seed, car, eb in segs:
+        x = tl.synth_msk(seconds=sec, bitrate=bitrate, baud=600, seed=seed, carrier=car, ebn0=eb, fs=fs)
+        step = int(fs * msg_s)
+        out += [(x[i:i + step], fs) for i in range(0, len(x), step)]
+    return out
+
+
+def test_msk_rate_change_matches_oracle(engine_lib):
+    import aero_engine as ae
+    msgs = [_messages(br, segs, m) for br, segs, m in CHANNELS]
+    eng = ae.Engine(max_channels=8, flags=ae.F_TRACE_SOFT | ae.F_TRACE_HOPS | ae.F_TRACE_FRAMES)
+    chans = [eng.open_channel(br) for br, _, _ in CHANNELS]
+    pos = [0] * len(msgs)
+    while any(p < len(m) for p, m in zip(pos, msgs)):
+        for k, ch in enumerate(chans):
+            if pos[k] < len(msgs[k]):
+                pcm, fs = msgs[k][pos[k]]
+                eng.push(ch, pcm, fs=fs)
+                pos[k] += 1
+        eng.run()
+    eng.flush()
+    items_total = 0
+    for k, ((br, segs, _), ch) in enumerate(zip(CHANNELS, chans)):
+        o = tl.Oracle(bitrate=br)
+        for pcm, fs in msgs[k]:
+            o.push(pcm, fs=fs)
+        sb, rsb = eng.softbits(ch), o.softbits()
+        assert len(rsb) > 1000
+        assert len(sb) == len(rsb) and np.array_equal(sb, rsb), 'channel %d soft bits differ (%d vs %d)' % (
+            k, len(sb), len(rsb))
+        h, rh = eng.hops(ch), o.hops()
+        assert h.shape == rh.shape and np.array_equal(h.view(np.int64), rh.view(np.int64)), \
+            'channel %d hop records differ' % k
+        assert np.array_equal(eng.frames(ch), o.frames()), 'channel %d frames differ' % k
+        items = eng.items(ch)
+        assert items == o.item_lines('A'), 'channel %d items differ' % k
+        items_total += len(items)
+    assert items_total > 0
+    eng.close()
+
+
+def test_msk_unsupported_rate_refused(engine_lib):
+    import aero_engine as ae
+    eng = ae.Engine(max_channels=2)
+    ch = eng.open_channel(600)
+    with pytest.raises(ae.AeroError) as ex:
+        eng.push(ch, np.zeros(1000, np.int16), fs=11025)
+    assert ex.value.rc == ae.AERO_E_RATE
+    eng.push(ch, np.zeros(1000, np.int16), fs=48000)  # a supported rate moves the channel
+    eng.close()
