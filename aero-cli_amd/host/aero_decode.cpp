@@ -14,10 +14,10 @@
  *    the engine and their items printed and forwarded before exit (the
  *    reference's synchronous chain has no tail to flush);
  *  - libacars enrichment (`parsed`) is absent (libacars is not in the image);
- *  - a continuous MSK channel runs at the rate aero-decode configures for its
- *    bit rate (12000 / 24000 Hz); a message at another rate is dropped with a
- *    CRIT line (MskDemodulator would re-apply its settings at that rate,
- *    decode/mskdemodulator.cpp:472-480);
+ *  - a continuous MSK channel re-applies its settings at a message's rate as
+ *    MskDemodulator::dataReceived does (decode/mskdemodulator.cpp:473-481)
+ *    for 12000, 24000 and 48000 Hz; a message at another rate is dropped
+ *    with a CRIT line;
  *  - the verbose DCD / frequency-centre lines (decode/decode.cpp:429-439)
  *    are printed after each engine run, not as the demodulator emits them;
  *  - extension: several -t options decode several topics in one process,
@@ -501,11 +501,11 @@ int main(int argc, char **argv) {
             // emit audioReceived -> dataReceived: len/2 int16 samples
             rc = aero_push_pcm(eng, t.ch, reinterpret_cast<const int16_t *>(samples.data()), bytes / 2, rate);
             if (rc == AERO_E_RATE) {
-              // MskDemodulator::dataReceived would re-apply its settings at
-              // this rate (mskdemodulator.cpp:472-480); this engine's MSK
-              // channels run at 12000 / 24000 Hz only, so the message is dropped
-              AH_CRIT("Sample rate %u differs from the %u Hz this bit rate's demodulator runs at; message "
-                      "dropped%s", rate, t.fs, tag(t).c_str());
+              // the engine re-applies an MSK channel's settings at 12000,
+              // 24000 or 48000 Hz (mskdemodulator.cpp:473-481); other rates
+              // are dropped
+              AH_CRIT("Sample rate %u is not one the MSK demodulator can be set to (12000, 24000, 48000); "
+                      "message dropped%s", rate, tag(t).c_str());
               rc = AERO_OK;
             }
             if (rc) break;

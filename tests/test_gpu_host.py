@@ -317,3 +317,39 @@ def test_multi_topic_decoder(engine_lib, cpu_libs, tmp_path):
     for v in range(nv):
         if wants[v]:
             assert sum(('Data carrier detected' in l and '[VFO%02d]' % (v + 1) in l) for l in lines) == 1
+
+
+def test_msk_vfo_at_explicit_out_rate(engine_lib, cpu_libs, tmp_path):
+    """aero-decode -b 600 subscribed to a VFO that aero-publish emits at an
+    explicit INI out_rate (publish/publisher.cpp:160-176), here 24000 Hz: the
+    MSK demodulator re-applies its settings at the message rate
+    (decode/mskdemodulator.cpp:473-481) and the topic decodes; the console
+    lines equal the oracle fed the same messages at that rate."""
+    import build
+    build.build_host()
+    pcm = tl.synth_msk(seconds=30.0, bitrate=600, baud=600, seed=0xE104, carrier=1800.0, ebn0=16.0, fs=24000)
+    ref = tl.Oracle(bitrate=600)
+    ref.push_chunked(pcm, 6000, fs=24000)
+    want = ref.item_lines('A')
+    assert len(want) >= 1
+    f = tmp_path / 'vfo.pcm'
+    pcm.astype('<i2').tofile(str(f))
+    port = free_port()
+    dec, lines, th = _start_decoder(['-p', 'tcp://127.0.0.1:%d' % port, '-t', 'VFO03', '-b', '600', '--format',
+                                     'jsondump', '-s', STATION], {})
+    try:
+        r = subprocess.run([PUB, '--bind', 'tcp://127.0.0.1:%d' % port, '--topic', 'VFO03', '--rate', '24000',
+                            '--chunk', '6000', '--wait-ms', '1500', str(f)], capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr
+        t0 = time.time()
+        while sum(l.startswith('{') for l in lines) < len(want) and time.time() - t0 < 90:
+            time.sleep(0.2)
+        time.sleep(1.0)
+    finally:
+        dec.send_signal(signal.SIGTERM)
+        rc = dec.wait(timeout=120)
+    th.join(timeout=10)
+    assert rc == 0, '\n'.join(lines[-20:])
+    assert not any('CRIT' in l for l in lines), '\n'.join(lines[-20:])
+    assert [l for l in lines if l.startswith('{')] == expected(want, 3)

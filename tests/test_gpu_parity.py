@@ -139,6 +139,6 @@ def test_documented_channel_config_per_bitrate(engine_lib):
         cfg = ae.ChannelCfg(bitrate, 0, fs, 0)
         ch = ctypes.c_int()
         assert lib.aero_channel_open(eng.h, ctypes.byref(cfg), ctypes.byref(ch)) == ae.AERO_OK, bitrate
-        bad = ae.ChannelCfg(bitrate, 0, 48000 if bitrate != 10500 else 12000, 0)
+        bad = ae.ChannelCfg(bitrate, 0, 11025, 0)
         assert lib.aero_channel_open(eng.h, ctypes.byref(bad), ctypes.byref(ch)) == ae.AERO_E_INVALID, bitrate
     eng.close()
