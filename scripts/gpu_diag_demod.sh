@@ -18,4 +18,4 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   find /tmp/pmc_${TAG}_$n -name '*counter_collection.csv' -exec cp {} $OUT/pmc_$n.csv \;
 done
 cd $R
-timeout -k 10 600 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_burst_scale.py > $OUT/pytest_burst_scale.log 2>&1
+
