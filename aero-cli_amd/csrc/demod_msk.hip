@@ -85,11 +85,8 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   __shared__ double s_qim[QREG ? 1 : NT][WG];
   __shared__ double s_qre[NRL > 0 ? NRL : 1][WG];
   __shared__ double s_taps[NT];
-  {
-    const int l = threadIdx.x;
-    if (l < NT) s_taps[l] = T.taps[l];
-    __syncthreads();
-  }
+  for (int l = threadIdx.x; l < NT; l += WG) s_taps[l] = T.taps[l];
+  __syncthreads();
   const int c = blockIdx.x * WG + threadIdx.x;
   const int lane = threadIdx.x;
   if (c >= nch) return;

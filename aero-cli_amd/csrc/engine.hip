@@ -305,7 +305,7 @@ size_t layout(DevState &S, DevTables &T, int mode, int C, int flags, char *base)
   T.tw = carve<double2>(p, g.nfft);
   T.twi = carve<double2>(p, g.nfft);
   T.scr = carve<uint8_t>(p, 5000);
-  T.taps = carve<double>(p, 128);
+  T.taps = carve<double>(p, MAX_TAPS);
   return (size_t)(p - base);
 }
 
@@ -839,7 +839,8 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
   }
   HIPCHK(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
   const int nfft = e->g.nfft;
-  std::vector<double> cis(2 * WTSIZE), tw(2 * nfft), twi(2 * nfft), taps(128, 0.0);
+  std::vector<double> cis(2 * WTSIZE), tw(2 * nfft), twi(2 * nfft), taps(MAX_TAPS, 0.0);
+  if (e->g.ntaps > MAX_TAPS) return AERO_E_INVALID;
   std::vector<uint8_t> scr(5000);
   host_cis(cis.data());
   host_twiddles(nfft, tw.data(), twi.data());
@@ -886,7 +887,7 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
     const double d8w[2] = {w, omw};
     upload_msk_constants(d8w);  // the st resonator design is per Fs (MskK)
   }
-  HIPCHK(hipMemcpy((void *)e->T.taps, taps.data(), sizeof(double) * 128, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy((void *)e->T.taps, taps.data(), sizeof(double) * MAX_TAPS, hipMemcpyHostToDevice));
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   out = std::move(e);

@@ -81,6 +81,7 @@ struct MskK {
   static constexpr double SR_A2 = F48 ? 0.999738234875681 : 0.998953350377616;
   static constexpr double EE = F48 ? 0.025 : 0.0125;
 };
+constexpr int MAX_TAPS = 192;           // matched filter / RRC taps a group table holds (MSK 48 kHz: 160)
 constexpr int MSK_NFFT = 8192;          // coarsefreqest_fft_power 13 (mskdemodulator.h:26)
 constexpr int MSK_HOP = 2048;           // 75 % overlap (mskdemodulator.cpp:289-291)
 constexpr int MSK_MSEMA = 600;          // msema = MovingAverage(600) (mskdemodulator.cpp:57)
