@@ -309,9 +309,10 @@ struct IIR {
 struct DelayThingC {
   std::vector<cpx> buffer;
   int buffer_ptr = 0, buffer_sz = 0;
-  void setLength(int length) {
+  DelayThingC() { setLength(12); }  // DSP.h:448
+  void setLength(int length) {  // DSP.h:449-455: QVector::resize keeps the contents
     length++;
-    buffer.assign(length, cpx(0, 0));
+    buffer.resize(length, cpx(0, 0));
     buffer_ptr = 0;
     buffer_sz = length;
   }

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-4 GPU check (c): MSK rate change (engine + host), the untraced burst
+# scale test, then the demod diagnosis.
+set -eo pipefail
+TAG=$1
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+cd $R
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_msk_rate.py tests/test_gpu_msk.py "tests/test_gpu_host.py::test_msk_vfo_at_explicit_out_rate" > $OUT/pytest_msk.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_burst_scale.py > $OUT/pytest_burst_scale.log 2>&1
+bash scripts/gpu_diag_demod.sh $TAG
