@@ -245,7 +245,11 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   for (int i = 0; i < 16; ++i) {
     const int j = bitrev<L>(epos<L, 0>(t, i));
     const long long s = s0 + j;
-    if (s < 0 || s < zero_before) {
+    // entries below zero_before were cleared (AFC, CenterFreqChangedSlot);
+    // entries of samples before the channel's first are the ring's own
+    // contents (zero for a new channel: CIS[0] x 0; a channel that changed
+    // rate keeps the ring it had, mskdemodulator.cpp:94-218)
+    if (s < zero_before) {
       x[i] = make_double2(0.0, 0.0);
     } else {
       const int q = (int)(s & (N - 1));

@@ -1225,7 +1225,8 @@ int msk_migrate(aero_engine *e, int ch, uint32_t fs) {
   ds[DS_MSE] = 10.0;
   is[IS_HOPS_DONE] = 0;
   is[IS_MS_OFF] = (int)((is[IS_MS_OFF] + ev_old) % MSK_MSEMA);
-  ls[LS_NSAMP] = ls[LS_AVAIL] = ls[LS_FILLED] = ls[LS_ZERO_BEFORE] = 0;
+  ls[LS_NSAMP] = ls[LS_AVAIL] = ls[LS_FILLED] = 0;
+  ls[LS_ZERO_BEFORE] = -(1LL << 62);  // the cleared entries are written as zeros below; the rest is read
   ls[LS_PT_N] = 0;
   ls[LS_EVENTS] = 0;
   HIPCHK(hipMemcpy2D(h->S.ds + c2, (size_t)8 * C2, ds.data(), 8, 8, DS_COUNT, hipMemcpyHostToDevice));
