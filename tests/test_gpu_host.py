@@ -336,7 +336,7 @@ def test_msk_vfo_at_explicit_out_rate(engine_lib, cpu_libs, tmp_path):
     pcm.astype('<i2').tofile(str(f))
     port = free_port()
     dec, lines, th = _start_decoder(['-p', 'tcp://127.0.0.1:%d' % port, '-t', 'VFO03', '-b', '600', '--format',
-                                     'jsondump', '-s', STATION], {})
+                                     'jsondump', '-s', STATION, '-v'], {})
     try:
         r = subprocess.run([PUB, '--bind', 'tcp://127.0.0.1:%d' % port, '--topic', 'VFO03', '--rate', '24000',
                             '--chunk', '6000', '--wait-ms', '1500', str(f)], capture_output=True, text=True,
