@@ -15,7 +15,7 @@ import aero_testlib as tl
 
 pytestmark = pytest.mark.gpu
 
-N, CHUNK, SECONDS = 192, 12000, 8.0
+N, CHUNK, SECONDS = 320, 12000, 8.0
 
 
 def _streams(kind):
