@@ -41,9 +41,13 @@ CXX_SRCS = ['tables_host.cpp', 'acars_host.cpp']
 # together (its loop's table gathers and ring loads issue back to back):
 # 14.9 -> 14.6 ms per hop (profiles/r04/ab/round3c/ab_sched_*.log; max-ilp
 # 14.8, and both strategies slow the coarse kernel, which keeps the default).
+# With the RRC partial sums on the helper wave, machine LICM's hoisted FP64
+# constants are what spills (211 SGPRs -> VGPR lanes; 15 without it):
+# 13.76 -> 12.83 ms (profiles/round4/ab_nolicm.txt).
 FILE_FLAGS = {'burst.hip': ['-mllvm', '-disable-machine-licm'],
               'burst_msk.hip': ['-mllvm', '-disable-machine-licm'],
-              'demod_oqpsk.hip': ['-mllvm', '--amdgpu-sched-strategy=max-memory-clause']}
+              'demod_oqpsk.hip': ['-mllvm', '--amdgpu-sched-strategy=max-memory-clause', '-mllvm',
+                                  '-disable-machine-licm']}
 
 
 def _run(cmd):

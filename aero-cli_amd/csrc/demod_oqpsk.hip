@@ -384,6 +384,17 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
     agc_next = S.agc[(size_t)agc_ptr * C + c];
   }
   const double PT = 0.4 * WTSIZE;  // IfHavePassedPoint(ee) with ee = 0.4 (oqpskdemodulator.cpp:225)
+  // the two CIS table entries a sample uses, gathered a sample ahead (an L2
+  // round trip the chain would otherwise wait for at the top of every
+  // sample): st_osc's once its pointer for the next sample is known (end of
+  // the sample), mixer2's speculatively at the top of the previous sample
+  // (its pointer then only advances by its step unless a carrier event
+  // moves it, and the event step gathers it again)
+  double2 cm_next = make_double2(0.0, 0.0), so_next = make_double2(0.0, 0.0);
+  if (work) {
+    cm_next = T.cis[cis_index(m2_ptr)];
+    so_next = T.cis[cis_index(so_ptr)];
+  }
 
   // Event-aligned iteration.  The carrier/MSE/soft-bit step runs at every
   // second sample instant (one channel in ~9 samples), but in lockstep
@@ -414,8 +425,13 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       pcm_next = pcm_next2;
       const double agc_old = agc_next;
       // table lookups of this sample first, then the prefetch for the next
-      const double2 cm = T.cis[cis_index(m2_ptr)];
-      const double2 so = T.cis[cis_index(so_ptr)];
+      const double2 cm = cm_next;
+      const double2 so = so_next;
+      {
+        double p = m2_ptr, st = m2_step;
+        nco_next(p, st);
+        cm_next = T.cis[cis_index(p)];
+      }
       {
         const int ap = agc_ptr + 1 == AGC_LEN ? 0 : agc_ptr + 1;
         pcm_next2 = S.pcm[(size_t)((pb + i + 2) & capm) * C + c];  // past the pushed samples: unused
@@ -542,6 +558,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       nco_next(mc_ptr, mc_step);
       so_last = so_ptr;
       nco_next(so_ptr, so_step);
+      so_next = T.cis[cis_index(so_ptr)];
       // coarse-ring fill of the next sample (:351-356), staged in LDS
       if (i + 1 < ia) {
         const int m = rb + i + 1;  // ring slot before masking
@@ -685,6 +702,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       sh.pi[PI_PM_P][pair] = pm_p;
       sh.pi[PI_MS_P][pair] = ms_p;
       nco_next(m2_ptr, m2_step);
+      cm_next = T.cis[cis_index(m2_ptr)];  // the event moved mixer2
       ++i;
     }
     XSTAMP(5);  // carrier event step
