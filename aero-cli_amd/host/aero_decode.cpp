@@ -48,6 +48,7 @@
 #include "forwarder.h"
 #include "log.h"
 #include "output.h"
+#include "section_timer.h"
 #include "zmq_dl.h"
 
 namespace aerohost {
@@ -473,12 +474,15 @@ int main(int argc, char **argv) {
   };
   if (g_running.load()) AH_DBG("Listening for samples...");
   char tbuf[256];
+  aerohost::SectionTimer tm;  // AERO_HOST_TIMING: loop-section totals at exit
+  tm.restart();
   while (g_running.load()) {
     int n;
     while ((n = z->recv(sub, tbuf, sizeof tbuf, ZMQ_DONTWAIT_)) < 0 && g_running.load()) {
       usleep(10000);
       check_scans();
     }
+    tm.mark("wait");
     if (!g_running.load()) break;
     // every message already queued goes in before one aero_run (the engine
     // re-blocks continuous channels into hop segments, burst channels keep
@@ -499,7 +503,10 @@ int main(int argc, char **argv) {
           for (auto &t : topics) {
             if (!t.live || (int)t.name.size() > tlen || memcmp(tbuf, t.name.data(), t.name.size())) continue;
             // emit audioReceived -> dataReceived: len/2 int16 samples
+            tm.mark("recv");
             rc = aero_push_pcm(eng, t.ch, reinterpret_cast<const int16_t *>(samples.data()), bytes / 2, rate);
+            tm.mark("push");
+            tm.count("messages");
             if (rc == AERO_E_RATE) {
               // the engine re-applies an MSK channel's settings at 12000,
               // 24000 or 48000 Hz (mskdemodulator.cpp:473-481); other rates
@@ -515,20 +522,27 @@ int main(int argc, char **argv) {
       if (rc || ++batch >= 256) break;
       n = z->recv(sub, tbuf, sizeof tbuf, ZMQ_DONTWAIT_);
     }
+    tm.mark("recv");
     if (!g_running.load()) break;
     if (rc || (rc = aero_run(eng))) {
       AH_CRIT("engine error: %s", aero_strerror(rc));
       rc_exit = 1;
       break;
     }
+    tm.mark("run");
     drain();
+    tm.mark("drain");
     check_scans();
+    tm.mark("events");
+    tm.count("batches");
   }
   // the tail of what was received
   if (aero_flush(eng) == AERO_OK) {
     drain();
     log_events();
   }
+  tm.mark("flush");
+  tm.print("aero-decode");
   for (auto &f : fwd) f->stop();
   aero_engine_destroy(eng);
   z->close(sub);

@@ -37,6 +37,7 @@
 #include "../../include/aero_chan.h"
 #include "ini.h"
 #include "log.h"
+#include "section_timer.h"
 #include "zmq_dl.h"
 
 namespace aerohost {
@@ -280,6 +281,8 @@ int main(int argc, char **argv) {
   const auto t0 = std::chrono::steady_clock::now();
   long long reads = 0;
   int rc_exit = 0;
+  aerohost::SectionTimer tm;  // AERO_HOST_TIMING: loop-section totals at exit
+  tm.restart();
   while (g_running.load()) {
     size_t got = fread(buf.data(), sizeof(float), buf.size(), src);
     if (got < buf.size()) {
@@ -292,10 +295,14 @@ int main(int argc, char **argv) {
       const auto due = t0 + std::chrono::microseconds((long long)(1e6 * (double)reads * B / Fs));
       std::this_thread::sleep_until(due);
     }
+    tm.mark("read");
     // Publisher::demodData -> vfo::process -> transmitData
     int rc = aero_chan_push(chan, buf.data(), 1, 0);
+    tm.mark("push");
     if (!rc) rc = aero_chan_run(chan);
+    tm.mark("run");
     if (!rc) rc = aero_chan_sync(chan);
+    tm.mark("sync");
     if (rc) {
       AH_CRIT("channeliser error: %s", aero_strerror(rc));
       rc_exit = 1;
@@ -308,7 +315,10 @@ int main(int argc, char **argv) {
           size_t n = 0;
           audio.resize(1 << 20);
           aero_chan_pop_audio(chan, (int)v, audio.data(), audio.size(), &n);
+          tm.mark("pop");
           bound.publish(audio.data(), n * sizeof(int16_t), topics[v], (uint32_t)rate[v]);
+          tm.mark("publish");
+          tm.count("messages");
         }
       } else if (mains[m].publish) {
         int info[3];
@@ -320,7 +330,10 @@ int main(int argc, char **argv) {
       }
     }
     reads++;
+    tm.count("reads");
+    tm.mark("publish");
   }
+  tm.print("aero-publish");
   AH_DBG("reader stopped after %lld reads", reads);
   fclose(src);
   int linger = 2000;

@@ -498,7 +498,12 @@ def run_c1(a):
     print(json.dumps(out), flush=True)
 
 
-C5BIN_SECONDS = 12.0  # wideband CF32 file the publisher reads without pacing
+C5BIN_SECONDS = 12.0
+
+
+def _is_item(line):
+    """a jsondump ACARS line of aero-decode (not its AERO_HOST_TIMING summary)"""
+    return line.startswith('{') and not line.startswith('{"aero_host_timing"')  # wideband CF32 file the publisher reads without pacing
 
 
 def run_c5bin(a):
@@ -549,7 +554,7 @@ def run_c5bin(a):
         args += ['-t', 'VFO%02d' % (v + 1), '-b', str(cfg['vfos'][v]['data_rate']), '-s', 'BENCH']
     # the publisher reads the file without pacing: unbounded ZeroMQ queues on
     # both ends (AERO_ZMQ_HWM=0) so nothing is dropped while the decoder catches up
-    env = dict(os.environ, AERO_ZMQ_HWM='0')
+    env = dict(os.environ, AERO_ZMQ_HWM='0', AERO_HOST_TIMING='1')
     dec = subprocess.Popen(args, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env)
     lines, stamps = [], []
 
@@ -579,23 +584,32 @@ def run_c5bin(a):
     # wait for the decoder to go quiet (every queued message decoded)
     n_last, t_last = -1, time.perf_counter()
     while time.perf_counter() - t_last < 3.0 and time.perf_counter() - t0 < 600:
-        n = sum(l.startswith('{') for l in lines)
+        n = sum(_is_item(l) for l in lines)
         if n != n_last:
             n_last, t_last = n, time.perf_counter()
         time.sleep(0.1)
-    got = [s for l, s in zip(lines, stamps) if l.startswith('{')]
+    got = [s for l, s in zip(lines, stamps) if _is_item(l)]
     t_end = got[-1] if got else time.perf_counter()
     n_run = len(got)
     dec.send_signal(signal.SIGTERM)
     dec.wait(timeout=120)
     th.join(timeout=10)
-    n_all = sum(l.startswith('{') for l in lines)  # with the flushed tail
+    n_all = sum(_is_item(l) for l in lines)  # with the flushed tail
     os.remove(wb)
     os.remove(ini)
     os.rmdir(tmp)
     if n_all != want:
         sys.exit('bench c5bin: %d ACARS items, the oracle chain gives %d' % (n_all, want))
     elapsed = t_end - t0
+    # where the binaries' wall time went (AERO_HOST_TIMING section totals)
+    split = {}
+    for l in plines + lines:
+        if l.startswith('{"aero_host_timing"'):
+            try:
+                d = json.loads(l)
+                split[d['aero_host_timing']] = dict(d['ms'], **{'n_' + k: v for k, v in d['counts'].items()})
+            except ValueError:
+                pass
     out = {'metric': 'Msamples/s end-to-end aero-publish -> ZeroMQ -> one 64-topic aero-decode -> ACARS JSON (C5)',
            'value': round(ch_samples / elapsed / 1e6, 4), 'unit': 'Msamples/s', 'n_gpus': 1, 'steps': 1,
            'warmup': 0, 'ms_per_step': round(elapsed * 1e3, 1), 'higher_is_better': True, 'scaling': 'none',
@@ -605,6 +619,7 @@ def run_c5bin(a):
                                   % C5BIN_SECONDS, 'vfos': nv, 'items': n_all, 'items_before_sigterm': n_run},
            'wideband_msps': round(nb * ref.block_len / elapsed / 1e6, 3),
            'realtime_factor': round(C5BIN_SECONDS / elapsed, 2),
+           'host_split_ms': split,
            'timing_note': "publisher's first read to the last ACARS JSON line before SIGTERM; audio after the "
                           'last frame counts as processed',
            'roofline': None,
