@@ -397,6 +397,10 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   double str_r = ds[BD_STR_RE * C], str_i = ds[BD_STR_IM * C];
   double ptd_r = ds[BD_PTD_RE * C], ptd_i = ds[BD_PTD_IM * C], s2l_r = ds[BD_S2L_RE * C], s2l_i = ds[BD_S2L_IM * C];
   double rotf = ds[BD_ROTF * C], mse = ds[BD_MSE * C], lastmse = ds[BD_LASTMSE * C];
+  // exp(i rotator_freq) changes only with rotator_freq (a symbol step or a
+  // trident decision), so it is kept rather than evaluated every sample
+  double rf_c, rf_s;
+  b_cexp_i(rotf, rf_c, rf_s);
   double msema_sum = ds[BD_MSEMA_SUM * C];
   int agc2_p = is[BI_AGC2_P * C];
   int dl_s = is[(BI_DL_P0 + BDL_S) * C], dl_41 = is[(BI_DL_P0 + BDL_41) * C], dl_42 = is[(BI_DL_P0 + BDL_42) * C];
@@ -490,6 +494,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         rot_i = 0;
         insertpre = 1;
         rotf = 0;
+        b_cexp_i(rotf, rf_c, rf_s);
         ave_r = 1;
         ave_i = 0;
         mse = 0;
@@ -635,7 +640,8 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     {  // sig2 *= symboltone_averotator; rotator *= exp(i rotator_freq); sig2 *= rotator
       const double ar = s2r * ave_r - s2i * ave_i, ai = s2r * ave_i + s2i * ave_r;
       double ec, es;
-      b_cexp_i(rotf, ec, es);
+      ec = rf_c;
+      es = rf_s;
       const double rr = rot_r * ec - rot_i * es, ri = rot_r * es + rot_i * ec;
       rot_r = rr;
       rot_i = ri;
@@ -729,6 +735,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
             rot_r = rr;
             rot_i = ri;
             rotf = rotf + ct_ec * 0.0001;
+            b_cexp_i(rotf, rf_c, rf_s);
           }
           if (cntr > ((128 + 10) * SPS)) {  // msema.Update (DSP.cpp:405-416)
             const double tda = (fabs(qr) - 1.0), tdb = (fabs(qi) - 1.0);

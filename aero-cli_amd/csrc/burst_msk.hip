@@ -263,6 +263,10 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
   double srx1 = ds[BM_SR_X1 * C], srx2 = ds[BM_SR_X2 * C], sry1 = ds[BM_SR_Y1 * C], sry2 = ds[BM_SR_Y2 * C];
   double ave_r = ds[BM_AVE_RE * C], ave_i = ds[BM_AVE_IM * C], rot_r = ds[BM_ROT_RE * C], rot_i = ds[BM_ROT_IM * C];
   double str_r = ds[BM_STR_RE * C], str_i = ds[BM_STR_IM * C], rotf = ds[BM_ROTF * C];
+  // exp(i rotator_freq) changes only with rotator_freq (a symbol step or a
+  // trident decision), so it is kept rather than evaluated every sample
+  double rf_c, rf_s;
+  b_cexp_i(rotf, rf_c, rf_s);
   double mse = ds[BM_MSE * C], msema_sum = ds[BM_MSEMA_SUM * C], diff_last = ds[BM_DIFF_LAST * C];
   int agc2_p = is[BMI_AGC2_P * C];
   int a1_p = is[BMI_A1_P * C], d8_p = is[BMI_D8_P * C], dsm_p = is[BMI_DSM_P * C];
@@ -344,6 +348,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         rot_r = 1;
         rot_i = 0;
         rotf = 0;
+        b_cexp_i(rotf, rf_c, rf_s);
         srx1 = srx2 = sry1 = sry2 = 0;
         b_set_phase_deg(so_ptr, 0);
         so_n = T.cis[b_cis_index(so_ptr)];
@@ -452,7 +457,8 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       {  // sig2 *= symboltone_averotator; rotator *= exp(i rotator_freq); sig2 *= rotator
         const double ar = s2r * ave_r - s2i * ave_i, ai = s2r * ave_i + s2i * ave_r;
         double ec, es;
-        b_cexp_i(rotf, ec, es);
+        ec = rf_c;
+        es = rf_s;
         const double rr = rot_r * ec - rot_i * es, ri = rot_r * es + rot_i * ec;
         rot_r = rr;
         rot_i = ri;
@@ -524,7 +530,10 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
             const double rr = rot_r * ec - rot_i * es, ri = rot_r * es + rot_i * ec;
             rot_r = rr;
             rot_i = ri;
-            if (cntr > M_ENDROT) rotf = rotf + ct_ec * 0.0001;
+            if (cntr > M_ENDROT) {
+              rotf = rotf + ct_ec * 0.0001;
+              b_cexp_i(rotf, rf_c, rf_s);
+            }
           }
           if (cntr > (M_START * MSPS)) {  // msema->Update (DSP.cpp:409-416)
             const double tda = (fabs(s2r * 0.75) - 1.0);
