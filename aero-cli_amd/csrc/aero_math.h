@@ -1,6 +1,6 @@
 /*
  * aero_math.h — the libm the demod kernels call, bit-compatible with the
- * host glibc 2.35 that the reference links (decode/*.cpp call std::abs on
+ * host glibc 2.35 that the reference links (the decode/ sources call std::abs on
  * complex (-> hypot), std::arg (-> atan2), tanh, sin, cos, log10).
  *
  * Compiles for host (g++/hipcc host pass) and device (gfx950).  Every file

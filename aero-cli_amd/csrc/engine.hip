@@ -286,7 +286,6 @@ size_t layout(DevState &S, DevTables &T, int mode, int C, int flags, char *base)
   S.pcm = carve<int16_t>(p, (size_t)PCM_CAP * C);
   S.pcm_cap = PCM_CAP;
   S.cring = carve<uint32_t>(p, (size_t)g.nfft * C);
-  S.bring = carve<double2>(p, msk ? 1 : (size_t)g.nfft * C);
   S.y = carve<double>(p, (size_t)(g.y_hi - g.y_lo + 1) * C);
   S.soft = carve<uint8_t>(p, (size_t)SOFT_RING * C);
   S.pt_cap = (flags & AERO_F_TRACE_PT) ? PT_CAP : 0;

@@ -190,7 +190,6 @@ struct DevState {
   int16_t *pcm;            // [PCM_CAP][C] input ring (time-major)
   long long pcm_cap;       // power of 2
   uint32_t *cring;         // [C][nfft] coarse ring: cis index | pcm << 16 (demod-written)
-  double2 *bring;          // OQPSK: [C][nfft] the same ring expanded to the mixed samples
                            // CIS * pcm / 32768 (coarse-written, one hop per run)
   double *y;               // [C][y_hi - y_lo + 1] coarse smoothing state
   uint8_t *soft;           // [C][SOFT_RING]

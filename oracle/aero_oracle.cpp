@@ -22,6 +22,14 @@
  * reference does (std::abs(complex) -> hypot, std::arg -> atan2, tanh, sin,
  * cos, log10, std::exp(complex) -> cexp).  Compile with -ffp-contract=off.
  *
+ * Built with -DORACLE_CR_LIBM (liboracle_cr.so) the per-sample atan2, sin,
+ * cos, log10 and cexp(i x) calls (the `olm` wrappers below) are correctly
+ * rounded instead (aero_math.h, the functions the kernels call; glibc's
+ * results differ from them by 1 ulp on ~0.1% of arguments,
+ * tests/test_math_host.py).  That build separates the algorithm's parity
+ * (bit for bit) from glibc's rounding at the scale where the latter shows
+ * (tests/test_gpu_fullscale.py).  Tables are glibc-computed in both builds.
+ *
  * PARITY STATUS.  The reference cannot be built in this container under the
  * round rules (it needs the QtCore library, moc-generated code and the
  * absent libcorrect), and it ships no tests, fixtures or recordings.  The
@@ -53,10 +61,32 @@
 #include <string>
 #include <vector>
 
+#ifdef ORACLE_CR_LIBM
+#include "aero_math.h"
+#endif
+
 namespace {
 
 typedef std::complex<double> cpx;
 const int WTSIZE = 19999;
+
+// the libm calls of the per-sample loops (header comment: ORACLE_CR_LIBM)
+namespace olm {
+#ifdef ORACLE_CR_LIBM
+double sin(double x) { return aero::aero_sin(x); }
+double cos(double x) { return aero::aero_cos(x); }
+double log10(double x) { return aero::aero_log10(x); }
+double arg(cpx z) { return aero::aero_atan2(z.imag(), z.real()); }
+// std::exp(i x) = cexp(+-0 + i x) = (cos x, sin x): glibc multiplies by exp(+-0) = 1
+cpx expi(cpx z) { return cpx(aero::aero_cos(z.imag()), aero::aero_sin(z.imag())); }
+#else
+double sin(double x) { return ::sin(x); }
+double cos(double x) { return ::cos(x); }
+double log10(double x) { return ::log10(x); }
+double arg(cpx z) { return std::arg(z); }
+cpx expi(cpx z) { return std::exp(z); }
+#endif
+}  // namespace olm
 
 /* ---------------------------------------------------------------- tables */
 // TrigLookUp::TrigLookUp (decode/DSP.cpp:10-33)
@@ -458,7 +488,7 @@ struct Coarse {
     jfft.fft(out.data(), false);
     for (int i = 0; i < N / 2; i++) std::swap(out[i + N / 2], out[i]);
     for (int i = 0; i < N; i++)
-      y[i] = y[i] * 0.9 + 0.1 * 10 * log10(fmax(std::abs(out[i]), 1));
+      y[i] = y[i] * 0.9 + 0.1 * 10 * olm::log10(fmax(std::abs(out[i]), 1));
     double zmax = 0;
     int zmaxloc = N / 2;
     for (int i = (int)round((-lockingbw / hzperbin) + ((double)(nfft / 2)));
@@ -1887,7 +1917,7 @@ struct Oqpsk {
       st_eta = st_iir_resonator.update(st_eta);
       cpx st_m1 = cpx(st_eta, -delayt8.update(st_eta));
       cpx st_out = st_osc.WTCISValue() * st_m1;
-      double st_angle_error = std::arg(st_out);
+      double st_angle_error = olm::arg(st_out);
       st_osc.IncreseFreqHz(-st_angle_error * 0.00000001);
       st_osc.AdvanceFractionOfWave(-st_angle_error * 0.01 / 360.0);
       if (st_osc.GetFreqHz() < (st_osc_ref.GetFreqHz() - 0.1))
@@ -1920,7 +1950,7 @@ struct Oqpsk {
           mixer2.IncreseFreqHz(0.01 * ct_ec);
           marg.UpdateSigned(ct_ec);
           dt.update(pt_qpsk);
-          pt_qpsk *= cpx(cos(marg.Val), sin(marg.Val));
+          pt_qpsk *= cpx(olm::cos(marg.Val), olm::sin(marg.Val));
           if (trace_pt) {
             pts.push_back(pt_qpsk.real());
             pts.push_back(pt_qpsk.imag());
@@ -2137,7 +2167,7 @@ struct Msk {
       double st_eta = st_iir_resonator.update(std::abs(pt_msk));
       cpx st_m1 = cpx(st_eta, -delayt8.update(st_eta));
       cpx st_out = st_osc.WTCISValue() * st_m1;
-      double st_angle_error = std::arg(st_out);
+      double st_angle_error = olm::arg(st_out);
       double weighting = fabs(tanh(st_angle_error));
       if (!dcd)
         st_osc.AdvanceFractionOfWave(-(1.0 - weighting) * st_angle_error * (0.05 / 360.0));
@@ -2157,7 +2187,7 @@ struct Msk {
         mixer2.IncreseFreqHz(carrier_aggression * 0.01 * ct_ec);
         marg.UpdateSigned(ct_ec / 2.0);
         dt.update(pt_msk);
-        pt_msk *= cpx(cos(marg.Val), sin(marg.Val));
+        pt_msk *= cpx(olm::cos(marg.Val), olm::sin(marg.Val));
         if (trace_pt) {
           pts.push_back(pt_msk.real());
           pts.push_back(pt_msk.imag());
@@ -2522,7 +2552,7 @@ struct BurstOqpsk {
     }
     const bool det = (maxval > 500.0) && (fabs((((double)(maxvalbin - minvalbin))) * hzperbin) < 20.0);
     if (det) {
-      double carrierphase = std::arg(out_base[(int)minvalbin]) - (M_PI / 4.0);
+      double carrierphase = olm::arg(out_base[(int)minvalbin]) - (M_PI / 4.0);
       mixer2.SetFreq(hzperbin * minvalbin);
       mixer2.SetPhaseDeg((180.0 / M_PI) * carrierphase);
       vol_gain = 1.4142 * 500.0 / minval;
@@ -2594,16 +2624,16 @@ struct BurstOqpsk {
                           (((256 - 10) * SamplesPerSymbol) - (SamplesPerSymbol * (128 + 10)));
         cpx symboltone_pt = sig2 * symboltone_rotator * imag;
         double er = std::tanh(symboltone_pt.imag()) * (symboltone_pt.real());
-        symboltone_rotator = symboltone_rotator * std::exp(imag * er * 0.01);
+        symboltone_rotator = symboltone_rotator * olm::expi(imag * er * 0.01);
         symboltone_averotator = symboltone_averotator * 0.95 + 0.05 * symboltone_rotator;
         symboltone_pt = cpx((symboltone_pt.real()), a1.update(symboltone_pt.real()));
-        double st_err = std::arg((st_osc_quarter.WTCISValue()) * std::conj(symboltone_pt));
+        double st_err = olm::arg((st_osc_quarter.WTCISValue()) * std::conj(symboltone_pt));
         st_err *= 1.5 * (1.0 - progress * progress);
         st_osc_quarter.AdvanceFractionOfWave(-(1.0 / (2.0 * M_PI)) * st_err * 0.1);
         st_osc.SetPhaseDeg((360.0 * st_osc_quarter.WTptr / ((double)WTSIZE)) * 4.0 + (360.0 * ee));
       }
       sig2 *= symboltone_averotator;
-      rotator = rotator * std::exp(imag * rotator_freq);
+      rotator = rotator * olm::expi(imag * rotator_freq);
       sig2 *= rotator;
       double sig2abs = std::abs(sig2);
       sig2 *= agc2.Update(sig2abs);
@@ -2617,7 +2647,7 @@ struct BurstOqpsk {
       if (cntr > SamplesPerSymbol * (128 + 128)) st_eta = st_iir_resonator.y;
       cpx st_m1 = cpx(st_eta, -delayt8.update(st_eta));
       cpx st_out = st_osc.WTCISValue() * st_m1;
-      double st_angle_error = std::arg(st_out);
+      double st_angle_error = olm::arg(st_out);
       if (cntr > SamplesPerSymbol * (128 + 64)) {
         st_osc.IncreseFreqHz(-st_angle_error * 0.00000001);
         st_osc.AdvanceFractionOfWave(-st_angle_error * 0.01 / 360.0);
@@ -2654,7 +2684,7 @@ struct BurstOqpsk {
           if (ct_ec > M_PI_2) ct_ec = M_PI_2;
           if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
           if (cntr > ((128 + 10) * SamplesPerSymbol)) {
-            rotator = rotator * std::exp(imag * ct_ec * 0.1);
+            rotator = rotator * olm::expi(imag * ct_ec * 0.1);
             if (cntr > ((128 + 10) * SamplesPerSymbol)) rotator_freq = rotator_freq + ct_ec * 0.0001;
           }
           if (trace_pt) {
@@ -2815,7 +2845,7 @@ struct BurstMsk {
                      !(cntr > 0 && cntr < (500 * SamplesPerSymbol));  // && !dcd
     if (det) {
       vol_gain = 1.4142 * (500.0 / (minval / 3));
-      const double carrierphase = std::arg(out_base[minvalbin]) - (M_PI / 4.0);
+      const double carrierphase = olm::arg(out_base[minvalbin]) - (M_PI / 4.0);
       mixer2.SetPhaseDeg((180.0 / M_PI) * carrierphase);
       mixer2.SetFreq(((maxtopposhigh + maxtoppos) / 2) * hzperbin);
       {  // CenterFreqChangedSlot (:299-317), afc on; mixer_center then mixer2 = its frequency
@@ -2889,19 +2919,19 @@ struct BurstMsk {
       if (cntr > (startProcessing * SamplesPerSymbol) && cntr < endRotation) {
         cpx symboltone_pt = sig2 * symboltone_rotator * imag;
         double er = std::tanh(symboltone_pt.imag()) * (symboltone_pt.real());
-        symboltone_rotator = symboltone_rotator * std::exp(imag * er * 0.5);
+        symboltone_rotator = symboltone_rotator * olm::expi(imag * er * 0.5);
         symboltone_averotator = symboltone_averotator * 0.999 + 0.001 * symboltone_rotator;
         symboltone_pt = cpx((symboltone_pt.real()), a1.update(symboltone_pt.real()));
         double progress = (double)cntr - (SamplesPerSymbol * (startProcessing));
         double goal = endRotation - (SamplesPerSymbol * startProcessing);
         progress = progress / goal;
-        double st_err = std::arg((st_osc_half.WTCISValue()) * std::conj(symboltone_pt));
+        double st_err = olm::arg((st_osc_half.WTCISValue()) * std::conj(symboltone_pt));
         st_err *= 0.5 * (1.0 - progress * progress);
         st_osc_half.AdvanceFractionOfWave(-(1.0 / (2.0 * M_PI)) * st_err * 0.05);
         st_osc.SetPhaseDeg((360.0 * st_osc_half.WTptr / ((double)WTSIZE)) + (360.0 * (1.0 - ee)));
       }
       sig2 *= symboltone_averotator;
-      rotator = rotator * std::exp(imag * rotator_freq);
+      rotator = rotator * olm::expi(imag * rotator_freq);
       sig2 *= rotator;
       sig2 *= agc2.Update(std::abs(sig2));
       double abval = std::abs(sig2);
@@ -2912,7 +2942,7 @@ struct BurstMsk {
       st_eta = st_iir_resonator.update(st_eta);
       cpx st_m1 = cpx(st_eta, -delayt8.update(st_eta));
       cpx st_out = st_osc.WTCISValue() * st_m1;
-      double st_angle_error = std::arg(st_out);
+      double st_angle_error = olm::arg(st_out);
       if (cntr > endRotation) st_osc.AdvanceFractionOfWave(-st_angle_error * 0.002 / 360.0);
       if (st_osc.IfHavePassedPoint(ee)) {
         double ct_xt = tanh(sig2.imag()) * sig2.real();
