@@ -84,18 +84,20 @@ __global__ void pcm_scatter_kernel(int16_t *ring, int C, long long capm, const i
   }
 }
 
-// one feed item: a device PCM run for one channel (aero_chan_feed)
+// one gather item: a device PCM run for one channel (aero_chan_feed, or a
+// queued host message); `later` = a later job of the same launch sets the
+// channel's counter (jobs run in parallel)
 struct GatherJob {
   const int16_t *src;
   long long n, start, avail_after;
-  int c, pad;
+  int c, later;
 };
 
 __global__ void pcm_gather_kernel(int16_t *ring, int C, long long capm, long long *avail, const GatherJob *jobs) {
   const GatherJob j = jobs[blockIdx.y];
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < j.n; t += (long long)gridDim.x * blockDim.x)
     ring[((j.start + t) & capm) * C + j.c] = j.src[t];
-  if (blockIdx.x == 0 && threadIdx.x == 0) avail[j.c] = j.avail_after;  // LS_AVAIL row
+  if (!j.later && blockIdx.x == 0 && threadIdx.x == 0) avail[j.c] = j.avail_after;  // LS_AVAIL row
 }
 
 __global__ void math_kernel(int fn, const double *x, const double *y, double *out, size_t n) {
@@ -226,11 +228,29 @@ struct Group {
   std::vector<hipEvent_t> ev_free;
   int vit_pending = -1;          // slot whose Viterbi launch is deferred
   hipEvent_t ev_in = nullptr;
-  // aero_chan_feed job tables (pinned -> device, reused once their event completed)
+  // gather job tables (aero_chan_feed, queued host messages; pinned ->
+  // device, reused once their event completed), GJOB_MIN or C entries
+  static constexpr int GJOB_MIN = 4096;
   GatherJob *pin_gjobs[NPIN] = {}, *d_gjobs[NPIN] = {};
   hipEvent_t gjob_ev[NPIN] = {};
   int next_gjob = 0;
   hipEvent_t ev_feed_done = nullptr;
+  // queued host messages (single-channel pageable pushes, e.g. one ZeroMQ
+  // message of one topic): copied into pinned staging when pushed, moved to
+  // the PCM rings by one H2D copy and one gather launch when the group next
+  // runs (hostq_flush) instead of a staged copy and a scatter launch each
+  struct HqItem {
+    int c;
+    size_t off;
+    long long n, start;
+  };
+  std::vector<HqItem> hq;
+  // two pinned stagings, alternating at each flush (filling one never waits
+  // for the copy out of the other); one device buffer (stream-ordered)
+  int16_t *pin_hq[2] = {}, *d_hq = nullptr;
+  size_t hq_cap = 0, hq_used = 0;
+  int hq_buf = 0;
+  hipEvent_t hq_ev[2] = {};  // after the last copy out of pin_hq[k]
   void *pin_stat = nullptr;  // aero_channel_stat staging
   std::map<std::string, TimingSlot> timing;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending_ev;
@@ -652,16 +672,86 @@ int note_consumed(Group *e) {
   return AERO_OK;
 }
 
-int run_group(Group *e, int flush) {
-  if (e->nch == 0) return AERO_OK;
+size_t gjob_cap(const Group *e) { return (size_t)std::max(e->C, Group::GJOB_MIN); }
+
+// a free gather-job table (pinned + device, gjob_cap entries)
+int gather_table(Group *e, int &k) {
+  k = e->next_gjob;
+  e->next_gjob = (k + 1) % Group::NPIN;
+  if (!e->pin_gjobs[k]) {
+    if (hipHostMalloc(&e->pin_gjobs[k], sizeof(GatherJob) * gjob_cap(e)) != hipSuccess) return AERO_E_NOMEM;
+    if (hipMalloc(&e->d_gjobs[k], sizeof(GatherJob) * gjob_cap(e)) != hipSuccess) return AERO_E_NOMEM;
+    HIPCHK(hipEventCreateWithFlags(&e->gjob_ev[k], hipEventDisableTiming));
+  }
+  HIPCHK(hipEventSynchronize(e->gjob_ev[k]));  // the table NPIN launches ago has been read
+  return AERO_OK;
+}
+
+// only a channel's last job of a launch writes its counter
+void mark_last_jobs(GatherJob *jobs, size_t nj, int C) {
+  std::vector<uint8_t> seen(C, 0);
+  for (size_t i = nj; i-- > 0;) {
+    jobs[i].later = seen[jobs[i].c];
+    seen[jobs[i].c] = 1;
+  }
+}
+
+// the queued host messages into the PCM rings: one H2D copy of the staging,
+// one gather launch (stream-ordered before the group's next kernels)
+int hostq_flush(Group *e) {
+  if (e->hq.empty()) return AERO_OK;
+  int k;
+  if (int rc = gather_table(e, k)) return rc;
+  const int b = e->hq_buf;
+  HIPCHK(hipMemcpyAsync(e->d_hq, e->pin_hq[b], sizeof(int16_t) * e->hq_used, hipMemcpyHostToDevice, e->st));
+  HIPCHK(hipEventRecord(e->hq_ev[b], e->st));
+  long long mx = 0;
+  const size_t nj = e->hq.size();
+  for (size_t i = 0; i < nj; i++) {
+    const Group::HqItem &it = e->hq[i];
+    GatherJob &j = e->pin_gjobs[k][i];
+    j.src = e->d_hq + it.off;
+    j.n = it.n;
+    j.start = it.start;
+    j.avail_after = it.start + it.n;
+    j.c = it.c;
+    j.later = 0;
+    mx = std::max(mx, it.n);
+  }
+  mark_last_jobs(e->pin_gjobs[k], nj, e->C);
+  HIPCHK(hipMemcpyAsync(e->d_gjobs[k], e->pin_gjobs[k], sizeof(GatherJob) * nj, hipMemcpyHostToDevice, e->st));
+  HIPCHK(hipEventRecord(e->gjob_ev[k], e->st));
+  const unsigned gx = (unsigned)std::max<long long>(1, std::min<long long>((mx + 255) / 256, 64));
+  hipLaunchKernelGGL(pcm_gather_kernel, dim3(gx, (unsigned)nj), dim3(256), 0, e->st, e->S.pcm, e->C,
+                     (long long)PCM_CAP - 1, e->S.ls + (size_t)LS_AVAIL * e->C, (const GatherJob *)e->d_gjobs[k]);
+  HIPCHK(hipGetLastError());
+  e->hq.clear();
+  e->hq_used = 0;
+  e->hq_buf = b ^ 1;
+  return AERO_OK;
+}
+
+// A run of a group is run_begin, passes until a pass has nothing to do,
+// run_end.  run_group runs one group; run_impl interleaves the groups' passes
+// so that each group's launches queue on its stream while the host waits for
+// another group's old job slot (the kinds of a mixed engine, e.g. the C5
+// receiver's OQPSK, MSK 600 and MSK 1200 groups, then run side by side).
+int run_begin(Group *e) {
   HIPCHK(hipSetDevice(e->device));
-  HOST_TIMER(e, "host_run");
   if (int rc = flush_pending_init(e)) return rc;
-  if (int rc = poll_slots(e, false)) return rc;
+  if (int rc = hostq_flush(e)) return rc;
+  return poll_slots(e, false);
+}
+
+// one pass (coarse, the previous pass's Viterbi, demod, framing); *more is
+// false when the group had nothing left to do
+int run_pass(Group *e, int flush, bool *more) {
+  HOST_TIMER(e, "host_run");
+  *more = true;
   const int tflags = AERO_F_TRACE_PT | AERO_F_TRACE_BLOCKS | AERO_F_TRACE_SOFT | AERO_F_TRACE_HOPS;
   const bool trace = (e->flags & tflags) != 0;
   const long long HOPN = e->g.hop;
-  for (int guard = 0; guard < 1000000; guard++) {
+  {
     // host mirror of the hop and segment rules of coarse.hip / demod_*.hip
     bool any_hop = false, progress = false;
     for (int c = 0; c < e->nch; c++) {
@@ -681,7 +771,10 @@ int run_group(Group *e, int flush) {
         progress = true;
       }
     }
-    if (!any_hop && !progress) break;
+    if (!any_hop && !progress) {
+      *more = false;
+      return AERO_OK;
+    }
     hipEvent_t a, b;
     if (any_hop) {
       ev_begin(e, "coarse", a, b);
@@ -689,7 +782,7 @@ int run_group(Group *e, int flush) {
       ev_end(e, b);
     }
     if (int rc = issue_viterbi(e)) return rc;  // the previous pass's decode, before this demod
-    if (!progress) continue;  // no new soft bits: framing has nothing to do
+    if (!progress) return AERO_OK;  // no new soft bits: framing has nothing to do
     ev_begin(e, "demod", a, b);
     if (e->mode == MODE_OQPSK)
       launch_demod(e->st, e->S, e->T, e->nch, flush, (e->flags & AERO_F_TRACE_PT) != 0);
@@ -728,10 +821,23 @@ int run_group(Group *e, int flush) {
       if (int rc = collect_traces(e)) return rc;
     }
   }
-  // the deferral only reorders passes inside this call: the last pass's
-  // decode is launched before aero_run returns, so its items never wait for
-  // more audio (the reference emits them as soon as they are decoded)
-  return issue_viterbi(e);
+  return AERO_OK;
+}
+
+// the deferral only reorders passes inside one run: the last pass's decode
+// is launched before the run returns, so its items never wait for more audio
+// (the reference emits them as soon as they are decoded)
+int run_end(Group *e) { return issue_viterbi(e); }
+
+int run_group(Group *e, int flush) {
+  if (e->nch == 0) return AERO_OK;
+  if (int rc = run_begin(e)) return rc;
+  for (int guard = 0; guard < 1000000; guard++) {
+    bool more;
+    if (int rc = run_pass(e, flush, &more)) return rc;
+    if (!more) break;
+  }
+  return run_end(e);
 }
 
 // waits for the group's GPU work and hands every completed slot over
@@ -761,10 +867,23 @@ int run_impl(aero_engine *e, int flush) {
   for (BurstGroup *b : e->burst)
     if (b)
       if (int rc = burst_run(b, flush)) return rc;
+  Group *act[MODE_COUNT];
+  int na = 0;
   for (auto &g : e->groups)
-    if (g) {
-      int rc = run_group(g.get(), flush);
-      if (rc) return rc;
+    if (g && g->nch) {
+      if (int rc = run_begin(g.get())) return rc;
+      act[na++] = g.get();
+    }
+  for (int guard = 0; na > 0 && guard < 1000000; guard++)
+    for (int i = 0; i < na;) {
+      bool more;
+      if (int rc = run_pass(act[i], flush, &more)) return rc;
+      if (more) {
+        i++;
+        continue;
+      }
+      if (int rc = run_end(act[i])) return rc;
+      act[i] = act[--na];
     }
   if (flush)  // aero_flush returns with every output of the pushed samples available
     for (auto &g : e->groups)
@@ -916,6 +1035,11 @@ void group_destroy(Group *e) {
     if (e->gjob_ev[k]) (void)hipEventDestroy(e->gjob_ev[k]);
   }
   if (e->ev_feed_done) (void)hipEventDestroy(e->ev_feed_done);
+  for (int k = 0; k < 2; k++) {
+    if (e->pin_hq[k]) (void)hipHostFree(e->pin_hq[k]);
+    if (e->hq_ev[k]) (void)hipEventDestroy(e->hq_ev[k]);
+  }
+  if (e->d_hq) (void)hipFree(e->d_hq);
   if (e->pin_stat) (void)hipHostFree(e->pin_stat);
   if (e->pin_pcm) (void)hipHostFree(e->pin_pcm);
   if (e->pin_pcm_ev) (void)hipEventDestroy(e->pin_pcm_ev);
@@ -970,6 +1094,36 @@ bool is_pinned_host(const void *p) {
   return a.type == hipMemoryTypeHost;
 }
 
+// one pageable single-channel message into the queue (hostq_flush)
+int hostq_push(Group *e, const int16_t *src, size_t n, int c) {
+  if (e->hq.size() >= gjob_cap(e) || e->hq_used + n > e->hq_cap)
+    if (int rc = hostq_flush(e)) return rc;
+  for (int k = 0; k < 2; k++)
+    if (!e->hq_ev[k]) HIPCHK(hipEventCreateWithFlags(&e->hq_ev[k], hipEventDisableTiming));
+  if (n > e->hq_cap) {
+    const size_t cap = std::max<size_t>(n, std::max<size_t>((size_t)1 << 22, 2 * e->hq_cap));
+    HIPCHK(hipStreamSynchronize(e->st));  // the last copies and gathers have used them
+    for (int k = 0; k < 2; k++) {
+      if (e->pin_hq[k]) (void)hipHostFree(e->pin_hq[k]);
+      e->pin_hq[k] = nullptr;
+    }
+    if (e->d_hq) (void)hipFree(e->d_hq);
+    e->d_hq = nullptr;
+    e->hq_cap = 0;
+    for (int k = 0; k < 2; k++)
+      if (hipHostMalloc(&e->pin_hq[k], sizeof(int16_t) * cap) != hipSuccess) return AERO_E_NOMEM;
+    if (hipMalloc(&e->d_hq, sizeof(int16_t) * cap) != hipSuccess) return AERO_E_NOMEM;
+    e->hq_cap = cap;
+  }
+  // the copy out of this staging two flushes ago is done
+  if (e->hq_used == 0) HIPCHK(hipEventSynchronize(e->hq_ev[e->hq_buf]));
+  memcpy(e->pin_hq[e->hq_buf] + e->hq_used, src, sizeof(int16_t) * n);
+  e->hq.push_back({c, e->hq_used, (long long)n, e->avail[c]});
+  e->hq_used += n;
+  e->avail[c] += (long long)n;
+  return AERO_OK;
+}
+
 int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int c0, bool dev) {
   HOST_TIMER(e, "host_push");
   if (dev)
@@ -991,6 +1145,8 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
       if (e->avail[c] + (long long)n - e->nsamp[c] > PCM_CAP - 2) return AERO_E_FULL;
     }
   }
+  if (!dev && nch == 1) return hostq_push(e, src, n, c0);
+  if (int rc = hostq_flush(e)) return rc;  // ring writes and counters in push order
   const int16_t *dsrc = src;
   if (!dev) {
     // the caller's buffer is copied before returning: into pinned staging
@@ -1102,16 +1258,11 @@ int feed_group(Group *e, const std::vector<std::pair<int, std::pair<const int16_
       if (e->avail[c] + n - e->nsamp[c] > PCM_CAP - 2) return AERO_E_FULL;
     }
   }
-  const int k = e->next_gjob;
-  e->next_gjob = (k + 1) % Group::NPIN;
-  if (!e->pin_gjobs[k]) {
-    if (hipHostMalloc(&e->pin_gjobs[k], sizeof(GatherJob) * e->C) != hipSuccess) return AERO_E_NOMEM;
-    if (hipMalloc(&e->d_gjobs[k], sizeof(GatherJob) * e->C) != hipSuccess) return AERO_E_NOMEM;
-    HIPCHK(hipEventCreateWithFlags(&e->gjob_ev[k], hipEventDisableTiming));
-  }
-  if (!e->ev_feed_done) HIPCHK(hipEventCreateWithFlags(&e->ev_feed_done, hipEventDisableTiming));
-  HIPCHK(hipEventSynchronize(e->gjob_ev[k]));  // the table NPIN feeds ago has been read
   if ((int)items.size() > e->C) return AERO_E_INVALID;
+  if (int rc = hostq_flush(e)) return rc;
+  int k;
+  if (int rc = gather_table(e, k)) return rc;
+  if (!e->ev_feed_done) HIPCHK(hipEventCreateWithFlags(&e->ev_feed_done, hipEventDisableTiming));
   long long mx = 0;
   for (size_t i = 0; i < items.size(); i++) {
     const int c = items[i].first;
@@ -1122,10 +1273,11 @@ int feed_group(Group *e, const std::vector<std::pair<int, std::pair<const int16_
     j.start = e->avail[c];
     j.avail_after = e->avail[c] + n;
     j.c = c;
-    j.pad = 0;
+    j.later = 0;
     e->avail[c] += n;
     mx = std::max(mx, n);
   }
+  mark_last_jobs(e->pin_gjobs[k], items.size(), e->C);
   HIPCHK(hipMemcpyAsync(e->d_gjobs[k], e->pin_gjobs[k], sizeof(GatherJob) * items.size(), hipMemcpyHostToDevice,
                         e->st));
   HIPCHK(hipEventRecord(e->gjob_ev[k], e->st));

@@ -84,9 +84,13 @@ int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out);
 /* One ZMQ message == one call: Decoder::audioReceived ->
  * OqpskDemodulator::dataReceived / MskDemodulator::dataReceived
  * (decode/decode.cpp:352, decode/oqpskdemodulator.cpp:624-630,
- * decode/mskdemodulator.cpp:472-481).  pcm: int16 LE real samples.  An MSK
- * channel refuses a rate other than its own (AERO_E_RATE): the reference
- * would re-apply its settings at the new rate. */
+ * decode/mskdemodulator.cpp:472-481).  pcm: int16 LE real samples, copied
+ * before returning (a continuous channel's message is staged in pinned host
+ * memory and reaches the GPU at the next aero_run).  fs: an OQPSK or burst
+ * channel only logs a mismatch; a continuous MSK channel re-applies its
+ * settings at 12000, 24000 or 48000 Hz, keeping the state
+ * MskDemodulator::setSettings keeps (decode/mskdemodulator.cpp:94-218), and
+ * refuses any other rate (AERO_E_RATE, the message is dropped). */
 int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t fs);
 
 /* Lockstep batch push for channels [0, nch): pcm is time-major, n samples

@@ -142,3 +142,49 @@ def test_documented_channel_config_per_bitrate(engine_lib):
         bad = ae.ChannelCfg(bitrate, 0, 11025, 0)
         assert lib.aero_channel_open(eng.h, ctypes.byref(bad), ctypes.byref(ch)) == ae.AERO_E_INVALID, bitrate
     eng.close()
+
+
+@pytest.mark.gpu
+def test_queued_host_messages_between_runs(engine_lib):
+    """Host messages are queued in pinned staging and reach the PCM rings as
+    one gather launch per run (engine.hip hostq_flush): several messages per
+    channel between two runs (the multi-topic aero-decode batch), of
+    different sizes, a device push on another channel in between (which
+    flushes the queue first), and a message larger than half the ring (the
+    overrun guard runs the group mid-queue).  Soft bits, hops and items equal
+    the oracle fed the same messages."""
+    import torch
+    import aero_engine as ae
+    streams = [tl.synth(seconds=9.0, seed=0xAE60 + k, carrier=9000.0 + 1500.0 * k) for k in range(3)]
+    eng = ae.Engine(max_channels=3, flags=ae.F_TRACE_SOFT | ae.F_TRACE_HOPS)
+    chans = [eng.open_channel(10500, 48000) for _ in streams]
+    sizes = [(1000, 2500, 700, 4096), (12000,), (5000, 20000)]
+    pos = [0, 0, 0]
+    dev = torch.from_numpy(streams[1]).to('cuda')
+    rnd = 0
+    while any(p < len(s) for p, s in zip(pos, streams)):
+        for k in (0, 2):
+            for sz in sizes[k] * 2:  # several messages of each channel before one run
+                if pos[k] < len(streams[k]):
+                    eng.push(chans[k], streams[k][pos[k]:pos[k] + sz])
+                    pos[k] += sz
+            if k == 0 and pos[1] < len(streams[1]):
+                n = min(12000, len(streams[1]) - pos[1])
+                torch.cuda.synchronize()
+                eng.push_device(chans[1], dev[pos[1]:pos[1] + n].data_ptr(), n)
+                pos[1] += n
+        if rnd % 3 == 2 and pos[0] < len(streams[0]):  # larger than half the PCM ring
+            eng.push(chans[0], streams[0][pos[0]:pos[0] + 40000])
+            pos[0] += 40000
+        eng.run()
+        rnd += 1
+    eng.flush()
+    for k, s in enumerate(streams):
+        o = tl.Oracle()
+        o.push_chunked(s, 4096)
+        assert len(o.softbits()) > 1000
+        assert np.array_equal(eng.softbits(chans[k]), o.softbits()), 'channel %d soft bits differ' % k
+        h = eng.hops(chans[k])
+        assert np.array_equal(h.view(np.int64), o.hops().view(np.int64)), 'channel %d hops differ' % k
+        assert eng.items(chans[k]) == o.item_lines('A') and o.item_lines('A'), 'channel %d items differ' % k
+    eng.close()
