@@ -142,30 +142,18 @@ __global__ __launch_bounds__(512) void hilbert_kernel(BurstState S, BurstTables 
 //
 // The RRC (FIR::FIRUpdateAndProcess, transposed form: the output is
 // ((0 + h0 d[n-55]) + h1 d[n-54]) + ... + h54 d[n-1], oldest term first).
-// AERO_BD_DIRECT (default): the partial sum of the oldest BD_LDS_TAPS taps is
-// formed directly, oldest first, from a per-lane LDS line of the last
-// BD_LDS_TAPS mixer outputs d (one 16-B read per tap and one write per
-// sample); the line slides back every BD_DBLK samples.  The same products are
-// added in the same order as in the transposed form, so every partial sum is
-// the same double.  The newest taps keep their transposed partial sums in
-// registers.  The state between launches holds the line (oldest first) in
-// place of those taps' partial sums: all zero at start in either form.
-// AERO_BD_DIRECT=0: the transposed partial sums of taps [0, BD_LDS_TAPS) in
-// LDS (a read and a write per tap and sample).
+// The partial sum of the oldest BD_LDS_TAPS taps is formed directly, oldest
+// first, from a per-lane LDS line of the last BD_LDS_TAPS mixer outputs d
+// (one 16-B read per tap and one write per sample); the line slides back
+// every BD_DBLK samples.  The same products are added in the same order as in
+// the transposed form, so every partial sum is the same double.  The newest
+// taps keep their transposed partial sums in registers.  The state between
+// launches holds the line (oldest first) in place of those taps' partial
+// sums: all zero at start in either form.
 constexpr int BD_BLOCK = 64;
-#ifndef AERO_BD_DIRECT
-#define AERO_BD_DIRECT 1
-#endif
-#ifndef AERO_BD_LDS_TAPS
-#define AERO_BD_LDS_TAPS (AERO_BD_DIRECT ? 36 : 40)
-#endif
-constexpr int BD_LDS_TAPS = AERO_BD_LDS_TAPS, BD_REG_TAPS = NTAPS - BD_LDS_TAPS;
-constexpr int BD_DBLK = 40 - BD_LDS_TAPS;  // direct form: samples per slide of the line
-#ifndef AERO_BD_DCH
-#define AERO_BD_DCH 8
-#endif
-constexpr int BD_DCH = AERO_BD_DCH;  // direct form: line entries read per chunk
-static_assert(!AERO_BD_DIRECT || (BD_LDS_TAPS >= 1 && BD_DBLK >= 1), "direct line within 40 KB per wave");
+constexpr int BD_LDS_TAPS = 36, BD_REG_TAPS = NTAPS - BD_LDS_TAPS;
+constexpr int BD_DBLK = 40 - BD_LDS_TAPS;  // samples per slide of the line
+constexpr int BD_DCH = 8;                  // line entries read per chunk
 
 // AERO_X_BSTAMPS (diagnostic build only): s_memtime cycle totals per section
 // of the demod loop, each wave's maximum over its lanes (the wave's time in
@@ -360,12 +348,7 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
 // wave per workgroup.  The transposed RRC partial sums of taps
 // [BD_LDS_TAPS, 55) live in registers, the rest (real and imaginary) in LDS.
 __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, BurstTables T, int nch, int trace) {
-#if AERO_BD_DIRECT
   __shared__ double2 s_d[BD_LDS_TAPS + BD_DBLK][BD_BLOCK];  // [slot][lane]: d of past samples
-#else
-  __shared__ double s_qre[BD_LDS_TAPS > 0 ? BD_LDS_TAPS : 1][BD_BLOCK];
-  __shared__ double s_qim[BD_LDS_TAPS > 0 ? BD_LDS_TAPS : 1][BD_BLOCK];
-#endif
   const int c = blockIdx.x * BD_BLOCK + threadIdx.x, col = threadIdx.x;
   if (c >= nch) return;
 #ifdef AERO_X_BSTAMPS
@@ -416,18 +399,10 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   long long chk_done = ls[BL_CHK_DONE * C];
   const long long chk_n = ls[BL_CHK_N * C];
   long long next_chk = chk_done < chk_n ? S.chk_n[(size_t)c * TRI_SLOTS + (chk_done & (TRI_SLOTS - 1))] : LLONG_MAX;
-#if AERO_BD_DIRECT
 #pragma unroll 1
   for (int j = 0; j < BD_LDS_TAPS; ++j)
     s_d[j][col] = make_double2(S.fir[(size_t)j * C + c], S.fir[(size_t)(NTAPS + j) * C + c]);
   int dt = 0;  // the line's oldest entry is slot dt
-#else
-#pragma unroll 1
-  for (int j = 0; j < BD_LDS_TAPS; ++j) {
-    s_qre[j][col] = S.fir[(size_t)j * C + c];
-    s_qim[j][col] = S.fir[(size_t)(NTAPS + j) * C + c];
-  }
-#endif
   double hre[BD_REG_TAPS], him[BD_REG_TAPS];  // partial sums of taps BD_LDS_TAPS..54
 #pragma unroll
   for (int j = 0; j < BD_REG_TAPS; ++j) {
@@ -535,7 +510,6 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       const double sc = vol_gain * vtd;
       const double ddr = m2.x * sc, ddi = m2.y * sc;
       // RRC (FIR::FIRUpdateAndProcess reads the 55 samples before the newest)
-#if AERO_BD_DIRECT
       // partial sum of taps 0..BD_LDS_TAPS-1 at sample n-1, oldest term first
       const int lbase = dt * BD_BLOCK + col;  // element index of the oldest entry in s_d
       double ar = 0.0, ai = 0.0;
@@ -567,7 +541,6 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
           asm volatile("" : "+v"(lp), "+s"(tz) : "v"(ar), "v"(ai));
         }
       }
-#endif
       const double *tp = c_btaps + tz;
       s2r = hre[BD_REG_TAPS - 1];
       s2i = him[BD_REG_TAPS - 1];
@@ -580,7 +553,6 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
           tp = c_btaps + tz;
         }
       }
-#if AERO_BD_DIRECT
       hre[0] = ar + tp[BD_LDS_TAPS] * ddr;
       him[0] = ai + tp[BD_LDS_TAPS] * ddi;
       (&s_d[0][0])[lbase + BD_LDS_TAPS * BD_BLOCK] = make_double2(ddr, ddi);
@@ -589,19 +561,6 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
 #pragma unroll 8
         for (int i = 0; i < BD_LDS_TAPS; ++i) s_d[i][col] = s_d[BD_DBLK + i][col];
       }
-#elif AERO_BD_LDS_TAPS > 0
-      hre[0] = s_qre[BD_LDS_TAPS - 1][col] + tp[BD_LDS_TAPS] * ddr;
-      him[0] = s_qim[BD_LDS_TAPS - 1][col] + tp[BD_LDS_TAPS] * ddi;
-      for (int j = BD_LDS_TAPS - 1; j >= 1; --j) {
-        s_qre[j][col] = s_qre[j - 1][col] + tp[j] * ddr;
-        s_qim[j][col] = s_qim[j - 1][col] + tp[j] * ddi;
-      }
-      s_qre[0][col] = 0.0 + tp[0] * ddr;
-      s_qim[0][col] = 0.0 + tp[0] * ddi;
-#else
-      hre[0] = 0.0 + tp[0] * ddr;
-      him[0] = 0.0 + tp[0] * ddi;
-#endif
     }
     BSTAMP(4);
     if (startstop > 0) {
@@ -783,20 +742,12 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   }
   BCOUNT(0, (unsigned long long)(n - n0));
   // state back
-#if AERO_BD_DIRECT
 #pragma unroll 1
   for (int j = 0; j < BD_LDS_TAPS; ++j) {
     const double2 v = s_d[dt + j][col];
     S.fir[(size_t)j * C + c] = v.x;
     S.fir[(size_t)(NTAPS + j) * C + c] = v.y;
   }
-#else
-#pragma unroll 1
-  for (int j = 0; j < BD_LDS_TAPS; ++j) {
-    S.fir[(size_t)j * C + c] = s_qre[j][col];
-    S.fir[(size_t)(NTAPS + j) * C + c] = s_qim[j][col];
-  }
-#endif
 #pragma unroll
   for (int j = 0; j < BD_REG_TAPS; ++j) {
     S.fir[(size_t)(BD_LDS_TAPS + j) * C + c] = hre[j];

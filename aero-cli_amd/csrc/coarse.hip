@@ -309,10 +309,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   double yp2 = yload(t + 2 * FT);
   __syncthreads();
   CSTAMP(4);
-#ifndef AERO_CO_LOG_UNROLL
-#define AERO_CO_LOG_UNROLL 1
-#endif
-#pragma unroll AERO_CO_LOG_UNROLL
+#pragma unroll 1
   for (int k = t; k < YLEN; k += FT) {
     const double yold = yp0;
     yp0 = yp1;

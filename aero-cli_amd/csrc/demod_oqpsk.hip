@@ -8,10 +8,13 @@
  * expression keeps the reference's operation order; std::complex products
  * are expanded as GCC does ((ac-bd), (ad+bc)); libm calls go to aero_math.h.
  *
- * One lane per channel.  The 55-tap RRC runs in transposed form with all
- * 110 partial sums (real and imaginary) in registers for the whole launch
- * (one wave per SIMD, up to 512 VGPR+AGPR); the QIM_LDS build switch puts
- * the imaginary ones back in LDS ([tap][lane]) for experiments only.
+ * One lane per channel, two waves per 64 channels on one SIMD: the chain
+ * wave runs the per-sample recurrence; its helper, the FIR wave, keeps the
+ * 55-tap RRC's transposed partial sums R_0..R_53 (60 in registers, 48 in
+ * LDS) and updates them from the mixed samples the chain publishes in LDS,
+ * handing R_53 back first so only R_54's update stays on the chain
+ * (demod_fir_wave; the sequence-word protocol at DemodShared).  Each wave
+ * fits the 256 VGPRs of two waves per SIMD.
  *
  * Segment contract: a launch advances every channel from nsamp up to (but
  * excluding) its next coarse-estimate hop sample, or to the pushed end; it

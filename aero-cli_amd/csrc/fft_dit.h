@@ -123,12 +123,6 @@ __device__ __forceinline__ void stage(double2 (&x)[16], int t, int lb, int n, co
 // BR: the destination reads bit-reversed positions (start of a new transform)
 template <int LOG2N, int PH_FROM, int PH_TO, bool BR>
 __device__ __forceinline__ void exchange(double2 (&x)[16], int t0, double *lds) {
-#ifdef AERO_X_NOEXCH  // timing experiment only (wrong results): no transposes
-  if (!BR) {
-    asm volatile("" : "+v"(x[0].x), "+v"(x[5].y), "+v"(x[15].x));
-    return;
-  }
-#endif
 #pragma unroll
   for (int part = 0; part < 2; ++part) {
     const int t = fresh(t0);
@@ -172,9 +166,6 @@ template <int LOG2N, bool INV, int LB>
 __device__ __forceinline__ void stage0(double2 (&x)[16], int t0, const double2 *__restrict__ TW,
                                        const double2 *stw) {
   constexpr int n = 1 << LB;
-#ifdef AERO_X_NOTRIV
-  stage<LOG2N, 0, INV>(x, t0, LB, n, TW, stw);
-#else
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     if (i & n) continue;
@@ -195,7 +186,6 @@ __device__ __forceinline__ void stage0(double2 (&x)[16], int t0, const double2 *
     x[i].x = x[i].x + yr;
     x[i].y = x[i].y + yi;
   }
-#endif
 }
 
 // full JFFT::fft on values already loaded in bit-reversed order in layout 0;
