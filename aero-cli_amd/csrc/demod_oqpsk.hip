@@ -418,12 +418,10 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
     it = __builtin_amdgcn_readfirstlane(lds_load(&sh.cseq[wv]));
     do {
       XSTAMP(0);  // loop control
-#ifndef DEMOD_SYNC_V1
       // the FIR wave's progress and R_53(n-1) (its iteration it - 1), read
       // first so their LDS latency passes while this sample is mixed
       const int fsv = lds_load(&sh.fseq[wv]);
       double2 r53 = sh.r53[(it & 1) ^ 1][pair];
-#endif
       const int16_t xs = pcm_next;
       pcm_next = pcm_next2;
       const double agc_old = agc_next;
@@ -449,33 +447,16 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
         const int par = it & 1;
         sh.x[par][pair] = make_double2(cv, cvi);
         sh.mask[par][wv] = __builtin_amdgcn_read_exec();
-#ifdef DEMOD_SYNC_V1
-        lds_release();
-#else
         // no wait: a wave's LDS writes are performed in order, so the FIR
         // wave (on the same SIMD, LDS port) that sees the new sequence word
         // sees the sample; only the compiler must keep the order
         __atomic_signal_fence(__ATOMIC_RELEASE);
-#endif
         lds_store(&sh.cseq[wv], it + 1);
       }
       // rrc output of this sample: R_54(n-1); then R_54(n) = R_53(n-1) + h[54] x(n)
       // with R_53(n-1) from the FIR wave's iteration it - 1
       double s2r = q54, s2i = q54i;
       {
-#ifdef DEMOD_SYNC_V1
-        if (it > 0) {
-          for (int spin = 0; __builtin_amdgcn_readfirstlane(lds_load(&sh.fseq[wv])) < it; ++spin) {
-            if (spin > spin_left) {  // broken hand-off: stop waiting for good
-              spin_left = 0;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-          lds_acquire();
-        }
-        const double2 r53 = sh.r53[(it & 1) ^ 1][pair];
-#else
         if (it > 0 && __builtin_amdgcn_readfirstlane(fsv) < it) {  // rare: the FIR wave is behind
           for (int spin = 0; __builtin_amdgcn_readfirstlane(lds_load(&sh.fseq[wv])) < it; ++spin) {
             if (spin > spin_left) {  // broken hand-off: stop waiting for good
@@ -487,7 +468,6 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
           lds_acquire();
           r53 = sh.r53[(it & 1) ^ 1][pair];
         }
-#endif
         const double t0 = c_taps[0];
         q54 = r53.x + t0 * cv;
         q54i = r53.y + t0 * cvi;
