@@ -185,7 +185,12 @@ def load_library(path=None):
         ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
     lib = ctypes.CDLL(path)
     for name, (res, args) in _SIGS.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if path == LIB_PATH:
+                raise
+            continue  # an older experimental build (A/B) without a newer entry point
         fn.restype = res
         fn.argtypes = args
     _lib = lib

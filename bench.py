@@ -498,12 +498,12 @@ def run_c1(a):
     print(json.dumps(out), flush=True)
 
 
-C5BIN_SECONDS = 12.0
+C5BIN_SECONDS = 12.0  # wideband CF32 file the publisher reads without pacing
 
 
 def _is_item(line):
     """a jsondump ACARS line of aero-decode (not its AERO_HOST_TIMING summary)"""
-    return line.startswith('{') and not line.startswith('{"aero_host_timing"')  # wideband CF32 file the publisher reads without pacing
+    return line.startswith('{') and not line.startswith('{"aero_host_timing"')
 
 
 def run_c5bin(a):
