@@ -1131,7 +1131,8 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
   // pinned host input goes straight into the PCM ring rows (a DMA on the
   // input stream, overlapping the kernels already queued: one 1-D copy when
   // the batch is whole ring rows, a 2-D copy otherwise), as a device source
-  // does; pageable input is staged
+  // does; a single channel's pageable message is queued (hostq_push), a
+  // pageable batch staged
   const bool pinned = !dev && nch >= 64 && is_pinned_host(src);
   const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   if (pinned) dev = true;
