@@ -214,12 +214,18 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
   int agc_p = is[BI_AGC_P * C], d1_p = is[BI_D1_P * C];
   int ma1_p = is[BI_MA1_P * C], mav1_p = is[BI_MAV1_P * C];
   int dl_bt = is[(BI_DL_P0 + BDL_BT) * C], dl_md = is[(BI_DL_P0 + BDL_MADIFF) * C];
-  int pd1_p = is[BI_PD1_P * C], pd2_p = is[BI_PD2_P * C], pd3_p = is[BI_PD3_P * C];
+  int pd3_p = is[BI_PD3_P * C];
   int pd_cntdown = is[BI_PD_CNTDOWN * C], pd_maxposcd = is[BI_PD_MAXPOSCD * C];
   int tri_ptr = is[BI_TRI_PTR * C];
   double *tri = S.tri + ((size_t)c * TRI_SLOTS + (chk_n & (TRI_SLOTS - 1))) * B_TRI;
-  const DlyRef dBT = dref(T, BDL_BT), dMD = dref(T, BDL_MADIFF);
+  const DlyRef dMD = dref(T, BDL_MADIFF);
+  double md_older = dly_carry_init(S.dl[BDL_MADIFF] + c, C, dl_md, dMD);  // bt_ma_diff, carried (burst_dev.h)
+  // bt_d1 (a complex delay of one symbol, 11 slots) in registers: its
+  // weights do not depend on the write pointer (host-checked)
   double2 *btr = reinterpret_cast<double2 *>(S.dl[BDL_BT]) + c;
+  double2 hBT[BDL_N_BT];
+  dly_regs_load2(hBT, btr, C, dl_bt);
+  const double wBT = T.dw[BDL_BT][0], oBT = T.domw[BDL_BT][0];
   long long n = n0;
   // the analytic sample and the AGC slot it replaces are loaded one sample
   // ahead: the sample's whole chain starts from them
@@ -233,16 +239,19 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
     // of its stores so the round trips overlap; none is the slot written
     // this sample (burst_dev.h dly_pre)
     const int d1r = d1_p + 1 == B_D1 ? 0 : d1_p + 1;
-    const int p1r = pd1_p + 1 == B_PD1 ? 0 : pd1_p + 1, p2r = pd2_p + 1 == B_PD2 ? 0 : pd2_p + 1;
+    // the peak detector's d1 (same length as d3) and d2 (half) see the same
+    // values as d3, so their outputs are d3's slots: the oldest one and the
+    // one written B_PD2 - 1 updates ago
+    const int p1r = pd3_p + 1 == B_PD3 ? 0 : pd3_p + 1;
+    const int p2r = pd3_p >= B_PD2 - 1 ? pd3_p - (B_PD2 - 1) : pd3_p + B_PD3 - (B_PD2 - 1);
     const double2 a = a_n;
     const double agc_old = agc_n;
     a_n = S.ana[(size_t)((n + 1) & (ANA_LEN - 1)) * C + c];  // past the Hilbert stage's output: unused
     const double2 cvd = S.d1[(size_t)d1r * C + c];  // d1.update_dont_touch(cval)
-    const DlyPre2 btp = dly_pre2(btr, C, dl_bt, dBT);
     const double2 ma_old = S.ma1[(size_t)ma1_p * C + c];
     const double mv_old = S.mav1[(size_t)mav1_p * C + c];
-    const DlyPre mdp = dly_pre(S.dl[BDL_MADIFF] + c, C, dl_md, dMD);
-    const double pd1_old = S.pd1[(size_t)p1r * C + c], pd2_old = S.pd2[(size_t)p2r * C + c];
+    const DlyPre mdp = dly_pre_carry(S.dl[BDL_MADIFF] + c, C, dl_md, dMD, md_older);
+    const double pd1_old = S.pd3[(size_t)p1r * C + c], pd2_old = S.pd3[(size_t)p2r * C + c];
     double cr = a.x, ci = a.y;
     {  // agc.Update(|cval|); cval *= AGCVal (:316-317)
       const double av = aero_hypot(cr, ci);
@@ -262,7 +271,7 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
     S.vring[(size_t)(n & (BV_LEN - 1)) * C + c] = cvd.x;
     double fastarm;
     {  // burst-timing statistic (:326-339)
-      const double2 bd = dly_commit2(btr, C, dl_bt, btp, make_double2(cr, ci));
+      const double2 bd = dly_reg2(hBT, wBT, oBT, make_double2(cr, ci));
       const double pr = cr * bd.x - ci * (-bd.y), pi = cr * (-bd.y) + ci * bd.x;  // cval * conj(bd)
       ma1r = ma1r - ma_old.x;
       ma1i = ma1i - ma_old.y;
@@ -277,20 +286,17 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
       mav1_p = mav1_p + 1 == B_MA ? 0 : mav1_p + 1;
       fastarm = mav1_sum / ((double)B_MA);
       fastarm -= dly_commit(S.dl[BDL_MADIFF] + c, C, dl_md, mdp, fastarm);
+      md_older = mdp.newer;
       if (fastarm < 0) fastarm = 0;
     }
     double bt = fastarm * fastarm;
     if (bt > 500) bt = 500;
     {  // PeakDetector::update (DSP.h:491-566)
       double val = bt;
-      S.pd3[(size_t)pd3_p * C + c] = val;
-      pd3_p = pd3_p + 1 == B_PD3 ? 0 : pd3_p + 1;
-      S.pd1[(size_t)pd1_p * C + c] = val;
-      pd1_p = p1r;
-      const double dy = val - pd1_old;
-      S.pd2[(size_t)pd2_p * C + c] = val;
-      pd2_p = p2r;
-      val = pd2_old;  // d2.update(val)
+      S.pd3[(size_t)pd3_p * C + c] = val;  // d3 (and so d1, d2)
+      pd3_p = p1r;
+      const double dy = val - pd1_old;     // d1.update_dont_touch(val)
+      val = pd2_old;                       // d2.update(val)
       if ((!pd_cntdown) && (val > 0.2) && ((pd_lastdy >= 0 && dy < 0))) {
         pd_cntdown = B_PD_MAXCD;
         pd_maxposcd = pd3_findmaxpos(S.pd3 + c, C, pd3_p, B_PD3);
@@ -330,10 +336,9 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
   is[BI_D1_P * C] = d1_p;
   is[BI_MA1_P * C] = ma1_p;
   is[BI_MAV1_P * C] = mav1_p;
-  is[(BI_DL_P0 + BDL_BT) * C] = dl_bt;
+  dly_regs_store2(hBT, btr, C);
+  is[(BI_DL_P0 + BDL_BT) * C] = 0;
   is[(BI_DL_P0 + BDL_MADIFF) * C] = dl_md;
-  is[BI_PD1_P * C] = pd1_p;
-  is[BI_PD2_P * C] = pd2_p;
   is[BI_PD3_P * C] = pd3_p;
   is[BI_PD_CNTDOWN * C] = pd_cntdown;
   is[BI_PD_MAXPOSCD * C] = pd_maxposcd;

@@ -26,6 +26,8 @@ constexpr int B_TRI = 2633;      // tridentbuffer_sz = qRound(288 * SPS)
 constexpr int B_TRI_HALF = 1170; // qRound(128 * SPS): base / top halves of the trident check
 constexpr int B_MA = 1170;       // bt_ma1 (complex) and mav1 lengths
 constexpr int B_PD1 = 1171, B_PD2 = 586, B_PD3 = 1171;  // PeakDetector d1 / d2 / d3 (length 585)
+// d1 and d2 are read from d3's ring (burst.hip front_burst_kernel)
+static_assert(B_PD1 == B_PD3 && B_PD2 <= B_PD3, "peak detector rings");
 constexpr int B_PD_MAXCD = 1170; // 2 * length
 constexpr int B_MSEMA = 128;
 constexpr int B_STARTSTOP = 9600;  // SPS * 1050
@@ -54,6 +56,8 @@ enum BurstDelay { BDL_S = 0, BDL_41, BDL_42, BDL_8, BDL_A1, BDL_BT, BDL_MADIFF, 
 // registers (delays 1, SPS/4, SPS/4, SPS/8, SPS/2 with SPS = 2 * 48000 /
 // 10500; burst_engine.hip checks them against the host tables)
 constexpr int BDL_N_S = 2, BDL_N_41 = 4, BDL_N_42 = 4, BDL_N_8 = 3, BDL_N_A1 = 6;
+// the front end's bt_d1 (one symbol, complex) in registers too
+constexpr int BDL_N_BT = 11;
 
 // double state fields
 enum BDS : int {
@@ -96,6 +100,7 @@ constexpr int M_BTD = 41;          // bt_d1.setdelay(SPS) (complex)
 constexpr int M_A1 = 21, M_D8 = 21;  // a1 / delayt8 .setdelay(SPS / 2)
 constexpr int M_DSM = 41;          // delayedsmpl.setLength(SPS)
 constexpr int M_PD1 = 5041, M_PD2 = 2521, M_PD3 = 5041;  // PeakDetector(2520, 0.1)
+static_assert(M_PD1 == M_PD3 && M_PD2 <= M_PD3, "peak detector rings (read from d3's)");
 constexpr int M_PD_MAXCD = 5040;
 constexpr int M_AGC2 = 5120;       // AGC(SPS * 128 / Fs, Fs)
 constexpr int M_MSEMA = 75;
@@ -158,7 +163,7 @@ struct BurstState {
   double *mav1;                 // [B_MA][C]
   double *dl[BDL_COUNT];        // Delay rings [size][C] (BDL_BT holds double2); MSK: bt_d1 (double2),
                                 // bt_ma_diff, a1, delayt8, delayedsmpl (double2) in slots 0-4
-  double *pd1, *pd2, *pd3;      // [len][C]
+  double *pd3;                  // [len][C] PeakDetector d3 (d1 and d2 read from it)
   double *tri;                  // [C][TRI_SLOTS][B_TRI or M_TRI] completed trident buffers
   long long *chk_n;             // [C][TRI_SLOTS] sample of each recorded check
   double *chk;                  // [C][TRI_SLOTS][CHK_REC] its decision (trident kernels)

@@ -199,8 +199,6 @@ size_t burst_layout(int kind, BurstState &S, BurstTables &T, int C, char *base, 
     for (int k = 0; k < BDL_COUNT; k++)  // sizes <= 1172 (bt_ma_diff); BDL_BT holds double2
       S.dl[k] = carve<double>(p, (size_t)(k == BDL_BT ? 2 : 1) * 1172 * C);
   }
-  S.pd1 = carve<double>(p, (size_t)(msk ? M_PD1 : B_PD1) * C);
-  S.pd2 = carve<double>(p, (size_t)(msk ? M_PD2 : B_PD2) * C);
   S.pd3 = carve<double>(p, (size_t)(msk ? M_PD3 : B_PD3) * C);
   S.tri = carve<double>(p, (size_t)TRI_SLOTS * (msk ? M_TRI : B_TRI) * C);
   S.chk_n = carve<long long>(p, (size_t)TRI_SLOTS * C);
@@ -521,9 +519,10 @@ int burst_group_create(int device, int flags, int max_channels, int kind, BurstG
     for (int q = 0; q < size; q++)
       if (io[q] != (q + 1) % size) return AERO_E_INVALID;
     if (k == BDL_BT && size <= 2) return AERO_E_INVALID;  // dly_pre2 has no newer-is-sig case
-    // the part-B delays live in registers (burst.hip): their sizes are
-    // compile-time and their weights must not depend on the write pointer
-    const int reg_n[BDL_COUNT] = {BDL_N_S, BDL_N_41, BDL_N_42, BDL_N_8, BDL_N_A1, 0, 0};
+    // the part-B delays and the front end's bt_d1 live in registers
+    // (burst.hip): their sizes are compile-time and their weights must not
+    // depend on the write pointer
+    const int reg_n[BDL_COUNT] = {BDL_N_S, BDL_N_41, BDL_N_42, BDL_N_8, BDL_N_A1, BDL_N_BT, 0};
     if (reg_n[k]) {
       if (size != reg_n[k]) return AERO_E_INVALID;
       for (int q = 1; q < size; q++)

@@ -110,12 +110,17 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
   int agc_p = is[BMI_AGC_P * C], d1_p = is[BMI_D1_P * C];
   int ma1_p = is[BMI_MA1_P * C], mav1_p = is[BMI_MAV1_P * C], madiff_p = is[BMI_MADIFF_P * C];
   int btd_p = is[BMI_BTD_P * C];
-  int pd1_p = is[BMI_PD1_P * C], pd2_p = is[BMI_PD2_P * C], pd3_p = is[BMI_PD3_P * C];
+  int pd3_p = is[BMI_PD3_P * C];
   int pd_cntdown = is[BMI_PD_CNTDOWN * C], pd_maxposcd = is[BMI_PD_MAXPOSCD * C];
   int tri_ptr = is[BMI_TRI_PTR * C];
   double *tri = S.tri + ((size_t)c * TRI_SLOTS + (chk_n & (TRI_SLOTS - 1))) * M_TRI;
   double2 *btd = reinterpret_cast<double2 *>(S.dl[0]) + c;
   double *madiff = S.dl[1] + c;
+  // both whole-sample delays read two slots per sample; the one read as
+  // "newer" is the next sample's "older" (nothing writes it in between), so
+  // it is carried in a register and each sample loads one slot per ring
+  double2 bt_older = btd[(size_t)(btd_p + 1 == M_BTD ? 0 : btd_p + 1) * C];
+  double md_older = madiff[(size_t)(madiff_p + 1 == M_MADIFF ? 0 : madiff_p + 1) * C];
   long long n = n0;
   // the analytic sample and the AGC slot it replaces are loaded one sample
   // ahead: the sample's whole chain starts from them
@@ -129,16 +134,20 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
     const int d1r = d1_p + 1 == M_D1 ? 0 : d1_p + 1;
     const int bto = btd_p + 1 == M_BTD ? 0 : btd_p + 1, btn = bto + 1 == M_BTD ? 0 : bto + 1;
     const int mdo = madiff_p + 1 == M_MADIFF ? 0 : madiff_p + 1, mdn = mdo + 1 == M_MADIFF ? 0 : mdo + 1;
-    const int p1r = pd1_p + 1 == M_PD1 ? 0 : pd1_p + 1, p2r = pd2_p + 1 == M_PD2 ? 0 : pd2_p + 1;
+    // the peak detector's d1 (same length as d3) and d2 (half) see the same
+    // values as d3, so their outputs are d3's slots: the oldest one and the
+    // one written M_PD2 - 1 updates ago
+    const int p1r = pd3_p + 1 == M_PD3 ? 0 : pd3_p + 1;
+    const int p2r = pd3_p >= M_PD2 - 1 ? pd3_p - (M_PD2 - 1) : pd3_p + M_PD3 - (M_PD2 - 1);
     const double2 a = a_n;
     const double agc_old = agc_n;
     a_n = S.ana[(size_t)((n + 1) & (ANA_LEN - 1)) * C + c];  // past the Hilbert stage's output: unused
     const double2 cvd = S.d1[(size_t)d1r * C + c];  // d1.update_dont_touch(cval)
-    const double2 bt_old = btd[(size_t)bto * C], bt_new = btd[(size_t)btn * C];
+    const double2 bt_old = bt_older, bt_new = btd[(size_t)btn * C];
     const double2 ma_old = S.ma1[(size_t)ma1_p * C + c];
     const double mv_old = S.mav1[(size_t)mav1_p * C + c];
-    const double md_old = madiff[(size_t)mdo * C], md_new = madiff[(size_t)mdn * C];
-    const double pd1_old = S.pd1[(size_t)p1r * C + c], pd2_old = S.pd2[(size_t)p2r * C + c];
+    const double md_old = md_older, md_new = madiff[(size_t)mdn * C];
+    const double pd1_old = S.pd3[(size_t)p1r * C + c], pd2_old = S.pd3[(size_t)p2r * C + c];
     double cr = a.x, ci = a.y;
     {  // agc->Update(abs(cval)); cval *= agc->AGCVal (:366-368)
       const double av = aero_hypot(cr, ci);
@@ -160,6 +169,7 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
     {  // burst-timing statistic (:376-385); bt_d1 = Delay(SPS): weights 0 / 1 (dly_int2)
       btd[(size_t)btd_p * C] = make_double2(cr, ci);
       btd_p = bto;
+      bt_older = bt_new;
       const double2 bd = make_double2(0.0 * bt_new.x + (1.0 - 0.0) * bt_old.x,
                                       0.0 * bt_new.y + (1.0 - 0.0) * bt_old.y);
       const double pr = cr * bd.x - ci * (-bd.y), pi = cr * (-bd.y) + ci * bd.x;  // cval * conj(bd)
@@ -177,6 +187,7 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
       fastarm = mav1_sum / ((double)M_MA);
       madiff[(size_t)madiff_p * C] = fastarm;  // bt_ma_diff.update(fastarm), whole-sample delay
       madiff_p = mdo;
+      md_older = md_new;
       fastarm -= (0.0 * md_new + (1.0 - 0.0) * md_old);
       if (fastarm < 0) fastarm = 0;
     }
@@ -184,14 +195,10 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
     if (bt > 500) bt = 500;
     {  // PeakDetector::update (DSP.h:491-566), setSettings(2520, 0.1)
       double val = bt;
-      S.pd3[(size_t)pd3_p * C + c] = val;
-      pd3_p = pd3_p + 1 == M_PD3 ? 0 : pd3_p + 1;
-      S.pd1[(size_t)pd1_p * C + c] = val;
-      pd1_p = p1r;
-      const double dy = val - pd1_old;
-      S.pd2[(size_t)pd2_p * C + c] = val;
-      pd2_p = p2r;
-      val = pd2_old;  // d2.update(val)
+      S.pd3[(size_t)pd3_p * C + c] = val;  // d3 (and so d1, d2)
+      pd3_p = p1r;
+      const double dy = val - pd1_old;     // d1.update_dont_touch(val)
+      val = pd2_old;                       // d2.update(val)
       if ((!pd_cntdown) && (val > 0.1) && ((pd_lastdy >= 0 && dy < 0))) {
         pd_cntdown = M_PD_MAXCD;
         pd_maxposcd = pd3_findmaxpos(S.pd3 + c, C, pd3_p, M_PD3);
@@ -233,8 +240,6 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
   is[BMI_MAV1_P * C] = mav1_p;
   is[BMI_MADIFF_P * C] = madiff_p;
   is[BMI_BTD_P * C] = btd_p;
-  is[BMI_PD1_P * C] = pd1_p;
-  is[BMI_PD2_P * C] = pd2_p;
   is[BMI_PD3_P * C] = pd3_p;
   is[BMI_PD_CNTDOWN * C] = pd_cntdown;
   is[BMI_PD_MAXPOSCD * C] = pd_maxposcd;
