@@ -59,7 +59,7 @@ using namespace aero;
 
 namespace {
 
-constexpr long long PCM_CAP = 32768;
+constexpr long long PCM_CAP = 65536;  // per-channel PCM ring: a second of 48 kHz audio per run without an early pass
 constexpr int PT_CAP = 4096;
 constexpr int HOP_CAP = 64;
 
