@@ -43,7 +43,7 @@ CXX_SRCS = ['tables_host.cpp', 'acars_host.cpp']
 # 14.8, and both strategies slow the coarse kernel, which keeps the default).
 # With the RRC partial sums on the helper wave, machine LICM's hoisted FP64
 # constants are what spills (211 SGPRs -> VGPR lanes; 15 without it):
-# 13.76 -> 12.83 ms (profiles/round4/ab_nolicm.txt).
+# 13.76 -> 12.83 ms (profiles/round4/ab/g8_licm.txt).
 FILE_FLAGS = {'burst.hip': ['-mllvm', '-disable-machine-licm'],
               'burst_msk.hip': ['-mllvm', '-disable-machine-licm'],
               'demod_oqpsk.hip': ['-mllvm', '--amdgpu-sched-strategy=max-memory-clause', '-mllvm',

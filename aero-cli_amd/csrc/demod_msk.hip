@@ -79,10 +79,14 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   constexpr double FS = (double)K::FS;
   // imaginary matched-filter partial sums: registers at 12 kHz (40 taps,
   // ~400 of the 512 registers with the real ones), LDS at 24 / 48 kHz (80 /
-  // 160 taps would not fit); at 48 kHz the oldest 100 real ones are LDS too
+  // 160 taps would not fit); at 48 kHz the oldest 100 real ones are LDS too.
+  // At 24 kHz the newest two stay in registers: 78 x 128 channels + the taps
+  // is 80.5 KB, so two workgroups (four waves) share a CU's LDS and 65536
+  // channels run in one round instead of two
   constexpr bool QREG = NT <= 40;
   constexpr int NRL = NT > 80 ? NT - 60 : 0;  // real partial sums 0..NRL-1 in LDS
-  __shared__ double s_qim[QREG ? 1 : NT][WG];
+  constexpr int NIL = QREG ? 0 : (NT == 80 ? NT - 2 : NT);  // imaginary partial sums 0..NIL-1 in LDS
+  __shared__ double s_qim[NIL > 0 ? NIL : 1][WG];
   __shared__ double s_qre[NRL > 0 ? NRL : 1][WG];
   __shared__ double s_taps[NT];
   for (int l = threadIdx.x; l < NT; l += WG) s_taps[l] = T.taps[l];
@@ -131,12 +135,12 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   long long ptn = S.ls[LS_PT_N * C + c];
 
   double qr[NT - NRL];
-  double qi[QREG ? NT : 1];
+  double qi[NT - NIL > 0 ? NT - NIL : 1];
   auto QI = [&](int j) -> double & {
-    if constexpr (QREG)
-      return qi[j];
+    if (j < NIL)
+      return s_qim[j < NIL ? j : 0][lane];
     else
-      return s_qim[j][lane];
+      return qi[j - NIL];
   };
   auto Q = [&](int j) -> double & {
     if (j < NRL)
