@@ -77,6 +77,7 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   constexpr int DTL = SPS / 2 + 1;       // dt.setLength(SPS / 2)
   constexpr int MARG = SPS;              // marg = MovingAverage(SPS)
   constexpr double FS = (double)K::FS;
+  static_assert(DSM >= 3 && D8 >= 4, "one-sample-ahead ring loads never read a slot the sample before writes");
   // imaginary matched-filter partial sums: registers at 12 kHz (40 taps,
   // ~400 of the 512 registers with the real ones), LDS at 24 / 48 kHz (80 /
   // 160 taps would not fit); at 48 kHz the oldest 100 real ones are LDS too.
@@ -164,6 +165,16 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   // at once)
   int16_t pcm_a = S.pcm[(size_t)(n0 & capm) * C + c];
   int16_t pcm_b = S.pcm[(size_t)((n0 + 1) & capm) * C + c];
+  // at 12 kHz a sample's AGC, delayedsmpl and delayt8 ring slots are loaded
+  // one sample ahead (an HBM round trip each, which the sample would
+  // otherwise wait for); none is a slot the sample before writes, and
+  // delayt8's "newer" slot is the next sample's "older".  (At 24 / 48 kHz the
+  // five extra live values spill: there they are loaded at the sample's top.)
+  constexpr bool AHEAD = QREG;
+  double agc_nx = S.agc[(size_t)(n0 % AGC) * C + c];
+  double2 dsm_nx = S.dsm[(size_t)((n0 + 1) % DSM) * C + c];
+  double d8o_nx = S.d8[(size_t)((n0 + 1) % D8) * C + c];
+  double d8n_nx = S.d8[(size_t)((n0 + 2) % D8) * C + c];
   while (i < ie) {
     bool pend = false;
     do {
@@ -174,10 +185,23 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       const int16_t xs = pcm_a;
       pcm_a = pcm_b;
       pcm_b = S.pcm[(size_t)((n + 2) & capm) * C + c];  // past the pushed samples: unused
-      const double agc_old = S.agc[(size_t)(n % AGC) * C + c];
-      const double2 dsm_old = S.dsm[(size_t)((n + 1) % DSM) * C + c];
-      const double d8_older = S.d8[(size_t)((n + 1) % D8) * C + c];
-      const double d8_newer = S.d8[(size_t)((n + 2) % D8) * C + c];
+      double agc_old, d8_older, d8_newer;
+      double2 dsm_old;
+      if constexpr (AHEAD) {
+        agc_old = agc_nx;
+        dsm_old = dsm_nx;
+        d8_older = d8o_nx;
+        d8_newer = d8n_nx;
+        agc_nx = S.agc[(size_t)((n + 1) % AGC) * C + c];
+        dsm_nx = S.dsm[(size_t)((n + 2) % DSM) * C + c];
+        d8o_nx = d8n_nx;
+        d8n_nx = S.d8[(size_t)((n + 3) % D8) * C + c];
+      } else {
+        agc_old = S.agc[(size_t)(n % AGC) * C + c];
+        dsm_old = S.dsm[(size_t)((n + 1) % DSM) * C + c];
+        d8_older = S.d8[(size_t)((n + 1) % D8) * C + c];
+        d8_newer = S.d8[(size_t)((n + 2) % D8) * C + c];
+      }
       const double dval = ((double)xs) / 32768.0;
       const double2 cm = T.cis[cis_index(m2_ptr)];
       const double cv = cm.x * dval, cvi = cm.y * dval;  // mixer2.WTCISValue() * dval
