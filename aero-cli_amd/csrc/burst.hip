@@ -219,7 +219,7 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
   int tri_ptr = is[BI_TRI_PTR * C];
   double *tri = S.tri + ((size_t)c * TRI_SLOTS + (chk_n & (TRI_SLOTS - 1))) * B_TRI;
   const DlyRef dMD = dref(T, BDL_MADIFF);
-  double md_older = dly_carry_init(S.dl[BDL_MADIFF] + c, C, dl_md, dMD);  // bt_ma_diff, carried (burst_dev.h)
+  double *mdr = S.dl[BDL_MADIFF] + c;
   // bt_d1 (a complex delay of one symbol, 11 slots) in registers: its
   // weights do not depend on the write pointer (host-checked)
   double2 *btr = reinterpret_cast<double2 *>(S.dl[BDL_BT]) + c;
@@ -231,6 +231,17 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
   // ahead: the sample's whole chain starts from them
   double2 a_n = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
   double agc_n = S.agc[(size_t)agc_p * C + c];
+  // so are the ring slots the sample reads (none is a slot the sample before
+  // writes: every ring is longer than 3); bt_ma_diff's "newer" slot is the
+  // next sample's "older"
+  auto nxt = [](int p, int len) { return p + 1 == len ? 0 : p + 1; };
+  auto pd2_slot = [](int p3) { return p3 >= B_PD2 - 1 ? p3 - (B_PD2 - 1) : p3 + B_PD3 - (B_PD2 - 1); };
+  double2 cvd_n = S.d1[(size_t)nxt(d1_p, B_D1) * C + c];
+  double2 ma_n = S.ma1[(size_t)ma1_p * C + c];
+  double mv_n = S.mav1[(size_t)mav1_p * C + c];
+  double md_older = mdr[(size_t)nxt(dl_md, dMD.size) * C];
+  double md_newer = mdr[(size_t)nxt(nxt(dl_md, dMD.size), dMD.size) * C];
+  double pd1_n = S.pd3[(size_t)nxt(pd3_p, B_PD3) * C + c], pd2_n = S.pd3[(size_t)pd2_slot(pd3_p) * C + c];
   while (n < end) {
     // every slot holds a check the demodulator has not applied: the buffer
     // this sample may start filling is one of them
@@ -238,20 +249,26 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
     // every ring slot (and Delay weight) this sample reads, loaded before any
     // of its stores so the round trips overlap; none is the slot written
     // this sample (burst_dev.h dly_pre)
-    const int d1r = d1_p + 1 == B_D1 ? 0 : d1_p + 1;
+    const int d1r = nxt(d1_p, B_D1);
     // the peak detector's d1 (same length as d3) and d2 (half) see the same
     // values as d3, so their outputs are d3's slots: the oldest one and the
     // one written B_PD2 - 1 updates ago
-    const int p1r = pd3_p + 1 == B_PD3 ? 0 : pd3_p + 1;
-    const int p2r = pd3_p >= B_PD2 - 1 ? pd3_p - (B_PD2 - 1) : pd3_p + B_PD3 - (B_PD2 - 1);
+    const int p1r = nxt(pd3_p, B_PD3);
     const double2 a = a_n;
     const double agc_old = agc_n;
+    const double2 cvd = cvd_n;  // d1.update_dont_touch(cval)
+    const double2 ma_old = ma_n;
+    const double mv_old = mv_n;
+    const double pd1_old = pd1_n, pd2_old = pd2_n;
+    const DlyPre mdp = {dMD.w[dl_md], dMD.omw[dl_md], md_older, md_newer, nxt(dl_md, dMD.size), false};
+    // the next sample's slots
     a_n = S.ana[(size_t)((n + 1) & (ANA_LEN - 1)) * C + c];  // past the Hilbert stage's output: unused
-    const double2 cvd = S.d1[(size_t)d1r * C + c];  // d1.update_dont_touch(cval)
-    const double2 ma_old = S.ma1[(size_t)ma1_p * C + c];
-    const double mv_old = S.mav1[(size_t)mav1_p * C + c];
-    const DlyPre mdp = dly_pre_carry(S.dl[BDL_MADIFF] + c, C, dl_md, dMD, md_older);
-    const double pd1_old = S.pd3[(size_t)p1r * C + c], pd2_old = S.pd3[(size_t)p2r * C + c];
+    cvd_n = S.d1[(size_t)nxt(d1r, B_D1) * C + c];
+    ma_n = S.ma1[(size_t)nxt(ma1_p, B_MA) * C + c];
+    mv_n = S.mav1[(size_t)nxt(mav1_p, B_MA) * C + c];
+    const double md_next = mdr[(size_t)nxt(nxt(mdp.next, dMD.size), dMD.size) * C];
+    pd1_n = S.pd3[(size_t)nxt(p1r, B_PD3) * C + c];
+    pd2_n = S.pd3[(size_t)pd2_slot(p1r) * C + c];
     double cr = a.x, ci = a.y;
     {  // agc.Update(|cval|); cval *= AGCVal (:316-317)
       const double av = aero_hypot(cr, ci);
@@ -285,8 +302,9 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
       S.mav1[(size_t)mav1_p * C + c] = fastarm;
       mav1_p = mav1_p + 1 == B_MA ? 0 : mav1_p + 1;
       fastarm = mav1_sum / ((double)B_MA);
-      fastarm -= dly_commit(S.dl[BDL_MADIFF] + c, C, dl_md, mdp, fastarm);
-      md_older = mdp.newer;
+      fastarm -= dly_commit(mdr, C, dl_md, mdp, fastarm);
+      md_older = md_newer;
+      md_newer = md_next;
       if (fastarm < 0) fastarm = 0;
     }
     double bt = fastarm * fastarm;

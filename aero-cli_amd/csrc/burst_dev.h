@@ -132,19 +132,6 @@ __device__ __forceinline__ double dly_commit(double *ring, int C, int &p, const 
   const double newer = r.newer_is_sig ? sig : r.newer;
   return (r.w * newer + r.om * r.older);
 }
-// dly_pre / dly_commit for a delay updated every sample, with the slot read
-// as "newer" carried into the next sample as its "older" (slot p + 2 now is
-// slot p + 1 then, and nothing writes it in between): one ring load per
-// sample instead of two.  `older` starts as ring[p + 1] (dly_carry_init);
-// rings of more than 2 slots.
-__device__ __forceinline__ double dly_carry_init(const double *ring, int C, int p, const DlyRef &d) {
-  return ring[(size_t)(p + 1 == d.size ? 0 : p + 1) * C];
-}
-__device__ __forceinline__ DlyPre dly_pre_carry(const double *ring, int C, int p, const DlyRef &d, double older) {
-  const int io = p + 1 == d.size ? 0 : p + 1, in = io + 1 == d.size ? 0 : io + 1;
-  return {d.w[p], d.omw[p], older, ring[(size_t)in * C], io, false};
-}
-
 // The demodulator's short fractional delays (sizes 2..6) held in registers,
 // h[i] = the value written i updates ago (h[0] the newest): the update
 // shifts and returns w * h[N-2] + om * h[N-1], exactly dly_commit's
