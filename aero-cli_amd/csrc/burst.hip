@@ -159,8 +159,8 @@ constexpr int BD_DCH = 8;                  // line entries read per chunk
 // of the demod loop, each wave's maximum over its lanes (the wave's time in
 // the section while the lane was in the loop), summed over waves: [0] loop
 // control, [1] message start + val_to_demod, [3] trident decision, [4] part
-// B loads + RRC, [5] PLL, rotators, AGC2, clip, [6] symbol timing + step +
-// NCOs, [7] entry + exit (state); counters summed over lanes: [8] samples
+// B loads + RRC, [5] PLL, rotators, AGC2, clip, [2] symbol timing, [6]
+// symbol step + NCOs, [7] entry + exit (state); counters summed over lanes: [8] samples
 // advanced, [10] lanes that entered the loop, [11] waves, [12] loop
 // iterations (max over the wave's lanes)
 #ifdef AERO_X_BSTAMPS
@@ -678,6 +678,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       if (so_freq < (10500.0 - 0.1)) b_set_freq(so_freq, so_step, (10500.0 - 0.1));
       if (so_freq > (10500.0 + 0.1)) b_set_freq(so_freq, so_step, (10500.0 + 0.1));
     }
+    BSTAMP(2);
     {  // IfHavePassedPoint(ee) (DSP.cpp:222-238) and the symbol step (:497-554)
       double tl = so_last - PT, tw = so_ptr - PT;
       if (tl < 0.0) tl += WTSIZE;

@@ -30,8 +30,8 @@ lib = ae.load_library()
 fn = lib.aero_x_burst_stamps
 fn.argtypes = [ctypes.c_void_p]
 out = (ctypes.c_ulonglong * 16)()
-names = ['loop control', 'part A (AGC, burst stat)', 'peak detector', 'trident store/resume', 'part B loads + RRC',
-         'PLL, rotators, AGC2', 'timing + symbol step', 'entry/exit state']
+names = ['loop control', 'val_to_demod', 'symbol timing (OQPSK)', 'trident decision', 'part B loads + RRC',
+         'PLL, rotators, AGC2', 'symbol step + NCOs', 'entry/exit state']
 
 
 def step_input(s):
