@@ -459,6 +459,14 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
   double2 m2_n = T.cis[b_cis_index(m2_ptr)];
   double2 so_n = T.cis[b_cis_index(so_ptr)];  // st_osc's entry (reloaded where the phase is set)
   double agc2_n = S.agc2[(size_t)agc2_p * C + c];
+  // the symbol-tone PLL's table entry and the msema slot an update replaces
+  // are loaded ahead too (q_ptr's entry after each NCO step, the slot after
+  // each update): with 64 channels a wave, some lane is in the PLL window or
+  // at a symbol step nearly every sample, so a load waited for there is
+  // waited for every sample
+  double2 q_n = T.cis[b_cis_index(q_ptr)];
+  double *const mm = S.msema + (size_t)c * B_MSEMA;
+  double mm_n = mm[msema_p];
   BSTAMP(7);
   while (n < end) {
     BSTAMP(0);
@@ -496,10 +504,10 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         ave_r = 1;
         ave_i = 0;
         mse = 0;
-        double *mm = S.msema + (size_t)c * B_MSEMA;
         for (int k = 0; k < B_MSEMA; k++) mm[k] = 0;
         msema_sum = 0;
         msema_p = 0;
+        mm_n = 0;
       }
       if (trace && hop_n < S.hop_cap) {
         double *h = S.hops + ((size_t)c * S.hop_cap + hop_n) * 6;
@@ -611,7 +619,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       ave_r = ave_r * 0.95 + 0.05 * str_r;
       ave_i = ave_i * 0.95 + 0.05 * str_i;
       const double spi2 = dly_reg(hA1, wA1, oA1, spr);
-      const double2 qv = T.cis[b_cis_index(q_ptr)];
+      const double2 qv = q_n;
       const double er_r = qv.x * spr - qv.y * (-spi2), er_i = qv.x * (-spi2) + qv.y * spr;
       double st_err = aero_atan2(er_i, er_r);
       st_err *= 1.5 * (1.0 - progress * progress);
@@ -688,7 +696,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         const double pt_this = 1.0 - pt_last;
         const double ptr_ = pt_this * s2r + pt_last * s2l_r, pti = pt_this * s2i + pt_last * s2l_i;
         const double twospeed =
-            -4.0 * ((fmod((360.0 * q_ptr / ((double)WTSIZE)) * 2.0 + (360.0 * 0.4 * 0.5), 360.0) / 360.0) -
+            -4.0 * ((b_fmod360((360.0 * q_ptr / ((double)WTSIZE)) * 2.0 + (360.0 * 0.4 * 0.5)) / 360.0) -
                     (0.34046 + 0.4111 * 0.4));
         const bool even = !(twospeed < 0);
         yui++;
@@ -723,11 +731,11 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
           if (cntr > ((128 + 10) * SPS)) {  // msema.Update (DSP.cpp:405-416)
             const double tda = (fabs(qr) - 1.0), tdb = (fabs(qi) - 1.0);
             const double v = (tda * tda) + (tdb * tdb);
-            double *mm = S.msema + (size_t)c * B_MSEMA;
-            msema_sum = msema_sum - mm[msema_p];
+            msema_sum = msema_sum - mm_n;
             msema_sum = msema_sum + fabs(v);
             mm[msema_p] = fabs(v);
             msema_p = msema_p + 1 == B_MSEMA ? 0 : msema_p + 1;
+            mm_n = mm[msema_p];  // written B_MSEMA updates ago
             mse = msema_sum / ((double)B_MSEMA);
           }
           if (startstop > 0) {
@@ -739,16 +747,19 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
             ibit = b_qround(0.75 * qr * 127.0 + 128.0);
             if (ibit > 255) ibit = 255;
             if (ibit < 0) ibit = 0;
-            soft[sp & (B_SOFT_RING - 1)] = (int16_t)ibit;
+            // RxDataBits emitted or dropped as a group (:548-551): the group's
+            // last entry carries the mark in the same store
+            const long long sp1 = sp;
             sp++;
-            if (sp - scommit >= 32) {  // RxDataBits emitted or dropped as a group (:548-551)
+            if (sp - scommit >= 32) {
               if (mse < 0.6 || lastmse < 0.6) {
-                soft[(sp - 1) & (B_SOFT_RING - 1)] |= B_SOFT_LAST;
+                ibit |= B_SOFT_LAST;
                 scommit = sp;
               } else {
                 sp = scommit;
               }
             }
+            soft[sp1 & (B_SOFT_RING - 1)] = (int16_t)ibit;
           }
         }
       }
@@ -761,6 +772,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     b_nco_next(so_ptr, so_step);
     so_n = T.cis[b_cis_index(so_ptr)];
     b_nco_next(q_ptr, q_step);
+    q_n = T.cis[b_cis_index(q_ptr)];
     n++;
     BSTAMP(6);
   }

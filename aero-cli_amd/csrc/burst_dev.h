@@ -33,8 +33,20 @@ __device__ __forceinline__ void b_set_freq(double &freq, double &step, double f)
   step = (freq) * ((double)WTSIZE) / 48000.0;
 }
 
+// fmod(x, 360.0) for the phases of the per-sample path: for 0 <= x < 1800
+// by repeated subtraction, which is exact there (x and 360 are multiples of
+// ulp(x), and each difference is no larger than x) and so equals fmod's
+// exact remainder; otherwise fmod itself
+__device__ __forceinline__ double b_fmod360(double x) {
+  if (x >= 0.0 && x < 1800.0) {
+    while (x >= 360.0) x -= 360.0;
+    return x;
+  }
+  return fmod(x, 360.0);
+}
+
 __device__ __forceinline__ void b_set_phase_deg(double &ptr, double phase_deg) {  // SetPhaseDeg (DSP.cpp:177-187)
-  phase_deg = fmod(phase_deg, 360.0);
+  phase_deg = b_fmod360(phase_deg);
   while (phase_deg < 0) phase_deg += 360.0;
   ptr = (phase_deg / 360.0) * ((double)WTSIZE);
 }

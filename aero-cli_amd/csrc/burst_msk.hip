@@ -309,6 +309,11 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
   double2 m2_n = T.cis[b_cis_index(m2_ptr)];
   double2 so_n = T.cis[b_cis_index(so_ptr)];  // st_osc's entry (reloaded where the phase is set)
   double agc2_n = S.agc2[(size_t)agc2_p * C + c];
+  // the symbol-tone PLL's table entry and the msema slot an update replaces,
+  // ahead as well (see demod_burst_kernel)
+  double2 h_n = T.cis[b_cis_index(sh_ptr)];
+  double *const mm = S.msema + (size_t)c * M_MSEMA;
+  double mm_n = mm[msema_p];
   while (n < end) {
     if (sp - scons > B_SOFT_RING - 64) break;  // soft ring full: framing frees it next
     // val_to_demod = d2.update_dont_touch(...): the front end's value M_D2 - 1 samples ago (zeros before)
@@ -342,10 +347,10 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         soft[sp & (B_SOFT_RING - 1)] = B_SOFT_MARK;  // start of burst
         sp++;
         mse = 0;
-        double *mm = S.msema + (size_t)c * M_MSEMA;
         for (int k = 0; k < M_MSEMA; k++) mm[k] = 0;
         msema_sum = 0;
         msema_p = 0;
+        mm_n = 0;
         ave_r = 1;
         ave_i = 0;
         str_r = 1;
@@ -358,6 +363,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         b_set_phase_deg(so_ptr, 0);
         so_n = T.cis[b_cis_index(so_ptr)];
         b_set_phase_deg(sh_ptr, 0);
+        h_n = T.cis[b_cis_index(sh_ptr)];
       }
       if (trace && hop_n < S.hop_cap) {
         double *h = S.hops + ((size_t)c * S.hop_cap + hop_n) * 6;
@@ -451,7 +457,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         double progress = (double)cntr - (MSPS * (M_START));
         const double goal = M_ENDROT - (MSPS * M_START);
         progress = progress / goal;
-        const double2 hv = T.cis[b_cis_index(sh_ptr)];
+        const double2 hv = h_n;
         const double er_r = hv.x * spr - hv.y * (-spi2), er_i = hv.x * (-spi2) + hv.y * spr;
         double st_err = aero_atan2(er_i, er_r);
         st_err *= 0.5 * (1.0 - progress * progress);
@@ -544,11 +550,11 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
             const double tda = (fabs(s2r * 0.75) - 1.0);
             const double tdb = (fabs(pdi * 0.75) - 1.0);
             const double v = (tda * tda) + (tdb * tdb);
-            double *mm = S.msema + (size_t)c * M_MSEMA;
-            msema_sum = msema_sum - mm[msema_p];
+            msema_sum = msema_sum - mm_n;
             msema_sum = msema_sum + fabs(v);
             mm[msema_p] = fabs(v);
             msema_p = msema_p + 1 == M_MSEMA ? 0 : msema_p + 1;
+            mm_n = mm[msema_p];  // written M_MSEMA updates ago
             mse = msema_sum / ((double)M_MSEMA);
           }
           {  // differential soft bits, imag first, real negated (:664-686)
@@ -563,12 +569,15 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
             ibit = b_qround((real) * 127.0 + 128.0);
             if (ibit > 255) ibit = 255;
             if (ibit < 0) ibit = 0;
-            soft[sp & (B_SOFT_RING - 1)] = (int16_t)ibit;
+            // emit processDemodulatedSoftBits (:689-692): the group's last
+            // entry carries the mark in the same store
+            const long long sp1 = sp;
             sp++;
-          }
-          if (sp - scommit >= M_SOFT_GROUP) {  // emit processDemodulatedSoftBits (:689-692)
-            soft[(sp - 1) & (B_SOFT_RING - 1)] |= B_SOFT_LAST;
-            scommit = sp;
+            if (sp - scommit >= M_SOFT_GROUP) {
+              ibit |= B_SOFT_LAST;
+              scommit = sp;
+            }
+            soft[sp1 & (B_SOFT_RING - 1)] = (int16_t)ibit;
           }
         }
       }
@@ -576,6 +585,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       b_nco_next(so_ptr, so_step);
       so_n = T.cis[b_cis_index(so_ptr)];
       b_nco_next(sh_ptr, sh_step);
+      h_n = T.cis[b_cis_index(sh_ptr)];
       b_nco_next(m2_ptr, m2_step);
       m2_n = T.cis[b_cis_index(m2_ptr)];
     }
