@@ -241,23 +241,28 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   __syncthreads();
   double2 x[16];
   const long long s0 = nk - (N - 1);  // sample of snapshot element 0 (oqpskdemodulator.cpp:359-365)
+  // every element's table entry is gathered before any is waited for (the
+  // compiler would otherwise sink each gather into its element's branch
+  // and wait for it there: 16 round trips one after another)
+  double2 cs[16];
+  double dval[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int j = bitrev<L>(epos<L, 0>(t, i));
-    const long long s = s0 + j;
+    const int q = (int)((s0 + bitrev<L>(epos<L, 0>(t, i))) & (N - 1));
+    const uint32_t w = ring_lds[q + (q >> 4)];
+    dval[i] = ((double)(int16_t)(w >> 16)) / 32768.0;
+    cs[i] = T.cis[w & 0xFFFF];
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(cs[i].x), "+v"(cs[i].y));
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
     // entries below zero_before were cleared (AFC, CenterFreqChangedSlot);
     // entries of samples before the channel's first are the ring's own
     // contents (zero for a new channel: CIS[0] x 0; a channel that changed
     // rate keeps the ring it had, mskdemodulator.cpp:94-218)
-    if (s < zero_before) {
-      x[i] = make_double2(0.0, 0.0);
-    } else {
-      const int q = (int)(s & (N - 1));
-      const uint32_t w = ring_lds[q + (q >> 4)];
-      const double dval = ((double)(int16_t)(w >> 16)) / 32768.0;
-      const double2 cs = T.cis[w & 0xFFFF];
-      x[i] = make_double2(cs.x * dval, cs.y * dval);
-    }
+    const long long s = s0 + bitrev<L>(epos<L, 0>(t, i));
+    x[i] = s < zero_before ? make_double2(0.0, 0.0) : make_double2(cs[i].x * dval[i], cs[i].y * dval[i]);
   }
   __syncthreads();  // the ring image is read: the LDS is the transforms' from here on
   CSTAMP(0);
