@@ -22,6 +22,7 @@ AERO_E_HIP = -3
 AERO_E_NOGPU = -4
 AERO_E_FULL = -5
 AERO_E_RATE = -6
+AERO_E_DEVICE = -7
 
 F_TRACE_PT = 0x1
 F_TRACE_BLOCKS = 0x2

@@ -116,7 +116,7 @@ def build_fftsim():
 
 def build_mathhost():
     src = os.path.join(ROOT, 'tools', 'mathhost.cpp')
-    deps = [src, os.path.join(CSRC, 'aero_math.h'), os.path.join(CSRC, 'aero_math_tables.h')]
+    deps = [src, os.path.join(CSRC, 'aero_math.h'), os.path.join(CSRC, 'aero_glibc_tables.h')]
     if _stale(MATHHOST_SO, deps):
         _run(['g++', '-O2', '-std=c++17', '-fPIC', '-shared', '-ffp-contract=off', '-o', MATHHOST_SO, src, '-lm'])
     return MATHHOST_SO
@@ -186,8 +186,18 @@ def build_all(jobs=4):
     build_mathhost()
     build_fftsim()
     so = build_engine(jobs)
+    build_diag(jobs)
     build_host(jobs)
     return so
+
+
+# Diagnostic builds the GPU tests load (never the product): the demod's wave
+# hand-off broken on purpose (tests/test_gpu_handoff.py)
+DIAG_VARIANTS = {'handoff_fail': ['AERO_X_HANDOFF_FAIL']}
+
+
+def build_diag(jobs=4):
+    return [build_engine(jobs, variant=v, defines=d) for v, d in DIAG_VARIANTS.items()]
 
 
 if __name__ == '__main__':

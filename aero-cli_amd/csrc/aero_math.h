@@ -1,21 +1,25 @@
 /*
- * aero_math.h — the libm the demod kernels call, bit-compatible with the
- * host glibc 2.35 that the reference links (the decode/ sources call std::abs on
- * complex (-> hypot), std::arg (-> atan2), tanh, sin, cos, log10).
+ * aero_math.h — the libm the demod kernels call, bit-for-bit the glibc 2.35
+ * that the reference links, as an x86-64 host with FMA + AVX2 resolves it
+ * (the decode/ sources call std::abs on complex -> hypot, std::arg -> atan2,
+ * tanh, cos/sin pairs -> sincos, std::exp(i x) -> cexp -> sincos, log10).
  *
  * Compiles for host (g++/hipcc host pass) and device (gfx950).  Every file
- * that includes it must be built with -ffp-contract=off; the only fused
- * operations are the explicit fma() calls of the double-double helpers,
- * which are exact by construction.
+ * that includes it must be built with -ffp-contract=off: the fused
+ * multiply-adds are the explicit fma() calls, placed exactly where glibc's
+ * FMA build has a vfmadd (atan2, log) and nowhere else (sincos, hypot,
+ * tanh are glibc's SSE2 code, no fusion).  Constants and tables come from
+ * the host libm itself (aero_glibc_tables.h, tools/gen_glibc_tables.cpp).
  *
- *  aero_hypot  : glibc 2.35 dbl-64 e_hypot.c algorithm (non-FMA kernel) ->
- *                bit-exact with glibc (tests/test_math.py, 2e7 samples).
- *  aero_tanh   : fdlibm s_tanh.c on glibc's s_expm1.c (Estrin-form
- *                polynomial) -> bit-exact with glibc.
- *  aero_atan2, aero_sin, aero_cos, aero_log10 : correctly rounded via
- *                double-double evaluation (~2^-100 relative); glibc's own
- *                results are correctly rounded in all but rare cases, the
- *                measured agreement is recorded by tests/test_math.py.
+ *  aero_hypot  : glibc 2.35 dbl-64 e_hypot.c (non-FMA kernel)
+ *  aero_tanh   : fdlibm s_tanh.c on glibc's s_expm1.c (Estrin-form polynomial)
+ *  aero_sincos : glibc s_sincos.c with s_sin.c's do_sin / do_cos /
+ *                reduce_sincos (SSE2 build, the only sincos in 2.35's libm)
+ *  aero_atan2  : __atan2_fma (e_atan2.c without its removed slow paths)
+ *  aero_log    : __log_fma (e_log.c, ARM optimized-routines log, 128-entry
+ *                table), aero_log10 the e_log10.c wrapper around it
+ * tests/test_math_host.py checks every one bitwise against the host glibc;
+ * tests/test_gpu_math.py checks the device build against the host build.
  */
 #pragma once
 #include <stdint.h>
@@ -30,7 +34,7 @@
 #define AERO_TABLE_DECL static constexpr
 #endif
 
-#include "aero_math_tables.h"
+#include "aero_glibc_tables.h"
 
 namespace aero {
 
@@ -190,456 +194,332 @@ AERO_HD double aero_tanh(double x) {
   return (jx >= 0) ? z : -z;
 }
 
-/* ---------------------------------------------------- double-double */
-struct dd {
-  double hi, lo;
-};
-AERO_HD dd two_sum(double a, double b) {
-  double s = a + b;
-  double bb = s - a;
-  double e = (a - (s - bb)) + (b - bb);
-  return {s, e};
-}
-AERO_HD dd quick_two_sum(double a, double b) {
-  double s = a + b;
-  return {s, b - (s - a)};
-}
-AERO_HD dd two_prod(double a, double b) {
-  double p = a * b;
-  return {p, fma(a, b, -p)};
-}
-AERO_HD dd dd_add(dd a, dd b) {
-  dd s = two_sum(a.hi, b.hi);
-  dd t = two_sum(a.lo, b.lo);
-  s.lo += t.hi;
-  s = quick_two_sum(s.hi, s.lo);
-  s.lo += t.lo;
-  return quick_two_sum(s.hi, s.lo);
-}
-AERO_HD dd dd_neg(dd a) { return {-a.hi, -a.lo}; }
-AERO_HD dd dd_mul(dd a, dd b) {
-  dd p = two_prod(a.hi, b.hi);
-  p.lo += a.hi * b.lo + a.lo * b.hi;
-  return quick_two_sum(p.hi, p.lo);
-}
-AERO_HD dd dd_mul_d(dd a, double b) {
-  dd p = two_prod(a.hi, b);
-  p.lo += a.lo * b;
-  return quick_two_sum(p.hi, p.lo);
-}
-AERO_HD dd dd_div(dd a, dd b) {
-  double q1 = a.hi / b.hi;
-  dd r = dd_add(a, dd_neg(dd_mul_d(b, q1)));
-  double q2 = r.hi / b.hi;
-  r = dd_add(r, dd_neg(dd_mul_d(b, q2)));
-  double q3 = r.hi / b.hi;
-  dd q = quick_two_sum(q1, q2);
-  return dd_add(q, dd{q3, 0.0});
+/* ------------------------------------------------------------ sincos
+ * glibc 2.35 sincos (sysdeps/ieee754/dbl-64/s_sincos.c + the do_sin /
+ * do_cos / reduce_sincos helpers of s_sin.c), SSE2 build: libm.so.6's
+ * `sincos` is not an ifunc in 2.35, so every host runs this code.  Read
+ * from its disassembly; the operation order below is the instructions'.
+ * |x| >= 105414350 would need __branred (not restated: the demods' arguments
+ * are loop corrections and averaged phase errors, |x| < 2*pi); NaN there. */
+AERO_HD double g_tab(int k) { return aero_g_sincostab[k]; }
+
+/* TAYLOR_SIN(xx, a, da) */
+AERO_HD double g_taylor_sin(double xx, double a, double da) {
+  double p = AERO_G_S5 * xx + AERO_G_S4;
+  p = p * xx - AERO_G_NS3;
+  p = p * xx + AERO_G_S2;
+  p = p * xx - AERO_G_NS1;
+  const double t = (p * a - AERO_G_CS2 * da) * xx + da;
+  return t + a;
 }
 
-/* atan(t), t = th + tl in [0, 1], returned as double-double */
-AERO_HD dd dd_atan01(double th, double tl) {
-  int k = (int)(th * 64.0 + 0.5);
-  double c = (double)k * (1.0 / 64.0);
-  dd num = two_sum(th - c, tl);              // th - c is exact (Sterbenz)
-  dd den = dd_add(dd{1.0, 0.0}, dd_mul_d(dd{th, tl}, c));
-  dd u = dd_div(num, den);                   // |u| <= 2^-7
-  dd u2 = dd_mul(u, u);
-  dd u3 = dd_mul(u2, u);
-  dd u5 = dd_mul(u3, u2);
-  double v = u2.hi;
-  // tail: -u^7/7 + u^9/9 - ... + u^17/17 in double
-  double tail = -1.0 / 7 + v * (1.0 / 9 + v * (-1.0 / 11 + v * (1.0 / 13 + v * (-1.0 / 15 + v * (1.0 / 17)))));
-  tail = tail * (u5.hi * v);
-  dd r = dd_add(u, dd_mul(u3, dd{-AERO_INV3_HI, -AERO_INV3_LO}));
-  r = dd_add(r, dd_mul(u5, dd{AERO_INV5_HI, AERO_INV5_LO}));
-  r = dd_add(r, dd{tail, 0.0});
-  return dd_add(dd{aero_atan_tab[k][0], aero_atan_tab[k][1]}, r);
+AERO_HD double g_do_sin(double x, double dx) {
+  if (__builtin_fabs(x) < 0.126) return g_taylor_sin(x * x, x, dx);
+  const double xold = x;
+  if (x <= 0) dx = -dx;
+  const double u = AERO_G_BIG + __builtin_fabs(x);
+  x = __builtin_fabs(x) - (u - AERO_G_BIG);
+  const double xx = x * x;
+  const double s = x + (dx + (x * xx) * (xx * AERO_G_SN5 - AERO_G_NSN3));
+  const double c = x * dx + xx * ((xx * AERO_G_CS6 - AERO_G_NCS4) * xx + AERO_G_CS2);
+  const int k = (int)(low(u) << 2);
+  const double sn = g_tab(k), ssn = g_tab(k + 1), cs = g_tab(k + 2), ccs = g_tab(k + 3);
+  const double cor = (ssn + s * ccs - sn * c) + cs * s;
+  return __builtin_copysign(sn + cor, xold);
 }
 
-AERO_HD double aero_atan2_dd(double y, double x) {
-  if (__builtin_isnan(x) || __builtin_isnan(y)) return x + y;
-  bool ny = __builtin_signbit(y) != 0, nx = __builtin_signbit(x) != 0;
-  double ay = __builtin_fabs(y), ax = __builtin_fabs(x);
-  if (ay == 0.0) {
-    if (!nx) return y;  // +-0
-    return ny ? -AERO_PI_HI : AERO_PI_HI;
-  }
-  if (ax == 0.0) return ny ? -AERO_PI_2_HI : AERO_PI_2_HI;
-  if (__builtin_isinf(ax)) {
-    if (__builtin_isinf(ay)) {
-      double r = nx ? 3.0 * AERO_PI_4_HI : AERO_PI_4_HI;
-      return ny ? -r : r;
-    }
-    double r = nx ? AERO_PI_HI : 0.0;
-    return ny ? -r : r;
-  }
-  if (__builtin_isinf(ay)) return ny ? -AERO_PI_2_HI : AERO_PI_2_HI;
-  bool swap = ay > ax;
-  double a = swap ? ax : ay, b = swap ? ay : ax;
-  // scale to keep the residual computation away from under/overflow
-  const int eb = (int)((hiw(b) >> 20) & 0x7ff) - 1023;
-  if (eb > 500) {  // only the ratio matters: scale by powers of two (exact)
-    a *= 0x1p-600;
-    b *= 0x1p-600;
-  } else if (eb < -500) {
-    a *= 0x1p600;
-    b *= 0x1p600;
-  }
-  double th = a / b;
-  if (th < 0x1p-1000) {
-    // tiny ratio: atan(t) = t to double precision
-    double r = th;
-    dd res = swap ? dd_add(dd{AERO_PI_2_HI, AERO_PI_2_LO}, dd{-r, 0.0}) : dd{r, 0.0};
-    if (nx) res = dd_add(dd{AERO_PI_HI, AERO_PI_LO}, dd_neg(res));
-    double out = res.hi + res.lo;
-    return ny ? -out : out;
-  }
-  double tl = fma(-th, b, a) / b;
-  dd r = dd_atan01(th, tl);
-  if (swap) r = dd_add(dd{AERO_PI_2_HI, AERO_PI_2_LO}, dd_neg(r));
-  if (nx) r = dd_add(dd{AERO_PI_HI, AERO_PI_LO}, dd_neg(r));
-  double out = r.hi + r.lo;
-  return ny ? -out : out;
+AERO_HD double g_do_cos(double x, double dx) {
+  if (x < 0) dx = -dx;
+  const double u = AERO_G_BIG + __builtin_fabs(x);
+  x = __builtin_fabs(x) - (u - AERO_G_BIG) + dx;
+  const double xx = x * x;
+  const double s = x + (x * xx) * (xx * AERO_G_SN5 - AERO_G_NSN3);
+  const double c = xx * ((xx * AERO_G_CS6 - AERO_G_NCS4) * xx + AERO_G_CS2);
+  const int k = (int)(low(u) << 2);
+  const double sn = g_tab(k), ssn = g_tab(k + 1), cs = g_tab(k + 2), ccs = g_tab(k + 3);
+  const double cor = (ccs - s * ssn - cs * c) - sn * s;
+  return cs + cor;
 }
 
-/* reciprocal to ~2^-100 relative after two Newton steps (device: v_rcp_f64) */
-AERO_HD double approx_rcp(double b) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  double r = __builtin_amdgcn_rcp(b);
-#else
-  double r = 1.0 / b;
-#endif
-  r = fma(r, fma(-b, r, 1.0), r);
-  r = fma(r, fma(-b, r, 1.0), r);
-  return r;
-}
-
-/* atan2 fast path (Ziv): atan(t) = atan(k/64) + atan(u) evaluated to about
- * 2^-65 relative without any IEEE division, returned only when that bound
- * proves the rounding; otherwise (≈2^-10 of arguments, and every special or
- * extreme-exponent argument) the double-double path decides.  Same results
- * as aero_atan2_dd by construction (tests/test_math_host.py compares them).
- * The quadrant (pi/2 - r when |y| > |x|, pi - r when x < 0) is folded into
- * one table row, C + s atan(k/64) in double-double, so the result is
- * B + s (u + corr) with a single two_sum, and the series runs in fused
- * Horner form (both only tighten the bound the rounding test assumes). */
-AERO_HD double aero_atan2(double y, double x) {
-  const double ay = __builtin_fabs(y), ax = __builtin_fabs(x);
-  if (!(ax >= 0x1p-500 && ax <= 0x1p500 && ay >= 0x1p-500 && ay <= 0x1p500)) return aero_atan2_dd(y, x);
-  const bool swap = ay > ax;
-  const double a = swap ? ax : ay, b = swap ? ay : ax;  // t = a/b in (0, 1]
-  const double rb = approx_rcp(b);
-  const double th = a * rb;
-  const double tl = fma(-th, b, a) * rb;
-  const int k = (int)(th * 64.0 + 0.5);
-  const double c = (double)k * (1.0 / 64.0);
-  // u = (t - c) / (1 + t c), |u| <= 2^-7
-  const dd num = two_sum(th - c, tl);  // th - c exact (Sterbenz)
-  const double ph = th * c, pl = fma(th, c, -ph);
-  const dd den0 = quick_two_sum(1.0, ph);  // ph = t c <= 1
-  const double dh = den0.hi, dl = den0.lo + (pl + tl * c);
-  const double rd = approx_rcp(dh);
-  const double uh = num.hi * rd;
-  const double ul = ((fma(-uh, dh, num.hi) + num.lo) - uh * dl) * rd;
-  // atan(u) - u = u^3 (-1/3 + u^2/5 - ...) - u^2 ul
-  const double v = uh * uh;
-  double p = fma(v, -1.0 / 15, 1.0 / 13);
-  p = fma(v, p, -1.0 / 11);
-  p = fma(v, p, 1.0 / 9);
-  p = fma(v, p, -1.0 / 7);
-  p = fma(v, p, 1.0 / 5);
-  p = fma(v, p, -AERO_INV3_HI);
-  const double corr = fma(v * uh, p, -v * ul);
-  // atan2 = C + s (A + u + corr): (C, s) = (0, 1), (pi/2, -1), (pi, -1),
-  // (pi/2, 1) for q = swap | 2 (x < 0); the row holds C + s A
-  const int q = (swap ? 1 : 0) | (__builtin_signbit(x) ? 2 : 0);
-  const double sg = (q == 1 || q == 2) ? -1.0 : 1.0;
-  const int row = q * 65 + k;
-  dd r = two_sum(aero_atan2_quad_tab[row][0], sg * uh);
-  r.lo += aero_atan2_quad_tab[row][1] + sg * (ul + corr);
-  r = quick_two_sum(r.hi, r.lo);
-  const double e = 0x1p-63 * __builtin_fabs(r.hi);
-  const double out = r.hi + r.lo;
-  if (out != r.hi + (r.lo + e) || out != r.hi + (r.lo - e)) return aero_atan2_dd(y, x);
-  return __builtin_signbit(y) ? -out : out;
-}
-
-/* sin/cos of r = rh + rl, |r| <= pi/4 + eps, as double-double */
-AERO_HD void dd_sincos_small(double rh, double rl, dd &s, dd &c, bool want_s, bool want_c) {
-  double ar = __builtin_fabs(rh);
-  int k = (int)(ar * 64.0 + 0.5);
-  if (k > 52) k = 52;
-  double kc = (double)k * (1.0 / 64.0);
-  double sgn = rh < 0 ? -1.0 : 1.0;
-  // d = |r| - k/64
-  dd d = two_sum(ar - kc, sgn * rl);
-  dd d2 = dd_mul(d, d);
-  double v = d2.hi;
-  // sin(d) = d - d^3/6 + d^5/120 - [d^7/5040 - d^9/9! + d^11/11!]
-  dd d3 = dd_mul(d2, d);
-  dd d5 = dd_mul(d3, d2);
-  double st = (-1.0 / 5040 + v * (1.0 / 362880 + v * (-1.0 / 39916800))) * (d5.hi * v);
-  dd sd = dd_add(d, dd_mul(d3, dd{-AERO_INV6_HI, -AERO_INV6_LO}));
-  sd = dd_add(sd, dd_mul(d5, dd{AERO_INV120_HI, AERO_INV120_LO}));
-  sd = dd_add(sd, dd{st, 0.0});
-  // cos(d) = 1 - d^2/2 + d^4/24 - [d^6/720 - d^8/8! + d^10/10!]
-  dd d4 = dd_mul(d2, d2);
-  double ct = (-1.0 / 720 + v * (1.0 / 40320 + v * (-1.0 / 3628800))) * (d4.hi * v);
-  dd cd = dd_add(dd{1.0, 0.0}, dd_mul_d(d2, -0.5));
-  cd = dd_add(cd, dd_mul(d4, dd{AERO_INV24_HI, AERO_INV24_LO}));
-  cd = dd_add(cd, dd{ct, 0.0});
-  dd sk = {aero_sin_tab[k][0], aero_sin_tab[k][1]};
-  dd ck = {aero_cos_tab[k][0], aero_cos_tab[k][1]};
-  if (want_s) {
-    // sin(|r|) = sin(k)cos(d) + cos(k)sin(d)
-    s = dd_add(dd_mul(sk, cd), dd_mul(ck, sd));
-    if (sgn < 0) s = dd_neg(s);
-  }
-  if (want_c) c = dd_add(dd_mul(ck, cd), dd_neg(dd_mul(sk, sd)));
-}
-
-/* x = n*pi/2 + r (Cody-Waite, fdlibm split constants); valid for |x| < 2^20.
- * aero_sin/aero_cos/aero_sincos return NaN outside that domain (the demod's
- * argument is a moving average of clipped loop errors, |x| <= pi/2). */
-AERO_HD int reduce_pio2(double x, double &rh, double &rl) {
-  const double pio2_1 = 1.57079632673412561417e+00, pio2_2 = 6.07710050630396597660e-11,
-               pio2_3 = 2.02226624871116645580e-21, pio2_3t = 8.47842766036889956997e-32;
-  if (__builtin_fabs(x) <= AERO_PI_4_HI) {
-    rh = x;
-    rl = 0.0;
-    return 0;
-  }
-  double fn = __builtin_rint(x * AERO_2_PI_HI);
-  int n = (int)fn;
-  double r = x - fn * pio2_1;  // exact
-  double w = fn * pio2_2;      // exact for |n| < 2^20
-  dd t = two_sum(r, -w);
-  dd u = two_sum(t.hi, -fn * pio2_3);
-  u.lo += t.lo - fn * pio2_3t;
-  dd res = quick_two_sum(u.hi, u.lo);
-  rh = res.hi;
-  rl = res.lo;
+AERO_HD int g_reduce_sincos(double x, double &a, double &da) {
+  const double t = x * AERO_G_HPINV + AERO_G_TOINT;
+  const double xn = t - AERO_G_TOINT;
+  const double y = (x - xn * AERO_G_MP1) - xn * AERO_G_MP2;
+  const int n = (int)(low(t) & 3);
+  double t1 = xn * AERO_G_PP3;
+  const double t2 = y - t1;
+  double db = (y - t2) - t1;
+  t1 = xn * AERO_G_PP4;
+  const double b = t2 - t1;
+  db += (t2 - b) - t1;
+  a = b;
+  da = db;
   return n;
 }
 
-AERO_HD double aero_sin(double x) {
-  if (!__builtin_isfinite(x)) return x - x;
-  if (__builtin_fabs(x) >= 0x1p20) return __builtin_nan("");
-  if (__builtin_fabs(x) < 0x1p-26) return x;
-  double rh, rl;
-  int n = reduce_pio2(x, rh, rl);
-  dd s, c;
-  if (n & 1)
-    dd_sincos_small(rh, rl, s, c, false, true);
-  else
-    dd_sincos_small(rh, rl, s, c, true, false);
-  double out;
-  switch (n & 3) {
-    case 0: out = s.hi + s.lo; break;
-    case 1: out = c.hi + c.lo; break;
-    case 2: out = -(s.hi + s.lo); break;
-    default: out = -(c.hi + c.lo); break;
-  }
-  return out;
-}
-
-AERO_HD double aero_cos(double x) {
-  if (!__builtin_isfinite(x)) return x - x;
-  if (__builtin_fabs(x) >= 0x1p20) return __builtin_nan("");
-  if (__builtin_fabs(x) < 0x1p-27) return 1.0;
-  double rh, rl;
-  int n = reduce_pio2(x, rh, rl);
-  dd s, c;
-  if (n & 1)
-    dd_sincos_small(rh, rl, s, c, true, false);
-  else
-    dd_sincos_small(rh, rl, s, c, false, true);
-  double out;
-  switch (n & 3) {
-    case 0: out = c.hi + c.lo; break;
-    case 1: out = -(s.hi + s.lo); break;
-    case 2: out = -(c.hi + c.lo); break;
-    default: out = s.hi + s.lo; break;
-  }
-  return out;
-}
-
-/* sin and cos of x together (one reduction, one table lookup); the same
- * correctly-rounded results as aero_sin / aero_cos */
-AERO_HD void aero_sincos_dd(double x, double &so, double &co) {
-  if (!__builtin_isfinite(x) || __builtin_fabs(x) >= 0x1p20) {
-    so = co = __builtin_nan("");
-    return;
-  }
-  double rh, rl;
-  int n = reduce_pio2(x, rh, rl);
-  dd s, c;
-  dd_sincos_small(rh, rl, s, c, true, true);
-  const double sv = s.hi + s.lo, cv = c.hi + c.lo;
-  switch (n & 3) {
-    case 0: so = sv; co = cv; break;
-    case 1: so = cv; co = -sv; break;
-    case 2: so = -sv; co = -cv; break;
-    default: so = -cv; co = sv; break;
-  }
-  if (__builtin_fabs(x) < 0x1p-26) so = x;
-  if (__builtin_fabs(x) < 0x1p-27) co = 1.0;
-}
-
-/* sincos fast path (Ziv) for 2^-26 <= |x| <= 1/4, the demods' usual loop
- * corrections.  Taylor series around 0 with the terms that matter at 2^-70
- * kept exact or in double-double: x^2 exact by fma, x^3/6 and x^5/120 (sin),
- * x^2/2 and x^4/24 (cos) as double-double products, the rest (|.| <= 2^-24
- * |x| for sin, 2^-21 for cos) in double; their sum carries at most ~2^-72
- * relative error, so when hi + (lo +- 2^-69 |hi|) round alike, hi + lo is the
- * correctly rounded value (aero_sincos_dd's result).  Otherwise (and outside
- * the range) the double-double path decides.  No IEEE division. */
 AERO_HD void aero_sincos(double x, double &so, double &co) {
-  const double ax = __builtin_fabs(x);
-  if (!(ax >= 0x1p-26 && ax <= 0.25)) {
-    aero_sincos_dd(x, so, co);
+  const uint32_t k = hiw(x) & 0x7fffffffu;
+  if (k < 0x400368fdu) {
+    if (k < 0x3e400000u) {
+      so = x;
+      co = 1.0;
+    } else if (k < 0x3feb6000u) {
+      so = g_do_sin(x, 0.0);
+      co = g_do_cos(x, 0.0);
+    } else {
+      const double y = AERO_G_HPI - __builtin_fabs(x);
+      const double a = y + AERO_G_HP1;
+      const double da = (y - a) + AERO_G_HP1;
+      so = __builtin_copysign(g_do_cos(a, da), x);
+      co = g_do_sin(a, da);
+    }
     return;
   }
-  const double x2 = ax * ax, x2l = fma(ax, ax, -x2);  // x^2 = x2 + x2l exactly
-  // sin |x| = |x| - x^3/6 + x^5/120 + x^7 P(x^2)
-  const double x3 = ax * x2, x3l = fma(ax, x2, -x3) + ax * x2l;
-  const double t3 = x3 * -AERO_INV6_HI, t3l = fma(x3, -AERO_INV6_HI, -t3) + (x3 * -AERO_INV6_LO + x3l * -AERO_INV6_HI);
-  const double x5 = x3 * x2, x5l = fma(x3, x2, -x5) + (x3 * x2l + x3l * x2);
-  const double t5 = x5 * AERO_INV120_HI, t5l = fma(x5, AERO_INV120_HI, -t5) + (x5 * AERO_INV120_LO + x5l * AERO_INV120_HI);
-  double p = fma(x2, 1.0 / 355687428096000.0, -1.0 / 1307674368000.0);
-  p = fma(x2, p, 1.0 / 6227020800.0);
-  p = fma(x2, p, -1.0 / 39916800.0);
-  p = fma(x2, p, 1.0 / 362880.0);
-  p = fma(x2, p, -1.0 / 5040.0);
-  const double r7 = (x5 * x2) * p;
-  const dd sa = two_sum(ax, t3);
-  const dd sb = two_sum(sa.hi, t5);
-  const double slo = (sa.lo + sb.lo) + ((t3l + t5l) + r7);
-  // cos x = 1 - x^2/2 + x^4/24 + x^6 Q(x^2)
-  const double h = 0.5 * x2, hl = 0.5 * x2l;  // exact
-  const double x4 = x2 * x2, x4l = fma(x2, x2, -x4) + 2.0 * (x2 * x2l);
-  const double t4 = x4 * AERO_INV24_HI, t4l = fma(x4, AERO_INV24_HI, -t4) + (x4 * AERO_INV24_LO + x4l * AERO_INV24_HI);
-  double q = fma(x2, 1.0 / 20922789888000.0, -1.0 / 87178291200.0);
-  q = fma(x2, q, 1.0 / 479001600.0);
-  q = fma(x2, q, -1.0 / 3628800.0);
-  q = fma(x2, q, 1.0 / 40320.0);
-  q = fma(x2, q, -1.0 / 720.0);
-  const double r6 = (x4 * x2) * q;
-  const dd ca = two_sum(1.0, -h);
-  const dd cb = two_sum(ca.hi, t4);
-  const double clo = (ca.lo + cb.lo) + ((t4l - hl) + r6);
-  const double sv = sb.hi + slo, cv = cb.hi + clo;
-  const double es = 0x1p-69 * sb.hi, ec = 0x1p-69 * cb.hi;
-  if (sv != sb.hi + (slo + es) || sv != sb.hi + (slo - es) || cv != cb.hi + (clo + ec) ||
-      cv != cb.hi + (clo - ec)) {
-    aero_sincos_dd(x, so, co);
+  if (k < 0x7ff00000u) {
+    if (k >= 0x419921fbu) {  // __branred range, not restated (header)
+      so = co = __builtin_nan("");
+      return;
+    }
+    double a, da;
+    const int n = g_reduce_sincos(x, a, da);
+    if ((unsigned)(n - 1) <= 1u) {
+      a = -a;
+      da = -da;
+    }
+    const double s = g_do_sin(a, da);
+    double c = g_do_cos(a, da);
+    if (n & 2) c = -c;
+    if (n & 1) {
+      so = c;
+      co = s;
+    } else {
+      so = s;
+      co = c;
+    }
     return;
   }
-  so = __builtin_signbit(x) ? -sv : sv;
-  co = cv;
+  so = co = x / x;
 }
 
-/* natural log of m in [1, 2) as double-double */
-AERO_HD dd dd_log12(double m) {
-  int k = (int)((m - 1.0) * 64.0 + 0.5);
-  double c = 1.0 + (double)k * (1.0 / 64.0);
-  // log(m/c) = 2 atanh(u), u = (m - c)/(m + c)
-  dd num = {m - c, 0.0};               // exact (Sterbenz)
-  dd den = two_sum(m, c);
-  dd u = dd_div(num, den);             // |u| <= 2^-8
-  dd u2 = dd_mul(u, u);
-  dd u3 = dd_mul(u2, u);
-  dd u5 = dd_mul(u3, u2);
-  double v = u2.hi;
-  double tail = (1.0 / 7 + v * (1.0 / 9 + v * (1.0 / 11 + v * (1.0 / 13)))) * (u5.hi * v);
-  dd r = dd_add(u, dd_mul(u3, dd{AERO_INV3_HI, AERO_INV3_LO}));
-  r = dd_add(r, dd_mul(u5, dd{AERO_INV5_HI, AERO_INV5_LO}));
-  r = dd_add(r, dd{tail, 0.0});
-  r = dd_mul_d(r, 2.0);
-  return dd_add(dd{aero_log_tab[k][0], aero_log_tab[k][1]}, r);
+AERO_HD double aero_sin(double x) {
+  double s, c;
+  aero_sincos(x, s, c);
+  return s;
+}
+AERO_HD double aero_cos(double x) {
+  double s, c;
+  aero_sincos(x, s, c);
+  return c;
 }
 
-/* correctly rounded natural log, double-double evaluation */
-AERO_HD double aero_log_dd(double x) {
-  if (!(x > 0.0) || !__builtin_isfinite(x)) {
-    if (x == 0.0) return -__builtin_inf();
-    if (x < 0.0 || __builtin_isnan(x)) return (x - x) / (x - x);
-    return x;  // +inf
+/* ------------------------------------------------------------- atan2
+ * glibc 2.35 __atan2_fma (sysdeps/ieee754/dbl-64/e_atan2.c built with
+ * -mfma -mavx2, the ifunc target on FMA + AVX2 hosts; the multi-precision
+ * slow paths were removed before 2.35).  Restated from its disassembly:
+ * every fma() below is a vfmadd/vfmsub/vfnmadd there, every other product
+ * and sum a separate rounding.  The x87-free SET_RESTORE_ROUND has no effect
+ * in round-to-nearest. */
+AERO_HD double g_atan2_poly(double v) {  // d3 + v (d5 + v (d7 + v (d9 + v (d11 + v d13))))
+  double p = fma(v, AERO_G_D13, AERO_G_D11);
+  p = fma(v, p, AERO_G_D9);
+  p = fma(v, p, AERO_G_D7);
+  p = fma(v, p, AERO_G_D5);
+  return fma(v, p, AERO_G_D3);
+}
+AERO_HD int g_atan2_row(double u) { return (int)(fma(u, AERO_G_TWO8, AERO_G_TWO52) - AERO_G_TWO52) - 16; }
+AERO_HD double g_atan2_tail(const double *c, double v) {  // c2 + v (c3 + v (c4 + v (c5 + v c6)))
+  double p = fma(v, c[6], c[5]);
+  p = fma(v, p, c[4]);
+  p = fma(v, p, c[3]);
+  return fma(v, p, c[2]);
+}
+
+AERO_HD double aero_atan2(double y, double x) {
+  const uint32_t ux = hiw(x), dx = low(x), uy = hiw(y), dy = low(y);
+  if ((ux & 0x7ff00000u) == 0x7ff00000u && ((ux & 0xfffffu) | dx) != 0) return x + y;
+  if ((uy & 0x7ff00000u) == 0x7ff00000u && ((uy & 0xfffffu) | dy) != 0) return y + y;
+  if (uy == 0 && dy == 0) return ((int32_t)ux < 0) ? AERO_G_OPI : 0.0;
+  if (uy == 0x80000000u && dy == 0) return ((int32_t)ux < 0) ? AERO_G_MOPI : -0.0;
+  if (x == 0) return ((int32_t)uy < 0) ? AERO_G_MHPI : AERO_G_HPI;
+  bool special = true;  // the infinite cases; a y with dy != 0 there is a NaN (above)
+  if (ux == 0x7ff00000u && dx == 0) {
+    if (uy == 0x7ff00000u) {
+      if (dy == 0) return AERO_G_QPI;
+    } else if (uy == 0xfff00000u) {
+      if (dy == 0) return AERO_G_MQPI;
+    } else {
+      return ((int32_t)uy < 0) ? -0.0 : 0.0;
+    }
+    special = false;
+  } else if (ux == 0xfff00000u && dx == 0) {
+    if (uy == 0x7ff00000u) {
+      if (dy == 0) return AERO_G_TQPI;
+    } else if (uy == 0xfff00000u) {
+      if (dy == 0) return AERO_G_MTQPI;
+    } else {
+      return ((int32_t)uy < 0) ? AERO_G_MOPI : AERO_G_OPI;
+    }
+    special = false;
   }
-  uint64_t u = d2u(x);
-  int e = (int)((u >> 52) & 0x7ff);
-  int k = 0;
-  if (e == 0) {  // subnormal
-    x *= 0x1p54;
-    u = d2u(x);
-    e = (int)((u >> 52) & 0x7ff);
-    k = -54;
+  if (special) {
+    if (uy == 0x7ff00000u) {
+      if (dy == 0) return AERO_G_HPI;
+    } else if (uy == 0xfff00000u && dy == 0) {
+      return AERO_G_MHPI;
+    }
   }
-  k += e - 1023;
-  double m = u2d((u & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL);
-  dd lm = dd_log12(m);
-  dd r = dd_add(dd_mul_d(dd{AERO_LN2_HI, AERO_LN2_LO}, (double)k), lm);
-  return r.hi + r.lo;
+
+  double ax = x < 0 ? -x : x, ay = y < 0 ? -y : y;
+  const int32_t de = (int32_t)((uy & 0x7ff00000u) - (ux & 0x7ff00000u));
+  if (de >= 59768832) return (0 < y) ? AERO_G_HPI : AERO_G_MHPI;
+  if (de <= -59768832) {
+    if (!(x > 0)) return (0 < y) ? AERO_G_OPI : AERO_G_MOPI;
+    return __builtin_copysign(ay / ax, y);
+  }
+  if (ax < AERO_G_TWOM500 || ay < AERO_G_TWOM500) {
+    ax *= AERO_G_TWO500;
+    ay *= AERO_G_TWO500;
+  }
+  if (ax > AERO_G_TWO500 || ay > AERO_G_TWO500) {
+    ax *= AERO_G_TWOM500;
+    ay *= AERO_G_TWOM500;
+  }
+  double u, du;
+  if (ax > ay) {
+    u = ay / ax;
+    const double v = ax * u, vv = fma(ax, u, -v);
+    du = ((ay - v) - vv) / ax;
+  } else {
+    u = ax / ay;
+    const double v = ay * u, vv = fma(ay, u, -v);
+    du = ((ax - v) - vv) / ay;
+  }
+  double z;
+  if (x > 0) {
+    if (ax > ay) {  // atan(u)
+      if (u < AERO_G_INV16) {
+        const double v = u * u;
+        const double zz = fma(u * v, g_atan2_poly(v), du);
+        return __builtin_copysign(u + zz, y);
+      }
+      const double *c = aero_g_cij[g_atan2_row(u)];
+      const double t3 = u - c[0];
+      const double v = t3 + du;
+      const double dv = (__builtin_fabs(t3) > __builtin_fabs(du)) ? ((t3 - v) + du) : ((du - v) + t3);
+      double p = fma(v, c[6], c[5]);
+      p = fma(v, p, c[4]);
+      p = fma(v, p, c[3]);
+      const double zz = fma(v, c[2], fma(dv, c[2], (v * v) * p));
+      return __builtin_copysign(zz + c[1], y);
+    }
+    // pi/2 - atan(u)
+    if (u < AERO_G_INV16) {
+      const double v = u * u;
+      const double zz = (u * v) * g_atan2_poly(v);
+      const double t = AERO_G_HPI - u;
+      const double cor = (AERO_G_HPI > __builtin_fabs(u)) ? ((AERO_G_HPI - t) - u) : (AERO_G_HPI - (u + t));
+      z = (((cor + AERO_G_HPI1) - du) - zz) + t;
+    } else {
+      const double *c = aero_g_cij[g_atan2_row(u)];
+      const double v = (u - c[0]) + du;
+      z = (AERO_G_HPI - c[1]) + fma(-v, g_atan2_tail(c, v), AERO_G_HPI1);
+    }
+    return __builtin_copysign(__builtin_fabs(z), y);
+  }
+  if (ay > ax) {  // pi/2 + atan(u)
+    if (u < AERO_G_INV16) {
+      const double v = u * u;
+      const double t = u + AERO_G_HPI;
+      const double zz = (v * u) * g_atan2_poly(v);
+      const double cor = (AERO_G_HPI > __builtin_fabs(u)) ? ((AERO_G_HPI - t) + u) : ((u - t) + AERO_G_HPI);
+      z = (((cor + AERO_G_HPI1) + du) + zz) + t;
+    } else {
+      const double *c = aero_g_cij[g_atan2_row(u)];
+      const double v = (u - c[0]) + du;
+      z = (AERO_G_HPI + c[1]) + fma(v, g_atan2_tail(c, v), AERO_G_HPI1);
+    }
+  } else {  // pi - atan(u)
+    if (u < AERO_G_INV16) {
+      const double v = u * u;
+      const double zz = (v * u) * g_atan2_poly(v);
+      const double t = AERO_G_OPI - u;
+      const double cor = (AERO_G_OPI > __builtin_fabs(u)) ? ((AERO_G_OPI - t) - u) : (AERO_G_OPI - (t + u));
+      z = (((cor + AERO_G_OPI1) - du) - zz) + t;
+    } else {
+      const double *c = aero_g_cij[g_atan2_row(u)];
+      const double v = (u - c[0]) + du;
+      z = (AERO_G_OPI - c[1]) + fma(-v, g_atan2_tail(c, v), AERO_G_OPI1);
+    }
+  }
+  return __builtin_copysign(__builtin_fabs(z), y);
 }
 
-/* log fast path (Ziv): log(x) = k ln2 + log(c) + 2 atanh(u), u = (m-c)/(m+c),
- * evaluated to about 2^-66 without IEEE division; returned only when that
- * bound proves the rounding, otherwise aero_log_dd decides (same results). */
+/* --------------------------------------------------------------- log
+ * glibc 2.35 __log_fma (sysdeps/ieee754/dbl-64/e_log.c built with -mfma
+ * -mavx2: r = fma(z, invc, -1) and GCC's contractions, read from its
+ * disassembly), the ifunc target the log10 wrapper calls on FMA hosts. */
 AERO_HD double aero_log(double x) {
-  if (!(x >= 0x1p-1000 && x <= 0x1p1000)) return aero_log_dd(x);
-  const uint64_t ux = d2u(x);
-  const int k = (int)((ux >> 52) & 0x7ff) - 1023;
-  const double m = u2d((ux & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL);
-  const int j = (int)((m - 1.0) * 64.0 + 0.5);
-  const double c = 1.0 + (double)j * (1.0 / 64.0);
-  const double nh = m - c;                 // exact (Sterbenz)
-  const dd den = two_sum(m, c);
-  const double rd = approx_rcp(den.hi);
-  const double uh = nh * rd;               // |u| <= 2^-8
-  const double ul = (fma(-uh, den.hi, nh) - uh * den.lo) * rd;
-  const double v = uh * uh;
-  double p = 1.0 / 13;
-  p = 1.0 / 11 + v * p;
-  p = 1.0 / 9 + v * p;
-  p = 1.0 / 7 + v * p;
-  p = 1.0 / 5 + v * p;
-  p = AERO_INV3_HI + v * p;
-  const double corr = 2.0 * ((v * uh) * p + v * ul);  // 2 atanh(u) - 2u
-  // log(c) + 2u + corr + k ln2
-  dd r = two_sum(aero_log_tab[j][0], 2.0 * uh);
-  r.lo += aero_log_tab[j][1] + (2.0 * ul + corr);
-  r = quick_two_sum(r.hi, r.lo);
-  if (k) r = dd_add(dd_mul_d(dd{AERO_LN2_HI, AERO_LN2_LO}, (double)k), r);
-  const double e = 0x1p-63 * __builtin_fabs(r.hi);
-  const double out = r.hi + r.lo;
-  if (out != r.hi + (r.lo + e) || out != r.hi + (r.lo - e)) return aero_log_dd(x);
-  return out;
+  const uint64_t ix = d2u(x);
+  const uint32_t top = (uint32_t)(ix >> 48);
+  if (ix - 0x3fee000000000000ULL < 0x3090000000000ULL) {  // |x - 1| < 0x1p-4 (LO..HI)
+    if (ix == 0x3ff0000000000000ULL) return 0.0;
+    const double *B = aero_g_log_poly1;
+    const double r = x - 1.0;
+    const double r2 = r * r, r3 = r * r2;
+    double p9 = fma(r3, B[10], fma(r2, B[9], fma(r, B[8], B[7])));
+    p9 = fma(p9, r3, fma(r2, B[6], fma(r, B[5], B[4])));
+    const double p = fma(p9, r3, fma(r2, B[3], fma(r, B[2], B[1])));
+    const double rhi = fma(-AERO_G_TWO27, r, fma(r, AERO_G_TWO27, r));
+    const double rlo = r - rhi;
+    const double hi = fma(rhi * rhi, B[0], r);
+    double lo = fma(rhi * rhi, B[0], r - hi);
+    lo = fma(B[0] * rlo, r + rhi, lo);
+    return hi + fma(p, r3, lo);
+  }
+  uint64_t jx = ix;
+  if (top - 0x0010u >= 0x7ff0u - 0x0010u) {
+    if ((ix << 1) == 0) return -1.0 / 0.0;  // __math_divzero
+    if (ix == 0x7ff0000000000000ULL) return x;
+    if ((top & 0x8000u) || (top & 0x7ff0u) == 0x7ff0u) return (x - x) / (x - x);  // __math_invalid
+    jx = d2u(x * 0x1p52) - (52ULL << 52);
+  }
+  const uint64_t tmp = jx - 0x3fe6000000000000ULL;
+  const int i = (int)((tmp >> 45) & 127);
+  const int k = (int)((int64_t)tmp >> 52);
+  const double z = u2d(jx - (tmp & (0xfffULL << 52)));
+  const double invc = aero_g_log_tab[i][0], logc = aero_g_log_tab[i][1];
+  const double r = fma(z, invc, -1.0);
+  const double kd = (double)k;
+  const double w = fma(kd, AERO_G_LN2HI, logc);
+  const double hi = w + r;
+  const double lo = fma(kd, AERO_G_LN2LO, (w - hi) + r);
+  const double r2 = r * r;
+  const double *A = aero_g_log_poly;
+  const double q = fma(fma(r, A[4], A[3]), r2, fma(r, A[2], A[1]));
+  return fma(r * r2, q, fma(r2, A[0], lo)) + hi;
 }
 
+/* log10 (e_log10.c, __log10_finite: SSE2, no fusion) around __log_fma */
 AERO_HD double aero_log10(double x) {
-  const double two54 = 1.80143985094819840000e+16, ivln10 = 4.34294481903251816668e-01,
-               log10_2hi = 3.01029995663611771306e-01, log10_2lo = 3.69423907715893078616e-13;
-  double y, z;
-  int32_t i, k, hx;
-  hx = (int32_t)hiw(x);
-  uint32_t lx = low(x);
-  k = 0;
-  if (hx < 0x00100000) {
-    if (((hx & 0x7fffffff) | (int32_t)lx) == 0) return -two54 / __builtin_fabs(x);
-    if (hx < 0) return (x - x) / (x - x);
-    k -= 54;
+  const double two54 = 0x1p54;
+  int64_t ix = (int64_t)d2u(x);
+  int64_t k;
+  if (ix > 0x000fffffffffffffLL) {
+    k = -1023;
+  } else {
+    if ((ix & 0x7fffffffffffffffLL) == 0) return -two54 / __builtin_fabs(x);
+    if (ix < 0) return (x - x) / (x - x);
     x *= two54;
-    hx = (int32_t)hiw(x);
+    ix = (int64_t)d2u(x);
+    k = -1023 - 54;
   }
-  if (hx >= 0x7ff00000) return x + x;
-  k += (hx >> 20) - 1023;
-  i = (int32_t)(((uint32_t)k & 0x80000000u) >> 31);
-  hx = (hx & 0x000fffff) | ((0x3ff - i) << 20);
-  y = (double)(k + i);
-  x = sethi(x, (uint32_t)hx);
-  z = y * log10_2lo + ivln10 * aero_log(x);
-  return z + y * log10_2hi;
+  if ((uint64_t)ix > 0x7fefffffffffffffULL) return x + x;
+  k += ix >> 52;
+  const int64_t i = (int64_t)((uint64_t)k >> 63);
+  const double y = (double)(k + i);
+  x = u2d((uint64_t)(ix & 0x000fffffffffffffLL) | ((uint64_t)(0x3ff - i) << 52));
+  const double z = y * AERO_G_LOG10_2LO + aero_log(x) * AERO_G_IVLN10;
+  return z + y * AERO_G_LOG10_2HI;
 }
 
 }  // namespace aero

@@ -141,8 +141,20 @@ constexpr int RING_GROUP = 8;
 // chain -> FIR sequence word: iterations published, | CSEQ_DONE at the end
 constexpr int CSEQ_DONE = 1 << 30;
 // a wait that never ends (a broken hand-off) gives up after ~2^24 polls
-// (about a second) instead of hanging the GPU; the parity tests then fail
+// (about a second) instead of hanging the GPU, and raises the group's device
+// error word: aero_run then fails with AERO_E_DEVICE instead of delivering
+// the garbage the run produced.  AERO_X_HANDOFF_FAIL (diagnostic build only,
+// tests/test_gpu_handoff.py) breaks the hand-off on purpose: the FIR waves
+// return at once and the chain waves' wait gives up after 2^12 polls.
+#ifdef AERO_X_HANDOFF_FAIL
+constexpr int SPIN_LIMIT = 1 << 12;
+#else
 constexpr int SPIN_LIMIT = 1 << 24;
+#endif
+
+__device__ __forceinline__ void raise_device_error(const DevState &S, int code) {
+  if (S.err) __hip_atomic_store(S.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // LDS ordering between the two waves of a pair: every LDS access issued
 // before this has completed (the workgroup-scope release of the AMDGPU memory
@@ -227,12 +239,16 @@ __device__ __forceinline__ void demod_fir_wave(const DevState &S, DemodShared &s
     for (int j = NIL; j < NTAPS - 1; ++j) qi[j] = fir[(size_t)(NTAPS + j) * C];
   }
   const unsigned long long vmask = __ballot(valid);
+#ifdef AERO_X_HANDOFF_FAIL
+  return;
+#endif
   for (int it = 0;; ++it) {
     int cs;
     for (int spin = 0;; ++spin) {
       cs = __builtin_amdgcn_readfirstlane(lds_load(&sh.cseq[wv]));
       if ((cs & (CSEQ_DONE - 1)) > it || (cs & CSEQ_DONE)) break;
       if (spin > SPIN_LIMIT) {
+        raise_device_error(S, DERR_HANDOFF);
         cs = CSEQ_DONE;
         break;
       }
@@ -421,6 +437,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       // the FIR wave's progress and R_53(n-1) (its iteration it - 1), read
       // first so their LDS latency passes while this sample is mixed
       const int fsv = lds_load(&sh.fseq[wv]);
+      lds_acquire();  // the R_53 read below stays after the sequence-word read
       double2 r53 = sh.r53[(it & 1) ^ 1][pair];
       const int16_t xs = pcm_next;
       pcm_next = pcm_next2;
@@ -460,6 +477,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
         if (it > 0 && __builtin_amdgcn_readfirstlane(fsv) < it) {  // rare: the FIR wave is behind
           for (int spin = 0; __builtin_amdgcn_readfirstlane(lds_load(&sh.fseq[wv])) < it; ++spin) {
             if (spin > spin_left) {  // broken hand-off: stop waiting for good
+              if (spin_left) raise_device_error(S, DERR_HANDOFF);
               spin_left = 0;
               break;
             }

@@ -210,6 +210,9 @@ struct Group {
   JobSlot slot[NSLOT];
   std::deque<int> pending_slots;
   int next_slot = 0, max_jobs_seen = 0;
+  // device-error word (DevState::err): mapped pinned, set by a kernel that
+  // gave up, checked by the host whenever a pass's slot completes
+  int *h_err = nullptr, *h_err_dev = nullptr;
   // pinned staging for host->device counters and PCM (reused once its event completed)
   static constexpr int NPIN = 4;
   long long *pin_avail[NPIN] = {};
@@ -431,6 +434,9 @@ int process_slot(Group *e, int si) {
   auto &sl = e->slot[si];
   const int C = e->C, nch = e->nch;
   const int njobs = *sl.h_n;
+  // the slot's event follows this pass's demod: a hand-off that gave up in
+  // it (or earlier) is visible now; the outputs of such a run are garbage
+  if (*(volatile int *)e->h_err) return AERO_E_DEVICE;
   e->max_jobs_seen = std::max(e->max_jobs_seen, njobs);
   HOST_TIMER(e, "host_frames");
   e->hpool->wait();  // previous slot's frames first (per-channel order)
@@ -929,6 +935,10 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
   HIPCHK(hipMemset(e->pool, 0, bytes));
   layout(e->S, e->T, mode, e->C, e->flags, reinterpret_cast<char *>(e->pool));
   HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
+  if (hipHostMalloc(&e->h_err, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return AERO_E_NOMEM;
+  *e->h_err = 0;
+  HIPCHK(hipHostGetDevicePointer((void **)&e->h_err_dev, e->h_err, 0));
+  e->S.err = e->h_err_dev;
   for (auto &sl : e->slot) {
     if (hipMalloc(&sl.d_n, 64) != hipSuccess) return AERO_E_NOMEM;
     // kernel-written zero-copy buffers: mapped (a device address for the
@@ -1025,6 +1035,7 @@ void group_destroy(Group *e) {
     if (sl.h_n) (void)hipHostFree(sl.h_n);
     if (sl.ev) (void)hipEventDestroy(sl.ev);
   }
+  if (e->h_err) (void)hipHostFree(e->h_err);
   for (int k = 0; k < Group::NPIN; k++) {
     if (e->pin_avail[k]) (void)hipHostFree(e->pin_avail[k]);
     if (e->pin_ev[k]) (void)hipEventDestroy(e->pin_ev[k]);
@@ -1457,6 +1468,7 @@ const char *aero_strerror(int rc) {
     case AERO_E_NOGPU: return "no usable gfx950 device";
     case AERO_E_FULL: return "channel table or ring full";
     case AERO_E_RATE: return "sample rate mismatch";
+    case AERO_E_DEVICE: return "device error: a demod wave hand-off timed out (outputs invalid)";
     default: return "unknown error";
   }
 }

@@ -206,6 +206,10 @@ struct DevState {
   uint8_t *jobout;         // [C][JOB_OUT] (the Viterbi writes it in pinned host memory)
   int *njobs_host;         // [1] pinned host copy of the job count, written by the Viterbi kernel
   uint8_t *blocks_dbg;     // [C][2500] decoded bits (trace)
+  int *err;                // [1] mapped pinned device-error word (DERR_*), sticky; read by the host
 };
+
+// device error codes (DevState::err)
+constexpr int DERR_HANDOFF = 1;  // a demod wave pair's LDS hand-off timed out
 
 }  // namespace aero

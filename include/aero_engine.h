@@ -29,6 +29,7 @@ extern "C" {
 #define AERO_E_NOGPU (-4)      /* no gfx950 device / kernels not loadable  */
 #define AERO_E_FULL (-5)       /* channel table or PCM ring full           */
 #define AERO_E_RATE (-6)       /* sample rate differs from the channel's   */
+#define AERO_E_DEVICE (-7)     /* a kernel gave up (wave hand-off timeout): the run's outputs are invalid */
 
 /* engine flags */
 #define AERO_F_TRACE_PT 0x1    /* keep the rotated pt_qpsk trace (parity tests)      */

@@ -19,16 +19,10 @@
  *     + ISUData / ParserISU / ACARSDefragmenter (decode/aerol.cpp:8-524)
  *
  * Every transcendental call goes to the host glibc (2.35) exactly as the
- * reference does (std::abs(complex) -> hypot, std::arg -> atan2, tanh, sin,
- * cos, log10, std::exp(complex) -> cexp).  Compile with -ffp-contract=off.
- *
- * Built with -DORACLE_CR_LIBM (liboracle_cr.so) the per-sample atan2, sin,
- * cos, log10 and cexp(i x) calls (the `olm` wrappers below) are correctly
- * rounded instead (aero_math.h, the functions the kernels call; glibc's
- * results differ from them by 1 ulp on ~0.1% of arguments,
- * tests/test_math_host.py).  That build separates the algorithm's parity
- * (bit for bit) from glibc's rounding at the scale where the latter shows
- * (tests/test_gpu_fullscale.py).  Tables are glibc-computed in both builds.
+ * reference does (std::abs(complex) -> hypot, std::arg -> atan2, tanh,
+ * cos(x)/sin(x) of one argument -> sincos (GCC merges the pair at -O2, as in
+ * the reference's own build), log10, std::exp(complex) -> cexp -> sincos).
+ * Compile with -ffp-contract=off.
  *
  * PARITY STATUS.  The reference cannot be built in this container under the
  * round rules (it needs the QtCore library, moc-generated code and the
@@ -61,31 +55,18 @@
 #include <string>
 #include <vector>
 
-#ifdef ORACLE_CR_LIBM
-#include "aero_math.h"
-#endif
-
 namespace {
 
 typedef std::complex<double> cpx;
 const int WTSIZE = 19999;
 
-// the libm calls of the per-sample loops (header comment: ORACLE_CR_LIBM)
+// the libm calls of the per-sample loops, as the reference makes them
 namespace olm {
-#ifdef ORACLE_CR_LIBM
-double sin(double x) { return aero::aero_sin(x); }
-double cos(double x) { return aero::aero_cos(x); }
-double log10(double x) { return aero::aero_log10(x); }
-double arg(cpx z) { return aero::aero_atan2(z.imag(), z.real()); }
-// std::exp(i x) = cexp(+-0 + i x) = (cos x, sin x): glibc multiplies by exp(+-0) = 1
-cpx expi(cpx z) { return cpx(aero::aero_cos(z.imag()), aero::aero_sin(z.imag())); }
-#else
 double sin(double x) { return ::sin(x); }
 double cos(double x) { return ::cos(x); }
 double log10(double x) { return ::log10(x); }
 double arg(cpx z) { return std::arg(z); }
 cpx expi(cpx z) { return std::exp(z); }
-#endif
 }  // namespace olm
 
 /* ---------------------------------------------------------------- tables */

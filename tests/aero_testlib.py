@@ -13,8 +13,6 @@ if PKG not in sys.path:
     sys.path.insert(0, PKG)
 
 ORACLE_SO = os.path.join(ROOT, 'oracle', 'liboracle.so')
-# the same oracle with correctly rounded per-sample libm calls (aero_oracle.cpp: ORACLE_CR_LIBM)
-ORACLE_CR_SO = os.path.join(ROOT, 'oracle', 'liboracle_cr.so')
 SYNTH_SO = os.path.join(ROOT, 'tools', 'libaero_synth.so')
 
 
@@ -139,15 +137,13 @@ def synth_burst_msk(seconds=10.0, bitrate=1200, seed=0xAE70, carrier=2500.0, ebn
 
 
 class Oracle:
-    """One reference channel (a whole `aero-decode -b <bitrate>` instance).
-    cr=True: the build whose per-sample atan2/sin/cos/log10/cexp are
-    correctly rounded (the kernels' libm) instead of glibc's."""
+    """One reference channel (a whole `aero-decode -b <bitrate>` instance)."""
     _libs = {}
 
     @classmethod
-    def lib(cls, cr=False):
-        if cr not in cls._libs:
-            L = ctypes.CDLL(ORACLE_CR_SO if cr else ORACLE_SO)
+    def lib(cls):
+        if 'L' not in cls._libs:
+            L = ctypes.CDLL(ORACLE_SO)
             L.oracle_create.restype = ctypes.c_void_p
             L.oracle_create.argtypes = [ctypes.c_int, ctypes.c_int]
             L.oracle_destroy.argtypes = [ctypes.c_void_p]
@@ -179,11 +175,11 @@ class Oracle:
             L.oracle_events.restype = ctypes.c_size_t
             L.oracle_events.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_void_p,
                                         ctypes.c_size_t]
-            cls._libs[cr] = L
-        return cls._libs[cr]
+            cls._libs['L'] = L
+        return cls._libs['L']
 
-    def __init__(self, trace_pt=False, bitrate=10500, burst=False, cr=False):
-        self.L = self.lib(cr)
+    def __init__(self, trace_pt=False, bitrate=10500, burst=False):
+        self.L = self.lib()
         self.bitrate = bitrate
         self.h = self.L.oracle_create(bitrate, (1 if trace_pt else 0) | (2 if burst else 0))
         assert self.h, 'oracle_create(%d) failed' % bitrate

@@ -7,8 +7,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, 'tools', 'libaero_mathhost.so')
 FN = {'hypot': 0, 'atan2': 1, 'tanh': 2, 'sin': 3, 'cos': 4, 'log10': 5, 'sqrt': 6, 'fmod360': 7, 'div': 8,
-      'sincos_s': 9, 'sincos_c': 10, 'atan2_dd': 11, 'log': 12, 'log_dd': 13,
-      'sincos_dd_s': 14, 'sincos_dd_c': 15}
+      'sincos_s': 9, 'sincos_c': 10, 'log': 12, 'glibc_sin': 13, 'glibc_cos': 14}
 _lib = None
 
 

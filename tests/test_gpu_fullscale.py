@@ -11,15 +11,10 @@ ACARS items.  Traces are kept for the sampled channels only
 (aero_trace_select).  Reference: OqpskDemodulator::writeData
 (decode/oqpskdemodulator.cpp:284-560) and the AeroL path after it.
 
-Two oracles.  The kernels' atan2/sin/cos/log10 are correctly rounded and
-glibc's are not always (1 ulp on ~0.1% of arguments, test_math_host.py): at
-this scale one sampled channel's rotated pt_qpsk differs from the glibc
-oracle by 1 ulp at 7 of 28,672 symbols, and its MSEcalc average, recorded
-in the hop records, by a few ulps from hop 55 on.  So the engine is held bit
-for bit to the oracle built with those calls correctly rounded
-(liboracle_cr.so: every output incl. the f64 hop records), and to the glibc
-oracle on the decoded outputs (soft bits, frames, items, hop decisions and
-frequencies) with the MSE column within 1e-12 relative."""
+The kernels' libm is glibc 2.35's, restated instruction for instruction
+(aero_math.h: __atan2_fma, __log_fma, sincos, hypot, tanh; bitwise in
+test_math_host.py), so every output is held bit for bit to the glibc
+oracle, the f64 hop records (frequency, MSE averages) included."""
 import concurrent.futures as cf
 import os
 import sys
@@ -43,8 +38,8 @@ def _pool(length):
         return np.stack(list(ex.map(lambda k: bench.synth_one(M, length / 48000.0, 0xAE20 + k, k), range(P))))
 
 
-def _oracle(pcm, cr):
-    o = tl.Oracle(cr=cr)
+def _oracle(pcm):
+    o = tl.Oracle()
     o.push_chunked(pcm, HOP)
     return o.softbits(), o.hops(), o.frames(), o.item_lines('A')
 
@@ -81,25 +76,14 @@ def test_fullscale_sample_matches_oracle(engine_lib):
     eng.close()
     wins = {c: pool_host[c % P, int(offsets[c // P]):int(offsets[c // P]) + span] for c in sel}
     with cf.ThreadPoolExecutor(max_workers=16) as ex:
-        refs_cr = dict(zip(sel, ex.map(lambda c: _oracle(wins[c], True), sel)))
-        refs = dict(zip(sel, ex.map(lambda c: _oracle(wins[c], False), sel)))
+        refs = dict(zip(sel, ex.map(lambda c: _oracle(wins[c]), sel)))
     assert total > C, 'the batch decoded %d frames' % total
     for c in sel:
         sb, hops, frames = got[c]
-        # correctly rounded libm: every output bit for bit
-        rsb, rhops, rframes, ritems = refs_cr[c]
+        rsb, rhops, rframes, ritems = refs[c]
         assert len(rsb) > 1000, 'oracle did not lock on channel %d' % c
         assert np.array_equal(sb, rsb), 'channel %d soft bits differ (%d vs %d)' % (c, len(sb), len(rsb))
         assert hops.shape == rhops.shape and np.array_equal(hops.view(np.int64), rhops.view(np.int64)), \
             'channel %d hop records differ' % c
         assert np.array_equal(frames, rframes), 'channel %d frames differ' % c
         assert ritems and items[c] == ritems, 'channel %d ACARS items differ' % c
-        # glibc libm: decoded outputs identical, the MSE column within 1e-12
-        gsb, ghops, gframes, gitems = refs[c]
-        assert np.array_equal(sb, gsb) and np.array_equal(frames, gframes) and items[c] == gitems, \
-            'channel %d decoded outputs differ from the glibc oracle' % c
-        assert hops.shape == ghops.shape
-        exact = [0, 1, 2, 3, 5]
-        assert np.array_equal(hops[:, exact].view(np.int64), ghops[:, exact].view(np.int64)), \
-            'channel %d hop decisions differ from the glibc oracle' % c
-        assert np.allclose(hops[:, 4], ghops[:, 4], rtol=1e-12, atol=0), 'channel %d MSE beyond 1e-12' % c

@@ -1,5 +1,6 @@
 // Host build of aero-cli_amd/csrc/aero_math.h (g++, -ffp-contract=off) for
-// tests/test_math_host.py and the device-vs-host check in tests/test_gpu_math.py.
+// tests/test_math_host.py (bitwise against the host glibc) and the
+// device-vs-host check in tests/test_gpu_math.py.
 #include <cmath>
 #include <cstddef>
 
@@ -21,32 +22,35 @@ extern "C" void aero_math_host_eval(int fn, const double *x, const double *y, do
       case 8: r = a / b; break;
       case 9: { double s, c; aero::aero_sincos(a, s, c); r = s; break; }
       case 10: { double s, c; aero::aero_sincos(a, s, c); r = c; break; }
-      case 11: r = aero::aero_atan2_dd(a, b); break;
       case 12: r = aero::aero_log(a); break;
-      case 13: r = aero::aero_log_dd(a); break;
-      case 14: { double s, c; aero::aero_sincos_dd(a, s, c); r = s; break; }
-      case 15: { double s, c; aero::aero_sincos_dd(a, s, c); r = c; break; }
       default: break;
     }
     out[i] = r;
   }
 }
 
-// glibc reference values (the calls the reference makes)
+// glibc reference values: the entry points the reference's loops reach
+// (sin/cos pairs of one argument compile to sincos; log10 calls log)
 extern "C" void aero_math_glibc_eval(int fn, const double *x, const double *y, double *out, size_t n) {
   for (size_t i = 0; i < n; i++) {
     const double a = x[i], b = y[i];
-    double r = 0;
+    volatile double va = a;  // keep GCC from merging the separate sin/cos calls
+    double r = 0, s, c;
     switch (fn) {
       case 0: r = hypot(a, b); break;
       case 1: r = atan2(a, b); break;
       case 2: r = tanh(a); break;
-      case 3: r = sin(a); break;
-      case 4: r = cos(a); break;
+      case 3: sincos(a, &s, &c); r = s; break;
+      case 4: sincos(a, &s, &c); r = c; break;
       case 5: r = log10(a); break;
       case 6: r = sqrt(a); break;
       case 7: r = fmod(a, 360.0); break;
       case 8: r = a / b; break;
+      case 9: sincos(a, &s, &c); r = s; break;
+      case 10: sincos(a, &s, &c); r = c; break;
+      case 12: r = log(a); break;
+      case 13: r = sin(va); break;  // the ifunc'd __sin_fma (host tables only)
+      case 14: r = cos(va); break;
       default: break;
     }
     out[i] = r;
