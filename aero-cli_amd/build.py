@@ -39,11 +39,11 @@ CXX_SRCS = ['tables_host.cpp', 'acars_host.cpp']
 # rematerialised at their use.
 # The continuous OQPSK demod schedules better with memory clauses kept
 # together (its loop's table gathers and ring loads issue back to back):
-# 14.9 -> 14.6 ms per hop (profiles/r04/ab/round3c/ab_sched_*.log; max-ilp
+# 14.9 -> 14.6 ms per hop (profiles/r03/ab/round3c/ab_sched_*.log; max-ilp
 # 14.8, and both strategies slow the coarse kernel, which keeps the default).
 # With the RRC partial sums on the helper wave, machine LICM's hoisted FP64
 # constants are what spills (211 SGPRs -> VGPR lanes; 15 without it):
-# 13.76 -> 12.83 ms (profiles/round4/ab/g8_licm.txt).
+# 13.76 -> 12.83 ms (profiles/r04/ab/g8_licm.txt).
 FILE_FLAGS = {'burst.hip': ['-mllvm', '-disable-machine-licm'],
               'burst_msk.hip': ['-mllvm', '-disable-machine-licm'],
               'demod_oqpsk.hip': ['-mllvm', '--amdgpu-sched-strategy=max-memory-clause', '-mllvm',
@@ -122,6 +122,19 @@ def build_mathhost():
     return MATHHOST_SO
 
 
+HOSTCHECK_SO = os.path.join(ROOT, 'tools', 'libaero_hostcheck.so')
+HOSTCHECK_SRCS = [os.path.join(ROOT, 'tools', 'hostcheck.cpp'), os.path.join(CSRC, 'acars_host.cpp'),
+                  os.path.join(CSRC, 'tables_host.cpp')]
+
+
+def build_hostcheck(out=HOSTCHECK_SO, extra=()):
+    """Test-only CPU harness over the engine's host C++ (acars_host, tables_host)."""
+    deps = HOSTCHECK_SRCS + [os.path.join(CSRC, h) for h in ('acars_host.h', 'tables_host.h')]
+    if _stale(out, deps):
+        _run(['g++'] + CXX_FLAGS + list(extra) + ['-shared', '-o', out] + HOSTCHECK_SRCS + ['-lm'])
+    return out
+
+
 def build_oracle():
     _run(['make', '-s', '-C', ORACLE_DIR])
     # the reference's own Qt-free sources (JFFT, Oscillator) as a second
@@ -180,11 +193,53 @@ def build_host(jobs=4):
     return out
 
 
+# AddressSanitizer + UndefinedBehaviorSanitizer builds of every host-compiled
+# source the CPU tests load: the oracle, the synthetic
+# transmitter, the device libm's host build, the engine's host C++
+# (acars_host, tables_host through tools/hostcheck.cpp) and the drop-in host
+# binaries.  Host code only (no GPU sanitizer on this pool); tests/asan_check.sh
+# runs the CPU tests against them.
+ASAN_DIR = os.path.join(BUILD, 'asan')
+SAN = ['-fsanitize=address,undefined', '-fno-sanitize-recover=undefined', '-fno-omit-frame-pointer', '-g']
+
+
+def build_asan(jobs=4):
+    d = ASAN_DIR
+    bindir = os.path.join(d, 'bin')
+    os.makedirs(bindir, exist_ok=True)
+    base = ['g++', '-O1', '-std=c++17', '-fPIC'] + FP + SAN
+    out = {}
+    jobsl = []
+    def lib(name, srcs, extra=()):
+        so = os.path.join(d, name)
+        out[name] = so
+        if _stale(so, srcs + [os.path.join(CSRC, 'aero_math.h'), os.path.join(CSRC, 'aero_glibc_tables.h')]):
+            jobsl.append(base + list(extra) + ['-shared', '-o', so] + srcs + ['-lm'])
+    lib('liboracle.so', [os.path.join(ORACLE_DIR, 'aero_oracle.cpp'), os.path.join(ORACLE_DIR, 'pub_oracle.cpp')])
+    lib('libaero_synth.so', [os.path.join(ROOT, 'tools', 'aero_synth.cpp')])
+    lib('libaero_mathhost.so', [os.path.join(ROOT, 'tools', 'mathhost.cpp')])
+    lib('libaero_hostcheck.so', HOSTCHECK_SRCS)
+    hs = [os.path.join(HOST, s) for s in HOST_COMMON]
+    lib(os.path.join('bin', 'libaero_host.so'), [os.path.join(HOST, 'host_capi.cpp')] + hs[:2])
+    for name, srcs in HOST_BINS.items():
+        exe = os.path.join(bindir, name)
+        out[name] = exe
+        allsrc = [os.path.join(HOST, s) for s in srcs] + hs
+        if _stale(exe, allsrc + [ENGINE_SO]):
+            jobsl.append(base + ['-o', exe] + allsrc + [ENGINE_SO, '-Wl,-rpath,' + HERE, '-rdynamic', '-ldl',
+                                                          '-lpthread'])
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for f in [ex.submit(_run, t) for t in jobsl]:
+            f.result()
+    return out
+
+
 def build_all(jobs=4):
     build_oracle()
     build_synth()
     build_mathhost()
     build_fftsim()
+    build_hostcheck()
     so = build_engine(jobs)
     build_diag(jobs)
     build_host(jobs)
@@ -206,8 +261,12 @@ if __name__ == '__main__':
     ap.add_argument('--synth', action='store_true')
     ap.add_argument('--oracle', action='store_true')
     ap.add_argument('--host', action='store_true')
+    ap.add_argument('--asan', action='store_true', help='sanitizer builds into build/asan (tests/asan_check.sh)')
     ap.add_argument('-j', type=int, default=4)
     a = ap.parse_args()
+    if a.asan:
+        print(build_asan(a.j))
+        sys.exit(0)
     if not (a.engine or a.synth or a.oracle or a.host):
         print(build_all(a.j))
         sys.exit(0)

@@ -162,7 +162,10 @@ struct Group {
   size_t pool_bytes = 0;
   HostPool *hpool = nullptr;  // the engine's
   std::vector<aero_channel_cfg> cfg;
-  std::vector<int> gch;  // local -> engine channel id
+  std::vector<int> gch;  // local -> engine channel id (-1: a free slot)
+  // local slots an MSK channel left for another rate's group (msk_migrate),
+  // reused by the next channel added to this group (group_add_channel)
+  std::vector<int> free_slots;
   // host mirrors of the per-channel counters
   std::vector<long long> avail, nsamp, hops;
   std::vector<std::unique_ptr<PChannelHost>> host;
@@ -363,9 +366,7 @@ void ev_collect(Group *e) {
 // decode/mskdemodulator.cpp:7-218 (both as Decoder applies them); AeroL ctor
 // (decode/aerol.cpp:875-954).  Opened channels are initialised lazily, one
 // strided copy per field for the whole pending range.
-int flush_pending_init(Group *e) {
-  const int lo = e->init_lo, hi = e->nch;
-  if (lo >= hi) return AERO_OK;
+int init_scalars(Group *e, int lo, int hi) {
   const int C = e->C, k = hi - lo;
   std::vector<double> ds(DS_COUNT, 0.0);
   std::vector<int> is(IS_COUNT, 0);
@@ -401,8 +402,57 @@ int flush_pending_init(Group *e) {
     std::fill(vl.begin(), vl.end(), ls[f]);
     HIPCHK(hipMemcpy(e->S.ls + (size_t)f * C + lo, vl.data(), 8 * (size_t)k, hipMemcpyHostToDevice));
   }
+  return AERO_OK;
+}
+
+int flush_pending_init(Group *e) {
+  const int lo = e->init_lo, hi = e->nch;
+  if (lo >= hi) return AERO_OK;
+  if (int rc = init_scalars(e, lo, hi)) return rc;
   e->init_lo = hi;
   return AERO_OK;
+}
+
+// A freed slot (free_slots) back to a new channel's state: every per-channel
+// row zeroed, as the zeroed pool leaves a slot never used, then the scalar
+// init.  The group is idle (its stream drained first).
+int reset_slot(Group *e, int c) {
+  const DevState &S = e->S;
+  const ModeGeom &g = e->g;
+  const size_t C = (size_t)e->C;
+  const bool msk = e->mode != MODE_OQPSK;
+  hipStream_t st = e->st;
+  HIPCHK(hipStreamSynchronize(st));
+  auto col = [&](void *base, size_t elem, size_t rows) {  // time-major [rows][C]: one element per row
+    return hipMemset2DAsync((char *)base + elem * c, elem * C, 0, elem, rows, st);
+  };
+  auto row = [&](void *base, size_t bytes) {  // channel-major [C][len]
+    return hipMemsetAsync((char *)base + bytes * c, 0, bytes, st);
+  };
+  HIPCHK(col(S.fir, 8, (size_t)2 * g.ntaps));
+  HIPCHK(col(S.agc, 8, (size_t)g.agc_len));
+  if (msk) {
+    HIPCHK(col(S.dsm, 16, (size_t)g.dsm_len));
+    HIPCHK(col(S.d8, 8, (size_t)g.d8_len));
+    HIPCHK(row(S.ms, (size_t)8 * g.ms_len));
+  } else {
+    HIPCHK(row(S.pm, (size_t)16 * g.ms_len));
+  }
+  HIPCHK(col(S.pcm, 2, (size_t)PCM_CAP));
+  HIPCHK(row(S.marg, (size_t)8 * g.marg_len));
+  HIPCHK(row(S.dt, (size_t)16 * g.dt_len));
+  HIPCHK(row(S.cring, (size_t)4 * g.nfft));
+  HIPCHK(row(S.y, (size_t)8 * (g.y_hi - g.y_lo + 1)));
+  HIPCHK(row(S.soft, (size_t)SOFT_RING));
+  if (S.pt_cap) HIPCHK(row(S.pt, (size_t)16 * S.pt_cap));
+  HIPCHK(row(S.hops, (size_t)8 * 6 * HOP_CAP));
+  HIPCHK(row(S.hop_n, 4));
+  HIPCHK(row(S.block, (size_t)2 * g.block));
+  HIPCHK(row(S.overlap, 64));
+  HIPCHK(row(S.dl2, (size_t)g.dl2_len));
+  if (e->flags & AERO_F_TRACE_BLOCKS) HIPCHK(row(S.blocks_dbg, 2500));
+  HIPCHK(hipStreamSynchronize(st));
+  return init_scalars(e, c, c + 1);
 }
 
 // CRC-16 of one SU (AeroLcrc16::calcusingbytes, decode/aerol.h:332-367) and the
@@ -1313,6 +1363,26 @@ int group_add_channel(aero_engine *e, int mode, const aero_channel_cfg &cfg, int
   if (!e->groups[mode])
     if (int rc = group_create(e, mode, e->groups[mode])) return rc;
   Group *g = e->groups[mode].get();
+  if (!g->free_slots.empty()) {  // a slot an MSK channel moved out of
+    if (int rc = flush_pending_init(g)) return rc;
+    const int c = g->free_slots.back();
+    if (int rc = reset_slot(g, c)) return rc;
+    g->free_slots.pop_back();
+    g->cfg[c] = cfg;
+    g->gch[c] = gc;
+    g->avail[c] = g->nsamp[c] = g->hops[c] = 0;
+    g->host[c].reset(new PChannelHost(cfg.disable_reassembly != 0));
+    g->infofield[c].clear();
+    g->soft_hold[c].clear();
+    g->hop_hold[c].clear();
+    g->pt_hold[c].clear();
+    g->blk_hold[c].clear();
+    g->frame_hold[c].clear();
+    g->soft_seen[c] = 0;
+    g->hop_base[c] = 0;
+    *local = c;
+    return AERO_OK;
+  }
   if (g->nch >= g->C) return AERO_E_FULL;
   const int c = g->nch;
   g->nch++;
@@ -1440,8 +1510,14 @@ int msk_migrate(aero_engine *e, int ch, uint32_t fs) {
     h->trace_mask.resize(h->C, 0);
     h->trace_mask[c2] = 1;
     h->trace_list.push_back(c2);
+    g->trace_mask[c] = 0;
+    g->trace_list.erase(std::remove(g->trace_list.begin(), g->trace_list.end(), c), g->trace_list.end());
   }
   e->chmap[ch] = {to, c2};
+  // the old slot is free for the next channel of that group (it has no
+  // samples left: the group ran and drained it above)
+  g->gch[c] = -1;
+  g->free_slots.push_back(c);
   return AERO_OK;
 }
 
@@ -1939,6 +2015,16 @@ int aero_engine_feed_dev(aero_engine *e, int nitems, const int *ch, const int16_
   if (!e || nitems < 0 || (nitems && (!ch || !src || !n || !fs))) return AERO_E_INVALID;
   HIPCHK(hipSetDevice(e->device));
   std::vector<std::pair<int, std::pair<const int16_t *, size_t>>> per[MODE_COUNT];
+  std::vector<uint8_t> queued(e->chmap.size(), 0);  // engine channels with an item in per[]
+  auto feed_queued = [&]() -> int {
+    for (int m = 0; m < MODE_COUNT; m++)
+      if (!per[m].empty()) {
+        if (int rc = feed_group(e->groups[m].get(), per[m], ready, producer)) return rc;
+        per[m].clear();
+      }
+    std::fill(queued.begin(), queued.end(), 0);
+    return AERO_OK;
+  };
   for (int i = 0; i < nitems; i++) {
     if (!n[i]) continue;
     BurstGroup *bg;
@@ -1949,15 +2035,21 @@ int aero_engine_feed_dev(aero_engine *e, int nitems, const int *ch, const int16_
       continue;
     }
     int c, rc;
+    {
+      // a rate change of a channel that already has an item of this call
+      // queued: those items go in first, at the old rate (messages are
+      // handled in order, MskDemodulator::dataReceived), then it moves
+      Group *g0 = route(e, ch[i], c);
+      if (g0 && g0->mode != MODE_OQPSK && fs[i] != (uint32_t)g0->g.fs && queued[ch[i]])
+        if (int rc2 = feed_queued()) return rc2;
+    }
     Group *g = route_rate(e, ch[i], fs[i], c, rc);
     if (rc) return rc;
     if (!g || !src[i]) return AERO_E_INVALID;
     per[g->mode].push_back({c, {src[i], n[i]}});
+    queued[ch[i]] = 1;
   }
-  for (int m = 0; m < MODE_COUNT; m++)
-    if (!per[m].empty())
-      if (int rc = feed_group(e->groups[m].get(), per[m], ready, producer)) return rc;
-  return AERO_OK;
+  return feed_queued();
 }
 
 // diagnostic builds (AERO_X_STAMPS): the demod's per-section cycle totals

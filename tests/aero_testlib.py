@@ -12,8 +12,9 @@ PKG = os.path.join(ROOT, 'aero-cli_amd')
 if PKG not in sys.path:
     sys.path.insert(0, PKG)
 
-ORACLE_SO = os.path.join(ROOT, 'oracle', 'liboracle.so')
-SYNTH_SO = os.path.join(ROOT, 'tools', 'libaero_synth.so')
+# AERO_ORACLE_SO / AERO_SYNTH_SO: the AddressSanitizer builds (tests/asan_check.sh)
+ORACLE_SO = os.environ.get('AERO_ORACLE_SO') or os.path.join(ROOT, 'oracle', 'liboracle.so')
+SYNTH_SO = os.environ.get('AERO_SYNTH_SO') or os.path.join(ROOT, 'tools', 'libaero_synth.so')
 
 
 class SynthCfg(ctypes.Structure):

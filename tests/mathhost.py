@@ -5,7 +5,7 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO = os.path.join(ROOT, 'tools', 'libaero_mathhost.so')
+SO = os.environ.get('AERO_MATHHOST_SO') or os.path.join(ROOT, 'tools', 'libaero_mathhost.so')
 FN = {'hypot': 0, 'atan2': 1, 'tanh': 2, 'sin': 3, 'cos': 4, 'log10': 5, 'sqrt': 6, 'fmod360': 7, 'div': 8,
       'sincos_s': 9, 'sincos_c': 10, 'log': 12, 'glibc_sin': 13, 'glibc_cos': 14}
 _lib = None
@@ -17,7 +17,8 @@ def lib():
         import sys
         sys.path.insert(0, os.path.join(ROOT, 'aero-cli_amd'))
         import build
-        build.build_mathhost()
+        if not os.environ.get('AERO_MATHHOST_SO'):
+            build.build_mathhost()
         _lib = ctypes.CDLL(SO)
         for f in ('aero_math_host_eval', 'aero_math_glibc_eval'):
             getattr(_lib, f).argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

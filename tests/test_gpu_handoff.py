@@ -19,11 +19,14 @@ import aero_engine as ae, aero_testlib as tl
 pcm = tl.synth(seconds=2.0, seed=0xAE20)
 eng = ae.Engine(max_channels=4)
 chs = [eng.open_channel(10500, 48000) for _ in range(4)]
-for c in chs:
-    eng.push(c, pcm)
-rc = eng.lib.aero_run(eng.h)
-if rc == 0:
-    rc = eng.lib.aero_flush(eng.h)
+rc = 0
+try:  # the error surfaces at the first call that waits for a demod pass
+    for c in chs:
+        eng.push(c, pcm)
+    eng.run()
+    eng.flush()
+except ae.AeroError as ex:
+    rc = ex.rc
 print('RC', rc)
 ''' % (os.path.join(ROOT, 'aero-cli_amd'), os.path.join(ROOT, 'tests'))
 

@@ -78,3 +78,38 @@ def test_msk_unsupported_rate_refused(engine_lib):
     assert ex.value.rc == ae.AERO_E_RATE
     eng.push(ch, np.zeros(1000, np.int16), fs=48000)  # a supported rate moves the channel
     eng.close()
+
+
+def test_msk_rate_change_in_a_full_group(engine_lib):
+    """A group whose every slot is taken (64 channels at 12 kHz, groups hold
+    max_channels rounded up to 64): one channel goes to 24 kHz and back.  The
+    slot it left is reused on the way back (engine.hip free_slots /
+    reset_slot) instead of the move failing with AERO_E_FULL, and the moving
+    channel and a neighbour still equal the oracle."""
+    import aero_engine as ae
+    segs = [(12000, 8.0, 0xE200, 1800.0, 14.0), (24000, 8.0, 0xE201, 1800.0, 14.0),
+            (12000, 16.0, 0xE202, 1800.0, 14.0)]
+    mover = _messages(600, segs, 0.25)
+    stay = _messages(600, [(12000, 32.0, 0xE210, 1500.0, 12.0)], 0.25)
+    eng = ae.Engine(max_channels=64, flags=ae.F_TRACE_SOFT | ae.F_TRACE_HOPS | ae.F_TRACE_FRAMES)
+    chans = [eng.open_channel(600) for _ in range(64)]
+    quiet = np.zeros(3000, np.int16)
+    for c in chans[2:]:
+        eng.push(c, quiet, fs=12000)
+    for k in range(max(len(mover), len(stay))):
+        if k < len(mover):
+            eng.push(chans[0], mover[k][0], fs=mover[k][1])
+        if k < len(stay):
+            eng.push(chans[1], stay[k][0], fs=stay[k][1])
+        eng.run()
+    eng.flush()
+    for ch, msgs in ((chans[0], mover), (chans[1], stay)):
+        o = tl.Oracle(bitrate=600)
+        for pcm, fs in msgs:
+            o.push(pcm, fs=fs)
+        sb, rsb = eng.softbits(ch), o.softbits()
+        assert len(rsb) > 1000 and np.array_equal(sb, rsb), 'channel %d soft bits differ' % ch
+        h, rh = eng.hops(ch), o.hops()
+        assert h.shape == rh.shape and np.array_equal(h.view(np.int64), rh.view(np.int64)), ch
+        assert eng.items(ch) == o.item_lines('A'), 'channel %d items differ' % ch
+    eng.close()

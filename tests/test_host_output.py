@@ -14,7 +14,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, 'tests', 'golden')
-BIN = os.path.join(ROOT, 'aero-cli_amd', 'bin')
+BIN = os.environ.get('AERO_HOST_BIN') or os.path.join(ROOT, 'aero-cli_amd', 'bin')  # asan_check.sh: sanitizer builds
 
 
 @pytest.fixture(scope='module')
