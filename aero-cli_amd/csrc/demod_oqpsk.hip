@@ -41,7 +41,8 @@ namespace aero {
 #define DM_TANH aero_tanh
 #define DM_SINCOS(x, s, c) aero_sincos(x, s, c)
 #endif
-#define DM_DIVC(a, c) ((a) / (c))
+// a / c for a literal c: the exact three-operation sequence (aero_math.h div_c)
+#define DM_DIVC(a, c) div_c((a), (c))
 
 // AERO_X_STAMPS (diagnostic build only): s_memtime cycle totals per loop
 // section of wave 0 of workgroup 0, with scheduling barriers at the stamps
@@ -492,14 +493,14 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       }
       it = __builtin_amdgcn_readfirstlane(it + 1);
       // AGC (DSP.cpp:371-380) on |sig2| (oqpskdemodulator.cpp:399-405)
-      const double dab = sqrt(s2r * s2r + s2i * s2i);
+      const double dab = sqrt_n(s2r * s2r + s2i * s2i);
       {
         agc_sum = agc_sum - agc_old;
         agc_sum = agc_sum + fabs(dab);
         S.agc[(size_t)agc_ptr * C + c] = fabs(dab);
         agc_ptr++;
         if (agc_ptr == AGC_LEN) agc_ptr = 0;
-        double g = 1.414213562 / fmax(DM_DIVC(agc_sum, ((double)AGC_LEN)), 0.000001);
+        double g = div_n(1.414213562, fmax(DM_DIVC(agc_sum, ((double)AGC_LEN)), 0.000001));
         g = fmax(g, 0.000001);
         s2r *= g;
         s2i *= g;
@@ -508,7 +509,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       XSTAMP(1);  // loads, FIR hand-off, AGC
       const double ab = DM_HYPOT(s2r, s2i);
       if (ab > 2.84) {
-        const double k = 2.84 / ab;
+        const double k = div_n(2.84, ab);
         s2r = k * s2r;
         s2i = k * s2i;
       }
@@ -539,7 +540,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       if (tl < 0.0) tl += WTSIZE;
       if (tw < 0.0) tw += WTSIZE;
       if ((tl > 3.0 * WTSIZE / 4.0) && (tw < 1.0 * WTSIZE / 4.0)) {
-        const double pt_last = tw / so_step;
+        const double pt_last = div_n(tw, so_step);
         const double pt_this = 1.0 - pt_last;
         const double pr = pt_this * s2r + pt_last * s2l_re;
         const double pi = pt_this * s2i + pt_last * s2l_im;
@@ -626,10 +627,10 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
       {  // mixer2.IncresePhaseDeg / SetPhaseDeg (DSP.cpp:177-187)
         double phase_deg = 1.0 * ct_ec;
-        phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
+        phase_deg += DM_DIVC(360.0 * m2_ptr, ((double)WTSIZE));
         phase_deg = fmod(phase_deg, 360.0);
         while (phase_deg < 0) phase_deg += 360.0;
-        m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+        m2_ptr = DM_DIVC(phase_deg, 360.0) * ((double)WTSIZE);
       }
       set_freq(m2_freq, m2_step, 0.01 * ct_ec + m2_freq);  // IncreseFreqHz
       // marg->UpdateSigned (DSP.cpp:419-427)
@@ -664,7 +665,8 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
         pm_p %= MSE_LEN;
         double mu = DM_DIVC(pm_sum, ((double)MSE_LEN));
         if (mu < 0.000001) mu = 0.000001;
-        const double tr = (1.4142135623730951 * qr) / mu, ti = (1.4142135623730951 * qi) / mu;
+        const double rmu = rcp_div(mu);  // one reciprocal for both quotients
+        const double tr = div_r(1.4142135623730951 * qr, mu, rmu), ti = div_r(1.4142135623730951 * qi, mu, rmu);
         const double tda = (fabs(tr) - 1.0), tdb = (fabs(ti) - 1.0);
         const double v = (tda * tda) + (tdb * tdb);
         ms_sum = ms_sum - ms_old;

@@ -115,6 +115,13 @@ __global__ void math_kernel(int fn, const double *x, const double *y, double *ou
     case 6: r = sqrt(a); break;
     case 7: r = fmod(a, 360.0); break;
     case 8: r = a / b; break;
+    // the short exact division / sqrt sequences (aero_math.h) against the
+    // IEEE operations above (tests/test_gpu_math.py)
+    case 9: r = div_c(a, 48000.0); break;
+    case 10: r = div_c(a, 360.0); break;
+    case 11: r = div_n(a, b); break;
+    case 12: r = sqrt_n(a); break;
+    case 13: r = div_c(a, 192000.0); break;
     default: break;
   }
   out[i] = r;

@@ -42,3 +42,41 @@ def test_device_math_matches_host_build(engine_lib):
         host = mathhost.evaluate(fn, x, y)
         assert np.array_equal(dev.view(np.uint64), host.view(np.uint64)), fn
     eng.close()
+
+
+def _edge_values(rng, n):
+    """Random magnitudes over the whole double range, plus zeros, subnormals,
+    the fast paths' range edges, infinities and NaN."""
+    e = rng.uniform(-1074, 1023, n)
+    x = rng.choice([-1.0, 1.0], n) * np.exp2(e) * rng.uniform(1, 2, n)
+    special = np.array([0.0, -0.0, 5e-324, -5e-324, 2.0 ** -1022, 2.0 ** -500, 2.0 ** 500, 2.0 ** -767,
+                        np.nextafter(2.0 ** -500, 0), np.nextafter(2.0 ** 500, np.inf), np.inf, -np.inf, np.nan,
+                        1.7976931348623157e308, 1.0, -1.0, 3.0])
+    return np.concatenate([x, special, rng.standard_normal(n) * 1e3])
+
+
+@pytest.mark.gpu
+def test_short_division_and_sqrt_sequences_are_ieee(engine_lib):
+    """div_c (constant divisor, Markstein), div_n (the compiler's sequence
+    without div_scale / div_fixup, zero numerators by select) and sqrt_n
+    (without the 2^-767 scaling) equal IEEE a / b and sqrt bit for bit,
+    including the operands that take their IEEE fallbacks."""
+    import aero_engine as ae
+    eng = ae.Engine(max_channels=1)
+    rng = np.random.default_rng(17)
+    a = _edge_values(rng, 300000)
+    b = rng.permutation(a)
+    with np.errstate(all='ignore'):
+        for fn, ref in (('div_c48000', a / 48000.0), ('div_c360', a / 360.0), ('div_c192000', a / 192000.0),
+                        ('div_n', a / b), ('sqrt_n', np.sqrt(np.abs(a)))):
+            x = np.abs(a) if fn == 'sqrt_n' else a
+            got = eng.device_math(fn, x, b)
+            same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
+            assert same.all(), (fn, x[~same][:4], b[~same][:4], got[~same][:4], ref[~same][:4])
+        # the demods' operand ranges, densely
+        m = rng.uniform(-1, 1, 400000) * np.exp(rng.uniform(-30, 30, 400000))
+        d = rng.uniform(0.5, 2, 400000) * np.exp(rng.uniform(-30, 30, 400000))
+        for fn, x, y, ref in (('div_n', m, d, m / d), ('div_c360', m, d, m / 360.0),
+                              ('sqrt_n', np.abs(m), d, np.sqrt(np.abs(m)))):
+            assert np.array_equal(eng.device_math(fn, x, y).view(np.uint64), ref.view(np.uint64)), fn
+    eng.close()
