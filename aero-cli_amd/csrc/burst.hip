@@ -607,7 +607,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     }
     if ((cntr > SPS * (128 + 10)) && (cntr < ((256 - 10) * SPS))) {  // symbol-tone PLL (:462-474)
       const double progress =
-          (((double)cntr) - (SPS * (128 + 10))) / (((256 - 10) * SPS) - (SPS * (128 + 10)));
+          div_c(((double)cntr) - (SPS * (128 + 10)), (double)(((256 - 10) * SPS) - (SPS * (128 + 10))));
       const double t1r = s2r * str_r - s2i * str_i, t1i = s2r * str_i + s2i * str_r;
       const double spr = t1r * 0.0 - t1i * 1.0, spi = t1r * 1.0 + t1i * 0.0;  // * imag
       const double er = aero_tanh(spi) * (spr);
@@ -696,7 +696,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         const double pt_this = 1.0 - pt_last;
         const double ptr_ = pt_this * s2r + pt_last * s2l_r, pti = pt_this * s2i + pt_last * s2l_i;
         const double twospeed =
-            -4.0 * ((b_fmod360((360.0 * q_ptr / ((double)WTSIZE)) * 2.0 + (360.0 * 0.4 * 0.5)) / 360.0) -
+            -4.0 * (div_c(b_fmod360(div_c(360.0 * q_ptr, ((double)WTSIZE)) * 2.0 + (360.0 * 0.4 * 0.5)), 360.0) -
                     (0.34046 + 0.4111 * 0.4));
         const bool even = !(twospeed < 0);
         yui++;

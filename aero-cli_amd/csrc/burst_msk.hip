@@ -456,7 +456,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         const double spi2 = (0.0 * a1_new + (1.0 - 0.0) * a1_old);
         double progress = (double)cntr - (MSPS * (M_START));
         const double goal = M_ENDROT - (MSPS * M_START);
-        progress = progress / goal;
+        progress = div_c(progress, goal);  // goal is a compile-time constant
         const double2 hv = h_n;
         const double er_r = hv.x * spr - hv.y * (-spi2), er_i = hv.x * (-spi2) + hv.y * spr;
         double st_err = aero_atan2(er_i, er_r);
