@@ -176,11 +176,13 @@ __device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<in
 }
 
 // AERO_X_STAMPS (diagnostic build only): s_memtime cycle totals per section
-// of wave 0 of every workgroup that ran a hop (prologue+ring, FFT 1,
-// boxcar+iFFT+square, FFT 3, hypot, log10 smoothing, fold+control), and the
-// number of such workgroups
+// of wave 0 of every workgroup that ran a hop (prologue, ring to LDS +
+// twiddles, table gathers + mix, FFT 1, boxcar+iFFT+square, FFT 3, hypot,
+// log10 smoothing, fold search; slots 0-8), and the number of such
+// workgroups (slot 11)
+constexpr int CSTAMP_N = 12;
 #ifdef AERO_X_STAMPS
-__device__ unsigned long long g_cstamps[8];
+__device__ unsigned long long g_cstamps[CSTAMP_N];
 #define CSTAMP(k)                                                  \
   do {                                                             \
     __builtin_amdgcn_sched_barrier(0);                             \
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   const long long avail = S.ls[LS_AVAIL * C + c];
   if (nsamp != nk || avail <= nk) return;
 #ifdef AERO_X_STAMPS
-  unsigned long long cst_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ctime_ = __builtin_amdgcn_s_memtime();
+  unsigned long long cst_[CSTAMP_N] = {}, ctime_ = __builtin_amdgcn_s_memtime();
 #endif
   const long long zero_before = S.ls[LS_ZERO_BEFORE * C + c];
   if (filled <= nk && t == 0) {
@@ -231,6 +233,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     S.ls[LS_FILLED * C + c] = nk + 1;
   }
   __syncthreads();
+  CSTAMP(0);
 
   load_tw_lds<L>(s_tw, T.tw, t, FT);
   // ring words -> LDS (uint32, one pad word per 16: the bit-reversed gather
@@ -239,6 +242,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   const uint32_t *ring = S.cring + (size_t)c * N;
   for (int j = t; j < N; j += FT) ring_lds[j + (j >> 4)] = ring[j];
   __syncthreads();
+  CSTAMP(1);
   double2 x[16];
   const long long s0 = nk - (N - 1);  // sample of snapshot element 0 (oqpskdemodulator.cpp:359-365)
   // every element's table entry is gathered before any is waited for (the
@@ -265,10 +269,10 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     x[i] = s < zero_before ? make_double2(0.0, 0.0) : make_double2(cs[i].x * dval[i], cs[i].y * dval[i]);
   }
   __syncthreads();  // the ring image is read: the LDS is the transforms' from here on
-  CSTAMP(0);
+  CSTAMP(2);
   // forward FFT
   chain::fft<L, true, false>(x, t, lds, T.tw, s_tw);
-  CSTAMP(1);
+  CSTAMP(3);
   // boxcar: zero bins startbin..stopbin (coarsefreqestimate.cpp:143-146)
   const int bin_t = chain::out_bin_thread<L>(t);
 #pragma unroll
@@ -291,9 +295,9 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     const double im = 2.0 * (x[i].x * x[i].y);
     x[i] = make_double2(r, im);
   }
-  CSTAMP(2);
+  CSTAMP(4);
   chain::fft<L, false, false>(x, t, lds, T.tw, s_tw);
-  CSTAMP(3);
+  CSTAMP(5);
   // fftshift + smoothing y = 0.9 y + 10 log10(max(|X|,1)) over the bins the fold reads:
   // |X| per bin to LDS first (keeps the log10 out of the register-heavy FFT scope)
   // the y history (HBM) is read three iterations ahead of its update, the
@@ -313,7 +317,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   }
   double yp2 = yload(t + 2 * FT);
   __syncthreads();
-  CSTAMP(4);
+  CSTAMP(6);
 #pragma unroll 1
   for (int k = t; k < YLEN; k += FT) {
     const double yold = yp0;
@@ -325,7 +329,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     ylds[fftl::ypad(k)] = ynew;
   }
   __syncthreads();
-  CSTAMP(5);
+  CSTAMP(7);
   // fold search (coarsefreqestimate.cpp:166-185): first strict maximum above 0
   double bv = 0.0;
   int bi = 0x7fffffff;
@@ -354,11 +358,11 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     red_i[t >> 6] = bi;
   }
   __syncthreads();
-  CSTAMP(6);
+  CSTAMP(8);
 #ifdef AERO_X_STAMPS
   if (t == 0) {
-    for (int k = 0; k < 7; ++k) atomicAdd(&g_cstamps[k], cst_[k]);
-    atomicAdd(&g_cstamps[7], 1ull);
+    for (int k = 0; k < 9; ++k) atomicAdd(&g_cstamps[k], cst_[k]);
+    atomicAdd(&g_cstamps[CSTAMP_N - 1], 1ull);
   }
 #endif
   if (t != 0) return;
@@ -430,11 +434,11 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
 
 void coarse_read_stamps(unsigned long long *out) {
 #ifdef AERO_X_STAMPS
-  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cstamps), sizeof(unsigned long long) * 8);
-  unsigned long long z[8] = {0};
-  hipMemcpyToSymbol(HIP_SYMBOL(g_cstamps), z, sizeof z);
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cstamps), sizeof(unsigned long long) * CSTAMP_N);
+  unsigned long long z[CSTAMP_N] = {0};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_cstamps), z, sizeof z);
 #else
-  for (int k = 0; k < 8; ++k) out[k] = 0;
+  for (int k = 0; k < CSTAMP_N; ++k) out[k] = 0;
 #endif
 }
 

@@ -2064,8 +2064,8 @@ int aero_engine_feed_dev(aero_engine *e, int nitems, const int *ch, const int16_
 // step, samples) of wave 0; zeros in the product build
 extern "C" void aero_x_demod_stamps(unsigned long long *out7) { demod_read_stamps(out7); }
 // the coarse kernel's per-section cycle totals over every hop's wave 0
-// (7 sections + the hop count)
-extern "C" void aero_x_coarse_stamps(unsigned long long *out8) { coarse_read_stamps(out8); }
+// (9 sections in slots 0-8, the hop count in slot 11)
+extern "C" void aero_x_coarse_stamps(unsigned long long *out12) { coarse_read_stamps(out12); }
 // the Viterbi kernel's per-section cycle totals over every job (3 sections + job count)
 extern "C" void aero_x_viterbi_stamps(unsigned long long *out4) { viterbi_read_stamps(out4); }
 // the burst OQPSK demod's per-section cycle totals (AERO_X_BSTAMPS build; burst.hip)

@@ -25,11 +25,12 @@ for _ in range(C):
 lib = ae.load_library()
 fn = lib.aero_x_coarse_stamps
 fn.argtypes = [ctypes.c_void_p]
-out = (ctypes.c_ulonglong * 8)()
+out = (ctypes.c_ulonglong * 12)()
 vfn = lib.aero_x_viterbi_stamps
 vfn.argtypes = [ctypes.c_void_p]
 vout = (ctypes.c_ulonglong * 4)()
-names = ['prologue+ring+cis', 'FFT 1', 'boxcar+iFFT+square', 'FFT 3', 'hypot', 'log10 smoothing', 'fold search']
+names = ['prologue', 'ring to LDS + twiddles', 'table gathers + mix', 'FFT 1', 'boxcar+iFFT+square', 'FFT 3',
+         'hypot', 'log10 smoothing', 'fold search']
 for s in range(steps):
     views = [pool[:, int(o) + s * 4096:int(o) + (s + 1) * 4096] for o in offs]
     x = torch.stack(views).permute(2, 0, 1).reshape(4096, C).contiguous()
@@ -42,10 +43,10 @@ for s in range(steps):
         vfn(vout)
 fn(out)
 vfn(vout)
-tot = sum(out[:7])
-n = out[7]
+tot = sum(out[:9])
+n = out[11]
 print('channels %d, hops %d, s_memtime cycles per hop (wave 0) %.0f' % (C, n, tot / max(n, 1)))
-for k in range(7):
+for k in range(9):
     print('  %-20s %9.0f  %5.1f %%' % (names[k], out[k] / max(n, 1), 100.0 * out[k] / max(tot, 1)))
 eng.close()
 vn = vout[3]
