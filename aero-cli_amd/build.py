@@ -255,6 +255,15 @@ def build_diag(jobs=4):
     return [build_engine(jobs, variant=v, defines=d) for v, d in DIAG_VARIANTS.items()]
 
 
+# Timing / traffic-attribution builds (not bit-exact, never loaded by a test):
+# the demod without one buffer's accesses (scripts/pmc_demod_buffers.sh)
+DROP_VARIANTS = {'drop%d' % k: ['AERO_X_DROP=%d' % k] for k in (1, 2, 4, 8)}
+
+
+def build_drop(jobs=4):
+    return [build_engine(jobs, variant=v, defines=d) for v, d in DROP_VARIANTS.items()]
+
+
 if __name__ == '__main__':
     ap = argparse.ArgumentParser()
     ap.add_argument('--engine', action='store_true')

@@ -41,6 +41,13 @@ namespace aero {
 #define DM_TANH aero_tanh
 #define DM_SINCOS(x, s, c) aero_sincos(x, s, c)
 #endif
+// AERO_X_DROP (diagnostic builds only, never bit-exact): leave out one
+// buffer's HBM accesses to attribute the demod's PMC traffic buffer by buffer
+// (scripts/pmc_demod_buffers.sh): 1 coarse-ring writes, 2 soft-bit writes,
+// 4 the carrier event's rings (marg, dt, MSEcalc), 8 the AGC ring
+#ifndef AERO_X_DROP
+#define AERO_X_DROP 0
+#endif
 // a / c for a literal c: the exact three-operation sequence (aero_math.h div_c)
 #define DM_DIVC(a, c) div_c((a), (c))
 
@@ -401,7 +408,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
     // i+1's PCM word, which one sample ahead would be waited for at once
     pcm_next = S.pcm[(size_t)pb * C + c];
     pcm_next2 = S.pcm[(size_t)((pb + 1) & capm) * C + c];
-    agc_next = S.agc[(size_t)agc_ptr * C + c];
+    agc_next = (AERO_X_DROP & 8) ? 0.0 : S.agc[(size_t)agc_ptr * C + c];
   }
   const double PT = 0.4 * WTSIZE;  // IfHavePassedPoint(ee) with ee = 0.4 (oqpskdemodulator.cpp:225)
   // the two CIS table entries a sample uses, gathered a sample ahead (an L2
@@ -454,7 +461,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       {
         const int ap = agc_ptr + 1 == AGC_LEN ? 0 : agc_ptr + 1;
         pcm_next2 = S.pcm[(size_t)((pb + i + 2) & capm) * C + c];  // past the pushed samples: unused
-        agc_next = S.agc[(size_t)ap * C + c];
+        agc_next = (AERO_X_DROP & 8) ? 0.0 : S.agc[(size_t)ap * C + c];
       }
       const double dval = ((double)xs) / 32768.0;
       // mix (oqpskdemodulator.cpp:390): cval = CIS * dval, componentwise
@@ -497,7 +504,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       {
         agc_sum = agc_sum - agc_old;
         agc_sum = agc_sum + fabs(dab);
-        S.agc[(size_t)agc_ptr * C + c] = fabs(dab);
+        if (!(AERO_X_DROP & 8)) S.agc[(size_t)agc_ptr * C + c] = fabs(dab);
         agc_ptr++;
         if (agc_ptr == AGC_LEN) agc_ptr = 0;
         double g = div_n(1.414213562, fmax(DM_DIVC(agc_sum, ((double)AGC_LEN)), 0.000001));
@@ -567,7 +574,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
         const int k = m & (RING_GROUP - 1);
         {
           sh.ring[k][pair] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)pcm_next << 16);
-          if (k == RING_GROUP - 1) {
+          if (k == RING_GROUP - 1 && !(AERO_X_DROP & 1)) {
             uint32_t *dst = S.cring + (size_t)c * NFFT + ((m - (RING_GROUP - 1)) & (NFFT - 1));
             if (i + 1 - (RING_GROUP - 1) >= 1) {  // the whole group was staged by this launch
 #pragma unroll
@@ -605,9 +612,9 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       // the four moving-average rings of this symbol, loaded together
       // before any ring store so their latencies overlap
       const int dt_rp = (dt_p + 1) % DT_LEN;
-      const double marg_old = marg[marg_p];
-      const double2 dv = dtb[dt_rp];
-      const double2 pms_old = pmsb[pm_p];
+      const double marg_old = (AERO_X_DROP & 4) ? 0.0 : marg[marg_p];
+      const double2 dv = (AERO_X_DROP & 4) ? make_double2(0.0, 0.0) : dtb[dt_rp];
+      const double2 pms_old = (AERO_X_DROP & 4) ? make_double2(0.0, 0.0) : pmsb[pm_p];
       const double pm_old = pms_old.x, ms_old = pms_old.y;
       double ctx1 = sh.pd[PD_CTX1][pair], ctx2 = sh.pd[PD_CTX2][pair];
       double cty1 = sh.pd[PD_CTY1][pair], cty2 = sh.pd[PD_CTY2][pair];
@@ -636,12 +643,12 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       // marg->UpdateSigned (DSP.cpp:419-427)
       marg_sum = marg_sum - marg_old;
       marg_sum = marg_sum + (ct_ec);
-      marg[marg_p] = ct_ec;
+      if (!(AERO_X_DROP & 4)) marg[marg_p] = ct_ec;
       marg_p++;
       marg_p %= MARG_LEN;
       const double mval = DM_DIVC(marg_sum, ((double)MARG_LEN));
       // dt.update (DSP.h:456-461): slot p written, slot p+1 read
-      dtb[dt_p] = make_double2(qr, qi);
+      if (!(AERO_X_DROP & 4)) dtb[dt_p] = make_double2(qr, qi);
       dt_p = dt_rp;
       qr = dv.x;
       qi = dv.y;
@@ -671,7 +678,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
         const double v = (tda * tda) + (tdb * tdb);
         ms_sum = ms_sum - ms_old;
         ms_sum = ms_sum + fabs(v);
-        pmsb[pms_slot] = make_double2(fabs(av), fabs(v));
+        if (!(AERO_X_DROP & 4)) pmsb[pms_slot] = make_double2(fabs(av), fabs(v));
         ms_p++;
         ms_p %= MSE_LEN;
         mse = DM_DIVC(ms_sum, ((double)MSE_LEN));
@@ -684,7 +691,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
         if (rbit > 255) rbit = 255;
         if (rbit < 0) rbit = 0;
         const long long softp = sh.pl[PL_SOFTP][pair];
-        {
+        if (!(AERO_X_DROP & 2)) {
           uint8_t *soft = S.soft + (size_t)cl * SOFT_RING;
           soft[softp & (SOFT_RING - 1)] = (uint8_t)ibit;
           soft[(softp + 1) & (SOFT_RING - 1)] = (uint8_t)rbit;
