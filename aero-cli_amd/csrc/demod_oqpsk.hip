@@ -179,7 +179,7 @@ __device__ __forceinline__ void lds_store(int *p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-constexpr int FIR_LDS_IM = (NTAPS - 1) / 2, FIR_LDS_RE = 21;
+constexpr int FIR_LDS_IM = 11, FIR_LDS_RE = 5;
 
 struct DemodShared {
   uint32_t ring[RING_GROUP][DEMOD_BLOCK];
@@ -192,9 +192,9 @@ struct DemodShared {
   double2 r53[2][DEMOD_BLOCK];
   unsigned long long mask[2][4];
   int cseq[4], fseq[4];
-  // the FIR wave's oldest partial sums: imaginary R_0..R_26 and real
-  // R_0..R_20 (the other 60 are registers; all 108 would leave the wave no
-  // room below the 256 VGPRs of two waves per SIMD)
+  // the FIR wave's oldest partial sums: imaginary R_0..R_10 and real
+  // R_0..R_4 (the other 92 are registers; with the short division sequences
+  // the kernel holds 227 VGPRs, and 4 sums fewer in LDS spill)
   double qil[FIR_LDS_IM][DEMOD_BLOCK];
   double qrl[FIR_LDS_RE][DEMOD_BLOCK];
 };
@@ -218,8 +218,8 @@ __device__ __forceinline__ void add_masked(double &dst, double a, double b, unsi
 // The RRC (FIR::FIRUpdateAndProcess, decode/DSP.cpp:290-304) in transposed
 // form, R_j(n) = R_{j-1}(n-1) + h[j] x(n), j = 0..54: the filter output used
 // at sample n is R_54(n-1), so only R_54's update is on the chain.  This wave
-// holds R_0..R_53 of its 64 channels (real R_21..R_53 and imaginary
-// R_27..R_53 in registers, the older ones in LDS) and, per chain iteration,
+// holds R_0..R_53 of its 64 channels (real R_5..R_53 and imaginary
+// R_11..R_53 in registers, the older ones in LDS) and, per chain iteration,
 // takes the mixed samples the chain wave published, forms R_53 first and
 // hands it back (the chain forms R_54 = R_53 + h[54] x itself), then updates
 // the rest while the chain runs on.  h[j] == h[54 - j] bit for bit
