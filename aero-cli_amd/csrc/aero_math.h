@@ -166,6 +166,44 @@ AERO_HD double aero_hypot(double x, double y) {
   return hypot_kernel(ax, ay);
 }
 
+/* aero_hypot for finite x, y with max(|x|, |y|) in [2^-200, 2^200], without
+ * a branch (callers check the range for a whole wave and fall back to
+ * aero_hypot otherwise): there glibc takes neither scaling path, the sum of
+ * squares needs no sqrt range scaling, and the correction's quotient
+ * (t1 + t2) / (2h) is zero or at least 2^-560 in magnitude (t1 + t2 is a
+ * multiple of ulp(ay^2 / 4) >= 2^-562 unless ay <= ax 2^-54, whose kernel
+ * result is discarded), so the division sequence needs neither v_div_scale
+ * nor v_div_fixup.  Both sides of the kernel's h <= 2ay test are evaluated
+ * and selected, as the wave executes both anyway when its lanes differ. */
+AERO_HD double aero_hypot_nr(double x, double y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  x = __builtin_fabs(x);
+  y = __builtin_fabs(y);
+  const double ax = x < y ? y : x, ay = x < y ? x : y;
+  const double s = ax * ax + ay * ay;
+  const double rs = __builtin_amdgcn_rsq(s);
+  double g = s * rs, hh = rs * 0.5;
+  const double r0 = fma(-hh, g, 0.5);
+  g = fma(g, r0, g);
+  hh = fma(hh, r0, hh);
+  g = fma(fma(-g, g, s), hh, g);
+  const double h = fma(fma(-g, g, s), hh, g);  // sqrt(s), the compiler's sequence
+  const double d1 = h - ay, d2 = h - ax;
+  const double t1a = ax * (2.0 * d1 - ax), t2a = (d1 - 2.0 * (ax - ay)) * d1;
+  const double t1b = 2.0 * d2 * (ax - 2.0 * ay), t2b = (4.0 * d2 - ay) * ay + d2 * d2;
+  const bool near = h <= 2.0 * ay;
+  const double num = (near ? t1a : t1b) + (near ? t2a : t2b), den = 2.0 * h;
+  double r = __builtin_amdgcn_rcp(den);
+  r = fma(r, fma(-den, r, 1.0), r);
+  r = fma(r, fma(-den, r, 1.0), r);
+  const double q0 = num * r;
+  const double q = num == 0.0 ? q0 : fma(fma(-den, q0, num), r, q0);
+  return ay <= ax * 0x1p-54 ? ax + ay : h - q;
+#else
+  return aero_hypot(x, y);
+#endif
+}
+
 /* ------------------------------------------------------ expm1 / tanh */
 AERO_HD double aero_expm1(double x) {
   const double o_threshold = 7.09782712893383973096e+02, ln2_hi = 6.93147180369123816490e-01,

@@ -26,9 +26,11 @@ namespace aero {
 
 #ifdef AERO_X_OCML  // timing experiment only (see demod_oqpsk.hip)
 #define CO_HYPOT ::hypot
+#define CO_HYPOT_NR ::hypot
 #define CO_LOG10 ::log10
 #else
 #define CO_HYPOT aero_hypot
+#define CO_HYPOT_NR aero_hypot_nr
 #define CO_LOG10 aero_log10
 #endif
 
@@ -310,10 +312,26 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   // one (chain::gx), after which every wave only works in registers, so the
   // LDS is free for |X| as soon as this wave gets here
   double *ylds = lds;  // [ypad(YLEN)]: bin k - YLO at ypad(k - YLO)
+  // |X| by aero_hypot_nr when every value of the wave is in its range (the
+  // usual case: |X| of a live channel is ~1e9), else by aero_hypot
+  bool nr = true;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int yi = (bin_t | chain::out_bin_reg<L>(i)) ^ (N / 2);
-    if (yi >= K::YLO && yi <= K::YHI) ylds[fftl::ypad(yi - K::YLO)] = CO_HYPOT(x[i].x, x[i].y);
+    const double a = fabs(x[i].x), b = fabs(x[i].y);
+    nr = nr && a <= 0x1p200 && b <= 0x1p200 && (a >= 0x1p-200 || b >= 0x1p-200);
+  }
+  if (__all(nr)) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int yi = (bin_t | chain::out_bin_reg<L>(i)) ^ (N / 2);
+      if (yi >= K::YLO && yi <= K::YHI) ylds[fftl::ypad(yi - K::YLO)] = CO_HYPOT_NR(x[i].x, x[i].y);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int yi = (bin_t | chain::out_bin_reg<L>(i)) ^ (N / 2);
+      if (yi >= K::YLO && yi <= K::YHI) ylds[fftl::ypad(yi - K::YLO)] = CO_HYPOT(x[i].x, x[i].y);
+    }
   }
   double yp2 = yload(t + 2 * FT);
   __syncthreads();

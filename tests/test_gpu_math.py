@@ -80,3 +80,26 @@ def test_short_division_and_sqrt_sequences_are_ieee(engine_lib):
                               ('sqrt_n', np.abs(m), d, np.sqrt(np.abs(m)))):
             assert np.array_equal(eng.device_math(fn, x, y).view(np.uint64), ref.view(np.uint64)), fn
     eng.close()
+
+
+@pytest.mark.gpu
+def test_hypot_normal_range_variant_is_glibc(engine_lib):
+    """aero_hypot_nr (the coarse kernel's branch-free |X| for waves whose
+    values are all in [2^-200, 2^200]) equals glibc hypot bit for bit there,
+    including ratios below 2^-54, exact cases and equal components."""
+    import aero_engine as ae
+    import mathhost
+    eng = ae.Engine(max_channels=1)
+    rng = np.random.default_rng(23)
+    n = 500000
+    a = rng.choice([-1.0, 1.0], n) * np.exp2(rng.uniform(-199, 199, n)) * rng.uniform(1, 2, n)
+    ints = rng.integers(1, 1 << 20, (2, n)).astype(np.float64)                  # exact cases (3, 4 -> 5, ...)
+    cases = [(a, rng.choice([-1.0, 1.0], n) * np.exp2(rng.uniform(-199, 199, n))),   # any ratio
+             (a, a * np.exp2(rng.uniform(-70, 0, n))),                                  # around the 2^-54 cut
+             (a, a * (1 + rng.standard_normal(n) * 1e-9)),                              # |x| ~ |y|
+             (ints[0], ints[1])]
+    for x, b in cases:
+        got = eng.device_math('hypot_nr', x, b)
+        ref = mathhost.glibc('hypot', x, b)
+        assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
+    eng.close()
