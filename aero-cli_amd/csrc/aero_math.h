@@ -47,41 +47,38 @@ AERO_HD double sethi(double x, uint32_t hi) {
 }
 AERO_HD double mkd(uint32_t hi, uint32_t lo) { return u2d(((uint64_t)hi << 32) | lo); }
 
-/* ------------------------------------------- IEEE division and sqrt
- * The same correctly rounded results as the `/` and sqrt() the compiler
- * emits, with shorter instruction chains where the operands are in a range
- * that needs none of the range handling (on the host these are the plain
- * IEEE operations):
+/* ----------------------------------------------------- IEEE division
+ * The same correctly rounded quotient as the `/` the compiler emits, in
+ * fewer dependent operations, for operands whose range the caller knows
+ * (host: the plain division):
  *
  *  div_c(a, c)     a / c for a compile-time constant c: q0 = RN(a rc) with
  *                  rc = RN(1/c) folded by the compiler, the residual a - c q0
  *                  exact by fma, q = RN(q0 + r rc) = RN(a / c) (Markstein's
  *                  theorem: rc within half an ulp of 1/c, q0 within one ulp
  *                  of a/c, no underflow).  3 dependent operations instead of
- *                  the 10 of a division.
+ *                  the 10 of a division; a power-of-two c is one product.
  *  rcp_div(b)      v_rcp_f64 and the two Newton steps of the compiler's f64
- *  div_r(a, b, r)  division, then its final q = a r, r' = a - b q, q + r' r.
- *                  Without v_div_scale (the identity for these operands) and
- *                  v_div_fixup (the identity for a finite normal quotient),
- *                  this is that sequence instruction for instruction; two
- *                  divisions by one b share the reciprocal.
- *  sqrt_n(x)       the compiler's f64 sqrt sequence (rsq, two Goldschmidt /
- *                  two Newton corrections) without its 2^-767 scaling and its
- *                  zero / infinity selects.
+ *  div_r(a, b, r)  division, then its final q = a r, r' = a - b q, q + r' r:
+ *                  that sequence instruction for instruction without
+ *                  v_div_scale (the identity when b and 1/b are normal, the
+ *                  quotient is normal and a's exponent exceeds -970) and
+ *                  v_div_fixup (the identity for a finite nonzero quotient);
+ *                  two divisions by one b share the reciprocal.
  *
- * Outside the ranges where those steps are identities (zero, tiny or huge
- * operands, NaN, infinity) each falls back to the IEEE operation, a branch
- * the demods' values never take.  tests/test_gpu_math.py compares every
- * helper with the IEEE operation on the device, edge ranges included. */
-AERO_HD bool div_ok(double a) { return __builtin_fabs(a) >= 0x1p-500 && __builtin_fabs(a) <= 0x1p500; }
-
+ * Contract, argued at every call site: a is zero (its signed zero quotient
+ * is selected, as IEEE gives) or |a| >= 2^-969 and the quotient is normal,
+ * or the caller's next step absorbs any tiny quotient (a max with a floor,
+ * a sum with a phase pointer).  No branch: a guarded version split the
+ * demods' basic blocks and cost more than it saved.  tests/test_gpu_math.py
+ * compares them with the IEEE division on the device. */
 AERO_HD double div_c(double a, double c) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const double rc = 1.0 / c;  // folded: c is a literal at every call site
   if ((d2u(c) & 0x000fffffffffffffULL) == 0) return a * rc;  // a power of two: exact product (folded)
-  if (__builtin_expect(!div_ok(a), 0)) return a / c;
   const double q0 = a * rc;
-  return fma(fma(-c, q0, a), rc, q0);
+  const double q = fma(fma(-c, q0, a), rc, q0);
+  return a == 0.0 ? q0 : q;
 #else
   return a / c;
 #endif
@@ -100,7 +97,6 @@ AERO_HD double rcp_div(double b) {
 
 AERO_HD double div_r(double a, double b, double r) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if (__builtin_expect(!((div_ok(a) || a == 0.0) && div_ok(b)), 0)) return a / b;
   const double q = a * r;  // a zero quotient keeps a r's sign, as IEEE 0 / b
   const double f = fma(fma(-b, q, a), r, q);
   return a == 0.0 ? q : f;
@@ -112,25 +108,10 @@ AERO_HD double div_r(double a, double b, double r) {
 
 AERO_HD double div_n(double a, double b) { return div_r(a, b, rcp_div(b)); }
 
-AERO_HD double sqrt_n(double x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  if (__builtin_expect(!(x >= 0x1p-767 && x <= 0x1.fffffffffffffp1023), 0)) return sqrt(x);
-  const double y = __builtin_amdgcn_rsq(x);
-  double g = x * y, h = y * 0.5;
-  const double r = fma(-h, g, 0.5);
-  g = fma(g, r, g);
-  h = fma(h, r, h);
-  g = fma(fma(-g, g, x), h, g);
-  return fma(fma(-g, g, x), h, g);
-#else
-  return sqrt(x);
-#endif
-}
-
 /* ------------------------------------------------------------- hypot */
 AERO_HD double hypot_kernel(double ax, double ay) {
   double t1, t2;
-  double h = sqrt_n(ax * ax + ay * ay);
+  double h = sqrt(ax * ax + ay * ay);
   if (h <= 2.0 * ay) {
     double delta = h - ay;
     t1 = ax * (2.0 * delta - ax);
@@ -140,7 +121,7 @@ AERO_HD double hypot_kernel(double ax, double ay) {
     t1 = 2.0 * delta * (ax - 2.0 * ay);
     t2 = (4.0 * delta - ay) * ay + delta * delta;
   }
-  h -= div_n(t1 + t2, 2.0 * h);
+  h -= (t1 + t2) / (2.0 * h);
   return h;
 }
 
@@ -204,6 +185,17 @@ AERO_HD double aero_hypot_nr(double x, double y) {
 #endif
 }
 
+/* aero_hypot with aero_hypot_nr when every active lane of the wave is in its
+ * range (one uniform branch), the general code otherwise */
+AERO_HD double aero_hypot_w(double x, double y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double a = __builtin_fabs(x), b = __builtin_fabs(y);
+  const bool nr = a <= 0x1p200 && b <= 0x1p200 && (a >= 0x1p-200 || b >= 0x1p-200);
+  if (__builtin_expect(__all(nr), 1)) return aero_hypot_nr(x, y);
+#endif
+  return aero_hypot(x, y);
+}
+
 /* ------------------------------------------------------ expm1 / tanh */
 AERO_HD double aero_expm1(double x) {
   const double o_threshold = 7.09782712893383973096e+02, ln2_hi = 6.93147180369123816490e-01,
@@ -259,7 +251,7 @@ AERO_HD double aero_expm1(double x) {
   R3 = Q4 + hxs * Q5;
   r1 = R1 + h2 * R2 + h4 * R3;
   t = 3.0 - r1 * hfx;
-  e = hxs * div_n(r1 - t, 6.0 - x * t);
+  e = hxs * ((r1 - t) / (6.0 - x * t));
   if (k == 0) return x - (x * e - hxs);
   e = (x * (e - c) - c);
   e -= hxs;
@@ -301,10 +293,10 @@ AERO_HD double aero_tanh(double x) {
     if (ix < 0x3c800000) return x * (1.0 + x);
     if (ix >= 0x3ff00000) {
       t = aero_expm1(2.0 * __builtin_fabs(x));
-      z = 1.0 - div_n(2.0, t + 2.0);
+      z = 1.0 - 2.0 / (t + 2.0);
     } else {
       t = aero_expm1(-2.0 * __builtin_fabs(x));
-      z = div_n(-t, t + 2.0);
+      z = -t / (t + 2.0);
     }
   } else {
     z = 1.0 - 1e-300;
@@ -504,7 +496,11 @@ AERO_HD double aero_atan2(double y, double x) {
   }
   double u, du;
   {
-    // u = a / b and du = ((a - v) - vv) / b: one reciprocal for both
+    // u = a / b and du = ((a - v) - vv) / b: one reciprocal for both.  After
+    // the early returns and the 2^+-500 scalings a, b are in [2^-574, 2^524]
+    // within 57 binades, u in [2^-58, 1], and du's numerator (the exact
+    // residual a - b u) is zero or at least a 2^-104, so div_r's contract
+    // holds.
     const double a = ax > ay ? ay : ax, b = ax > ay ? ax : ay;
     const double r = rcp_div(b);
     u = div_r(a, b, r);

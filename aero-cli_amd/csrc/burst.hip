@@ -277,6 +277,7 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
       S.agc[(size_t)agc_p * C + c] = fabs(av);
       agc_p = agc_p + 1 == B_AGC ? 0 : agc_p + 1;
       agc_n = S.agc[(size_t)agc_p * C + c];  // written B_AGC samples ago
+      // short exact divisions (aero_math.h): a tiny agc_sum / B_AGC is floored at 1e-6
       double g = div_n(1.414213562, fmax(div_c(agc_sum, ((double)B_AGC)), 0.000001));
       g = fmax(g, 0.000001);
       cr *= g;
@@ -296,12 +297,12 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
       ma1i = ma1i + pi;
       S.ma1[(size_t)ma1_p * C + c] = make_double2(pr, pi);
       ma1_p = ma1_p + 1 == B_MA ? 0 : ma1_p + 1;
-      fastarm = aero_hypot(div_c(ma1r, ((double)B_MA)), div_c(ma1i, ((double)B_MA)));
+      fastarm = aero_hypot(ma1r / ((double)B_MA), ma1i / ((double)B_MA));
       mav1_sum = mav1_sum - mv_old;
       mav1_sum = mav1_sum + (fastarm);
       S.mav1[(size_t)mav1_p * C + c] = fastarm;
       mav1_p = mav1_p + 1 == B_MA ? 0 : mav1_p + 1;
-      fastarm = div_c(mav1_sum, ((double)B_MA));
+      fastarm = mav1_sum / ((double)B_MA);
       fastarm -= dly_commit(mdr, C, dl_md, mdp, fastarm);
       md_older = md_newer;
       md_newer = md_next;
@@ -607,7 +608,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
     }
     if ((cntr > SPS * (128 + 10)) && (cntr < ((256 - 10) * SPS))) {  // symbol-tone PLL (:462-474)
       const double progress =
-          div_c(((double)cntr) - (SPS * (128 + 10)), (double)(((256 - 10) * SPS) - (SPS * (128 + 10))));
+          div_c(((double)cntr) - (SPS * (128 + 10)), (double)(((256 - 10) * SPS) - (SPS * (128 + 10))));  // integer numerator
       const double t1r = s2r * str_r - s2i * str_i, t1i = s2r * str_i + s2i * str_r;
       const double spr = t1r * 0.0 - t1i * 1.0, spi = t1r * 1.0 + t1i * 0.0;  // * imag
       const double er = aero_tanh(spi) * (spr);
@@ -624,7 +625,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       double st_err = aero_atan2(er_i, er_r);
       st_err *= 1.5 * (1.0 - progress * progress);
       b_advance(q_ptr, -(1.0 / (2.0 * M_PI)) * st_err * 0.1);
-      b_set_phase_deg(so_ptr, div_c(360.0 * q_ptr, ((double)WTSIZE)) * 4.0 + (360.0 * 0.4));
+      b_set_phase_deg(so_ptr, (360.0 * q_ptr / ((double)WTSIZE)) * 4.0 + (360.0 * 0.4));
       so_n = T.cis[b_cis_index(so_ptr)];
     }
     {  // sig2 *= symboltone_averotator; rotator *= exp(i rotator_freq); sig2 *= rotator
@@ -645,14 +646,14 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       S.agc2[(size_t)agc2_p * C + c] = fabs(sa);
       agc2_p = agc2_p + 1 == B_AGC2 ? 0 : agc2_p + 1;
       agc2_n = S.agc2[(size_t)agc2_p * C + c];  // written B_AGC2 samples ago
-      double g = div_n(1.414213562, fmax(div_c(agc2_sum, ((double)B_AGC2)), 0.000001));
+      double g = div_n(1.414213562, fmax(div_c(agc2_sum, ((double)B_AGC2)), 0.000001));  // as the AGC above
       g = fmax(g, 0.000001);
       s2r *= g;
       s2i *= g;
     }
     const double abval = aero_hypot(s2r, s2i);
     if (abval > 2.84) {
-      const double k = div_n(2.84, abval);
+      const double k = div_n(2.84, abval);  // abval > 2.84
       s2r = k * s2r;
       s2i = k * s2i;
     }
@@ -681,7 +682,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       const double st_angle_error = aero_atan2(oim, ore);
       if (cntr > SPS * (128 + 64)) {
         b_set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
-        b_advance(so_ptr, div_c(-st_angle_error * 0.01, 360.0));
+        b_advance(so_ptr, div_c(-st_angle_error * 0.01, 360.0));  // a tiny quotient vanishes in so_ptr + x W
       }
       if (so_freq < (10500.0 - 0.1)) b_set_freq(so_freq, so_step, (10500.0 - 0.1));
       if (so_freq > (10500.0 + 0.1)) b_set_freq(so_freq, so_step, (10500.0 + 0.1));
@@ -692,11 +693,11 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       if (tl < 0.0) tl += WTSIZE;
       if (tw < 0.0) tw += WTSIZE;
       if ((tl > 3.0 * WTSIZE / 4.0) && (tw < 1.0 * WTSIZE / 4.0)) {
-        const double pt_last = div_n(tw, so_step);
+        const double pt_last = div_n(tw, so_step);  // tw: 0 or >= 2^-40, so_step ~4375
         const double pt_this = 1.0 - pt_last;
         const double ptr_ = pt_this * s2r + pt_last * s2l_r, pti = pt_this * s2i + pt_last * s2l_i;
         const double twospeed =
-            -4.0 * (div_c(b_fmod360(div_c(360.0 * q_ptr, ((double)WTSIZE)) * 2.0 + (360.0 * 0.4 * 0.5)), 360.0) -
+            -4.0 * ((b_fmod360((360.0 * q_ptr / ((double)WTSIZE)) * 2.0 + (360.0 * 0.4 * 0.5)) / 360.0) -
                     (0.34046 + 0.4111 * 0.4));
         const bool even = !(twospeed < 0);
         yui++;

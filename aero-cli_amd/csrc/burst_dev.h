@@ -30,6 +30,7 @@ __device__ __forceinline__ void b_nco_next(double &ptr, double &step) {  // WTne
 __device__ __forceinline__ void b_set_freq(double &freq, double &step, double f) {  // SetFreq (DSP.cpp:163-168)
   freq = f;
   if (freq < 0) freq = 0;
+  // freq: 10500 +- 0.1 (st_osc), a multiple of 48000 / 32768 (trident decisions) or 0
   step = div_c((freq) * ((double)WTSIZE), 48000.0);
 }
 
@@ -48,7 +49,7 @@ __device__ __forceinline__ double b_fmod360(double x) {
 __device__ __forceinline__ void b_set_phase_deg(double &ptr, double phase_deg) {  // SetPhaseDeg (DSP.cpp:177-187)
   phase_deg = b_fmod360(phase_deg);
   while (phase_deg < 0) phase_deg += 360.0;
-  ptr = div_c(phase_deg, 360.0) * ((double)WTSIZE);
+  ptr = (phase_deg / 360.0) * ((double)WTSIZE);
 }
 
 __device__ __forceinline__ void b_advance(double &ptr, double frac) {  // AdvanceFractionOfWave (DSP.h:59-65)

@@ -156,6 +156,7 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
       S.agc[(size_t)agc_p * C + c] = fabs(av);
       agc_p = agc_p + 1 == B_AGC ? 0 : agc_p + 1;
       agc_n = S.agc[(size_t)agc_p * C + c];  // written B_AGC samples ago
+      // short exact divisions (aero_math.h): a tiny agc_sum / B_AGC is floored at 1e-6
       double g = div_n(1.414213562, fmax(div_c(agc_sum, ((double)B_AGC)), 0.000001));
       g = fmax(g, 0.000001);
       cr *= g;
@@ -179,12 +180,12 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
       ma1i = ma1i + pi;
       S.ma1[(size_t)ma1_p * C + c] = make_double2(pr, pi);
       ma1_p = ma1_p + 1 == M_MA ? 0 : ma1_p + 1;
-      fastarm = aero_hypot(div_c(ma1r, ((double)M_MA)), div_c(ma1i, ((double)M_MA)));
+      fastarm = aero_hypot(ma1r / ((double)M_MA), ma1i / ((double)M_MA));
       mav1_sum = mav1_sum - mv_old;
       mav1_sum = mav1_sum + (fastarm);
       S.mav1[(size_t)mav1_p * C + c] = fastarm;
       mav1_p = mav1_p + 1 == M_MA ? 0 : mav1_p + 1;
-      fastarm = div_c(mav1_sum, ((double)M_MA));
+      fastarm = mav1_sum / ((double)M_MA);
       madiff[(size_t)madiff_p * C] = fastarm;  // bt_ma_diff.update(fastarm), whole-sample delay
       madiff_p = mdo;
       md_older = md_new;
@@ -456,13 +457,13 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         const double spi2 = (0.0 * a1_new + (1.0 - 0.0) * a1_old);
         double progress = (double)cntr - (MSPS * (M_START));
         const double goal = M_ENDROT - (MSPS * M_START);
-        progress = div_c(progress, goal);  // goal is a compile-time constant
+        progress = div_c(progress, goal);  // goal a compile-time constant, progress an integer
         const double2 hv = h_n;
         const double er_r = hv.x * spr - hv.y * (-spi2), er_i = hv.x * (-spi2) + hv.y * spr;
         double st_err = aero_atan2(er_i, er_r);
         st_err *= 0.5 * (1.0 - progress * progress);
         b_advance(sh_ptr, -(1.0 / (2.0 * M_PI)) * st_err * 0.05);
-        b_set_phase_deg(so_ptr, div_c(360.0 * sh_ptr, ((double)WTSIZE)) + (360.0 * (1.0 - M_EE)));
+        b_set_phase_deg(so_ptr, (360.0 * sh_ptr / ((double)WTSIZE)) + (360.0 * (1.0 - M_EE)));
         so_n = T.cis[b_cis_index(so_ptr)];
       }
       {  // sig2 *= symboltone_averotator; rotator *= exp(i rotator_freq); sig2 *= rotator
@@ -483,14 +484,14 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         S.agc2[(size_t)agc2_p * C + c] = fabs(sa);
         agc2_p = agc2_p + 1 == M_AGC2 ? 0 : agc2_p + 1;
         agc2_n = S.agc2[(size_t)agc2_p * C + c];  // written M_AGC2 samples ago
-        double g = div_n(1.414213562, fmax(div_c(agc2_sum, ((double)M_AGC2)), 0.000001));
+        double g = div_n(1.414213562, fmax(div_c(agc2_sum, ((double)M_AGC2)), 0.000001));  // as above
         g = fmax(g, 0.000001);
         s2r *= g;
         s2i *= g;
       }
       const double abval = aero_hypot(s2r, s2i);
       if (abval > 2.84) {
-        const double k = div_n(2.84, abval);
+        const double k = div_n(2.84, abval);  // abval > 2.84
         s2r = k * s2r;
         s2i = k * s2i;
       }
@@ -522,7 +523,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       const double2 so = so_n;
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
       const double st_angle_error = aero_atan2(oim, ore);
-      if (cntr > M_ENDROT) b_advance(so_ptr, div_c(-st_angle_error * 0.002, 360.0));
+      if (cntr > M_ENDROT) b_advance(so_ptr, div_c(-st_angle_error * 0.002, 360.0));  // tiny: vanishes in so_ptr
       {  // IfHavePassedPoint(ee) (DSP.cpp:222-238) and the symbol step (:617-693)
         double tl = so_last - PT, tw = so_ptr - PT;
         if (tl < 0.0) tl += WTSIZE;
@@ -555,7 +556,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
             mm[msema_p] = fabs(v);
             msema_p = msema_p + 1 == M_MSEMA ? 0 : msema_p + 1;
             mm_n = mm[msema_p];  // written M_MSEMA updates ago
-            mse = div_c(msema_sum, ((double)M_MSEMA));
+            mse = msema_sum / ((double)M_MSEMA);
           }
           {  // differential soft bits, imag first, real negated (:664-686)
             const double imagin = m_diff_soft(diff_last, pdi);

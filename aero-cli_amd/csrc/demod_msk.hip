@@ -219,19 +219,20 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
         if (!QREG && (j & 7) == 0) asm volatile("" : : : "memory");
       }
       QI(0) = 0.0 + s_taps[0] * cvi;
-      const double dab = sqrt_n(s2r * s2r + s2i * s2i);
+      const double dab = sqrt(s2r * s2r + s2i * s2i);
       {  // AGC::Update (DSP.cpp:371-380)
         agc_sum = agc_sum - agc_old;
         agc_sum = agc_sum + fabs(dab);
         S.agc[(size_t)(n % AGC) * C + c] = fabs(dab);
+        // short exact divisions (aero_math.h): a tiny agc_sum / AGC is floored at 1e-6
         double g = div_n(1.414213562, fmax(div_c(agc_sum, ((double)AGC)), 0.000001));
         g = fmax(g, 0.000001);
         s2r *= g;
         s2i *= g;
       }
-      const double ab = sqrt_n(s2r * s2r + s2i * s2i);
+      const double ab = sqrt(s2r * s2r + s2i * s2i);
       if (ab > 2.84) {
-        const double k = div_n(2.84, ab);
+        const double k = div_n(2.84, ab);  // ab > 2.84
         s2r = k * s2r;
         s2i = k * s2i;
       }
@@ -316,17 +317,17 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       const double carrier_aggression = 12.0 * 1.0;  // correctionfactor 1.0 (fb < 1200)
       {  // mixer2.IncresePhaseDeg (DSP.cpp:177-187)
         double phase_deg = carrier_aggression * 1.0 * ct_ec;
-        phase_deg += div_c(360.0 * m2_ptr, ((double)WTSIZE));
+        phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
         phase_deg = fmod(phase_deg, 360.0);
         while (phase_deg < 0) phase_deg += 360.0;
-        m2_ptr = div_c(phase_deg, 360.0) * ((double)WTSIZE);
+        m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
       }
       {  // mixer2.IncreseFreqHz -> SetFreq(double) (DSP.cpp:163-175)
         double f = carrier_aggression * 0.01 * ct_ec;
         f += m2_freq;
         m2_freq = f;
         if (m2_freq < 0) m2_freq = 0;
-        m2_step = div_c((m2_freq) * ((double)WTSIZE), FS);
+        m2_step = (m2_freq) * ((double)WTSIZE) / FS;
       }
       int cl = c;
       asm volatile("" : "+v"(cl));
@@ -339,7 +340,7 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
         marg_sum = marg_sum - mb[p];
         marg_sum = marg_sum + (nv);
         mb[p] = nv;
-        mval = div_c(marg_sum, ((double)MARG));
+        mval = marg_sum / ((double)MARG);
       }
       // dt.update(pt_msk) (DSP.h:463-467)
       double pr, pi;
@@ -370,7 +371,7 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
         ms_sum = ms_sum - mb[p];
         ms_sum = ms_sum + fabs(v);
         mb[p] = fabs(v);
-        mse = div_c(ms_sum, ((double)MSK_MSEMA));
+        mse = ms_sum / ((double)MSK_MSEMA);
       }
       {  // differential soft bits, imag first, real negated (mskdemodulator.cpp:381-401)
         const double imagin = diff_soft(diff_last, pi);

@@ -36,7 +36,7 @@ namespace aero {
 #define DM_TANH ::tanh
 #define DM_SINCOS(x, s, c) ::sincos(x, &(s), &(c))
 #else
-#define DM_HYPOT aero_hypot
+#define DM_HYPOT aero_hypot_w
 #define DM_ATAN2 aero_atan2
 #define DM_TANH aero_tanh
 #define DM_SINCOS(x, s, c) aero_sincos(x, s, c)
@@ -48,8 +48,7 @@ namespace aero {
 #ifndef AERO_X_DROP
 #define AERO_X_DROP 0
 #endif
-// a / c for a literal c: the exact three-operation sequence (aero_math.h div_c)
-#define DM_DIVC(a, c) div_c((a), (c))
+#define DM_DIVC(a, c) ((a) / (c))
 
 // AERO_X_STAMPS (diagnostic build only): s_memtime cycle totals per loop
 // section of wave 0 of workgroup 0, with scheduling barriers at the stamps
@@ -93,6 +92,13 @@ __device__ __forceinline__ void set_freq(double &freq, double &step, double f) {
   freq = f;
   if (freq < 0) freq = 0;
   step = DM_DIVC((freq) * ((double)WTSIZE), 48000.0);
+}
+// the same for st_osc, whose frequency stays within 10500 +- 0.1 (+ one
+// nudge of at most pi 1e-8): the short exact division (aero_math.h div_c)
+__device__ __forceinline__ void set_freq_st(double &freq, double &step, double f) {
+  freq = f;
+  if (freq < 0) freq = 0;
+  step = div_c((freq) * ((double)WTSIZE), 48000.0);
 }
 
 // Delay<double>::update (DSP.h:365-384) as a shift register: h[0] is the
@@ -500,14 +506,16 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       }
       it = __builtin_amdgcn_readfirstlane(it + 1);
       // AGC (DSP.cpp:371-380) on |sig2| (oqpskdemodulator.cpp:399-405)
-      const double dab = sqrt_n(s2r * s2r + s2i * s2i);
+      const double dab = sqrt(s2r * s2r + s2i * s2i);
       {
         agc_sum = agc_sum - agc_old;
         agc_sum = agc_sum + fabs(dab);
         if (!(AERO_X_DROP & 8)) S.agc[(size_t)agc_ptr * C + c] = fabs(dab);
         agc_ptr++;
         if (agc_ptr == AGC_LEN) agc_ptr = 0;
-        double g = div_n(1.414213562, fmax(DM_DIVC(agc_sum, ((double)AGC_LEN)), 0.000001));
+        // short exact divisions: a tiny quotient of agc_sum is floored at 1e-6, so
+        // the divisor of g is in [1e-6, ~10]
+        double g = div_n(1.414213562, fmax(div_c(agc_sum, ((double)AGC_LEN)), 0.000001));
         g = fmax(g, 0.000001);
         s2r *= g;
         s2i *= g;
@@ -530,12 +538,14 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       const double m1r = st_eta, m1i = -delay_tap<3, 2, 1>(d8, c_dly[3], st_eta);
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
       const double st_angle_error = DM_ATAN2(oim, ore);
-      set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
-      so_ptr += DM_DIVC(-st_angle_error * 0.01, 360.0) * WTSIZE;
+      set_freq_st(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
+      // (a quotient below 2^-969 could differ from IEEE in its last
+      // subnormal bit, and vanishes in so_ptr + x W either way)
+      so_ptr += div_c(-st_angle_error * 0.01, 360.0) * WTSIZE;
       while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
       while (so_ptr < 0) so_ptr += WTSIZE;
-      if (so_freq < (10500.0 - 0.1)) set_freq(so_freq, so_step, (10500.0 - 0.1));
-      if (so_freq > (10500.0 + 0.1)) set_freq(so_freq, so_step, (10500.0 + 0.1));
+      if (so_freq < (10500.0 - 0.1)) set_freq_st(so_freq, so_step, (10500.0 - 0.1));
+      if (so_freq > (10500.0 + 0.1)) set_freq_st(so_freq, so_step, (10500.0 + 0.1));
       if (!s2l_init) {
         s2l_re = s2r;
         s2l_im = s2i;
@@ -547,7 +557,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       if (tl < 0.0) tl += WTSIZE;
       if (tw < 0.0) tw += WTSIZE;
       if ((tl > 3.0 * WTSIZE / 4.0) && (tw < 1.0 * WTSIZE / 4.0)) {
-        const double pt_last = div_n(tw, so_step);
+        const double pt_last = div_n(tw, so_step);  // tw: 0 or >= 2^-40 (a phase difference), so_step ~4375
         const double pt_this = 1.0 - pt_last;
         const double pr = pt_this * s2r + pt_last * s2l_re;
         const double pi = pt_this * s2i + pt_last * s2l_im;
@@ -634,10 +644,10 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
       {  // mixer2.IncresePhaseDeg / SetPhaseDeg (DSP.cpp:177-187)
         double phase_deg = 1.0 * ct_ec;
-        phase_deg += DM_DIVC(360.0 * m2_ptr, ((double)WTSIZE));
+        phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
         phase_deg = fmod(phase_deg, 360.0);
         while (phase_deg < 0) phase_deg += 360.0;
-        m2_ptr = DM_DIVC(phase_deg, 360.0) * ((double)WTSIZE);
+        m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
       }
       set_freq(m2_freq, m2_step, 0.01 * ct_ec + m2_freq);  // IncreseFreqHz
       // marg->UpdateSigned (DSP.cpp:419-427)
@@ -670,9 +680,10 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
         const int pms_slot = pm_p;
         pm_p++;
         pm_p %= MSE_LEN;
-        double mu = DM_DIVC(pm_sum, ((double)MSE_LEN));
+        double mu = div_c(pm_sum, ((double)MSE_LEN));  // a tiny mu is floored at 1e-6 below
         if (mu < 0.000001) mu = 0.000001;
-        const double rmu = rcp_div(mu);  // one reciprocal for both quotients
+        const double rmu = rcp_div(mu);  // mu >= 1e-6; one reciprocal for both quotients (a tiny one only
+                                         // makes |t| - 1 == -1)
         const double tr = div_r(1.4142135623730951 * qr, mu, rmu), ti = div_r(1.4142135623730951 * qi, mu, rmu);
         const double tda = (fabs(tr) - 1.0), tdb = (fabs(ti) - 1.0);
         const double v = (tda * tda) + (tdb * tdb);
@@ -681,7 +692,8 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
         if (!(AERO_X_DROP & 4)) pmsb[pms_slot] = make_double2(fabs(av), fabs(v));
         ms_p++;
         ms_p %= MSE_LEN;
-        mse = DM_DIVC(ms_sum, ((double)MSE_LEN));
+        // ms_sum sums (|t| - 1)^2 terms: 0 or a multiple of 2^-158, so the short division is exact
+        mse = div_c(ms_sum, ((double)MSE_LEN));
       }
       if (mse < 0.65) {  // soft bits, imag first (:516-530)
         int ibit = qround(0.75 * qi * 127.0 + 128.0);

@@ -120,7 +120,6 @@ __global__ void math_kernel(int fn, const double *x, const double *y, double *ou
     case 9: r = div_c(a, 48000.0); break;
     case 10: r = div_c(a, 360.0); break;
     case 11: r = div_n(a, b); break;
-    case 12: r = sqrt_n(a); break;
     case 13: r = div_c(a, 192000.0); break;
     case 14: r = aero_hypot_nr(a, b); break;
     default: break;

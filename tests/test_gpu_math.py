@@ -44,41 +44,36 @@ def test_device_math_matches_host_build(engine_lib):
     eng.close()
 
 
-def _edge_values(rng, n):
-    """Random magnitudes over the whole double range, plus zeros, subnormals,
-    the fast paths' range edges, infinities and NaN."""
-    e = rng.uniform(-1074, 1023, n)
-    x = rng.choice([-1.0, 1.0], n) * np.exp2(e) * rng.uniform(1, 2, n)
-    special = np.array([0.0, -0.0, 5e-324, -5e-324, 2.0 ** -1022, 2.0 ** -500, 2.0 ** 500, 2.0 ** -767,
-                        np.nextafter(2.0 ** -500, 0), np.nextafter(2.0 ** 500, np.inf), np.inf, -np.inf, np.nan,
-                        1.7976931348623157e308, 1.0, -1.0, 3.0])
-    return np.concatenate([x, special, rng.standard_normal(n) * 1e3])
-
-
 @pytest.mark.gpu
-def test_short_division_and_sqrt_sequences_are_ieee(engine_lib):
-    """div_c (constant divisor, Markstein), div_n (the compiler's sequence
-    without div_scale / div_fixup, zero numerators by select) and sqrt_n
-    (without the 2^-767 scaling) equal IEEE a / b and sqrt bit for bit,
-    including the operands that take their IEEE fallbacks."""
+def test_short_division_sequences_are_ieee(engine_lib):
+    """div_c (constant divisor, Markstein's correction) and div_n (the
+    compiler's division sequence without div_scale / div_fixup, zero
+    numerators by select) equal the IEEE quotient bit for bit inside their
+    contract (aero_math.h): zero or |a| >= 2^-969 with a normal quotient,
+    divisors and their reciprocals normal; dense sampling of the demods'
+    operand ranges, the contract's edges and signed zeros."""
     import aero_engine as ae
     eng = ae.Engine(max_channels=1)
     rng = np.random.default_rng(17)
-    a = _edge_values(rng, 300000)
-    b = rng.permutation(a)
-    with np.errstate(all='ignore'):
-        for fn, ref in (('div_c48000', a / 48000.0), ('div_c360', a / 360.0), ('div_c192000', a / 192000.0),
-                        ('div_n', a / b), ('sqrt_n', np.sqrt(np.abs(a)))):
-            x = np.abs(a) if fn == 'sqrt_n' else a
-            got = eng.device_math(fn, x, b)
-            same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
-            assert same.all(), (fn, x[~same][:4], b[~same][:4], got[~same][:4], ref[~same][:4])
-        # the demods' operand ranges, densely
-        m = rng.uniform(-1, 1, 400000) * np.exp(rng.uniform(-30, 30, 400000))
-        d = rng.uniform(0.5, 2, 400000) * np.exp(rng.uniform(-30, 30, 400000))
-        for fn, x, y, ref in (('div_n', m, d, m / d), ('div_c360', m, d, m / 360.0),
-                              ('sqrt_n', np.abs(m), d, np.sqrt(np.abs(m)))):
-            assert np.array_equal(eng.device_math(fn, x, y).view(np.uint64), ref.view(np.uint64)), fn
+    n = 400000
+    sgn = rng.choice([-1.0, 1.0], n)
+    wide = sgn * np.exp2(rng.uniform(-960, 1000, n)) * rng.uniform(1, 2, n)
+    dem = rng.uniform(-1, 1, n) * np.exp(rng.uniform(-30, 30, n))
+    edge = np.concatenate([[0.0, -0.0, 2.0 ** -969, -2.0 ** -969, 1.0, 360.0, 48000.0, 1e308],
+                           sgn[:1000] * np.exp2(rng.uniform(-969, -950, 1000))])
+    for a in (wide, dem, edge):
+        for fn, c in (('div_c48000', 48000.0), ('div_c360', 360.0), ('div_c192000', 192000.0)):
+            got = eng.device_math(fn, a)
+            assert np.array_equal(got.view(np.uint64), (a / c).view(np.uint64)), fn
+    # div_n: divisor and quotient normal, numerator zero or >= 2^-969
+    b = sgn * np.exp2(rng.uniform(-500, 500, n)) * rng.uniform(1, 2, n)
+    a = rng.permutation(sgn) * np.exp2(rng.uniform(-460, 460, n)) * rng.uniform(1, 2, n)
+    a[:64] = 0.0
+    a[64:128] = -0.0
+    d = rng.uniform(1e-6, 10.0, n)  # the AGC gain's divisor
+    for x, y in ((a, b), (dem, d), (np.full(n, 1.414213562), d), (np.full(n, 2.84), 2.84 + np.abs(dem))):
+        got = eng.device_math('div_n', x, y)
+        assert np.array_equal(got.view(np.uint64), (x / y).view(np.uint64))
     eng.close()
 
 
