@@ -311,7 +311,6 @@ AERO_HD double aero_tanh(double x) {
  * from its disassembly; the operation order below is the instructions'.
  * |x| >= 105414350 would need __branred (not restated: the demods' arguments
  * are loop corrections and averaged phase errors, |x| < 2*pi); NaN there. */
-AERO_HD double g_tab(int k) { return aero_g_sincostab[k]; }
 
 /* TAYLOR_SIN(xx, a, da) */
 AERO_HD double g_taylor_sin(double xx, double a, double da) {
@@ -323,7 +322,7 @@ AERO_HD double g_taylor_sin(double xx, double a, double da) {
   return t + a;
 }
 
-AERO_HD double g_do_sin(double x, double dx) {
+AERO_HD double g_do_sin(double x, double dx, const double *sct) {
   if (__builtin_fabs(x) < 0.126) return g_taylor_sin(x * x, x, dx);
   const double xold = x;
   if (x <= 0) dx = -dx;
@@ -333,12 +332,12 @@ AERO_HD double g_do_sin(double x, double dx) {
   const double s = x + (dx + (x * xx) * (xx * AERO_G_SN5 - AERO_G_NSN3));
   const double c = x * dx + xx * ((xx * AERO_G_CS6 - AERO_G_NCS4) * xx + AERO_G_CS2);
   const int k = (int)(low(u) << 2);
-  const double sn = g_tab(k), ssn = g_tab(k + 1), cs = g_tab(k + 2), ccs = g_tab(k + 3);
+  const double sn = sct[k], ssn = sct[k + 1], cs = sct[k + 2], ccs = sct[k + 3];
   const double cor = (ssn + s * ccs - sn * c) + cs * s;
   return __builtin_copysign(sn + cor, xold);
 }
 
-AERO_HD double g_do_cos(double x, double dx) {
+AERO_HD double g_do_cos(double x, double dx, const double *sct) {
   if (x < 0) dx = -dx;
   const double u = AERO_G_BIG + __builtin_fabs(x);
   x = __builtin_fabs(x) - (u - AERO_G_BIG) + dx;
@@ -346,7 +345,7 @@ AERO_HD double g_do_cos(double x, double dx) {
   const double s = x + (x * xx) * (xx * AERO_G_SN5 - AERO_G_NSN3);
   const double c = xx * ((xx * AERO_G_CS6 - AERO_G_NCS4) * xx + AERO_G_CS2);
   const int k = (int)(low(u) << 2);
-  const double sn = g_tab(k), ssn = g_tab(k + 1), cs = g_tab(k + 2), ccs = g_tab(k + 3);
+  const double sn = sct[k], ssn = sct[k + 1], cs = sct[k + 2], ccs = sct[k + 3];
   const double cor = (ccs - s * ssn - cs * c) - sn * s;
   return cs + cor;
 }
@@ -367,21 +366,23 @@ AERO_HD int g_reduce_sincos(double x, double &a, double &da) {
   return n;
 }
 
-AERO_HD void aero_sincos(double x, double &so, double &co) {
+/* sct: __sincostab (aero_g_sincostab, 440 doubles) or a copy of it, e.g. in
+ * LDS (aero_sincos_t); the results do not depend on where it lives */
+AERO_HD void aero_sincos_t(double x, double &so, double &co, const double *sct) {
   const uint32_t k = hiw(x) & 0x7fffffffu;
   if (k < 0x400368fdu) {
     if (k < 0x3e400000u) {
       so = x;
       co = 1.0;
     } else if (k < 0x3feb6000u) {
-      so = g_do_sin(x, 0.0);
-      co = g_do_cos(x, 0.0);
+      so = g_do_sin(x, 0.0, sct);
+      co = g_do_cos(x, 0.0, sct);
     } else {
       const double y = AERO_G_HPI - __builtin_fabs(x);
       const double a = y + AERO_G_HP1;
       const double da = (y - a) + AERO_G_HP1;
-      so = __builtin_copysign(g_do_cos(a, da), x);
-      co = g_do_sin(a, da);
+      so = __builtin_copysign(g_do_cos(a, da, sct), x);
+      co = g_do_sin(a, da, sct);
     }
     return;
   }
@@ -396,8 +397,8 @@ AERO_HD void aero_sincos(double x, double &so, double &co) {
       a = -a;
       da = -da;
     }
-    const double s = g_do_sin(a, da);
-    double c = g_do_cos(a, da);
+    const double s = g_do_sin(a, da, sct);
+    double c = g_do_cos(a, da, sct);
     if (n & 2) c = -c;
     if (n & 1) {
       so = c;
@@ -410,6 +411,8 @@ AERO_HD void aero_sincos(double x, double &so, double &co) {
   }
   so = co = x / x;
 }
+
+AERO_HD void aero_sincos(double x, double &so, double &co) { aero_sincos_t(x, so, co, aero_g_sincostab); }
 
 AERO_HD double aero_sin(double x) {
   double s, c;
@@ -444,7 +447,8 @@ AERO_HD double g_atan2_tail(const double *c, double v) {  // c2 + v (c3 + v (c4 
   return fma(v, p, c[2]);
 }
 
-AERO_HD double aero_atan2(double y, double x) {
+/* cij: uatan2.tbl's cij[241][7] (aero_g_cij) or a copy of it, e.g. in LDS */
+AERO_HD double aero_atan2_t(double y, double x, const double (*cij)[7]) {
   const uint32_t ux = hiw(x), dx = low(x), uy = hiw(y), dy = low(y);
   if ((ux & 0x7ff00000u) == 0x7ff00000u && ((ux & 0xfffffu) | dx) != 0) return x + y;
   if ((uy & 0x7ff00000u) == 0x7ff00000u && ((uy & 0xfffffu) | dy) != 0) return y + y;
@@ -515,7 +519,7 @@ AERO_HD double aero_atan2(double y, double x) {
         const double zz = fma(u * v, g_atan2_poly(v), du);
         return __builtin_copysign(u + zz, y);
       }
-      const double *c = aero_g_cij[g_atan2_row(u)];
+      const double *c = cij[g_atan2_row(u)];
       const double t3 = u - c[0];
       const double v = t3 + du;
       const double dv = (__builtin_fabs(t3) > __builtin_fabs(du)) ? ((t3 - v) + du) : ((du - v) + t3);
@@ -533,7 +537,7 @@ AERO_HD double aero_atan2(double y, double x) {
       const double cor = (AERO_G_HPI > __builtin_fabs(u)) ? ((AERO_G_HPI - t) - u) : (AERO_G_HPI - (u + t));
       z = (((cor + AERO_G_HPI1) - du) - zz) + t;
     } else {
-      const double *c = aero_g_cij[g_atan2_row(u)];
+      const double *c = cij[g_atan2_row(u)];
       const double v = (u - c[0]) + du;
       z = (AERO_G_HPI - c[1]) + fma(-v, g_atan2_tail(c, v), AERO_G_HPI1);
     }
@@ -547,7 +551,7 @@ AERO_HD double aero_atan2(double y, double x) {
       const double cor = (AERO_G_HPI > __builtin_fabs(u)) ? ((AERO_G_HPI - t) + u) : ((u - t) + AERO_G_HPI);
       z = (((cor + AERO_G_HPI1) + du) + zz) + t;
     } else {
-      const double *c = aero_g_cij[g_atan2_row(u)];
+      const double *c = cij[g_atan2_row(u)];
       const double v = (u - c[0]) + du;
       z = (AERO_G_HPI + c[1]) + fma(v, g_atan2_tail(c, v), AERO_G_HPI1);
     }
@@ -559,12 +563,76 @@ AERO_HD double aero_atan2(double y, double x) {
       const double cor = (AERO_G_OPI > __builtin_fabs(u)) ? ((AERO_G_OPI - t) - u) : (AERO_G_OPI - (t + u));
       z = (((cor + AERO_G_OPI1) - du) - zz) + t;
     } else {
-      const double *c = aero_g_cij[g_atan2_row(u)];
+      const double *c = cij[g_atan2_row(u)];
       const double v = (u - c[0]) + du;
       z = (AERO_G_OPI - c[1]) + fma(-v, g_atan2_tail(c, v), AERO_G_OPI1);
     }
   }
   return __builtin_copysign(__builtin_fabs(z), y);
+}
+
+AERO_HD double aero_atan2(double y, double x) { return aero_atan2_t(y, x, aero_g_cij); }
+
+/* aero_atan2_t without branches for the main path, when every active lane
+ * of the wave has finite nonzero |x|, |y| in [2^-500, 2^500] within 56
+ * binades of each other (no special case, no 2^+-500 scaling, none of the
+ * extreme-ratio returns); the general code otherwise.  The main path's six
+ * instruction sequences (x > 0 with |x| > |y|, or the pi/2 - , pi/2 + and
+ * pi - forms; each with the small-ratio series or a table row) are the
+ * ones aero_atan2_t runs, evaluated side by side and selected, because a
+ * wave whose 64 channels spread over the quadrants would run them one
+ * after another:
+ *   - the three non-primary forms differ only in (K, K1, s) = (pi/2, hpi1,
+ *     -1), (pi/2, hpi1, +1), (pi, opi1, -1): t = K + s u, cor = (K - t) + s u,
+ *     z = (((cor + K1) + s du) + s zz) + t (series), z = (K + s c1) +
+ *     fma(s v, P, K1) (table), where multiplying by s = +-1 is exact and
+ *     x + (-y) is x - y bit for bit;
+ *   - the table forms share v = (u - c0) + du and P = fma(v, p3, c2). */
+AERO_HD double aero_atan2_bf(double y, double x, const double (*cij)[7]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double ax = __builtin_fabs(x), ay = __builtin_fabs(y);
+  const int32_t de = (int32_t)((hiw(y) & 0x7ff00000u) - (hiw(x) & 0x7ff00000u));
+  const bool ok = ax >= 0x1p-500 && ax <= 0x1p500 && ay >= 0x1p-500 && ay <= 0x1p500 && de < 59768832 &&
+                  de > -59768832;
+  if (!__builtin_expect(__all(ok), 1)) return aero_atan2_t(y, x, cij);
+  const bool gt = ax > ay;  // u = ay / ax, else u = ax / ay
+  const double a = gt ? ay : ax, b = gt ? ax : ay;
+  const double r = rcp_div(b);
+  const double u = div_r(a, b, r);
+  const double vb = b * u, vvb = fma(b, u, -vb);
+  const double du = div_r((a - vb) - vvb, b, r);
+  const bool pos = x > 0;
+  const bool prim = pos && gt;
+  const bool cpi = !pos && !(ay > ax);                 // pi - atan(u)
+  const double K = cpi ? AERO_G_OPI : AERO_G_HPI, K1 = cpi ? AERO_G_OPI1 : AERO_G_HPI1;
+  const double s = (!pos && ay > ax) ? 1.0 : -1.0;     // pi/2 + atan(u)
+  // small-ratio series
+  const double vs = u * u;
+  const double poly = g_atan2_poly(vs);
+  const double uv = u * vs;
+  const double zp_s = u + fma(uv, poly, du);
+  const double zz = uv * poly;
+  const double ts = K + s * u;
+  const double cor = (K - ts) + s * u;
+  const double zg_s = (((cor + K1) + s * du) + s * zz) + ts;
+  // table row
+  int row = g_atan2_row(u);
+  row = row < 0 ? 0 : row;  // u < 1/16: the row is not used
+  const double *c = cij[row];
+  const double t3 = u - c[0];
+  const double v = t3 + du;
+  const double dv = (__builtin_fabs(t3) > __builtin_fabs(du)) ? ((t3 - v) + du) : ((du - v) + t3);
+  double p3 = fma(v, c[6], c[5]);
+  p3 = fma(v, p3, c[4]);
+  p3 = fma(v, p3, c[3]);
+  const double zp_t = fma(v, c[2], fma(dv, c[2], (v * v) * p3)) + c[1];
+  const double P = fma(v, p3, c[2]);
+  const double zg_t = (K + s * c[1]) + fma(s * v, P, K1);
+  const double z = u < AERO_G_INV16 ? (prim ? zp_s : zg_s) : (prim ? zp_t : zg_t);
+  return __builtin_copysign(z, y);
+#else
+  return aero_atan2_t(y, x, cij);
+#endif
 }
 
 /* --------------------------------------------------------------- log

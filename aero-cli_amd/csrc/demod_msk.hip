@@ -90,7 +90,18 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   __shared__ double s_qim[NIL > 0 ? NIL : 1][WG];
   __shared__ double s_qre[NRL > 0 ? NRL : 1][WG];
   __shared__ double s_taps[NT];
+  // at 12 kHz (one 256-lane workgroup per CU, LDS to spare) the libm tables
+  // the chain gathers from (atan2's cij rows every sample, sincos's table
+  // every event) are copied to LDS; the 24 kHz workgroups pack two per CU
+  // and the 48 kHz ones fill it, so those read the global copies
+  constexpr bool LTAB = SPS == 20;
+  __shared__ double s_cij[LTAB ? 241 : 1][7];
+  __shared__ double s_sct[LTAB ? 440 : 1];
   for (int l = threadIdx.x; l < NT; l += WG) s_taps[l] = T.taps[l];
+  if (LTAB) {
+    for (int k = threadIdx.x; k < 241 * 7; k += WG) (&s_cij[0][0])[k] = (&aero_g_cij[0][0])[k];
+    for (int k = threadIdx.x; k < 440; k += WG) s_sct[k] = aero_g_sincostab[k];
+  }
   __syncthreads();
   const int c = blockIdx.x * WG + threadIdx.x;
   const int lane = threadIdx.x;
@@ -268,7 +279,7 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       const double m1r = st_eta, m1i = -d8v;
       const double2 so = T.cis[cis_index(so_ptr)];
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
-      const double ang = aero_atan2(oim, ore);
+      const double ang = LTAB ? aero_atan2_t(oim, ore, s_cij) : aero_atan2(oim, ore);
       const double weighting = fabs(aero_tanh(ang));
       {  // st_osc.AdvanceFractionOfWave (DSP.h:59-65), dcd false
         so_ptr += (-(1.0 - weighting) * ang * (0.05 / 360.0)) * WTSIZE;
@@ -353,7 +364,10 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       }
       {  // pt_msk *= cpx(cos(marg->Val), sin(marg->Val))
         double rs, rc;
-        aero_sincos(mval, rs, rc);
+        if (LTAB)
+          aero_sincos_t(mval, rs, rc, s_sct);
+        else
+          aero_sincos(mval, rs, rc);
         const double rr = pr * rc - pi * rs, ri = pr * rs + pi * rc;
         pr = rr;
         pi = ri;

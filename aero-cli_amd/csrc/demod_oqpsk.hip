@@ -37,9 +37,9 @@ namespace aero {
 #define DM_SINCOS(x, s, c) ::sincos(x, &(s), &(c))
 #else
 #define DM_HYPOT aero_hypot_w
-#define DM_ATAN2 aero_atan2
+#define DM_ATAN2(y, x) aero_atan2_t(y, x, sh.cij)
 #define DM_TANH aero_tanh
-#define DM_SINCOS(x, s, c) aero_sincos(x, s, c)
+#define DM_SINCOS(x, s, c) aero_sincos_t(x, s, c, sh.sct)
 #endif
 // AERO_X_DROP (diagnostic builds only, never bit-exact): leave out one
 // buffer's HBM accesses to attribute the demod's PMC traffic buffer by buffer
@@ -203,6 +203,11 @@ struct DemodShared {
   // the kernel holds 227 VGPRs, and 4 sums fewer in LDS spill)
   double qil[FIR_LDS_IM][DEMOD_BLOCK];
   double qrl[FIR_LDS_RE][DEMOD_BLOCK];
+  // the libm tables the chain gathers from every sample (atan2's cij rows,
+  // sincos's __sincostab), copied from global memory once per launch: an
+  // LDS gather instead of an L2 round trip on the per-sample chain
+  double cij[241][7];
+  double sct[440];
 };
 
 // dst += a (dst = a + b) for the lanes in m only, the rest keep dst: one
@@ -814,6 +819,8 @@ __global__ __launch_bounds__(DEMOD_THREADS) void demod_oqpsk_kernel(DevState S, 
     sh.cseq[threadIdx.x] = 0;
     sh.fseq[threadIdx.x] = 0;
   }
+  for (int k = threadIdx.x; k < 241 * 7; k += DEMOD_THREADS) (&sh.cij[0][0])[k] = (&aero_g_cij[0][0])[k];
+  for (int k = threadIdx.x; k < 440; k += DEMOD_THREADS) sh.sct[k] = aero_g_sincostab[k];
   __syncthreads();
   if (threadIdx.x >= DEMOD_BLOCK)
     demod_fir_wave(S, sh, c, pair, wv, valid);
