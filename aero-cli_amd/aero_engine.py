@@ -33,7 +33,7 @@ F_TRACE_FRAMES = 0x20
 F_TRACE_ALL = F_TRACE_PT | F_TRACE_BLOCKS | F_TRACE_SOFT | F_TRACE_HOPS | F_TRACE_FRAMES
 
 MATH_FN = {'hypot': 0, 'atan2': 1, 'tanh': 2, 'sin': 3, 'cos': 4, 'log10': 5, 'sqrt': 6, 'fmod360': 7,
-           'div': 8, 'div_c48000': 9, 'div_c360': 10, 'div_n': 11, 'div_c192000': 13, 'hypot_nr': 14}
+           'div': 8, 'div_c48000': 9, 'div_c360': 10, 'div_n': 11, 'div_c192000': 13, 'hypot_nr': 14, 'atan2_bf': 15}
 
 
 class EngineCfg(ctypes.Structure):

@@ -622,7 +622,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       const double spi2 = dly_reg(hA1, wA1, oA1, spr);
       const double2 qv = q_n;
       const double er_r = qv.x * spr - qv.y * (-spi2), er_i = qv.x * (-spi2) + qv.y * spr;
-      double st_err = aero_atan2(er_i, er_r);
+      double st_err = aero_atan2_bf(er_i, er_r, aero_g_cij);
       st_err *= 1.5 * (1.0 - progress * progress);
       b_advance(q_ptr, -(1.0 / (2.0 * M_PI)) * st_err * 0.1);
       b_set_phase_deg(so_ptr, (360.0 * q_ptr / ((double)WTSIZE)) * 4.0 + (360.0 * 0.4));
@@ -679,7 +679,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       const double m1r = st_eta, m1i = -dly_reg(h8, w8, o8, st_eta);
       const double2 so = so_n;
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
-      const double st_angle_error = aero_atan2(oim, ore);
+      const double st_angle_error = aero_atan2_bf(oim, ore, aero_g_cij);
       if (cntr > SPS * (128 + 64)) {
         b_set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
         b_advance(so_ptr, div_c(-st_angle_error * 0.01, 360.0));  // a tiny quotient vanishes in so_ptr + x W

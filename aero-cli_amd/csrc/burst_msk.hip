@@ -460,7 +460,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         progress = div_c(progress, goal);  // goal a compile-time constant, progress an integer
         const double2 hv = h_n;
         const double er_r = hv.x * spr - hv.y * (-spi2), er_i = hv.x * (-spi2) + hv.y * spr;
-        double st_err = aero_atan2(er_i, er_r);
+        double st_err = aero_atan2_bf(er_i, er_r, aero_g_cij);
         st_err *= 0.5 * (1.0 - progress * progress);
         b_advance(sh_ptr, -(1.0 / (2.0 * M_PI)) * st_err * 0.05);
         b_set_phase_deg(so_ptr, (360.0 * sh_ptr / ((double)WTSIZE)) + (360.0 * (1.0 - M_EE)));
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       const double m1r = st_eta, m1i = -(0.0 * d8_new + (1.0 - 0.0) * d8_old);
       const double2 so = so_n;
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
-      const double st_angle_error = aero_atan2(oim, ore);
+      const double st_angle_error = aero_atan2_bf(oim, ore, aero_g_cij);
       if (cntr > M_ENDROT) b_advance(so_ptr, div_c(-st_angle_error * 0.002, 360.0));  // tiny: vanishes in so_ptr
       {  // IfHavePassedPoint(ee) (DSP.cpp:222-238) and the symbol step (:617-693)
         double tl = so_last - PT, tw = so_ptr - PT;

@@ -279,7 +279,7 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       const double m1r = st_eta, m1i = -d8v;
       const double2 so = T.cis[cis_index(so_ptr)];
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
-      const double ang = LTAB ? aero_atan2_t(oim, ore, s_cij) : aero_atan2(oim, ore);
+      const double ang = LTAB ? aero_atan2_bf(oim, ore, s_cij) : aero_atan2_bf(oim, ore, aero_g_cij);
       const double weighting = fabs(aero_tanh(ang));
       {  // st_osc.AdvanceFractionOfWave (DSP.h:59-65), dcd false
         so_ptr += (-(1.0 - weighting) * ang * (0.05 / 360.0)) * WTSIZE;

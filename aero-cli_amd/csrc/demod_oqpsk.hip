@@ -37,7 +37,7 @@ namespace aero {
 #define DM_SINCOS(x, s, c) ::sincos(x, &(s), &(c))
 #else
 #define DM_HYPOT aero_hypot_w
-#define DM_ATAN2(y, x) aero_atan2_t(y, x, sh.cij)
+#define DM_ATAN2(y, x) aero_atan2_bf(y, x, sh.cij)
 #define DM_TANH aero_tanh
 #define DM_SINCOS(x, s, c) aero_sincos_t(x, s, c, sh.sct)
 #endif

@@ -122,6 +122,7 @@ __global__ void math_kernel(int fn, const double *x, const double *y, double *ou
     case 11: r = div_n(a, b); break;
     case 13: r = div_c(a, 192000.0); break;
     case 14: r = aero_hypot_nr(a, b); break;
+    case 15: r = aero_atan2_bf(a, b, aero_g_cij); break;
     default: break;
   }
   out[i] = r;

@@ -98,3 +98,37 @@ def test_hypot_normal_range_variant_is_glibc(engine_lib):
         ref = mathhost.glibc('hypot', x, b)
         assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
     eng.close()
+
+
+@pytest.mark.gpu
+def test_atan2_branch_free_main_path_is_glibc(engine_lib):
+    """aero_atan2_bf (the demods' per-sample atan2: the main path's six forms
+    side by side, selected per lane, the general code when any lane of the
+    wave is special) equals glibc's __atan2_fma bit for bit: every quadrant,
+    |y/x| on both sides of 1 and of 1/16, table-row centres, equal
+    magnitudes, and waves mixing special lanes (zeros, infinities, NaN,
+    extreme ratios) with normal ones."""
+    import aero_engine as ae
+    import mathhost
+    eng = ae.Engine(max_channels=1)
+    rng = np.random.default_rng(29)
+    n = 600000
+    x = rng.standard_normal(n) * np.exp(rng.uniform(-20, 20, n))
+    cases = [rng.standard_normal(n) * np.exp(rng.uniform(-20, 20, n)),
+             x * rng.uniform(-1 / 16, 1 / 16, n),
+             x * (rng.integers(16, 257, n) / 256) * (1 + rng.standard_normal(n) * 1e-12) * rng.choice([-1, 1], n),
+             x * rng.choice([-1.0, 1.0], n),
+             x * np.exp2(rng.uniform(-60, 60, n))]
+    mixed = cases[0].copy()
+    mixed[::97] = 0.0
+    mixed[1::89] = np.inf
+    mixed[2::83] = np.nan
+    mixed[3::79] = 1e-300
+    cases.append(mixed)
+    for y in cases:
+        for xx, yy in ((x, y), (y, x), (-x, y), (x, -y)):
+            got = eng.device_math('atan2_bf', yy, xx)
+            ref = mathhost.glibc('atan2', yy, xx)
+            same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
+            assert same.all(), (yy[~same][:3], xx[~same][:3])
+    eng.close()
