@@ -264,6 +264,26 @@ def build_drop(jobs=4):
     return [build_engine(jobs, variant=v, defines=d) for v, d in DROP_VARIANTS.items()]
 
 
+# the burst demods with the general libm forms (same results; scripts/gpu_steps.sh ab=blibmK:burst10500)
+BLIBM_VARIANTS = {'blibm%d' % k: ['AERO_X_BURST_LIBM=%d' % k] for k in (1, 2, 3)}
+
+
+def build_blibm(jobs=4):
+    return [build_engine(jobs, variant=v, defines=d) for v, d in BLIBM_VARIANTS.items()]
+
+
+# per-section s_memtime totals of the coarse kernel, the demod chain and the
+# Viterbi (scripts/coarse_stamps.py, scripts/demod_stamps.py)
+def build_stamps(jobs=4):
+    return [build_engine(jobs, variant='stamps', defines=['AERO_X_STAMPS']),
+            build_engine(jobs, variant='stamps16', defines=['AERO_X_STAMPS', 'AERO_COARSE_YDMA=16'])]
+
+
+# the coarse kernel's y history through 16-byte direct-to-LDS loads
+def build_ydma(jobs=4):
+    return [build_engine(jobs, variant='ydma16', defines=['AERO_COARSE_YDMA=16'])]
+
+
 if __name__ == '__main__':
     ap = argparse.ArgumentParser()
     ap.add_argument('--engine', action='store_true')
@@ -271,8 +291,11 @@ if __name__ == '__main__':
     ap.add_argument('--oracle', action='store_true')
     ap.add_argument('--host', action='store_true')
     ap.add_argument('--asan', action='store_true', help='sanitizer builds into build/asan (tests/asan_check.sh)')
+    ap.add_argument('--variants', default='', help='comma list of timing builds: drop, blibm, stamps')
     ap.add_argument('-j', type=int, default=4)
     a = ap.parse_args()
+    for v in filter(None, a.variants.split(',')):
+        print({'drop': build_drop, 'blibm': build_blibm, 'stamps': build_stamps, 'ydma': build_ydma}[v](a.j))
     if a.asan:
         print(build_asan(a.j))
         sys.exit(0)

@@ -271,7 +271,7 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
     pd2_n = S.pd3[(size_t)pd2_slot(p1r) * C + c];
     double cr = a.x, ci = a.y;
     {  // agc.Update(|cval|); cval *= AGCVal (:316-317)
-      const double av = aero_hypot(cr, ci);
+      const double av = B_HYPOT(cr, ci);
       agc_sum = agc_sum - agc_old;
       agc_sum = agc_sum + fabs(av);
       S.agc[(size_t)agc_p * C + c] = fabs(av);
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
       ma1i = ma1i + pi;
       S.ma1[(size_t)ma1_p * C + c] = make_double2(pr, pi);
       ma1_p = ma1_p + 1 == B_MA ? 0 : ma1_p + 1;
-      fastarm = aero_hypot(ma1r / ((double)B_MA), ma1i / ((double)B_MA));
+      fastarm = B_HYPOT(ma1r / ((double)B_MA), ma1i / ((double)B_MA));
       mav1_sum = mav1_sum - mv_old;
       mav1_sum = mav1_sum + (fastarm);
       S.mav1[(size_t)mav1_p * C + c] = fastarm;
@@ -622,7 +622,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       const double spi2 = dly_reg(hA1, wA1, oA1, spr);
       const double2 qv = q_n;
       const double er_r = qv.x * spr - qv.y * (-spi2), er_i = qv.x * (-spi2) + qv.y * spr;
-      double st_err = aero_atan2_bf(er_i, er_r, aero_g_cij);
+      double st_err = B_ATAN2(er_i, er_r);
       st_err *= 1.5 * (1.0 - progress * progress);
       b_advance(q_ptr, -(1.0 / (2.0 * M_PI)) * st_err * 0.1);
       b_set_phase_deg(so_ptr, (360.0 * q_ptr / ((double)WTSIZE)) * 4.0 + (360.0 * 0.4));
@@ -640,7 +640,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       s2i = ar * rot_i + ai * rot_r;
     }
     {  // agc2 (AGC(SPS*64/Fs)) and clip (:478-481)
-      const double sa = aero_hypot(s2r, s2i);
+      const double sa = B_HYPOT(s2r, s2i);
       agc2_sum = agc2_sum - agc2_old;
       agc2_sum = agc2_sum + fabs(sa);
       S.agc2[(size_t)agc2_p * C + c] = fabs(sa);
@@ -651,7 +651,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       s2r *= g;
       s2i *= g;
     }
-    const double abval = aero_hypot(s2r, s2i);
+    const double abval = B_HYPOT(s2r, s2i);
     if (abval > 2.84) {
       const double k = div_n(2.84, abval);  // abval > 2.84
       s2r = k * s2r;
@@ -679,7 +679,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       const double m1r = st_eta, m1i = -dly_reg(h8, w8, o8, st_eta);
       const double2 so = so_n;
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
-      const double st_angle_error = aero_atan2_bf(oim, ore, aero_g_cij);
+      const double st_angle_error = B_ATAN2(oim, ore);
       if (cntr > SPS * (128 + 64)) {
         b_set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
         b_advance(so_ptr, div_c(-st_angle_error * 0.01, 360.0));  // a tiny quotient vanishes in so_ptr + x W
@@ -964,7 +964,7 @@ __global__ __launch_bounds__(1024) void trident_kernel(BurstState S, BurstTables
       const double ar = x[i].x * da.x - x[i].y * da.y, ai = x[i].x * da.y + x[i].y * da.x;
       const double br = db.x * g[i].x - db.y * (-g[i].y), bi = db.x * (-g[i].y) + db.y * g[i].x;
       const double orr = ar + br, oi = ai + bi;
-      const double ab = aero_hypot(orr, oi);
+      const double ab = B_HYPOT(orr, oi);
       x[i] = make_double2(orr, oi);
       if (pass == 0) {
         absb[p] = ab;

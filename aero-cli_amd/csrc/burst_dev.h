@@ -11,6 +11,21 @@
 #include "burst_common.h"
 #include "engine_common.h"
 
+// The per-sample libm of the burst demods: hypot with the wave-uniform
+// branch-free fast path, atan2's branch-free main path over the global cij
+// table.  AERO_X_BURST_LIBM (timing builds only, bit-identical results)
+// selects the general forms: 1 plain hypot, 2 general atan2, 3 both.
+#if !defined(AERO_X_BURST_LIBM) || AERO_X_BURST_LIBM == 0 || AERO_X_BURST_LIBM == 2
+#define B_HYPOT aero_hypot_w
+#else
+#define B_HYPOT aero_hypot
+#endif
+#if defined(AERO_X_BURST_LIBM) && AERO_X_BURST_LIBM >= 2
+#define B_ATAN2(y, x) aero_atan2(y, x)
+#else
+#define B_ATAN2(y, x) aero_atan2_bf(y, x, aero_g_cij)
+#endif
+
 namespace aero {
 namespace {
 

@@ -150,7 +150,7 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
     const double pd1_old = S.pd3[(size_t)p1r * C + c], pd2_old = S.pd3[(size_t)p2r * C + c];
     double cr = a.x, ci = a.y;
     {  // agc->Update(abs(cval)); cval *= agc->AGCVal (:366-368)
-      const double av = aero_hypot(cr, ci);
+      const double av = B_HYPOT(cr, ci);
       agc_sum = agc_sum - agc_old;
       agc_sum = agc_sum + fabs(av);
       S.agc[(size_t)agc_p * C + c] = fabs(av);
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
       ma1i = ma1i + pi;
       S.ma1[(size_t)ma1_p * C + c] = make_double2(pr, pi);
       ma1_p = ma1_p + 1 == M_MA ? 0 : ma1_p + 1;
-      fastarm = aero_hypot(ma1r / ((double)M_MA), ma1i / ((double)M_MA));
+      fastarm = B_HYPOT(ma1r / ((double)M_MA), ma1i / ((double)M_MA));
       mav1_sum = mav1_sum - mv_old;
       mav1_sum = mav1_sum + (fastarm);
       S.mav1[(size_t)mav1_p * C + c] = fastarm;
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         progress = div_c(progress, goal);  // goal a compile-time constant, progress an integer
         const double2 hv = h_n;
         const double er_r = hv.x * spr - hv.y * (-spi2), er_i = hv.x * (-spi2) + hv.y * spr;
-        double st_err = aero_atan2_bf(er_i, er_r, aero_g_cij);
+        double st_err = B_ATAN2(er_i, er_r);
         st_err *= 0.5 * (1.0 - progress * progress);
         b_advance(sh_ptr, -(1.0 / (2.0 * M_PI)) * st_err * 0.05);
         b_set_phase_deg(so_ptr, (360.0 * sh_ptr / ((double)WTSIZE)) + (360.0 * (1.0 - M_EE)));
@@ -478,7 +478,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         s2i = ar * rot_i + ai * rot_r;
       }
       {  // agc2 and clip (:592-598)
-        const double sa = aero_hypot(s2r, s2i);
+        const double sa = B_HYPOT(s2r, s2i);
         agc2_sum = agc2_sum - agc2_old;
         agc2_sum = agc2_sum + fabs(sa);
         S.agc2[(size_t)agc2_p * C + c] = fabs(sa);
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         s2r *= g;
         s2i *= g;
       }
-      const double abval = aero_hypot(s2r, s2i);
+      const double abval = B_HYPOT(s2r, s2i);
       if (abval > 2.84) {
         const double k = div_n(2.84, abval);  // abval > 2.84
         s2r = k * s2r;
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         pdr = pd_slot.x;
         pdi = pd_slot.y;
       }
-      double st_eta = aero_hypot(s2r, pdi);  // abs(pt_msk), pt_msk = (sig2.re, pt_d.im)
+      double st_eta = B_HYPOT(s2r, pdi);  // abs(pt_msk), pt_msk = (sig2.re, pt_d.im)
       {  // st_iir_resonator.update (DSP.cpp:635-685)
         double y = 0;
         y += srx2 * c_msr_b[2];
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       const double m1r = st_eta, m1i = -(0.0 * d8_new + (1.0 - 0.0) * d8_old);
       const double2 so = so_n;
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
-      const double st_angle_error = aero_atan2_bf(oim, ore, aero_g_cij);
+      const double st_angle_error = B_ATAN2(oim, ore);
       if (cntr > M_ENDROT) b_advance(so_ptr, div_c(-st_angle_error * 0.002, 360.0));  // tiny: vanishes in so_ptr
       {  // IfHavePassedPoint(ee) (DSP.cpp:222-238) and the symbol step (:617-693)
         double tl = so_last - PT, tw = so_ptr - PT;
@@ -731,7 +731,7 @@ __global__ __launch_bounds__(1024) void trident_bmsk_kernel(BurstState S, BurstT
       const double ar = x[i].x * da.x - x[i].y * da.y, ai = x[i].x * da.y + x[i].y * da.x;
       const double br = db.x * g[i].x - db.y * (-g[i].y), bi = db.x * (-g[i].y) + db.y * g[i].x;
       const double orr = ar + br, oi = ai + bi;
-      const double ab = aero_hypot(orr, oi);
+      const double ab = B_HYPOT(orr, oi);
       x[i] = make_double2(orr, oi);
       if (pass == 0) {
         offer(ab, p, lv, li);

@@ -73,6 +73,21 @@ struct CoarseK {
   static constexpr double FS = (double)msk_fs(M);
 };
 
+// the bins and rate one launch works with: compile-time for the fixed-rate
+// groups, the group's MskGen for a generic-rate one
+struct CoarseBins {
+  int start, stop, ilo, ihi, epb;
+  double fs;
+};
+template <int M>
+__device__ __forceinline__ CoarseBins coarse_bins(const DevState &S) {
+  using K = CoarseK<M>;
+  if constexpr (msk_generic(M))
+    return {S.mg.start, S.mg.stop, S.mg.ilo, S.mg.ihi, S.mg.epb, S.mg.fs};
+  else
+    return {K::START, K::STOP, K::ILO, K::IHI, K::EPB, K::FS};
+}
+
 __device__ __forceinline__ void set_freq1(double &freq, double &step, double f, double fs) {  // SetFreq (DSP.cpp:163-168)
   freq = f;
   if (freq < 0) freq = 0;
@@ -91,7 +106,7 @@ struct HopCtl {
 // SignalHunter (decode/hunter.cpp:21-42; maxTries 15, params 0/25000/10500,
 // decode/decode.cpp:161,169) and CenterFreqChangedSlot (:256-280).  dcd is
 // never set (DCDstatSlot unconnected, decode/decode.cpp:168-241).
-__device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<int, MODE_OQPSK>, double est,
+__device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<int, MODE_OQPSK>, double, double est,
                                             double mse, unsigned &iter, int &scans, long long nk) {
   const double thr = 0.65, lockingbw = 10500.0, Fs = 48000.0;
   if (mse < thr) {
@@ -146,9 +161,9 @@ __device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<in
 // its AFC branch needs dcd, never set), SignalHunter with params 0/6000/900
 // (decode/decode.cpp:193) and MskDemodulator::CenterFreqChangedSlot (:220-240).
 template <int M>
-__device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<int, M>, double est, double mse,
-                                            unsigned &iter, int &scans, long long nk) {
-  const double thr = 0.5, lockingbw = 900.0, fb = 600.0, Fs = CoarseK<M>::FS;
+__device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<int, M>, double Fs, double est,
+                                            double mse, unsigned &iter, int &scans, long long nk) {
+  const double thr = 0.5, lockingbw = 900.0, fb = 600.0;
   if ((mse > thr) && (fabs(h.m2f - (h.mcf + est)) > 0.0)) set_freq1(h.m2f, h.m2s, h.mcf + est, Fs);
   h.countdown = 4;
   const bool gotasignal = !(mse > thr);
@@ -179,8 +194,8 @@ __device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<in
 
 // AERO_X_STAMPS (diagnostic build only): s_memtime cycle totals per section
 // of wave 0 of every workgroup that ran a hop (prologue, ring to LDS +
-// twiddles, table gathers + mix, FFT 1, boxcar+iFFT+square, FFT 3, hypot,
-// log10 smoothing, fold search; slots 0-8), and the number of such
+// twiddles, table gathers + mix, FFT 1, boxcar+iFFT+square, FFT 3, y history
+// loads + |X| + log10, y update + store, fold search; slots 0-8), and the number of such
 // workgroups (slot 11)
 constexpr int CSTAMP_N = 12;
 #ifdef AERO_X_STAMPS
@@ -202,6 +217,7 @@ __device__ unsigned long long g_cstamps[CSTAMP_N];
 template <int M>
 __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 13 ? 4 : 1) void coarse_kernel(DevState S, DevTables T, int nch) {
   using K = CoarseK<M>;
+  const CoarseBins KB = coarse_bins<M>(S);
   constexpr int L = K::LOG2N, N = 1 << L, FT = N / 16, PADDED = N + N / 16;
   constexpr int YLEN = K::YHI - K::YLO + 1;
   __shared__ double lds[PADDED];
@@ -280,7 +296,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int p = bin_t | chain::out_bin_reg<L>(i);
-    if (p >= K::START && p <= K::STOP) x[i] = make_double2(0.0, 0.0);
+    if (p >= KB.start && p <= KB.stop) x[i] = make_double2(0.0, 0.0);
   }
   // inverse FFT.  JFFT scales by 1/N and FFTWrapper multiplies by N
   // (jfft.cpp:206-212, fftwrapper.cpp:22-29): x * 2^-L * 2^L == x exactly for every
@@ -300,63 +316,87 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   CSTAMP(4);
   chain::fft<L, false, false>(x, t, lds, T.tw, s_tw);
   CSTAMP(5);
-  // fftshift + smoothing y = 0.9 y + 10 log10(max(|X|,1)) over the bins the fold reads:
-  // |X| per bin to LDS first (keeps the log10 out of the register-heavy FFT scope)
-  // the y history (HBM) is read three iterations ahead of its update, the
-  // first loads overlapping the |X| work below
+  // fftshift + smoothing y = 0.9 y + 10 log10(max(|X|,1)) over the bins the
+  // fold reads.  The y history (HBM, YLEN doubles) is copied into LDS by
+  // direct-to-LDS loads issued first, so its round trip overlaps the |X| and
+  // log10 work, which stays in registers (each thread on its own bins of the
+  // transform's output layout).  No barrier before the loads: the third
+  // transform's workgroup exchange ended with one (chain::gx), after which
+  // every wave only works in registers, so the LDS is free.
   double *yg = S.y + (size_t)c * YLEN;
   const int yreset = S.is[IS_YRESET * C + c];
-  auto yload = [&](int k) { return (k < YLEN && !yreset) ? yg[k] : 20.0; };
-  double yp0 = yload(t), yp1 = yload(t + FT);
-  // no barrier here: the third transform's workgroup exchange ended with
-  // one (chain::gx), after which every wave only works in registers, so the
-  // LDS is free for |X| as soon as this wave gets here
-  double *ylds = lds;  // [ypad(YLEN)]: bin k - YLO at ypad(k - YLO)
-  // |X| by aero_hypot_nr when every value of the wave is in its range (the
-  // usual case: |X| of a live channel is ~1e9), else by aero_hypot
+  double *ylds = lds;  // bin k - YLO at ypad(k - YLO): one pad double per DMA block
+  // direct-to-LDS loads of AERO_COARSE_YDMA bytes per lane (4, or 16:
+  // gfx950's b128 form), one block of 16 x AERO_COARSE_YDMA doubles per wave
+  // instruction, blocks dealt to waves
+#ifndef AERO_COARSE_YDMA
+#define AERO_COARSE_YDMA 4
+#endif
+  constexpr int DMA = AERO_COARSE_YDMA, DPB = 8 * DMA, PS = DMA == 4 ? 5 : 7;  // doubles per block, log2
+  auto ypad = [](int q) { return fftl::ypadn<PS>(q); };
+  if (!yreset) {
+    constexpr int NB = (YLEN + DPB - 1) / DPB;
+    static_assert(NB * (DPB + 1) <= PADDED, "the y history fits the transform's LDS");
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
+    for (int b = wv; b < NB; b += FT / 64) {
+      const int k = b * DPB + ln * DMA / 8;
+      const char *src = reinterpret_cast<const char *>(yg + (k < YLEN ? k : 0)) + (DMA == 4 ? 4 * (ln & 1) : 0);
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)(ylds + b * (DPB + 1)), DMA, 0,
+                                       0);
+    }
+  }
+  // a thread's outputs in the kept bins: all lanes', none or some (fixed by the layout)
+  constexpr fftl::YClass YC = fftl::yclass<L>(K::YLO, K::YHI);
+  auto yin = [&](int i) {
+    const int yi = (bin_t | chain::out_bin_reg<L>(i)) ^ (N / 2);
+    return YC.v[i] == 1 || (YC.v[i] == 2 && yi >= K::YLO && yi <= K::YHI);
+  };
+  auto yq = [&](int i) { return ((bin_t | chain::out_bin_reg<L>(i)) ^ (N / 2)) - K::YLO; };
+  // log10(max(|X|, 1)) in registers; |X| by aero_hypot_nr when every value
+  // of the wave is in its range (the usual case: |X| of a live channel is
+  // ~1e9), else by aero_hypot
+  double hx[16];
   bool nr = true;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
+    if (YC.v[i] == 0) continue;
     const double a = fabs(x[i].x), b = fabs(x[i].y);
     nr = nr && a <= 0x1p200 && b <= 0x1p200 && (a >= 0x1p-200 || b >= 0x1p-200);
   }
   if (__all(nr)) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int yi = (bin_t | chain::out_bin_reg<L>(i)) ^ (N / 2);
-      if (yi >= K::YLO && yi <= K::YHI) ylds[fftl::ypad(yi - K::YLO)] = CO_HYPOT_NR(x[i].x, x[i].y);
-    }
+    for (int i = 0; i < 16; ++i)
+      if (YC.v[i] != 0 && yin(i)) hx[i] = CO_LOG10(fmax(CO_HYPOT_NR(x[i].x, x[i].y), 1.0));
   } else {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int yi = (bin_t | chain::out_bin_reg<L>(i)) ^ (N / 2);
-      if (yi >= K::YLO && yi <= K::YHI) ylds[fftl::ypad(yi - K::YLO)] = CO_HYPOT(x[i].x, x[i].y);
+    for (int i = 0; i < 16; ++i)
+      if (YC.v[i] != 0 && yin(i)) hx[i] = CO_LOG10(fmax(CO_HYPOT(x[i].x, x[i].y), 1.0));
+  }
+  CSTAMP(6);
+  __builtin_amdgcn_s_waitcnt(0);  // this wave's y loads have landed in LDS
+  __syncthreads();                // and every other wave's
+  CSTAMP(9);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (YC.v[i] != 0 && yin(i)) {
+      const int q = yq(i);
+      const double yold = yreset ? 20.0 : ylds[ypad(q)];
+      const double ynew = yold * 0.9 + 0.1 * 10 * hx[i];
+      ylds[ypad(q)] = ynew;
     }
   }
-  double yp2 = yload(t + 2 * FT);
   __syncthreads();
-  CSTAMP(6);
-#pragma unroll 1
-  for (int k = t; k < YLEN; k += FT) {
-    const double yold = yp0;
-    yp0 = yp1;
-    yp1 = yp2;
-    yp2 = yload(k + 3 * FT);
-    const double ynew = yold * 0.9 + 0.1 * 10 * CO_LOG10(fmax(ylds[fftl::ypad(k)], 1.0));
-    yg[k] = ynew;
-    ylds[fftl::ypad(k)] = ynew;
-  }
-  __syncthreads();
+  for (int k = t; k < YLEN; k += FT) yg[k] = ylds[ypad(k)];
   CSTAMP(7);
   // fold search (coarsefreqestimate.cpp:166-185): first strict maximum above 0
   double bv = 0.0;
   int bi = 0x7fffffff;
   for (int r = 0;; ++r) {
-    const int i = K::ILO + t + FT * r;
-    if (i >= K::IHI) break;
+    const int i = KB.ilo + t + FT * r;
+    if (i >= KB.ihi) break;
     double val = 0;
     for (int j = -1; j <= 1; j++)
-      val += (ylds[fftl::ypad(i - K::EPB - j - K::YLO)] + ylds[fftl::ypad(i + K::EPB + j - K::YLO)]);
+      val += (ylds[ypad(i - KB.epb - j - K::YLO)] + ylds[ypad(i + KB.epb + j - K::YLO)]);
     if (val > bv) {
       bv = val;
       bi = i;
@@ -379,7 +419,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   CSTAMP(8);
 #ifdef AERO_X_STAMPS
   if (t == 0) {
-    for (int k = 0; k < 9; ++k) atomicAdd(&g_cstamps[k], cst_[k]);
+    for (int k = 0; k < 10; ++k) atomicAdd(&g_cstamps[k], cst_[k]);
     atomicAdd(&g_cstamps[CSTAMP_N - 1], 1ull);
   }
 #endif
@@ -392,7 +432,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   }
   const int zmaxloc = (bv > 0.0) ? bi : N / 2;
   const double nfft = (double)N;
-  const double freq_offset_est = -((double)(zmaxloc - nfft / 2)) * (K::FS / nfft) * 0.5;
+  const double freq_offset_est = -((double)(zmaxloc - nfft / 2)) * (KB.fs / nfft) * 0.5;
   double est;
   int ecd = S.is[IS_EMPTYCD * C + c];
   if (ecd <= 0) {
@@ -419,7 +459,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   h.step_fc = 0.0;
   unsigned iter = (unsigned)is[IS_HUNT_ITER * C + c];
   int scans = is[IS_HUNT_SCANS * C + c];
-  const bool gotasignal = hop_control(h, std::integral_constant<int, M>(), est, mse, iter, scans, nk);
+  const bool gotasignal = hop_control(h, std::integral_constant<int, M>(), KB.fs, est, mse, iter, scans, nk);
   is[IS_HUNT_ITER * C + c] = (int)iter;
   is[IS_HUNT_SCANS * C + c] = scans;
   if (h.stepped) {
@@ -474,7 +514,12 @@ void launch_coarse(hipStream_t st, int mode, const DevState &S, const DevTables 
     case MODE_MSK1200_12K:
       hipLaunchKernelGGL(coarse_kernel<MODE_MSK1200_12K>, dim3(nch), dim3(512), 0, st, S, T, nch);
       break;
-    default: hipLaunchKernelGGL(coarse_kernel<MODE_MSK1200_48K>, dim3(nch), dim3(512), 0, st, S, T, nch); break;
+    case MODE_MSK1200_48K:
+      hipLaunchKernelGGL(coarse_kernel<MODE_MSK1200_48K>, dim3(nch), dim3(512), 0, st, S, T, nch);
+      break;
+    default:  // generic-rate MSK (the kernel does not depend on the bit rate)
+      hipLaunchKernelGGL(coarse_kernel<MODE_MSKG600>, dim3(nch), dim3(512), 0, st, S, T, nch);
+      break;
   }
 }
 

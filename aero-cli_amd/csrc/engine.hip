@@ -155,14 +155,18 @@ struct HostTimer {
 }  // namespace
 
 
-// One group per channel kind (Mode): its own device pool, stream, tables and
-// kernels.  aero_engine routes every channel to its kind's group.
+// One group per channel kind: OQPSK, each fixed-rate MSK Mode, and each
+// (bit rate, Fs) of the generic-rate MSK kernels; its own device pool,
+// stream, tables and kernels.  aero_engine routes every channel to its
+// group (engine group id gid: the Mode for the fixed kinds, above MODE_COUNT
+// for generic-rate groups).
 struct Group {
   ~Group();  // releases every device/host resource (also on a failed group_create)
-  int mode = MODE_OQPSK;
+  int mode = MODE_OQPSK;  // kernel family: a Mode, MODE_MSKG600 or MODE_MSKG1200
+  int gid = 0;            // engine group id
   ModeGeom g{};
   int device = 0, flags = 0, C = 0, nch = 0;
-  const char *tag = "";  // timing-name prefix ("" for OQPSK, "msk600_", "msk1200_", "msk600_48k_", ...)
+  std::string tag;  // timing-name prefix ("" for OQPSK, "msk600_", "msk1200_", "msk600_48k_", "msk600_16000_", ...)
   hipStream_t st = nullptr;
   DevState S{};
   DevTables T{};
@@ -277,13 +281,13 @@ struct Group {
 };
 
 // chmap kinds of burst-mode channels (burst_engine.hip): MODE_BURST + BurstKind
-constexpr int MODE_BURST = MODE_COUNT;
+constexpr int MODE_BURST = 1 << 20;
 
 struct aero_engine {
   int device = 0, flags = 0, max_channels = 0;
-  std::unique_ptr<Group> groups[MODE_COUNT];
+  std::vector<std::unique_ptr<Group>> groups = std::vector<std::unique_ptr<Group>>(MODE_COUNT);  // by gid
   BurstGroup *burst[2] = {nullptr, nullptr};  // BURST_OQPSK, BURST_MSK
-  std::vector<std::pair<int, int>> chmap;  // engine channel -> (mode, local index)
+  std::vector<std::pair<int, int>> chmap;  // engine channel -> (gid or MODE_BURST + kind, local index)
   std::unique_ptr<HostPool> hpool;
   std::map<std::string, TimingSlot> timing;  // engine-level host sections
 };
@@ -298,8 +302,7 @@ T *carve(char *&p, size_t count) {
   return r;
 }
 
-size_t layout(DevState &S, DevTables &T, int mode, int C, int flags, char *base) {
-  const ModeGeom g = mode_geom(mode);
+size_t layout(DevState &S, DevTables &T, int mode, const ModeGeom &g, int C, int flags, char *base) {
   const bool msk = mode != MODE_OQPSK;
   char *p = base;
   S.C = C;
@@ -342,7 +345,7 @@ size_t layout(DevState &S, DevTables &T, int mode, int C, int flags, char *base)
   return (size_t)(p - base);
 }
 
-std::string tname(const Group *e, const char *name) { return std::string(e->tag) + name; }
+std::string tname(const Group *e, const char *name) { return e->tag + name; }
 
 void ev_begin(Group *e, const char *name, hipEvent_t &a, hipEvent_t &b, hipStream_t st = nullptr) {
   if (!(e->flags & AERO_F_TIMING)) return;
@@ -931,7 +934,7 @@ int run_impl(aero_engine *e, int flush) {
   for (BurstGroup *b : e->burst)
     if (b)
       if (int rc = burst_run(b, flush)) return rc;
-  Group *act[MODE_COUNT];
+  std::vector<Group *> act(e->groups.size());
   int na = 0;
   for (auto &g : e->groups)
     if (g && g->nch) {
@@ -974,24 +977,65 @@ int pop_vec(std::vector<T> &v, T *dst, size_t cap, size_t *n) {
 }
 
 // group tables and kernel constants (host glibc, g++-compiled: tables_host.cpp)
-int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
+// the rate-dependent constants of a generic-rate MSK group at sample rate fs
+// (MskDemodulator::setSettings with fb 600, decode/mskdemodulator.cpp:94-218;
+// CoarseFreqEstimate::setSettings(13, 900, 600, Fs), coarsefreqestimate.cpp:39-76,
+// and the fold search bounds of :166-185), or false when the kernels'
+// assumptions do not hold at that rate
+bool msk_gen_consts(int fs, MskGen &m) {
+  if (fs < MSK_FS_MIN || fs > MSK_FS_MAX) return false;
+  m = MskGen{};
+  m.fs = fs;
+  m.sps = fs / 600;
+  // fb < 1200 and Fs != 48000: the "300hz / 4hz / 12000" design, ee 0.0125
+  m.sr_b0 = 5.233248111921052e-04;
+  m.sr_b2 = -5.233248111921052e-04;
+  m.sr_a1 = -1.974342917561558;
+  m.sr_a2 = 0.998953350377616;
+  m.ee = 0.0125;
+  int size;
+  if (!host_delay_uniform(m.sps / 2.0, size, m.d8_old, m.d8_new, m.d8w, m.d8omw)) return false;
+  if (size != msk_geom(600, fs).d8_len || m.d8_new < 1 || m.d8_old >= size) return false;
+  const double nfft = MSK_NFFT, hzperbin = (double)fs / nfft, lockingbw = 900.0, fb = 600.0;
+  const double startbin = std::max(std::round(lockingbw / hzperbin), 1.0);
+  m.start = (int)startbin;
+  m.stop = (int)(nfft - startbin);
+  m.epb = (int)std::round(fb / (2.0 * hzperbin));
+  m.ilo = (int)std::round((-lockingbw / hzperbin) + ((double)(MSK_NFFT / 2)));
+  m.ihi = (int)std::round((lockingbw / hzperbin) + ((double)(MSK_NFFT / 2)));
+  // every fold term inside the y bins an MSK group keeps (no "jic" skips)
+  return m.ilo - m.epb - 1 >= MSK_YLO && m.ihi - 1 + m.epb + 1 <= MSK_YHI && m.ilo < m.ihi;
+}
+
+// gid: the group's engine id; fs: the sample rate of a generic-rate group
+// (mode MODE_MSKG600 / MODE_MSKG1200), 0 for a fixed kind
+int group_create(aero_engine *E, int mode, int gid, int fs, std::unique_ptr<Group> &out) {
   std::unique_ptr<Group> e(new Group());  // ~Group releases what an early return leaves allocated
   e->mode = mode;
-  e->g = mode_geom(mode);
+  e->gid = gid;
   e->device = E->device;
   e->flags = E->flags;
   e->hpool = E->hpool.get();
-  static const char *const tags[MODE_COUNT] = {"", "msk600_", "msk1200_", "msk600_24k_", "msk600_48k_",
-                                                "msk1200_12k_", "msk1200_48k_"};
-  e->tag = tags[mode];
+  MskGen mg{};
+  if (msk_generic(mode)) {
+    if (!msk_gen_consts(fs, mg)) return AERO_E_RATE;
+    e->g = msk_geom(msk_bitrate(mode), fs);
+    e->tag = "msk" + std::to_string(msk_bitrate(mode)) + "_" + std::to_string(fs) + "_";
+  } else {
+    static const char *const tags[MODE_COUNT] = {"", "msk600_", "msk1200_", "msk600_24k_", "msk600_48k_",
+                                                  "msk1200_12k_", "msk1200_48k_"};
+    e->g = mode_geom(mode);
+    e->tag = tags[mode];
+  }
   e->C = (E->max_channels + 63) & ~63;
   DevState S{};
   DevTables T{};
-  const size_t bytes = layout(S, T, mode, e->C, e->flags, nullptr) + 4096;
+  const size_t bytes = layout(S, T, mode, e->g, e->C, e->flags, nullptr) + 4096;
   if (hipMalloc(&e->pool, bytes) != hipSuccess) return AERO_E_NOMEM;
   e->pool_bytes = bytes;
   HIPCHK(hipMemset(e->pool, 0, bytes));
-  layout(e->S, e->T, mode, e->C, e->flags, reinterpret_cast<char *>(e->pool));
+  layout(e->S, e->T, mode, e->g, e->C, e->flags, reinterpret_cast<char *>(e->pool));
+  e->S.mg = mg;
   HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
   if (hipHostMalloc(&e->h_err, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return AERO_E_NOMEM;
   *e->h_err = 0;
@@ -1060,6 +1104,8 @@ int group_create(aero_engine *E, int mode, std::unique_ptr<Group> &out) {
     const double ct_b[3] = {0.0010275610653672064, 0.0020551221307344128, 0.0010275610653672064};
     const double ct_a[3] = {1, -1.9207386815577139, 0.92509247310306331};
     upload_demod_constants(taps.data(), dly, sr_b, sr_a, ct_b, ct_a);
+  } else if (msk_generic(mode)) {
+    host_msk_taps(e->g.fs / 600, taps.data());  // delayt8 ages and weights: S.mg
   } else {
     // matched filter sin(pi i / 2SPS) / 2SPS (mskdemodulator.cpp:126-133)
     const int sps = e->g.fs / 600;
@@ -1367,10 +1413,32 @@ namespace {
 
 // A new local channel of the group of `mode` (created on first use) for
 // engine channel gc; its device state is initialised by flush_pending_init
-int group_add_channel(aero_engine *e, int mode, const aero_channel_cfg &cfg, int gc, int *local) {
-  if (!e->groups[mode])
-    if (int rc = group_create(e, mode, e->groups[mode])) return rc;
-  Group *g = e->groups[mode].get();
+// the gid of the continuous MSK group serving (bit rate, fs), creating a
+// generic-rate group when fs has no fixed one; AERO_E_RATE for rates the
+// engine does not serve
+int msk_gid(aero_engine *e, int bitrate, int fs, int &gid) {
+  const int m = msk_mode(bitrate, fs);
+  if (m >= 0) {
+    gid = m;
+    return AERO_OK;
+  }
+  const int gm = bitrate == 600 ? MODE_MSKG600 : MODE_MSKG1200;
+  for (size_t k = MODE_COUNT; k < e->groups.size(); k++)
+    if (e->groups[k] && e->groups[k]->mode == gm && e->groups[k]->g.fs == fs) {
+      gid = (int)k;
+      return AERO_OK;
+    }
+  std::unique_ptr<Group> g;
+  if (int rc = group_create(e, gm, (int)e->groups.size(), fs, g)) return rc;
+  gid = (int)e->groups.size();
+  e->groups.push_back(std::move(g));
+  return AERO_OK;
+}
+
+int group_add_channel(aero_engine *e, int gid, const aero_channel_cfg &cfg, int gc, int *local) {
+  if (!e->groups[gid])
+    if (int rc = group_create(e, gid, gid, 0, e->groups[gid])) return rc;
+  Group *g = e->groups[gid].get();
   if (!g->free_slots.empty()) {  // a slot an MSK channel moved out of
     if (int rc = flush_pending_init(g)) return rc;
     const int c = g->free_slots.back();
@@ -1431,10 +1499,10 @@ int group_add_channel(aero_engine *e, int mode, const aero_channel_cfg &cfg, int
 //     resonator (its design follows Fs), mse = 10.
 int msk_migrate(aero_engine *e, int ch, uint32_t fs) {
   const int from = e->chmap[ch].first, c = e->chmap[ch].second;
-  Group *g = e->groups[from].get();
-  const int to = msk_mode(msk_bitrate(from), (int)fs);
-  if (to < 0) return AERO_E_RATE;
   HIPCHK(hipSetDevice(e->device));
+  int to;
+  if (int rc = msk_gid(e, msk_bitrate(e->groups[from]->mode), (int)fs, to)) return rc;
+  Group *g = e->groups[from].get();
   if (int rc = flush_pending_init(g)) return rc;
   if (int rc = run_group(g, 1)) return rc;
   if (int rc = drain_group(g)) return rc;
@@ -1618,20 +1686,20 @@ int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) 
     e->chmap.push_back({MODE_BURST + kind, local});
     return AERO_OK;
   }
-  int mode;
-  if (cfg->bitrate == 10500 && cfg->fs == 48000)
-    mode = MODE_OQPSK;
-  else if (cfg->bitrate == 600 || cfg->bitrate == 1200)  // 12 / 24 kHz as decode/decode.cpp:145, or 48 kHz
-    mode = msk_mode(cfg->bitrate, (int)cfg->fs);
-  else
-    mode = -1;
-  if (mode < 0) return AERO_E_INVALID;  // decode/decode.h:42 validBitRates, with their rates
+  // decode/decode.h:42 validBitRates: 10500 (48 kHz), 600 and 1200 at any
+  // rate MSK is served at (12 / 24 kHz as decode/decode.cpp:145)
+  if (!(cfg->bitrate == 10500 && cfg->fs == 48000) && !(cfg->bitrate == 600 || cfg->bitrate == 1200))
+    return AERO_E_INVALID;
+  if (cfg->bitrate != 10500 && (cfg->fs < (uint32_t)MSK_FS_MIN || cfg->fs > (uint32_t)MSK_FS_MAX)) return AERO_E_RATE;
   HIPCHK(hipSetDevice(e->device));
   host_wait(e);  // the host task indexes the per-channel tables
+  int gid = MODE_OQPSK;
+  if (cfg->bitrate != 10500)
+    if (int rc = msk_gid(e, (int)cfg->bitrate, (int)cfg->fs, gid)) return rc;
   int c;
-  if (int rc = group_add_channel(e, mode, *cfg, (int)e->chmap.size(), &c)) return rc;
+  if (int rc = group_add_channel(e, gid, *cfg, (int)e->chmap.size(), &c)) return rc;
   *ch_out = (int)e->chmap.size();
-  e->chmap.push_back({mode, c});
+  e->chmap.push_back({gid, c});
   return AERO_OK;
 }
 
@@ -2022,10 +2090,11 @@ int aero_engine_feed_dev(aero_engine *e, int nitems, const int *ch, const int16_
                          const uint32_t *fs, hipEvent_t ready, hipStream_t producer) {
   if (!e || nitems < 0 || (nitems && (!ch || !src || !n || !fs))) return AERO_E_INVALID;
   HIPCHK(hipSetDevice(e->device));
-  std::vector<std::pair<int, std::pair<const int16_t *, size_t>>> per[MODE_COUNT];
+  // per group (gid; a rate change below may add a generic-rate group)
+  std::vector<std::vector<std::pair<int, std::pair<const int16_t *, size_t>>>> per(e->groups.size());
   std::vector<uint8_t> queued(e->chmap.size(), 0);  // engine channels with an item in per[]
   auto feed_queued = [&]() -> int {
-    for (int m = 0; m < MODE_COUNT; m++)
+    for (size_t m = 0; m < per.size(); m++)
       if (!per[m].empty()) {
         if (int rc = feed_group(e->groups[m].get(), per[m], ready, producer)) return rc;
         per[m].clear();
@@ -2054,7 +2123,8 @@ int aero_engine_feed_dev(aero_engine *e, int nitems, const int *ch, const int16_
     Group *g = route_rate(e, ch[i], fs[i], c, rc);
     if (rc) return rc;
     if (!g || !src[i]) return AERO_E_INVALID;
-    per[g->mode].push_back({c, {src[i], n[i]}});
+    if (per.size() < e->groups.size()) per.resize(e->groups.size());
+    per[g->gid].push_back({c, {src[i], n[i]}});
     queued[ch[i]] = 1;
   }
   return feed_queued();

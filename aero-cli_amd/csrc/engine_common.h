@@ -39,8 +39,11 @@ constexpr int JOB_OUT = 328;          // 312 infofield + len + mask + formatid +
 // message at another rate re-applies the MSK settings at that rate
 // (MskDemodulator::dataReceived, decode/mskdemodulator.cpp:473-481, settings
 // :94-218) and the channel moves to the group of that rate (engine.hip
-// msk_migrate).  Supported MSK rates: 12000, 24000, 48000 (the VFO rates
-// aero-publish produces by default, publish/publisher.cpp:164-176).
+// msk_migrate).  12000, 24000 and 48000 (the VFO rates aero-publish is
+// configured with by default, publish/publisher.cpp:164-176) have groups of
+// their own, compiled for that rate; every other rate in [MSK_FS_MIN,
+// MSK_FS_MAX] runs in a group of the generic-rate kernels (MODE_MSKG600 /
+// MODE_MSKG1200, rate-dependent constants in DevState::mg).
 enum Mode : int {
   MODE_OQPSK = 0,
   MODE_MSK600 = 1,       // 600 bps, 12 kHz
@@ -51,14 +54,28 @@ enum Mode : int {
   MODE_MSK1200_48K = 6,
   MODE_COUNT = 7
 };
+// the kernel families of the generic-rate MSK groups (engine group ids of
+// such groups are above MODE_COUNT; Group::mode holds one of these)
+constexpr int MODE_MSKG600 = 8, MODE_MSKG1200 = 9;
+constexpr bool msk_generic(int m) { return m == MODE_MSKG600 || m == MODE_MSKG1200; }
+// MSK sample rates served.  Below 12000 the coarse estimator's fold search
+// would read y bins outside the range every MSK group keeps (MSK_YLO..MSK_YHI,
+// which a channel carries over a rate change); aero-publish's VFO rate is
+// at least the configured out_rate (its decimation count is
+// int(log2(Fs / out_rate)), publish/publisher.cpp:196-210), 12000 by default
+// for 600 bps.  Above 96000 the per-channel AGC ring (Fs doubles) and matched
+// filter (2 Fs / 600 taps) grow past what a group is sized for; aero-publish
+// produces less than twice out_rate (48000 at most by default).
+constexpr int MSK_FS_MIN = 12000, MSK_FS_MAX = 96000;
 constexpr int msk_fs(int m) {
   return (m == MODE_MSK600 || m == MODE_MSK1200_12K) ? 12000
                                                       : ((m == MODE_MSK1200 || m == MODE_MSK600_24K) ? 24000 : 48000);
 }
 constexpr int msk_bitrate(int m) {
-  return (m == MODE_MSK600 || m == MODE_MSK600_24K || m == MODE_MSK600_48K) ? 600 : 1200;
+  return (m == MODE_MSK600 || m == MODE_MSK600_24K || m == MODE_MSK600_48K || m == MODE_MSKG600) ? 600 : 1200;
 }
-// the MSK group of (AeroL bit rate, sample rate), or -1 for an unsupported rate
+// the fixed-rate MSK group of (AeroL bit rate, sample rate), or -1 (a
+// generic-rate group serves the rate, or none)
 inline int msk_mode(int bitrate, int fs) {
   for (int m = MODE_MSK600; m < MODE_COUNT; ++m)
     if (msk_bitrate(m) == bitrate && msk_fs(m) == fs) return m;
@@ -81,7 +98,7 @@ struct MskK {
   static constexpr double SR_A2 = F48 ? 0.999738234875681 : 0.998953350377616;
   static constexpr double EE = F48 ? 0.025 : 0.0125;
 };
-constexpr int MAX_TAPS = 192;           // matched filter / RRC taps a group table holds (MSK 48 kHz: 160)
+constexpr int MAX_TAPS = 2 * (MSK_FS_MAX / 600);  // matched filter / RRC taps a group table holds (MSK 96 kHz: 320)
 constexpr int MSK_NFFT = 8192;          // coarsefreqest_fft_power 13 (mskdemodulator.h:26)
 constexpr int MSK_HOP = 2048;           // 75 % overlap (mskdemodulator.cpp:289-291)
 constexpr int MSK_MSEMA = 600;          // msema = MovingAverage(600) (mskdemodulator.cpp:57)
@@ -99,12 +116,31 @@ struct ModeGeom {
   int fs, nfft, hop, agc_len, ntaps, marg_len, dt_len, ms_len, dsm_len, d8_len, block, leaver, dl2_len, y_lo,
       y_hi, soft_group;
 };
+// MSK at sample rate fs: SPS = int(Fs / fb) (mskdemodulator.cpp:110), the
+// matched filter 2 SPS taps, AGC(1, Fs), marg SPS, dt SPS/2 (+1 slot),
+// delayedsmpl SPS (+1), delayt8 ceil(SPS/2) + 1 (DSP.h:360-362)
+inline ModeGeom msk_geom(int bitrate, int fs) {
+  const int sps = fs / 600, leaver = bitrate == 600 ? 6 : 9;
+  return {fs,      MSK_NFFT,          MSK_HOP,     fs,          2 * sps, sps,     sps / 2 + 1, MSK_MSEMA,
+          sps + 1, (sps + 1) / 2 + 1, leaver * 64, leaver, MSK_DL2_LEN, MSK_YLO, MSK_YHI, 12};
+}
 inline ModeGeom mode_geom(int m) {
   if (m == MODE_OQPSK) return {48000, 16384, 4096, 192000, 55, 800, 401, 400, 0, 0, 4992, 78, 4987, 2815, 13568, 32};
-  const int fs = msk_fs(m), sps = fs / 600, leaver = msk_bitrate(m) == 600 ? 6 : 9;
-  return {fs,      MSK_NFFT,   MSK_HOP,     fs,          2 * sps, sps,     sps / 2 + 1, MSK_MSEMA,
-          sps + 1, sps / 2 + 1, leaver * 64, leaver, MSK_DL2_LEN, MSK_YLO, MSK_YHI, 12};
+  return msk_geom(msk_bitrate(m), msk_fs(m));
 }
+
+// the rate-dependent constants of a generic-rate MSK group, host-computed as
+// MskDemodulator::setSettings (decode/mskdemodulator.cpp:94-218, fb 600) and
+// CoarseFreqEstimate::setSettings(13, 900, 600, Fs)
+// (decode/coarsefreqestimate.cpp:39-76) compute them
+struct MskGen {
+  double fs;
+  double sr_b0, sr_b2, sr_a1, sr_a2;  // st_iir_resonator ("300hz / 4hz / 12000" design: Fs != 48000)
+  double ee;                          // IfHavePassedPoint(ee)
+  double d8w, d8omw;                  // delayt8 weights (the same at every ring pointer)
+  int sps, d8_old, d8_new;            // delayt8 ages of older / newer
+  int start, stop, ilo, ihi, epb;     // boxcar startbin..stopbin, fold [ilo, ihi), expectedpeakbin
+};
 
 // double state fields
 enum DS : int {
@@ -177,6 +213,7 @@ struct DevState {
   int C;                   // channel stride
   int mode;                // Mode
   ModeGeom g;              // ring and block sizes of this group
+  MskGen mg;               // generic-rate MSK groups: the rate's constants
   double *ds;              // [DS_COUNT][C]
   int *is;                 // [IS_COUNT][C]
   long long *ls;           // [LS_COUNT][C]

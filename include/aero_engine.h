@@ -28,7 +28,7 @@ extern "C" {
 #define AERO_E_HIP (-3)        /* HIP runtime error                        */
 #define AERO_E_NOGPU (-4)      /* no gfx950 device / kernels not loadable  */
 #define AERO_E_FULL (-5)       /* channel table or PCM ring full           */
-#define AERO_E_RATE (-6)       /* sample rate differs from the channel's   */
+#define AERO_E_RATE (-6)       /* sample rate the channel kind does not serve (MSK: outside [12000, 96000] Hz) */
 #define AERO_E_DEVICE (-7)     /* a kernel gave up (wave hand-off timeout): the run's outputs are invalid */
 
 /* engine flags */
@@ -79,7 +79,11 @@ int aero_engine_create(const aero_engine_cfg *cfg, aero_engine **out);
 void aero_engine_destroy(aero_engine *e);
 
 /* Opens one VFO channel: the Decoder ctor's demod + AeroL + hunter wiring
- * (decode/decode.cpp:117-241) for one -t topic. */
+ * (decode/decode.cpp:117-241) for one -t topic.  bitrate 10500 at fs 48000,
+ * or 600 / 1200 (MSK) at any fs in [12000, 96000] Hz: 12000, 24000 and
+ * 48000 run kernels compiled for the rate, other rates the generic-rate MSK
+ * kernels.  AERO_E_INVALID for another bit rate or OQPSK rate, AERO_E_RATE
+ * for an MSK rate outside that range. */
 int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out);
 
 /* One ZMQ message == one call: Decoder::audioReceived ->
@@ -89,9 +93,9 @@ int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out);
  * before returning (a continuous channel's message is staged in pinned host
  * memory and reaches the GPU at the next aero_run).  fs: an OQPSK or burst
  * channel only logs a mismatch; a continuous MSK channel re-applies its
- * settings at 12000, 24000 or 48000 Hz, keeping the state
+ * settings at any rate in [12000, 96000] Hz, keeping the state
  * MskDemodulator::setSettings keeps (decode/mskdemodulator.cpp:94-218), and
- * refuses any other rate (AERO_E_RATE, the message is dropped). */
+ * refuses a rate outside it (AERO_E_RATE, the message is dropped). */
 int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t fs);
 
 /* Lockstep batch push for channels [0, nch): pcm is time-major, n samples

@@ -1,0 +1,46 @@
+#!/bin/bash
+# One GPU call made of named steps, each under its own time limit, output to
+# gpurun_out/TAG/.  A step that fails its checks (pytest / bench exit 1-3) is
+# recorded and the call goes on; a fault, abort, segfault or time limit ends it.
+#   tests[=K_EXPR]     the GPU suite (or a -k subset; '+' stands for ' or ')
+#   vtests=VARIANT:K   a -k subset of the GPU suite on libaero_engine_VARIANT.so
+#   smoke              __graft_entry__.smoke()
+#   bench[=ARGS]       bench.py (default: the headline line), ARGS comma-separated
+#   mode=M             bench.py --mode M with its CPU baseline (one run)
+#   ab=VARIANT:M       bench.py --mode M on libaero_engine_VARIANT.so, no CPU baseline
+#   stamps[=VARIANT]   per-section cycle totals (libaero_engine_stamps.so or _VARIANT.so)
+# Usage: bash scripts/gpu_steps.sh TAG STEP...
+set -o pipefail
+TAG=$1; shift
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+cd $R
+step() {  # SECONDS OUTFILE cmd...
+  local s=$1 f=$2; shift 2
+  timeout -k 10 "$s" "$@" > "$OUT/$f" 2>&1
+  local rc=$?
+  echo "[step] rc=$rc $*" | tee -a "$OUT/$f"
+  [ $rc -ge 4 ] && exit $rc
+  return 0
+}
+for st in "$@"; do
+  case $st in
+    tests) step 900 pytest_gpu.log python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests ;;
+    tests=*) k=${st#tests=}; step 900 pytest_gpu_${k//+/_}.log python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu -k "${k//+/ or }" tests ;;
+    vtests=*) v=${st#vtests=}; k=${v#*:}; v=${v%%:*}
+      AERO_ENGINE_SO=$R/aero-cli_amd/libaero_engine_$v.so step 900 pytest_gpu_${v}_${k//+/_}.log python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu -k "${k//+/ or }" tests ;;
+    smoke) step 300 smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step 400 bench.log python bench.py ;;
+    bench=*) a=${st#bench=}; step 400 "bench_${a//[ ,=-]/_}.log" python bench.py ${a//,/ } ;;
+    mode=*) m=${st#mode=}; step 400 bench_$m.log python bench.py --mode $m --cpu-runs 1 ;;
+    ab=*) v=${st#ab=}; m=${v#*:}; v=${v%%:*}
+      so=$R/aero-cli_amd/libaero_engine${v:+_$v}.so; [ "$v" = prod ] && so=$R/aero-cli_amd/libaero_engine.so
+      AERO_ENGINE_SO=$so step 300 bench_${m}_$v.log python bench.py --mode $m --no-cpu-baseline ;;
+    stamps) AERO_ENGINE_SO=$R/aero-cli_amd/libaero_engine_stamps.so step 300 coarse_stamps.log python -u scripts/coarse_stamps.py
+      AERO_ENGINE_SO=$R/aero-cli_amd/libaero_engine_stamps.so step 300 demod_stamps.log python -u scripts/demod_stamps.py ;;
+    stamps=*) v=${st#stamps=}
+      AERO_ENGINE_SO=$R/aero-cli_amd/libaero_engine_$v.so step 300 coarse_stamps_$v.log python -u scripts/coarse_stamps.py ;;
+    *) echo "unknown step $st"; exit 2 ;;
+  esac
+done

@@ -69,14 +69,72 @@ def test_msk_rate_change_matches_oracle(engine_lib):
     eng.close()
 
 
+# rates without a fixed-rate group: the generic-rate kernels (demod_msk.hip
+# demod_mskg_kernel, coarse bins from MskGen).  16000 and 15000 are what
+# aero-publish emits for a 12 kHz out_rate from 2.048 / 1.92 Msps receivers
+# (Fs / 2^int(log2(Fs / out_rate)), publish/publisher.cpp:196-210); 18750
+# has an odd SPS (31: delayt8 of 15.5 samples, weights 0.5 / 0.5); 96000 is
+# the largest rate served
+GENERIC = [
+    (600, [(16000, 20.0, 0xE300, 1800.0, 14.0)], 0.25),
+    (600, [(12000, 6.0, 0xE310, 1500.0, 14.0), (18750, 12.0, 0xE311, 1500.0, 14.0),
+           (15000, 8.0, 0xE312, 1500.0, 14.0), (24000, 6.0, 0xE313, 1500.0, 14.0)], 0.25),
+    (1200, [(24000, 6.0, 0xE320, 2100.0, 14.0), (40000, 10.0, 0xE321, 2100.0, 14.0),
+            (96000, 4.0, 0xE322, 2100.0, 14.0)], 0.25),
+    (600, [(96000, 5.0, 0xE330, 1800.0, 14.0)], 0.125),
+]
+
+
+def _run_vs_oracle(eng, chans, spec, msgs):
+    pos = [0] * len(msgs)
+    while any(p < len(m) for p, m in zip(pos, msgs)):
+        for k, ch in enumerate(chans):
+            if pos[k] < len(msgs[k]):
+                pcm, fs = msgs[k][pos[k]]
+                eng.push(ch, pcm, fs=fs)
+                pos[k] += 1
+        eng.run()
+    eng.flush()
+    items_total = 0
+    for k, ((br, _, _), ch) in enumerate(zip(spec, chans)):
+        o = tl.Oracle(bitrate=br)
+        for pcm, fs in msgs[k]:
+            o.push(pcm, fs=fs)
+        sb, rsb = eng.softbits(ch), o.softbits()
+        assert len(rsb) > 500
+        assert len(sb) == len(rsb) and np.array_equal(sb, rsb), 'channel %d soft bits differ (%d vs %d)' % (
+            k, len(sb), len(rsb))
+        h, rh = eng.hops(ch), o.hops()
+        assert h.shape == rh.shape and np.array_equal(h.view(np.int64), rh.view(np.int64)), \
+            'channel %d hop records differ' % k
+        assert np.array_equal(eng.frames(ch), o.frames()), 'channel %d frames differ' % k
+        items = eng.items(ch)
+        assert items == o.item_lines('A'), 'channel %d items differ' % k
+        items_total += len(items)
+    return items_total
+
+
+def test_msk_generic_rates_match_oracle(engine_lib):
+    """Channels at and through rates with no fixed-rate group, beside each
+    other, against the oracle's setSettings at those rates."""
+    import aero_engine as ae
+    msgs = [_messages(br, segs, m) for br, segs, m in GENERIC]
+    eng = ae.Engine(max_channels=8, flags=ae.F_TRACE_SOFT | ae.F_TRACE_HOPS | ae.F_TRACE_FRAMES)
+    chans = [eng.open_channel(br) for br, _, _ in GENERIC]
+    assert _run_vs_oracle(eng, chans, GENERIC, msgs) > 0
+    eng.close()
+
+
 def test_msk_unsupported_rate_refused(engine_lib):
     import aero_engine as ae
     eng = ae.Engine(max_channels=2)
     ch = eng.open_channel(600)
-    with pytest.raises(ae.AeroError) as ex:
-        eng.push(ch, np.zeros(1000, np.int16), fs=11025)
-    assert ex.value.rc == ae.AERO_E_RATE
+    for fs in (11025, 96001):  # outside [MSK_FS_MIN, MSK_FS_MAX]
+        with pytest.raises(ae.AeroError) as ex:
+            eng.push(ch, np.zeros(1000, np.int16), fs=fs)
+        assert ex.value.rc == ae.AERO_E_RATE
     eng.push(ch, np.zeros(1000, np.int16), fs=48000)  # a supported rate moves the channel
+    eng.push(ch, np.zeros(1000, np.int16), fs=22050)  # and a generic one
     eng.close()
 
 

@@ -129,7 +129,9 @@ def test_many_channels_multiple_waves(engine_lib):
 def test_documented_channel_config_per_bitrate(engine_lib):
     """INTEGRATION.md's binding: aero_channel_open with the rate each bit
     rate's audio arrives at (decode/decode.cpp:145, 152-159) for every
-    aero-decode bit rate, and AERO_E_INVALID for a mismatched rate."""
+    aero-decode bit rate; AERO_E_INVALID for 10500 bps at another rate,
+    AERO_E_RATE for MSK at a rate outside [12000, 96000] Hz, and any MSK rate
+    inside it (a generic-rate group)."""
     import ctypes
     import aero_engine as ae
     eng = ae.Engine(max_channels=4)
@@ -140,7 +142,10 @@ def test_documented_channel_config_per_bitrate(engine_lib):
         ch = ctypes.c_int()
         assert lib.aero_channel_open(eng.h, ctypes.byref(cfg), ctypes.byref(ch)) == ae.AERO_OK, bitrate
         bad = ae.ChannelCfg(bitrate, 0, 11025, 0)
-        assert lib.aero_channel_open(eng.h, ctypes.byref(bad), ctypes.byref(ch)) == ae.AERO_E_INVALID, bitrate
+        want = ae.AERO_E_INVALID if bitrate == 10500 else ae.AERO_E_RATE
+        assert lib.aero_channel_open(eng.h, ctypes.byref(bad), ctypes.byref(ch)) == want, bitrate
+    cfg = ae.ChannelCfg(600, 0, 16000, 0)
+    assert lib.aero_channel_open(eng.h, ctypes.byref(cfg), ctypes.byref(ch)) == ae.AERO_OK
     eng.close()
 
 
