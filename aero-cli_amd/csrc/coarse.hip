@@ -194,8 +194,8 @@ __device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<in
 
 // AERO_X_STAMPS (diagnostic build only): s_memtime cycle totals per section
 // of wave 0 of every workgroup that ran a hop (prologue, ring to LDS +
-// twiddles, table gathers + mix, FFT 1, boxcar+iFFT+square, FFT 3, y history
-// loads + |X| + log10, y update + store, fold search; slots 0-8), and the number of such
+// twiddles, table gathers + mix, FFT 1, boxcar+iFFT+square, FFT 3, |X|,
+// log10 smoothing, fold search; slots 0-8), and the number of such
 // workgroups (slot 11)
 constexpr int CSTAMP_N = 12;
 #ifdef AERO_X_STAMPS
@@ -317,76 +317,59 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   chain::fft<L, false, false>(x, t, lds, T.tw, s_tw);
   CSTAMP(5);
   // fftshift + smoothing y = 0.9 y + 10 log10(max(|X|,1)) over the bins the
-  // fold reads.  The y history (HBM, YLEN doubles) is copied into LDS by
-  // direct-to-LDS loads issued first, so its round trip overlaps the |X| and
-  // log10 work, which stays in registers (each thread on its own bins of the
-  // transform's output layout).  No barrier before the loads: the third
-  // transform's workgroup exchange ended with one (chain::gx), after which
-  // every wave only works in registers, so the LDS is free.
+  // fold reads: |X| per bin to LDS first (keeps the log10 out of the
+  // register-heavy FFT scope), then a dense log10 loop; the y history (HBM)
+  // is read three iterations ahead of its update, the first loads
+  // overlapping the |X| work.  (Round 5 measured the alternatives on one box:
+  // the whole history brought into LDS by direct-to-LDS loads as the third
+  // transform ends, |X| and log10 in registers meanwhile, 21.49 ms; plain
+  // register loads of the whole history, 21.58 ms; this, 20.97 ms.  The
+  // history's 86 KB take ~46k cycles from issue to arrival whichever way,
+  // more than the |X| and log10 work that can overlap them.)
   double *yg = S.y + (size_t)c * YLEN;
   const int yreset = S.is[IS_YRESET * C + c];
-  double *ylds = lds;  // bin k - YLO at ypad(k - YLO): one pad double per DMA block
-  // direct-to-LDS loads of AERO_COARSE_YDMA bytes per lane (4, or 16:
-  // gfx950's b128 form), one block of 16 x AERO_COARSE_YDMA doubles per wave
-  // instruction, blocks dealt to waves
-#ifndef AERO_COARSE_YDMA
-#define AERO_COARSE_YDMA 4
-#endif
-  constexpr int DMA = AERO_COARSE_YDMA, DPB = 8 * DMA, PS = DMA == 4 ? 5 : 7;  // doubles per block, log2
-  auto ypad = [](int q) { return fftl::ypadn<PS>(q); };
-  if (!yreset) {
-    constexpr int NB = (YLEN + DPB - 1) / DPB;
-    static_assert(NB * (DPB + 1) <= PADDED, "the y history fits the transform's LDS");
-    const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
-    for (int b = wv; b < NB; b += FT / 64) {
-      const int k = b * DPB + ln * DMA / 8;
-      const char *src = reinterpret_cast<const char *>(yg + (k < YLEN ? k : 0)) + (DMA == 4 ? 4 * (ln & 1) : 0);
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)(ylds + b * (DPB + 1)), DMA, 0,
-                                       0);
-    }
-  }
-  // a thread's outputs in the kept bins: all lanes', none or some (fixed by the layout)
-  constexpr fftl::YClass YC = fftl::yclass<L>(K::YLO, K::YHI);
-  auto yin = [&](int i) {
-    const int yi = (bin_t | chain::out_bin_reg<L>(i)) ^ (N / 2);
-    return YC.v[i] == 1 || (YC.v[i] == 2 && yi >= K::YLO && yi <= K::YHI);
-  };
-  auto yq = [&](int i) { return ((bin_t | chain::out_bin_reg<L>(i)) ^ (N / 2)) - K::YLO; };
-  // log10(max(|X|, 1)) in registers; |X| by aero_hypot_nr when every value
-  // of the wave is in its range (the usual case: |X| of a live channel is
-  // ~1e9), else by aero_hypot
-  double hx[16];
+  auto yload = [&](int k) { return (k < YLEN && !yreset) ? yg[k] : 20.0; };
+  double yp0 = yload(t), yp1 = yload(t + FT);
+  // no barrier here: the third transform's workgroup exchange ended with
+  // one (chain::gx), after which every wave only works in registers, so the
+  // LDS is free for |X| as soon as this wave gets here
+  double *ylds = lds;  // bin k - YLO at ypad(k - YLO)
+  auto ypad = [](int q) { return fftl::ypadn<6>(q); };
+  // |X| by aero_hypot_nr when every value of the wave is in its range (the
+  // usual case: |X| of a live channel is ~1e9), else by aero_hypot
   bool nr = true;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    if (YC.v[i] == 0) continue;
     const double a = fabs(x[i].x), b = fabs(x[i].y);
     nr = nr && a <= 0x1p200 && b <= 0x1p200 && (a >= 0x1p-200 || b >= 0x1p-200);
   }
   if (__all(nr)) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (YC.v[i] != 0 && yin(i)) hx[i] = CO_LOG10(fmax(CO_HYPOT_NR(x[i].x, x[i].y), 1.0));
+    for (int i = 0; i < 16; ++i) {
+      const int yi = (bin_t | chain::out_bin_reg<L>(i)) ^ (N / 2);
+      if (yi >= K::YLO && yi <= K::YHI) ylds[ypad(yi - K::YLO)] = CO_HYPOT_NR(x[i].x, x[i].y);
+    }
   } else {
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (YC.v[i] != 0 && yin(i)) hx[i] = CO_LOG10(fmax(CO_HYPOT(x[i].x, x[i].y), 1.0));
-  }
-  CSTAMP(6);
-  __builtin_amdgcn_s_waitcnt(0);  // this wave's y loads have landed in LDS
-  __syncthreads();                // and every other wave's
-  CSTAMP(9);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    if (YC.v[i] != 0 && yin(i)) {
-      const int q = yq(i);
-      const double yold = yreset ? 20.0 : ylds[ypad(q)];
-      const double ynew = yold * 0.9 + 0.1 * 10 * hx[i];
-      ylds[ypad(q)] = ynew;
+    for (int i = 0; i < 16; ++i) {
+      const int yi = (bin_t | chain::out_bin_reg<L>(i)) ^ (N / 2);
+      if (yi >= K::YLO && yi <= K::YHI) ylds[ypad(yi - K::YLO)] = CO_HYPOT(x[i].x, x[i].y);
     }
   }
+  double yp2 = yload(t + 2 * FT);
   __syncthreads();
-  for (int k = t; k < YLEN; k += FT) yg[k] = ylds[ypad(k)];
+  CSTAMP(6);
+#pragma unroll 1
+  for (int k = t; k < YLEN; k += FT) {
+    const double yold = yp0;
+    yp0 = yp1;
+    yp1 = yp2;
+    yp2 = yload(k + 3 * FT);
+    const double ynew = yold * 0.9 + 0.1 * 10 * CO_LOG10(fmax(ylds[ypad(k)], 1.0));
+    yg[k] = ynew;
+    ylds[ypad(k)] = ynew;
+  }
+  __syncthreads();
   CSTAMP(7);
   // fold search (coarsefreqestimate.cpp:166-185): first strict maximum above 0
   double bv = 0.0;
@@ -419,7 +402,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   CSTAMP(8);
 #ifdef AERO_X_STAMPS
   if (t == 0) {
-    for (int k = 0; k < 10; ++k) atomicAdd(&g_cstamps[k], cst_[k]);
+    for (int k = 0; k < 9; ++k) atomicAdd(&g_cstamps[k], cst_[k]);
     atomicAdd(&g_cstamps[CSTAMP_N - 1], 1ull);
   }
 #endif

@@ -182,7 +182,10 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
   // otherwise wait for); none is a slot the sample before writes, and
   // delayt8's "newer" slot is the next sample's "older".  (At 24 / 48 kHz the
   // five extra live values spill: there they are loaded at the sample's top.)
-  constexpr bool AHEAD = QREG;
+#ifndef AERO_MSK_AHEAD_ALL
+#define AERO_MSK_AHEAD_ALL 0
+#endif
+  constexpr bool AHEAD = QREG || AERO_MSK_AHEAD_ALL;
   double agc_nx = S.agc[(size_t)(n0 % AGC) * C + c];
   double2 dsm_nx = S.dsm[(size_t)((n0 + 1) % DSM) * C + c];
   double d8o_nx = S.d8[(size_t)((n0 + 1) % D8) * C + c];

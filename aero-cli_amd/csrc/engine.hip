@@ -1062,11 +1062,10 @@ int group_create(aero_engine *E, int mode, int gid, int fs, std::unique_ptr<Grou
   }
   HIPCHK(hipEventCreateWithFlags(&e->pin_pcm_ev, hipEventDisableTiming));
   if (hipHostMalloc(&e->pin_stat, 128) != hipSuccess) return AERO_E_NOMEM;
-  {
-    int lo = 0, hi = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIPCHK(hipStreamCreateWithPriority(&e->st_in, hipStreamNonBlocking, hi));
-  }
+  // (st_in is created by the first batch push that needs it: HIP deals its
+  // streams round-robin over GPU_MAX_HW_QUEUES hardware queues, 4 by default,
+  // and a stream this group never uses would put two groups' kernel streams
+  // on one queue, where they run one after the other)
   HIPCHK(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
   const int nfft = e->g.nfft;
   std::vector<double> cis(2 * WTSIZE), tw(2 * nfft), twi(2 * nfft), taps(MAX_TAPS, 0.0);
@@ -1292,6 +1291,11 @@ int push_common(Group *e, const int16_t *src, size_t n, size_t ld, int nch, int 
     const long long start = e->avail[c0];
     for (int j = 1; j < nch; j++)
       if (e->avail[c0 + j] != start) return AERO_E_INVALID;  // batch pushes are lockstep
+    if (!e->st_in) {
+      int lo = 0, hi = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIPCHK(hipStreamCreateWithPriority(&e->st_in, hipStreamNonBlocking, hi));
+    }
     // rows of samples [start, start + n) overwrite those of samples below
     // start + n - PCM_CAP: wait for the demod launch that consumed them
     const long long need = start + (long long)n - PCM_CAP;

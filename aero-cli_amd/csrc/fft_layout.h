@@ -158,37 +158,9 @@ AERO_HD constexpr int wl_w(int lane, int i) { return (lane >> 4) * 272 + (lane &
 AERO_HD constexpr int wl_r(int lane, int i) { return (lane >> 4) * 272 + i * 17 + (lane & 15); }
 // the |X| bins after the last transform: lanes hold bin bits 4..9 (G
 // layout), one pad per 64 keeps the 16-lane store groups on distinct banks
-// the coarse y history in LDS: one pad double per 2^S (a direct-to-LDS load
-// fills 2^S doubles contiguously: S = 5 for 4-byte lanes, 7 for 16-byte
-// lanes); with S = 5 the output layout's lanes, bins 8 or 16 apart, fall two
-// to a bank pair
+// the coarse kernel's |X| / y history in LDS: one pad double per 2^S
 template <int S>
 AERO_HD constexpr int ypadn(int q) { return q + (q >> S); }
-
-// which of a thread's 16 transform outputs (layout G) hold bins whose
-// fftshifted index lies in [lo, hi]: on every lane (1), on none (0), on some
-// (2).  A register's bins are the p with (p & ~thread bits) == its bits.
-struct YClass {
-  int v[16];
-};
-template <int L>
-constexpr YClass yclass(int lo, int hi) {
-  YClass r{};
-  const int n = 1 << L, tm = thread_mask(lay_g<L>(), L);
-  for (int i = 0; i < 16; ++i) {
-    const int reg = areg(lay_g<L>(), L, i);
-    bool any = false, all = true;
-    for (int p = 0; p < n; ++p)
-      if ((p & ~tm) == reg) {
-        const int yi = p ^ (n / 2);
-        const bool in = yi >= lo && yi <= hi;
-        any = any || in;
-        all = all && in;
-      }
-    r.v[i] = all ? 1 : (any ? 2 : 0);
-  }
-  return r;
-}
 
 // static checks of the closed forms for the two transform sizes in use
 template <int L, int KIND, bool FIRST>

@@ -30,8 +30,8 @@ vfn = lib.aero_x_viterbi_stamps
 vfn.argtypes = [ctypes.c_void_p]
 vout = (ctypes.c_ulonglong * 4)()
 names = ['prologue', 'ring to LDS + twiddles', 'table gathers + mix', 'FFT 1', 'boxcar+iFFT+square', 'FFT 3',
-         'y DMA issue + log10 |X|', 'y update + store', 'fold search', 'y DMA wait']
-order = [0, 1, 2, 3, 4, 5, 6, 9, 7, 8]
+         'hypot', 'log10 smoothing', 'fold search']
+order = list(range(9))
 for s in range(steps):
     views = [pool[:, int(o) + s * 4096:int(o) + (s + 1) * 4096] for o in offs]
     x = torch.stack(views).permute(2, 0, 1).reshape(4096, C).contiguous()
@@ -44,7 +44,7 @@ for s in range(steps):
         vfn(vout)
 fn(out)
 vfn(vout)
-tot = sum(out[:10])
+tot = sum(out[:9])
 n = out[11]
 print('channels %d, hops %d, s_memtime cycles per hop (wave 0) %.0f' % (C, n, tot / max(n, 1)))
 for k in order:

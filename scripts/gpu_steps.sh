@@ -8,6 +8,9 @@
 #   bench[=ARGS]       bench.py (default: the headline line), ARGS comma-separated
 #   mode=M             bench.py --mode M with its CPU baseline (one run)
 #   ab=VARIANT:M       bench.py --mode M on libaero_engine_VARIANT.so, no CPU baseline
+#   env=VAR=VALUE      export VAR=VALUE for the steps after it
+#   pmcdrop            demod HBM traffic per buffer (scripts/pmc_demod_buffers.sh)
+#   trace=M            rocprofv3 kernel trace of bench.py --mode M (kernel_trace_M.csv)
 #   stamps[=VARIANT]   per-section cycle totals (libaero_engine_stamps.so or _VARIANT.so)
 # Usage: bash scripts/gpu_steps.sh TAG STEP...
 set -o pipefail
@@ -36,11 +39,16 @@ for st in "$@"; do
     mode=*) m=${st#mode=}; step 400 bench_$m.log python bench.py --mode $m --cpu-runs 1 ;;
     ab=*) v=${st#ab=}; m=${v#*:}; v=${v%%:*}
       so=$R/aero-cli_amd/libaero_engine${v:+_$v}.so; [ "$v" = prod ] && so=$R/aero-cli_amd/libaero_engine.so
-      AERO_ENGINE_SO=$so step 300 bench_${m}_$v.log python bench.py --mode $m --no-cpu-baseline ;;
+      AERO_ENGINE_SO=$so step 300 bench_${m}_$v${GPU_MAX_HW_QUEUES:+_q$GPU_MAX_HW_QUEUES}.log python bench.py --mode $m --no-cpu-baseline ;;
     stamps) AERO_ENGINE_SO=$R/aero-cli_amd/libaero_engine_stamps.so step 300 coarse_stamps.log python -u scripts/coarse_stamps.py
       AERO_ENGINE_SO=$R/aero-cli_amd/libaero_engine_stamps.so step 300 demod_stamps.log python -u scripts/demod_stamps.py ;;
     stamps=*) v=${st#stamps=}
       AERO_ENGINE_SO=$R/aero-cli_amd/libaero_engine_$v.so step 300 coarse_stamps_$v.log python -u scripts/coarse_stamps.py ;;
+    trace=*) m=${st#trace=}${GPU_MAX_HW_QUEUES:+_q$GPU_MAX_HW_QUEUES}
+      cd /tmp; TMPDIR=/tmp step 400 trace_$m.log rocprofv3 --kernel-trace --output-format csv -d /tmp/tr_${TAG}_$m -o tr -- python3 $R/bench.py --mode ${st#trace=} --no-cpu-baseline; cd $R
+      find /tmp/tr_${TAG}_$m -name '*kernel_trace.csv' -exec cp {} $OUT/kernel_trace_$m.csv \; ;;
+    pmcdrop) step 900 pmcdrop.log bash scripts/pmc_demod_buffers.sh $TAG ;;
+    env=*) export "${st#env=}"; echo "[step] export ${st#env=}" ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done

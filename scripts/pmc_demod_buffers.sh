@@ -16,7 +16,9 @@ for v in base drop1 drop2 drop4 drop8; do
   for c in FETCH_SIZE WRITE_SIZE; do
     AERO_ENGINE_SO=$so timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex 'demod_oqpsk' --output-format csv \
       -d /tmp/pmcd_${TAG}_${v}_$c -o pmc -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --h2d-steps 0 \
-      > $OUT/pmcd_${v}_$c.log 2>&1 || exit $?
+      > $OUT/pmcd_${v}_$c.log 2>&1
+    rc=$?  # 1-3: bench checks (a drop build decodes nothing), not a fault
+    [ $rc -ge 4 ] && exit $rc
     find /tmp/pmcd_${TAG}_${v}_$c -name '*counter_collection.csv' -exec cp {} $OUT/pmcd_${v}_$c.csv \;
   done
 done
