@@ -44,7 +44,7 @@ namespace aero {
 void launch_demod(hipStream_t, const DevState &, const DevTables &, int, int, bool);
 void upload_demod_constants(const double *, const DelayDesc *, const double *, const double *, const double *,
                             const double *);
-void launch_demod_msk(hipStream_t, int, const DevState &, const DevTables &, int, int);
+void launch_demod_msk(hipStream_t, int, const DevState &, const DevTables &, int, int, bool);
 void upload_msk_constants(const double *);
 void demod_read_stamps(unsigned long long *);
 void coarse_read_stamps(unsigned long long *);
@@ -164,6 +164,9 @@ struct Group {
   ~Group();  // releases every device/host resource (also on a failed group_create)
   int mode = MODE_OQPSK;  // kernel family: a Mode, MODE_MSKG600 or MODE_MSKG1200
   int gid = 0;            // engine group id
+  // MSK: the few-channel kernel (16 lanes per channel, demod_msk.hip) runs
+  // while nch <= wide_max (AERO_MSK_WIDE, default MSKW_MAX_DEFAULT; 0: never)
+  int wide_max = 0;
   ModeGeom g{};
   int device = 0, flags = 0, C = 0, nch = 0;
   std::string tag;  // timing-name prefix ("" for OQPSK, "msk600_", "msk1200_", "msk600_48k_", "msk600_16000_", ...)
@@ -854,7 +857,7 @@ int run_pass(Group *e, int flush, bool *more) {
     if (e->mode == MODE_OQPSK)
       launch_demod(e->st, e->S, e->T, e->nch, flush, (e->flags & AERO_F_TRACE_PT) != 0);
     else
-      launch_demod_msk(e->st, e->mode, e->S, e->T, e->nch, flush);
+      launch_demod_msk(e->st, e->mode, e->S, e->T, e->nch, flush, e->nch <= e->wide_max);
     ev_end(e, b);
     if (int rc = note_consumed(e)) return rc;
     // framing + Viterbi into the next job slot (at most one job per channel per pass)
@@ -987,12 +990,14 @@ bool msk_gen_consts(int fs, MskGen &m) {
   m = MskGen{};
   m.fs = fs;
   m.sps = fs / 600;
-  // fb < 1200 and Fs != 48000: the "300hz / 4hz / 12000" design, ee 0.0125
-  m.sr_b0 = 5.233248111921052e-04;
-  m.sr_b2 = -5.233248111921052e-04;
-  m.sr_a1 = -1.974342917561558;
-  m.sr_a2 = 0.998953350377616;
-  m.ee = 0.0125;
+  // fb < 1200: the "300hz / 4hz / 48000" design at Fs 48000, else the
+  // "300hz / 4hz / 12000" one (mskdemodulator.cpp:177-203)
+  const bool f48 = fs == 48000;
+  m.sr_b0 = f48 ? 1.308825621597620e-04 : 5.233248111921052e-04;
+  m.sr_b2 = -m.sr_b0;
+  m.sr_a1 = f48 ? -1.998196509168551 : -1.974342917561558;
+  m.sr_a2 = f48 ? 0.999738234875681 : 0.998953350377616;
+  m.ee = f48 ? 0.025 : 0.0125;
   int size;
   if (!host_delay_uniform(m.sps / 2.0, size, m.d8_old, m.d8_new, m.d8w, m.d8omw)) return false;
   if (size != msk_geom(600, fs).d8_len || m.d8_new < 1 || m.d8_old >= size) return false;
@@ -1007,6 +1012,12 @@ bool msk_gen_consts(int fs, MskGen &m) {
   return m.ilo - m.epb - 1 >= MSK_YLO && m.ihi - 1 + m.epb + 1 <= MSK_YHI && m.ilo < m.ihi;
 }
 
+// the few-channel MSK kernel's default limit: up to 4096 channels (256
+// waves of 16-lane groups) the chip has lanes to spare, and a channel's
+// per-sample latency, not lane count, sets the time; above it the one-lane
+// kernels' throughput wins (C3 at 65536 channels)
+constexpr int MSKW_MAX_DEFAULT = 4096;
+
 // gid: the group's engine id; fs: the sample rate of a generic-rate group
 // (mode MODE_MSKG600 / MODE_MSKG1200), 0 for a fixed kind
 int group_create(aero_engine *E, int mode, int gid, int fs, std::unique_ptr<Group> &out) {
@@ -1017,8 +1028,14 @@ int group_create(aero_engine *E, int mode, int gid, int fs, std::unique_ptr<Grou
   e->flags = E->flags;
   e->hpool = E->hpool.get();
   MskGen mg{};
+  if (mode != MODE_OQPSK) {
+    // every MSK group carries its rate's constants (the generic-rate and the
+    // few-channel kernels read them)
+    if (!msk_gen_consts(msk_generic(mode) ? fs : msk_fs(mode), mg)) return AERO_E_RATE;
+    const char *w = getenv("AERO_MSK_WIDE");
+    e->wide_max = w ? atoi(w) : MSKW_MAX_DEFAULT;
+  }
   if (msk_generic(mode)) {
-    if (!msk_gen_consts(fs, mg)) return AERO_E_RATE;
     e->g = msk_geom(msk_bitrate(mode), fs);
     e->tag = "msk" + std::to_string(msk_bitrate(mode)) + "_" + std::to_string(fs) + "_";
   } else {

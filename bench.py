@@ -24,9 +24,12 @@ import numpy as np
 
 # The engine runs one HIP stream per channel kind (and the channeliser one
 # more); HIP deals streams round-robin over GPU_MAX_HW_QUEUES hardware
-# queues, 4 unless set, so the C5 receiver's kinds shared a queue and ran one
-# after the other.  Set before anything initialises HIP.
-os.environ.setdefault('GPU_MAX_HW_QUEUES', '8')
+# queues (4 by default, and the GPU boxes set 4), so the C5 receiver's kinds
+# shared a queue and ran one after the other.  At least 8,
+# set before anything initialises HIP.
+if int(os.environ.get('GPU_MAX_HW_QUEUES', '4')) < 8:
+    os.environ['GPU_MAX_HW_QUEUES'] = '8'
+
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for p in (os.path.join(ROOT, 'aero-cli_amd'), os.path.join(ROOT, 'tests')):

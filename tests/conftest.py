@@ -25,3 +25,16 @@ def engine_lib():
     aero_testlib.build_all()
     import aero_engine
     return aero_engine.load_library()
+
+
+@pytest.fixture(params=['few', 'one'])
+def msk_kernel(request, monkeypatch):
+    """Both continuous-MSK kernel shapes (demod_msk.hip): the few-channel one
+    (16 lanes per channel, the default up to 4096 channels) and the
+    one-lane-per-channel kernels (AERO_MSK_WIDE=0, what C3's 65536 channels
+    run); the engine reads the variable when it creates a group."""
+    if request.param == 'one':
+        monkeypatch.setenv('AERO_MSK_WIDE', '0')
+    else:
+        monkeypatch.delenv('AERO_MSK_WIDE', raising=False)
+    return request.param

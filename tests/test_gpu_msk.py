@@ -36,7 +36,7 @@ def _run(eng, chans, streams, chunks):
 
 
 @pytest.mark.gpu
-def test_msk_engine_matches_oracle(engine_lib):
+def test_msk_engine_matches_oracle(engine_lib, msk_kernel):
     import aero_engine as ae
     streams = _streams(CASES)
     chunks = [c[6] for c in CASES]
@@ -99,7 +99,7 @@ def test_mixed_kinds_one_engine(engine_lib):
 
 
 @pytest.mark.gpu
-def test_msk_many_channels(engine_lib):
+def test_msk_many_channels(engine_lib, msk_kernel):
     """300 MSK-600 channels (two 256-lane workgroups, out of step: carriers,
     phases, noise, push sizes) against the oracle, channel by channel."""
     import aero_engine as ae

@@ -35,7 +35,7 @@ def _messages(bitrate, segs, msg_s):
     return out
 
 
-def test_msk_rate_change_matches_oracle(engine_lib):
+def test_msk_rate_change_matches_oracle(engine_lib, msk_kernel):
     import aero_engine as ae
     msgs = [_messages(br, segs, m) for br, segs, m in CHANNELS]
     eng = ae.Engine(max_channels=8, flags=ae.F_TRACE_SOFT | ae.F_TRACE_HOPS | ae.F_TRACE_FRAMES)
@@ -114,7 +114,7 @@ def _run_vs_oracle(eng, chans, spec, msgs):
     return items_total
 
 
-def test_msk_generic_rates_match_oracle(engine_lib):
+def test_msk_generic_rates_match_oracle(engine_lib, msk_kernel):
     """Channels at and through rates with no fixed-rate group, beside each
     other, against the oracle's setSettings at those rates."""
     import aero_engine as ae
