@@ -272,11 +272,6 @@ def build_blibm(jobs=4):
     return [build_engine(jobs, variant=v, defines=d) for v, d in BLIBM_VARIANTS.items()]
 
 
-# the MSK demod loading its ring slots one sample ahead at every rate
-def build_mskahead(jobs=4):
-    return [build_engine(jobs, variant='mskahead', defines=['AERO_MSK_AHEAD_ALL=1'])]
-
-
 # per-section s_memtime totals of the coarse kernel, the demod chain and the
 # Viterbi (scripts/coarse_stamps.py, scripts/demod_stamps.py)
 def build_stamps(jobs=4):
@@ -294,7 +289,7 @@ if __name__ == '__main__':
     ap.add_argument('-j', type=int, default=4)
     a = ap.parse_args()
     for v in filter(None, a.variants.split(',')):
-        print({'drop': build_drop, 'blibm': build_blibm, 'stamps': build_stamps, 'mskahead': build_mskahead}[v](a.j))
+        print({'drop': build_drop, 'blibm': build_blibm, 'stamps': build_stamps}[v](a.j))
     if a.asan:
         print(build_asan(a.j))
         sys.exit(0)

@@ -11,11 +11,12 @@
 #include "burst_common.h"
 #include "engine_common.h"
 
-// The per-sample libm of the burst demods: hypot with the wave-uniform
-// branch-free fast path, atan2's branch-free main path over the global cij
-// table.  AERO_X_BURST_LIBM (timing builds only, bit-identical results)
-// selects the general forms: 1 plain hypot, 2 general atan2, 3 both.
-#if !defined(AERO_X_BURST_LIBM) || AERO_X_BURST_LIBM == 0 || AERO_X_BURST_LIBM == 2
+// The per-sample libm of the burst demods: glibc's hypot as it is (the
+// wave-uniform branch-free form measured 1.5% slower here), atan2's
+// branch-free main path over the global cij table.  AERO_X_BURST_LIBM
+// (timing builds only, bit-identical results): 1 the wave-uniform hypot,
+// 2 general atan2, 3 both.
+#if defined(AERO_X_BURST_LIBM) && (AERO_X_BURST_LIBM == 1 || AERO_X_BURST_LIBM == 3)
 #define B_HYPOT aero_hypot_w
 #else
 #define B_HYPOT aero_hypot
