@@ -719,6 +719,13 @@ __global__ __launch_bounds__(MSKW_WG) void demod_mskw_kernel(DevState S, DevTabl
   const int SPS = G.sps, NT = 2 * SPS, AGC = S.g.agc_len, DSM = S.g.dsm_len, D8 = S.g.d8_len, DTL = S.g.dt_len,
             MARG = S.g.marg_len;
   const double FS = G.fs;
+  // atan2's and sincos's glibc tables in LDS: their row gathers sit on the
+  // chain every sample / every event
+  __shared__ double s_cij[241][7];
+  __shared__ double s_sct[440];
+  for (int q = threadIdx.x; q < 241 * 7; q += MSKW_WG) (&s_cij[0][0])[q] = (&aero_g_cij[0][0])[q];
+  for (int q = threadIdx.x; q < 440; q += MSKW_WG) s_sct[q] = aero_g_sincostab[q];
+  __syncthreads();
   const int lane = threadIdx.x, k = lane & (MSKW_G - 1), top = (lane & ~(MSKW_G - 1)) + MSKW_G - 1;
   const int c = blockIdx.x * (MSKW_WG / MSKW_G) + lane / MSKW_G;
   if (c >= nch) return;  // the whole 16-lane group
@@ -772,13 +779,28 @@ __global__ __launch_bounds__(MSKW_WG) void demod_mskw_kernel(DevState S, DevTabl
   }
 
   const double PT = G.ee * WTSIZE;  // IfHavePassedPoint(ee) (mskdemodulator.cpp:177-203)
+  // a sample's PCM word and ring slots are loaded one sample ahead (their
+  // HBM / L2 round trips would otherwise open every sample): none is a slot
+  // the sample before writes (AGC >= 2, DSM > 2, delayt8 ages >= 2, host-checked)
+  auto ld_pcm = [&](long long m) { return S.pcm[(size_t)(m & capm) * C + c]; };
+  auto ld_agc = [&](long long m) { return S.agc[(size_t)(m % AGC) * C + c]; };
+  auto ld_dsm = [&](long long m) { return S.dsm[(size_t)((m + 1) % DSM) * C + c]; };
+  auto ld_d8 = [&](long long m, int age) { return S.d8[(size_t)((m - age + D8) % D8) * C + c]; };
+  int16_t xs_nx = ld_pcm(n0);
+  double agc_nx = ld_agc(n0), d8o_nx = ld_d8(n0, G.d8_old), d8n_nx = ld_d8(n0, G.d8_new);
+  double2 dsm_nx = ld_dsm(n0);
   for (int i = 0; i < ie; ++i) {
     const long long n = n0 + i;
-    const int16_t xs = S.pcm[(size_t)(n & capm) * C + c];
-    const double agc_old = S.agc[(size_t)(n % AGC) * C + c];
-    const double2 dsm_old = S.dsm[(size_t)((n + 1) % DSM) * C + c];
-    const double d8_older = S.d8[(size_t)((n - G.d8_old + D8) % D8) * C + c];
-    const double d8_newer = S.d8[(size_t)((n - G.d8_new + D8) % D8) * C + c];
+    const int16_t xs = xs_nx;
+    const double agc_old = agc_nx;
+    const double2 dsm_old = dsm_nx;
+    const double d8_older = d8o_nx;
+    const double d8_newer = d8n_nx;
+    xs_nx = ld_pcm(n + 1);  // past the pushed samples: unused
+    agc_nx = ld_agc(n + 1);
+    dsm_nx = ld_dsm(n + 1);
+    d8o_nx = ld_d8(n + 1, G.d8_old);
+    d8n_nx = ld_d8(n + 1, G.d8_new);
     const double dval = ((double)xs) / 32768.0;
     const double2 cm = T.cis[cis_index(m2_ptr)];
     const double cv = cm.x * dval, cvi = cm.y * dval;  // mixer2.WTCISValue() * dval
@@ -846,7 +868,7 @@ __global__ __launch_bounds__(MSKW_WG) void demod_mskw_kernel(DevState S, DevTabl
     const double m1r = st_eta, m1i = -d8v;
     const double2 so = T.cis[cis_index(so_ptr)];
     const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
-    const double ang = aero_atan2_bf(oim, ore, aero_g_cij);
+    const double ang = aero_atan2_bf(oim, ore, s_cij);
     const double weighting = fabs(aero_tanh(ang));
     {  // st_osc.AdvanceFractionOfWave (DSP.h:59-65), dcd false
       so_ptr += (-(1.0 - weighting) * ang * (0.05 / 360.0)) * WTSIZE;
@@ -919,7 +941,7 @@ __global__ __launch_bounds__(MSKW_WG) void demod_mskw_kernel(DevState S, DevTabl
       }
       {  // pt_msk *= cpx(cos(marg->Val), sin(marg->Val))
         double rs, rc;
-        aero_sincos(mval, rs, rc);
+        aero_sincos_t(mval, rs, rc, s_sct);
         const double rr = pr * rc - pi * rs, ri = pr * rs + pi * rc;
         pr = rr;
         pi = ri;

@@ -828,7 +828,361 @@ __global__ __launch_bounds__(DEMOD_THREADS) void demod_oqpsk_kernel(DevState S, 
     demod_chain_wave<TRACE>(S, T, sh, c, pair, wv, valid, flush);
 }
 
-void launch_demod(hipStream_t st, const DevState &S, const DevTables &T, int nch, int flush, bool trace) {
+// The few-channel kernel (a receiver's handful of VFOs, C1 / C5): one channel
+// per 16 lanes, no helper wave.  Lane k of a channel's group holds four of
+// the RRC's transposed partial sums (right-aligned: lane 15 holds R_51..R_54,
+// so R_54, the filter output, is its last slot); per sample the one partial
+// sum that crosses a lane boundary moves by a shuffle before the update, and
+// the output R_54(n-1) is broadcast from lane 15 first.  All 16 lanes run the
+// chain on identical values (their identical stores coalesce).  The
+// arithmetic is demod_chain_wave's and demod_fir_wave's operation for
+// operation, and the state layout is theirs, so a group may switch kernels
+// from one launch to the next.
+constexpr int DMW_G = 16, DMW_WG = 64, DMW_B = 4;  // lanes per channel, workgroup, taps per lane
+static_assert(DMW_G * DMW_B >= NTAPS, "every tap has a lane");
+struct DemodWShared {
+  double cij[241][7];
+  double sct[440];
+};
+template <bool TRACE>
+__global__ __launch_bounds__(DMW_WG) void demod_oqpskw_kernel(DevState S, DevTables T, int nch, int flush) {
+  __shared__ DemodWShared sh;
+  for (int q = threadIdx.x; q < 241 * 7; q += DMW_WG) (&sh.cij[0][0])[q] = (&aero_g_cij[0][0])[q];
+  for (int q = threadIdx.x; q < 440; q += DMW_WG) sh.sct[q] = aero_g_sincostab[q];
+  __syncthreads();
+  const int lane = threadIdx.x, k = lane & (DMW_G - 1), top = (lane & ~(DMW_G - 1)) + DMW_G - 1;
+  const int c = blockIdx.x * (DMW_WG / DMW_G) + lane / DMW_G;
+  if (c >= nch) return;  // the whole 16-lane group
+  const int j0 = NTAPS - (DMW_G - k) * DMW_B;  // this lane's first tap (negative: slots without one)
+  const int C = S.C;
+  const long long n0 = S.ls[LS_NSAMP * C + c];
+  const long long avail = S.ls[LS_AVAIL * C + c];
+  const long long filled0 = S.ls[LS_FILLED * C + c];
+  const int hops_done = S.is[IS_HOPS_DONE * C + c];
+  const long long boundary = (long long)HOP * (hops_done + 1) - 1;
+  long long end = avail < boundary ? avail : boundary;
+  if (!flush && avail <= boundary) end = n0;
+  const int capm = (int)S.pcm_cap - 1;
+  const int ia = (int)(avail - n0);
+  const int ie = (int)(end - n0);
+  int ifl = (int)(filled0 - n0);
+  double mc_ptr = S.ds[DS_MC_PTR * C + c], mc_step = S.ds[DS_MC_STEP * C + c];
+  if (ifl == 0 && ia > 0) {  // coarse-ring entry of sample n0
+    const int16_t x = S.pcm[(size_t)(n0 & capm) * C + c];
+    S.cring[(size_t)c * NFFT + (n0 & (NFFT - 1))] = (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
+    ifl = 1;
+  }
+  if (ie <= 0) {
+    S.ls[LS_FILLED * C + c] = n0 + ifl;
+    return;
+  }
+  double m2_ptr = S.ds[DS_M2_PTR * C + c], m2_step = S.ds[DS_M2_STEP * C + c];
+  double so_ptr = S.ds[DS_SO_PTR * C + c], so_last = S.ds[DS_SO_LAST * C + c];
+  double so_step = S.ds[DS_SO_STEP * C + c], so_freq = S.ds[DS_SO_FREQ * C + c];
+  double agc_sum = S.ds[DS_AGC_SUM * C + c];
+  double d1[2], d41[4], d42[4], d8[3];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) d1[q] = S.ds[(DS_D1_0 + q) * C + c];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) d41[q] = S.ds[(DS_D41_0 + q) * C + c];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) d42[q] = S.ds[(DS_D42_0 + q) * C + c];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) d8[q] = S.ds[(DS_D8_0 + q) * C + c];
+  double srx1 = S.ds[DS_SR_X1 * C + c], srx2 = S.ds[DS_SR_X2 * C + c];
+  double sry1 = S.ds[DS_SR_Y1 * C + c], sry2 = S.ds[DS_SR_Y2 * C + c];
+  double s2l_re = S.ds[DS_S2L_RE * C + c], s2l_im = S.ds[DS_S2L_IM * C + c];
+  double ctx1 = S.ds[DS_CT_X1 * C + c], ctx2 = S.ds[DS_CT_X2 * C + c];
+  double cty1 = S.ds[DS_CT_Y1 * C + c], cty2 = S.ds[DS_CT_Y2 * C + c];
+  double marg_sum = S.ds[DS_MARG_SUM * C + c], pm_sum = S.ds[DS_PM_SUM * C + c];
+  double ms_sum = S.ds[DS_MS_SUM * C + c], mse = S.ds[DS_MSE * C + c];
+  double ptd_re = S.ds[DS_PTD_RE * C + c], ptd_im = S.ds[DS_PTD_IM * C + c];
+  double m2_freq = S.ds[DS_M2_FREQ * C + c];
+  int agc_ptr = S.is[IS_AGC_PTR * C + c];
+  int yui = S.is[IS_YUI * C + c], s2l_init = S.is[IS_S2L_INIT * C + c];
+  int marg_p = S.is[IS_MARG_P * C + c], dt_p = S.is[IS_DT_P * C + c];
+  int pm_p = S.is[IS_PM_P * C + c], ms_p = S.is[IS_MS_P * C + c];
+  long long softp = S.ls[LS_SOFT_P * C + c];
+  long long ptn = TRACE ? S.ls[LS_PT_N * C + c] : 0;
+  double qre[DMW_B], qim[DMW_B], tp[DMW_B];
+#pragma unroll
+  for (int jj = 0; jj < DMW_B; ++jj) {
+    const int j = j0 + jj;
+    tp[jj] = j >= 0 ? c_taps[j] : 0.0;
+    qre[jj] = j >= 0 ? S.fir[(size_t)j * C + c] : 0.0;
+    qim[jj] = j >= 0 ? S.fir[(size_t)(NTAPS + j) * C + c] : 0.0;
+  }
+  double *marg = S.marg + (size_t)c * MARG_LEN;
+  double2 *dtb = S.dt + (size_t)c * DT_LEN;
+  double2 *pmsb = reinterpret_cast<double2 *>(S.pm) + (size_t)c * MSE_LEN;
+  uint8_t *soft = S.soft + (size_t)c * SOFT_RING;
+  const double PT = 0.4 * WTSIZE;  // IfHavePassedPoint(ee) with ee = 0.4 (oqpskdemodulator.cpp:225)
+  // a sample's PCM word and AGC slot, and its two table entries, loaded one
+  // sample ahead (mixer2's speculatively: a carrier event reloads it)
+  int16_t xs_nx = S.pcm[(size_t)(n0 & capm) * C + c];
+  double agc_nx = S.agc[(size_t)agc_ptr * C + c];
+  double2 cm_nx = T.cis[cis_index(m2_ptr)], so_nx = T.cis[cis_index(so_ptr)];
+  int i = 0;
+  for (; i < ie; ++i) {
+    const long long n = n0 + i;
+    const int16_t xs = xs_nx;
+    const double agc_old = agc_nx;
+    const double2 cm = cm_nx, so = so_nx;
+    xs_nx = S.pcm[(size_t)((n + 1) & capm) * C + c];  // past the pushed samples: unused
+    {
+      const int ap = agc_ptr + 1 == AGC_LEN ? 0 : agc_ptr + 1;
+      agc_nx = S.agc[(size_t)ap * C + c];
+      double p = m2_ptr, st = m2_step;
+      nco_next(p, st);
+      cm_nx = T.cis[cis_index(p)];
+    }
+    const double dval = ((double)xs) / 32768.0;
+    const double cv = cm.x * dval, cvi = cm.y * dval;  // mix (oqpskdemodulator.cpp:390)
+    // RRC: output R_54(n-1) (lane 15's last slot), the boundary partial sums
+    // of the lanes below, both before the update
+    double s2r = __shfl(qre[DMW_B - 1], top, 64), s2i = __shfl(qim[DMW_B - 1], top, 64);
+    const double bre = __shfl_up(qre[DMW_B - 1], 1, DMW_G), bim = __shfl_up(qim[DMW_B - 1], 1, DMW_G);
+#pragma unroll
+    for (int jj = DMW_B - 1; jj >= 1; --jj) {
+      const int j = j0 + jj;
+      if (j > 0) {
+        qre[jj] = qre[jj - 1] + tp[jj] * cv;
+        qim[jj] = qim[jj - 1] + tp[jj] * cvi;
+      } else if (j == 0) {
+        qre[jj] = 0.0 + tp[jj] * cv;
+        qim[jj] = 0.0 + tp[jj] * cvi;
+      }
+    }
+    if (j0 > 0) {
+      qre[0] = bre + tp[0] * cv;
+      qim[0] = bim + tp[0] * cvi;
+    } else if (j0 == 0) {
+      qre[0] = 0.0 + tp[0] * cv;
+      qim[0] = 0.0 + tp[0] * cvi;
+    }
+    // AGC (DSP.cpp:371-380) on |sig2| (oqpskdemodulator.cpp:399-405)
+    const double dab = sqrt(s2r * s2r + s2i * s2i);
+    {
+      agc_sum = agc_sum - agc_old;
+      agc_sum = agc_sum + fabs(dab);
+      S.agc[(size_t)agc_ptr * C + c] = fabs(dab);
+      agc_ptr++;
+      if (agc_ptr == AGC_LEN) agc_ptr = 0;
+      double g = div_n(1.414213562, fmax(div_c(agc_sum, ((double)AGC_LEN)), 0.000001));
+      g = fmax(g, 0.000001);
+      s2r *= g;
+      s2i *= g;
+    }
+    const double ab = aero_hypot_w(s2r, s2i);  // clipping (:408-410)
+    if (ab > 2.84) {
+      const double kk = div_n(2.84, ab);
+      s2r = kk * s2r;
+      s2i = kk * s2i;
+    }
+    // symbol timer (:413-426)
+    const double st_diff = delay_tap<2, 1, 0>(d1, c_dly[0], ab * ab) - (ab * ab);
+    const double st_d1out = delay_tap<4, 3, 2>(d41, c_dly[1], st_diff);
+    const double st_d2out = delay_tap<4, 3, 2>(d42, c_dly[2], st_d1out);
+    double st_eta = (st_d2out - st_diff) * st_d1out;
+    st_eta = iir3(srx1, srx2, sry1, sry2, c_sr_b, c_sr_a, st_eta);
+    const double m1r = st_eta, m1i = -delay_tap<3, 2, 1>(d8, c_dly[3], st_eta);
+    const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
+    const double st_angle_error = aero_atan2_bf(oim, ore, sh.cij);
+    set_freq_st(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
+    so_ptr += div_c(-st_angle_error * 0.01, 360.0) * WTSIZE;
+    while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
+    while (so_ptr < 0) so_ptr += WTSIZE;
+    if (so_freq < (10500.0 - 0.1)) set_freq_st(so_freq, so_step, (10500.0 - 0.1));
+    if (so_freq > (10500.0 + 0.1)) set_freq_st(so_freq, so_step, (10500.0 + 0.1));
+    if (!s2l_init) {
+      s2l_re = s2r;
+      s2l_im = s2i;
+      s2l_init = 1;
+    }
+    // sample instant (:430) IfHavePassedPoint (DSP.cpp:222-238)
+    bool pend = false;
+    double ev_pr = 0.0, ev_pi = 0.0;
+    {
+      double tl = so_last - PT, tw = so_ptr - PT;
+      if (tl < 0.0) tl += WTSIZE;
+      if (tw < 0.0) tw += WTSIZE;
+      if ((tl > 3.0 * WTSIZE / 4.0) && (tw < 1.0 * WTSIZE / 4.0)) {
+        const double pt_last = div_n(tw, so_step);
+        const double pt_this = 1.0 - pt_last;
+        const double pr = pt_this * s2r + pt_last * s2l_re;
+        const double pi = pt_this * s2i + pt_last * s2l_im;
+        yui++;
+        yui %= 2;
+        if (!yui) {
+          ptd_re = pr;
+          ptd_im = pi;
+        } else {
+          ev_pr = pr;
+          ev_pi = pi;
+          pend = true;
+        }
+      }
+    }
+    s2l_re = s2r;
+    s2l_im = s2i;
+    nco_next(mc_ptr, mc_step);
+    so_last = so_ptr;
+    nco_next(so_ptr, so_step);
+    so_nx = T.cis[cis_index(so_ptr)];
+    if (i + 1 < ia) {  // coarse-ring entry of the next sample (:351-356)
+      const long long n1 = n + 1;
+      S.cring[(size_t)c * NFFT + (n1 & (NFFT - 1))] =
+          (uint32_t)cis_index(mc_ptr) | ((uint32_t)(uint16_t)xs_nx << 16);
+      ifl = i + 2;
+    }
+    if (pend) {  // carrier step (:455-541)
+      const int dt_rp = (dt_p + 1) % DT_LEN;
+      const double marg_old = marg[marg_p];
+      const double2 dv = dtb[dt_rp];
+      const double2 pms_old = pmsb[pm_p];
+      const double pm_old = pms_old.x, ms_old = pms_old.y;
+      const double pr = ev_pr, pi = ev_pi;
+      double qr = pr, qi = ptd_im;  // pt_qpsk
+      const double ct_xt = aero_tanh(pi) * pr;
+      const double ct_xt_d = aero_tanh(ptd_re) * ptd_im;
+      double ct_ec = ct_xt_d - ct_xt;
+      if (ct_ec > M_PI) ct_ec = M_PI;
+      if (ct_ec < -M_PI) ct_ec = -M_PI;
+      ct_ec = iir3(ctx1, ctx2, cty1, cty2, c_ct_b, c_ct_a, ct_ec);
+      if (ct_ec > M_PI_2) ct_ec = M_PI_2;
+      if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
+      {  // mixer2.IncresePhaseDeg / SetPhaseDeg (DSP.cpp:177-187)
+        double phase_deg = 1.0 * ct_ec;
+        phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
+        phase_deg = fmod(phase_deg, 360.0);
+        while (phase_deg < 0) phase_deg += 360.0;
+        m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+      }
+      set_freq(m2_freq, m2_step, 0.01 * ct_ec + m2_freq);  // IncreseFreqHz
+      marg_sum = marg_sum - marg_old;  // marg->UpdateSigned (DSP.cpp:419-427)
+      marg_sum = marg_sum + (ct_ec);
+      marg[marg_p] = ct_ec;
+      marg_p++;
+      marg_p %= MARG_LEN;
+      const double mval = DM_DIVC(marg_sum, ((double)MARG_LEN));
+      dtb[dt_p] = make_double2(qr, qi);  // dt.update (DSP.h:456-461)
+      dt_p = dt_rp;
+      qr = dv.x;
+      qi = dv.y;
+      double rs, rc;
+      aero_sincos_t(mval, rs, rc, sh.sct);
+      const double rr = qr * rc - qi * rs, ri = qr * rs + qi * rc;
+      qr = rr;
+      qi = ri;
+      if (TRACE) {
+        if (ptn < S.pt_cap) S.pt[(size_t)c * S.pt_cap + ptn] = make_double2(qr, qi);
+        ptn++;
+      }
+      {  // MSEcalc::Update (DSP.cpp:449-461)
+        const double av = aero_hypot_w(qr, qi);
+        pm_sum = pm_sum - pm_old;
+        pm_sum = pm_sum + fabs(av);
+        const int pms_slot = pm_p;
+        pm_p++;
+        pm_p %= MSE_LEN;
+        double mu = div_c(pm_sum, ((double)MSE_LEN));
+        if (mu < 0.000001) mu = 0.000001;
+        const double rmu = rcp_div(mu);
+        const double tr = div_r(1.4142135623730951 * qr, mu, rmu), ti = div_r(1.4142135623730951 * qi, mu, rmu);
+        const double tda = (fabs(tr) - 1.0), tdb = (fabs(ti) - 1.0);
+        const double v = (tda * tda) + (tdb * tdb);
+        ms_sum = ms_sum - ms_old;
+        ms_sum = ms_sum + fabs(v);
+        pmsb[pms_slot] = make_double2(fabs(av), fabs(v));
+        ms_p++;
+        ms_p %= MSE_LEN;
+        mse = div_c(ms_sum, ((double)MSE_LEN));
+      }
+      if (mse < 0.65) {  // soft bits, imag first (:516-530)
+        int ibit = qround(0.75 * qi * 127.0 + 128.0);
+        if (ibit > 255) ibit = 255;
+        if (ibit < 0) ibit = 0;
+        int rbit = qround(0.75 * qr * 127.0 + 128.0);
+        if (rbit > 255) rbit = 255;
+        if (rbit < 0) rbit = 0;
+        soft[softp & (SOFT_RING - 1)] = (uint8_t)ibit;
+        soft[(softp + 1) & (SOFT_RING - 1)] = (uint8_t)rbit;
+        softp += 2;
+      }
+      nco_next(m2_ptr, m2_step);
+      cm_nx = T.cis[cis_index(m2_ptr)];  // the event moved mixer2
+    } else {
+      nco_next(m2_ptr, m2_step);
+    }
+  }
+#pragma unroll
+  for (int jj = 0; jj < DMW_B; ++jj) {
+    const int j = j0 + jj;
+    if (j >= 0) {
+      S.fir[(size_t)j * C + c] = qre[jj];
+      S.fir[(size_t)(NTAPS + j) * C + c] = qim[jj];
+    }
+  }
+  double *ds = S.ds + c;
+  int *is = S.is + c;
+  long long *ls = S.ls + c;
+  ls[LS_NSAMP * C] = n0 + i;
+  ls[LS_FILLED * C] = n0 + ifl;
+  ls[LS_SOFT_P * C] = softp;
+  if (TRACE) ls[LS_PT_N * C] = ptn;
+  ds[DS_CT_X1 * C] = ctx1;
+  ds[DS_CT_X2 * C] = ctx2;
+  ds[DS_CT_Y1 * C] = cty1;
+  ds[DS_CT_Y2 * C] = cty2;
+  ds[DS_MARG_SUM * C] = marg_sum;
+  ds[DS_PM_SUM * C] = pm_sum;
+  ds[DS_MS_SUM * C] = ms_sum;
+  ds[DS_MSE * C] = mse;
+  ds[DS_PTD_RE * C] = ptd_re;
+  ds[DS_PTD_IM * C] = ptd_im;
+  ds[DS_M2_FREQ * C] = m2_freq;
+  is[IS_MARG_P * C] = marg_p;
+  is[IS_DT_P * C] = dt_p;
+  is[IS_PM_P * C] = pm_p;
+  is[IS_MS_P * C] = ms_p;
+  ds[DS_M2_PTR * C] = m2_ptr;
+  ds[DS_M2_STEP * C] = m2_step;
+  ds[DS_MC_PTR * C] = mc_ptr;
+  ds[DS_MC_STEP * C] = mc_step;
+  ds[DS_SO_PTR * C] = so_ptr;
+  ds[DS_SO_LAST * C] = so_last;
+  ds[DS_SO_STEP * C] = so_step;
+  ds[DS_SO_FREQ * C] = so_freq;
+  ds[DS_AGC_SUM * C] = agc_sum;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) ds[(DS_D1_0 + q) * C] = d1[q];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) ds[(DS_D41_0 + q) * C] = d41[q];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) ds[(DS_D42_0 + q) * C] = d42[q];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) ds[(DS_D8_0 + q) * C] = d8[q];
+  ds[DS_SR_X1 * C] = srx1;
+  ds[DS_SR_X2 * C] = srx2;
+  ds[DS_SR_Y1 * C] = sry1;
+  ds[DS_SR_Y2 * C] = sry2;
+  ds[DS_S2L_RE * C] = s2l_re;
+  ds[DS_S2L_IM * C] = s2l_im;
+  is[IS_AGC_PTR * C] = agc_ptr;
+  is[IS_YUI * C] = yui;
+  is[IS_S2L_INIT * C] = s2l_init;
+}
+
+void launch_demod(hipStream_t st, const DevState &S, const DevTables &T, int nch, int flush, bool trace, bool wide) {
+  if (wide) {
+    constexpr int CPB = DMW_WG / DMW_G;
+    dim3 grid((nch + CPB - 1) / CPB), block(DMW_WG);
+    if (trace)
+      hipLaunchKernelGGL(demod_oqpskw_kernel<true>, grid, block, 0, st, S, T, nch, flush);
+    else
+      hipLaunchKernelGGL(demod_oqpskw_kernel<false>, grid, block, 0, st, S, T, nch, flush);
+    return;
+  }
   dim3 grid((nch + DEMOD_BLOCK - 1) / DEMOD_BLOCK), block(DEMOD_THREADS);
   if (trace)
     hipLaunchKernelGGL(demod_oqpsk_kernel<true>, grid, block, 0, st, S, T, nch, flush);

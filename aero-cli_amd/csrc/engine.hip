@@ -41,7 +41,7 @@
 #include "tables_host.h"
 
 namespace aero {
-void launch_demod(hipStream_t, const DevState &, const DevTables &, int, int, bool);
+void launch_demod(hipStream_t, const DevState &, const DevTables &, int, int, bool, bool);
 void upload_demod_constants(const double *, const DelayDesc *, const double *, const double *, const double *,
                             const double *);
 void launch_demod_msk(hipStream_t, int, const DevState &, const DevTables &, int, int, bool);
@@ -164,8 +164,9 @@ struct Group {
   ~Group();  // releases every device/host resource (also on a failed group_create)
   int mode = MODE_OQPSK;  // kernel family: a Mode, MODE_MSKG600 or MODE_MSKG1200
   int gid = 0;            // engine group id
-  // MSK: the few-channel kernel (16 lanes per channel, demod_msk.hip) runs
-  // while nch <= wide_max (AERO_MSK_WIDE, default MSKW_MAX_DEFAULT; 0: never)
+  // the few-channel demod kernels (16 lanes per channel, demod_oqpsk.hip /
+  // demod_msk.hip) run while nch <= wide_max (AERO_OQPSK_WIDE /
+  // AERO_MSK_WIDE, default WIDE_MAX_DEFAULT; 0: never)
   int wide_max = 0;
   ModeGeom g{};
   int device = 0, flags = 0, C = 0, nch = 0;
@@ -855,7 +856,7 @@ int run_pass(Group *e, int flush, bool *more) {
     if (!progress) return AERO_OK;  // no new soft bits: framing has nothing to do
     ev_begin(e, "demod", a, b);
     if (e->mode == MODE_OQPSK)
-      launch_demod(e->st, e->S, e->T, e->nch, flush, (e->flags & AERO_F_TRACE_PT) != 0);
+      launch_demod(e->st, e->S, e->T, e->nch, flush, (e->flags & AERO_F_TRACE_PT) != 0, e->nch <= e->wide_max);
     else
       launch_demod_msk(e->st, e->mode, e->S, e->T, e->nch, flush, e->nch <= e->wide_max);
     ev_end(e, b);
@@ -1000,7 +1001,8 @@ bool msk_gen_consts(int fs, MskGen &m) {
   m.ee = f48 ? 0.025 : 0.0125;
   int size;
   if (!host_delay_uniform(m.sps / 2.0, size, m.d8_old, m.d8_new, m.d8w, m.d8omw)) return false;
-  if (size != msk_geom(600, fs).d8_len || m.d8_new < 1 || m.d8_old >= size) return false;
+  // (ages >= 2: the few-channel kernel loads a sample's slots one sample ahead)
+  if (size != msk_geom(600, fs).d8_len || m.d8_new < 2 || m.d8_old >= size) return false;
   const double nfft = MSK_NFFT, hzperbin = (double)fs / nfft, lockingbw = 900.0, fb = 600.0;
   const double startbin = std::max(std::round(lockingbw / hzperbin), 1.0);
   m.start = (int)startbin;
@@ -1012,11 +1014,11 @@ bool msk_gen_consts(int fs, MskGen &m) {
   return m.ilo - m.epb - 1 >= MSK_YLO && m.ihi - 1 + m.epb + 1 <= MSK_YHI && m.ilo < m.ihi;
 }
 
-// the few-channel MSK kernel's default limit: up to 4096 channels (256
+// the few-channel demod kernels' default limit: up to 4096 channels (1024
 // waves of 16-lane groups) the chip has lanes to spare, and a channel's
 // per-sample latency, not lane count, sets the time; above it the one-lane
-// kernels' throughput wins (C3 at 65536 channels)
-constexpr int MSKW_MAX_DEFAULT = 4096;
+// kernels' throughput wins (C2 / C3 at 65536 channels)
+constexpr int WIDE_MAX_DEFAULT = 4096;
 
 // gid: the group's engine id; fs: the sample rate of a generic-rate group
 // (mode MODE_MSKG600 / MODE_MSKG1200), 0 for a fixed kind
@@ -1032,8 +1034,10 @@ int group_create(aero_engine *E, int mode, int gid, int fs, std::unique_ptr<Grou
     // every MSK group carries its rate's constants (the generic-rate and the
     // few-channel kernels read them)
     if (!msk_gen_consts(msk_generic(mode) ? fs : msk_fs(mode), mg)) return AERO_E_RATE;
-    const char *w = getenv("AERO_MSK_WIDE");
-    e->wide_max = w ? atoi(w) : MSKW_MAX_DEFAULT;
+  }
+  {
+    const char *w = getenv(mode == MODE_OQPSK ? "AERO_OQPSK_WIDE" : "AERO_MSK_WIDE");
+    e->wide_max = w ? atoi(w) : WIDE_MAX_DEFAULT;
   }
   if (msk_generic(mode)) {
     e->g = msk_geom(msk_bitrate(mode), fs);

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round evidence on one GPU box, in two parts (each within one gpurun call).
+# Round evidence on one GPU box, in three parts (each within one gpurun call).
 #  part a: the headline bench line under the driver's own command, rocprofv3
 #    kernel stats of that command, PMC HBM traffic of the demod and coarse
 #    kernels at the bench config (FETCH_SIZE and WRITE_SIZE in separate

@@ -38,3 +38,16 @@ def msk_kernel(request, monkeypatch):
     else:
         monkeypatch.delenv('AERO_MSK_WIDE', raising=False)
     return request.param
+
+
+@pytest.fixture(params=['few', 'one'])
+def oqpsk_kernel(request, monkeypatch):
+    """Both continuous-OQPSK kernel shapes (demod_oqpsk.hip): the few-channel
+    one (16 lanes per channel, the default up to 4096 channels) and the
+    chain + FIR helper-wave kernel (AERO_OQPSK_WIDE=0, what C2's 65536
+    channels run)."""
+    if request.param == 'one':
+        monkeypatch.setenv('AERO_OQPSK_WIDE', '0')
+    else:
+        monkeypatch.delenv('AERO_OQPSK_WIDE', raising=False)
+    return request.param

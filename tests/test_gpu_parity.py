@@ -34,7 +34,7 @@ def _run_engine(streams, chunks, flags):
 
 
 @pytest.mark.gpu
-def test_engine_matches_oracle(engine_lib):
+def test_engine_matches_oracle(engine_lib, oqpsk_kernel):
     import aero_engine as ae
     streams = [tl.synth(seconds=sec, seed=seed, carrier=f, ebn0=eb) for seed, f, eb, sec, _ in CASES]
     chunks = [c[4] for c in CASES]
@@ -78,7 +78,7 @@ def test_fragment_items_disable_reassembly(engine_lib):
 
 
 @pytest.mark.gpu
-def test_batch_push_equals_channel_push(engine_lib):
+def test_batch_push_equals_channel_push(engine_lib, oqpsk_kernel):
     """Lockstep batch ingest (bench path) == per-channel ZMQ-message ingest."""
     import aero_engine as ae
     nch = 6
@@ -105,7 +105,7 @@ def test_batch_push_equals_channel_push(engine_lib):
 
 
 @pytest.mark.gpu
-def test_many_channels_multiple_waves(engine_lib):
+def test_many_channels_multiple_waves(engine_lib, oqpsk_kernel):
     """70 channels (three wavefronts, out of step with each other: different
     carriers, phases, noise and push sizes) against the oracle, channel by
     channel: soft bits and ACARS items."""
