@@ -2167,3 +2167,16 @@ extern "C" void aero_x_viterbi_stamps(unsigned long long *out4) { viterbi_read_s
 // the burst OQPSK demod's per-section cycle totals (AERO_X_BSTAMPS build; burst.hip)
 extern "C" void aero_x_burst_stamps(unsigned long long *out16) { burst_read_stamps(out16); }
 
+// host check (tests/test_abi.py): the constants a generic-rate MSK group
+// would run with at sample rate fs (msk_gen_consts); iout: sps, d8_old,
+// d8_new, start, stop, ilo, ihi, epb, d8_len; dout: fs, sr_b0, sr_b2, sr_a1,
+// sr_a2, ee, d8w, d8omw.  AERO_E_RATE for a rate the engine does not serve.
+extern "C" int aero_x_msk_rate_consts(int fs, int *iout, double *dout) {
+  MskGen m;
+  if (!msk_gen_consts(fs, m)) return AERO_E_RATE;
+  const int iv[9] = {m.sps, m.d8_old, m.d8_new, m.start, m.stop, m.ilo, m.ihi, m.epb, msk_geom(600, fs).d8_len};
+  const double dv[8] = {m.fs, m.sr_b0, m.sr_b2, m.sr_a1, m.sr_a2, m.ee, m.d8w, m.d8omw};
+  for (int k = 0; k < 9; k++) iout[k] = iv[k];
+  for (int k = 0; k < 8; k++) dout[k] = dv[k];
+  return AERO_OK;
+}

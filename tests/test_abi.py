@@ -69,7 +69,7 @@ def test_engine_tables_match_oracle(engine_lib, cpu_libs):
         assert np.array_equal(a.view(np.int64), b.view(np.int64))
 
 
-@pytest.mark.parametrize('sps', [20, 40])
+@pytest.mark.parametrize('sps', [20, 25, 26, 31, 40, 66, 80, 160])
 def test_engine_msk_tables_match_oracle(engine_lib, cpu_libs, sps):
     """MSK group tables (8192-point twiddles, 2*sps-tap half-sine matched
     filter, decode/mskdemodulator.cpp:126-133) == the oracle's."""
@@ -122,3 +122,55 @@ def test_chan_filter_designs_match_oracle(engine_lib, cpu_libs, args):
     engine_lib.aero_host_pub_hilbert(ctypes.c_int(125), ctypes.c_int(12000), h1.ctypes.data_as(ctypes.c_void_p))
     tl.OraclePublisher.lib().oracle_pub_hilbert(125, 12000, h2.ctypes.data)
     assert np.array_equal(h1.view(np.int32), h2.view(np.int32))
+
+
+def _msk_consts(L, fs):
+    iv = (ctypes.c_int * 9)()
+    dv = (ctypes.c_double * 8)()
+    rc = L.aero_x_msk_rate_consts(ctypes.c_int(fs), iv, dv)
+    return rc, list(iv), list(dv)
+
+
+# coarse.hip MskCoarseBins<Fs> (the fixed-rate kernels' compile-time bins):
+# START, STOP, ILO, IHI, EPB
+FIXED_BINS = {12000: (614, 7578, 3482, 4710, 205), 24000: (307, 7885, 3789, 4403, 102),
+              48000: (154, 8038, 3942, 4250, 51)}
+
+
+@pytest.mark.parametrize('fs', sorted(FIXED_BINS))
+def test_generic_msk_constants_equal_fixed_rate_ones(engine_lib, fs):
+    """The host computation the generic-rate MSK groups run with
+    (engine.hip msk_gen_consts: CoarseFreqEstimate::setSettings(13, 900, 600,
+    Fs), decode/coarsefreqestimate.cpp:39-76, and MskDemodulator::setSettings,
+    decode/mskdemodulator.cpp:94-218) gives, at the three compiled rates, the
+    constants the compiled kernels were built with."""
+    rc, iv, dv = _msk_consts(engine_lib, fs)
+    assert rc == 0
+    sps, d8_old, d8_new, start, stop, ilo, ihi, epb, d8_len = iv
+    assert (start, stop, ilo, ihi, epb) == FIXED_BINS[fs]
+    assert sps == fs // 600 and (d8_old, d8_new) == (sps // 2, sps // 2 - 1) and d8_len == sps // 2 + 1
+    f48 = fs == 48000
+    assert dv[1:6] == ([1.308825621597620e-04, -1.308825621597620e-04, -1.998196509168551, 0.999738234875681, 0.025]
+                       if f48 else
+                       [5.233248111921052e-04, -5.233248111921052e-04, -1.974342917561558, 0.998953350377616, 0.0125])
+
+
+def test_generic_msk_constants_at_other_rates(engine_lib):
+    """Rates without a compiled kernel: an odd SPS gives delayt8 a half-sample
+    delay (ages ceil / floor of SPS/2, weights 0.5 / 0.5, DSP.h:358-384); the
+    fold search stays inside the y bins every MSK group keeps; rates outside
+    [12000, 96000] are refused."""
+    for fs in (15000, 16000, 18750, 22050, 40000, 96000):
+        rc, iv, dv = _msk_consts(engine_lib, fs)
+        assert rc == 0, fs
+        sps, d8_old, d8_new, start, stop, ilo, ihi, epb, d8_len = iv
+        assert sps == fs // 600
+        if sps % 2:
+            assert (d8_old, d8_new, d8_len) == (sps // 2 + 1, sps // 2, sps // 2 + 2) and dv[6:8] == [0.5, 0.5]
+        else:
+            assert (d8_old, d8_new, d8_len) == (sps // 2, sps // 2 - 1, sps // 2 + 1)
+        hz = fs / 8192.0
+        assert start == max(round(900 / hz), 1) and stop == 8192 - start and epb == round(600 / (2 * hz))
+        assert 3276 <= ilo - epb - 1 and ihi + epb <= 4915  # MSK_YLO / MSK_YHI
+    for fs in (11025, 8000, 96001, 192000):
+        assert _msk_consts(engine_lib, fs)[0] == -6  # AERO_E_RATE
