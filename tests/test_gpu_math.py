@@ -119,6 +119,11 @@ def test_atan2_branch_free_main_path_is_glibc(engine_lib):
              x * (rng.integers(16, 257, n) / 256) * (1 + rng.standard_normal(n) * 1e-12) * rng.choice([-1, 1], n),
              x * rng.choice([-1.0, 1.0], n),
              x * np.exp2(rng.uniform(-60, 60, n))]
+    # whole waves in one form (the wave-uniform shortcuts): x > 0, |y| < |x|,
+    # on the small-ratio series or on the table rows
+    xp = np.abs(x)
+    cases.append(xp * rng.uniform(-1 / 16, 1 / 16, n) * 0.999)
+    cases.append(xp * rng.uniform(1 / 16, 1.0, n) * rng.choice([-1, 1], n))
     mixed = cases[0].copy()
     mixed[::97] = 0.0
     mixed[1::89] = np.inf
@@ -126,7 +131,7 @@ def test_atan2_branch_free_main_path_is_glibc(engine_lib):
     mixed[3::79] = 1e-300
     cases.append(mixed)
     for y in cases:
-        for xx, yy in ((x, y), (y, x), (-x, y), (x, -y)):
+        for xx, yy in ((x, y), (y, x), (-x, y), (x, -y), (xp, y)):
             got = eng.device_math('atan2_bf', yy, xx)
             ref = mathhost.glibc('atan2', yy, xx)
             same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
