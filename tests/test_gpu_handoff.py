@@ -34,6 +34,9 @@ print('RC', rc)
 def _run(so):
     env = dict(os.environ)
     env.pop('AERO_ENGINE_SO', None)
+    # the hand-off exists in the chain + FIR-wave kernel only: four channels
+    # would otherwise run the few-channel kernel (engine.hip wide_max)
+    env['AERO_OQPSK_WIDE'] = '0'
     if so:
         env['AERO_ENGINE_SO'] = so
     r = subprocess.run([sys.executable, '-c', CHILD], env=env, capture_output=True, text=True, timeout=300)
