@@ -52,8 +52,9 @@ def shard_vfos(vfos, world):
 
 def broadcast_reads(buf, src=0):
     """The C5 exchange step: the wideband reads in `buf` (a CUDA tensor on
-    the NCCL/RCCL backend, a CPU tensor on gloo) go from rank `src` to all."""
+    the NCCL/RCCL backend, a CPU tensor on gloo) go from rank `src` to all
+    (under a one-rank group too, so that `bench.py --dist` runs the call)."""
     import torch.distributed as dist
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized():
         dist.broadcast(buf, src=src)
     return buf

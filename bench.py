@@ -116,6 +116,9 @@ def parse():
                     help='continuous modes: steps of the second, H2D-inclusive timed region (int16 blocks pushed '
                          'from pinned host memory inside it; default: as many as --steps, so both regions carry '
                          'the same pipeline fill and drain); 0 skips it')
+    ap.add_argument('--dist', action='store_true',
+                    help='run under an RCCL process group even with one rank (rehearses the N>1 path: init, '
+                         'barriers, max / sum all-reduces, on a one-GPU box)')
     ap.add_argument('--pmc', default=None,
                     help='rocprofv3 PMC summary for the roofline traffic field (default profiles/pmc_<mode>.json; '
                          'used only when it was captured at this mode and channel count)')
@@ -315,6 +318,7 @@ def c5_cpu_baseline(cfg, x, procs):
 
 
 def run_c5(a, rank, world, local):
+    use_dist = world > 1 or a.dist
     """C5: one 1.536 Msps receiver (3 main VFOs, 64 [vfos], BASELINE
     configs[4]); the wideband CF32 sits in HBM on rank 0, every read is
     broadcast to all ranks (RCCL over xGMI, the path's one exchange step,
@@ -332,7 +336,7 @@ def run_c5(a, rank, world, local):
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local)
-    if world > 1:
+    if use_dist:
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     import aero_engine as ae
     ch = ae.Channeliser(cfg['sample_rate'], cfg['center_frequency'], cfg['mains'], cfg['vfos'], max_blocks=1,
@@ -366,7 +370,7 @@ def run_c5(a, rank, world, local):
     torch.cuda.synchronize()
     eng.timing_reset()
     s0 = eng.samples_processed()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -377,12 +381,12 @@ def run_c5(a, rank, world, local):
     ch.sync()
     items += eng.drain_items()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     samples = eng.samples_processed() - s0
     t = torch.tensor([elapsed, float(samples), float(items)], dtype=torch.float64, device='cuda')
-    if world > 1:
+    if use_dist:
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
@@ -400,7 +404,8 @@ def run_c5(a, rank, world, local):
         achieved = step_bytes * a.steps / elapsed / 1e9
         out = {
             'metric': 'Msamples/s demod+Viterbi, C5 64-VFO channeliser + mixed 600/1200/10500 (channel samples)',
-            'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
+            'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world,
+            'process_group': 'nccl' if use_dist else None, 'steps': a.steps, 'warmup': a.warmup,
             'preroll_reads': 16, 'ms_per_step': round(elapsed / a.steps * 1e3, 3), 'higher_is_better': True,
             'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32 channeliser / f64 demod', 'data': 'synthetic',
             'config': {'workload': 'C5: 1.536 Msps receiver, 3 main VFOs, 64 [vfos] (6 x 10500, 29 x 600/1200 '
@@ -419,7 +424,7 @@ def run_c5(a, rank, world, local):
         print(json.dumps(out), flush=True)
     eng.close()
     ch.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
@@ -651,11 +656,12 @@ def _c5_items_one(arg):
 
 def main():
     a = parse()
-    if a.gpus > 1 and 'RANK' not in os.environ:
+    if (a.gpus > 1 or a.dist) and 'RANK' not in os.environ:
         sys.exit(spawn_ranks(a.gpus))
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
+    use_dist = world > 1 or a.dist
     if a.mode == 'c5':
         return run_c5(a, rank, world, local)
     if a.mode == 'c1':
@@ -686,7 +692,7 @@ def main():
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local)
-    if world > 1:
+    if use_dist:
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     import aero_engine as ae
     pool = torch.from_numpy(pool_host).to('cuda')
@@ -714,7 +720,7 @@ def main():
     eng.timing_reset()
     s0 = eng.samples_processed()
     st0 = {k: eng.stat(k) for k in stat_names}
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -727,7 +733,7 @@ def main():
     eng.sync()
     items += eng.drain_items()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     t_end = time.perf_counter()
     elapsed = t_end - t0
@@ -751,7 +757,7 @@ def main():
         eng.drain_items()
         torch.cuda.synchronize()
         s1 = eng.samples_processed()
-        if world > 1:
+        if use_dist:
             dist.barrier()
         eng.timing_reset()
         t1 = time.perf_counter()
@@ -770,12 +776,12 @@ def main():
         eng.sync()
         eng.drain_items()
         torch.cuda.synchronize()
-        if world > 1:
+        if use_dist:
             dist.barrier()
         h_el = time.perf_counter() - t1
         h_smp = eng.samples_processed() - s1
         th = torch.tensor([h_el, float(h_smp)], dtype=torch.float64, device='cuda')
-        if world > 1:
+        if use_dist:
             dist.all_reduce(th[:1], op=dist.ReduceOp.MAX)
             dist.all_reduce(th[1:], op=dist.ReduceOp.SUM)
         h_el, h_smp = float(th[0]), float(th[1])
@@ -793,7 +799,7 @@ def main():
     keys = sorted(stats)
     t = torch.tensor([elapsed, float(samples)] + [float(stats[k]) for k in keys], dtype=torch.float64,
                      device='cuda')
-    if world > 1:
+    if use_dist:
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
@@ -843,7 +849,8 @@ def main():
                           'frac': round(tf / FP64_PEAK_TFLOPS, 4)}
         out = {
             'metric': M['metric'],
-            'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world, 'steps': a.steps,
+            'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world,
+            'process_group': 'nccl' if use_dist else None, 'steps': a.steps,
             'warmup': a.warmup, 'preroll_hops': preroll, 'ms_per_step': round(elapsed / a.steps * 1e3, 3),
             'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
@@ -887,7 +894,7 @@ def main():
             out['vs_cpu'] = round(value / cpu['value'], 1)
         print(json.dumps(out), flush=True)
     eng.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
     if rank == 0 and (stats[stat_names[0]] <= 0 or stats['acars_items'] <= 0):
         # the metric names demod + Viterbi: a timed region without decoded frames measured something else
