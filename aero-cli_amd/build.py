@@ -272,6 +272,15 @@ def build_blibm(jobs=4):
     return [build_engine(jobs, variant=v, defines=d) for v, d in BLIBM_VARIANTS.items()]
 
 
+# the coarse kernel with every CIS gather on one line / without the y
+# history reads (what each costs: scripts/gpu_steps.sh ab=cisline:oqpsk10500)
+COARSE_VARIANTS = {'cisline': ['AERO_X_CISLINE'], 'noyread': ['AERO_X_NOYREAD']}
+
+
+def build_coarse(jobs=4):
+    return [build_engine(jobs, variant=v, defines=d) for v, d in COARSE_VARIANTS.items()]
+
+
 # per-section s_memtime totals of the coarse kernel, the demod chain and the
 # Viterbi (scripts/coarse_stamps.py, scripts/demod_stamps.py)
 def build_stamps(jobs=4):
@@ -285,11 +294,11 @@ if __name__ == '__main__':
     ap.add_argument('--oracle', action='store_true')
     ap.add_argument('--host', action='store_true')
     ap.add_argument('--asan', action='store_true', help='sanitizer builds into build/asan (tests/asan_check.sh)')
-    ap.add_argument('--variants', default='', help='comma list of timing builds: drop, blibm, stamps')
+    ap.add_argument('--variants', default='', help='comma list of timing builds: drop, blibm, coarse, stamps')
     ap.add_argument('-j', type=int, default=4)
     a = ap.parse_args()
     for v in filter(None, a.variants.split(',')):
-        print({'drop': build_drop, 'blibm': build_blibm, 'stamps': build_stamps}[v](a.j))
+        print({'drop': build_drop, 'blibm': build_blibm, 'coarse': build_coarse, 'stamps': build_stamps}[v](a.j))
     if a.asan:
         print(build_asan(a.j))
         sys.exit(0)

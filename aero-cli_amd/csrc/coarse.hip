@@ -273,7 +273,11 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     const int q = (int)((s0 + bitrev<L>(epos<L, 0>(t, i))) & (N - 1));
     const uint32_t w = ring_lds[q + (q >> 4)];
     dval[i] = ((double)(int16_t)(w >> 16)) / 32768.0;
+#ifdef AERO_X_CISLINE
+    cs[i] = T.cis[w & 0x7];  // timing build: every gather on one line
+#else
     cs[i] = T.cis[w & 0xFFFF];
+#endif
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(cs[i].x), "+v"(cs[i].y));
@@ -328,7 +332,11 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   // more than the |X| and log10 work that can overlap them.)
   double *yg = S.y + (size_t)c * YLEN;
   const int yreset = S.is[IS_YRESET * C + c];
+#ifdef AERO_X_NOYREAD
+  auto yload = [&](int k) { return 20.0 + 0.0 * k; };  // timing build: no y history reads
+#else
   auto yload = [&](int k) { return (k < YLEN && !yreset) ? yg[k] : 20.0; };
+#endif
   double yp0 = yload(t), yp1 = yload(t + FT);
   // no barrier here: the third transform's workgroup exchange ended with
   // one (chain::gx), after which every wave only works in registers, so the
