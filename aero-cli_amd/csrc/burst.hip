@@ -90,17 +90,14 @@ __global__ __launch_bounds__(512) void hilbert_kernel(BurstState S, BurstTables 
   const long long avail = S.ls[BL_AVAIL * C + c];
   const long long capm = S.pcm_cap - 1;
   double2 *rem = S.hb_rem + (size_t)c * HB_REM;
+  const int16_t *pcm = S.pcm + (size_t)c * S.pcm_cap;  // this channel's run of the ring
   for (; (j + 1) * HB_SNZ <= avail; ++j) {
     double2 x[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int p = bitrev<L>(epos<L, 0>(t, i));
-      if (p < HB_SNZ) {
-        const long long s = j * HB_SNZ + p;
-        x[i] = make_double2(((double)S.pcm[(size_t)(s & capm) * C + c]) / 32768.0, 0.0);
-      } else {
-        x[i] = make_double2(0.0, 0.0);
-      }
+      x[i] = p < HB_SNZ ? make_double2(((double)pcm[(j * HB_SNZ + p) & capm]) / 32768.0, 0.0)
+                        : make_double2(0.0, 0.0);
     }
     fft_dit<L, false>(x, t, lds, T.tw8, s_tw);
 #pragma unroll

@@ -153,7 +153,7 @@ struct BurstState {
   long long *ls;
   double *fir;      // [2 * 55][C] transposed RRC partial sums (MSK: [2 * 80][C] matched filter)
   double2 *ana;     // [ANA_LEN][C] analytic signal
-  int16_t *pcm;     // [pcm_cap][C]
+  int16_t *pcm;     // [C][pcm_cap], channel-major (burst_engine.hip b_batch_scatter_kernel)
   long long pcm_cap;
   double2 *hb_rem;  // [C][HB_REM]
   double *agc, *agc2;           // [len][C]

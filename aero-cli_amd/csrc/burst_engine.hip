@@ -61,22 +61,35 @@ namespace {
 constexpr long long B_PCM_CAP = 32768;
 constexpr int B_HOP_CAP = 256;
 
-__global__ void b_scatter_kernel(int16_t *ring, int C, long long capm, const int16_t *src, long long n, int c,
+__global__ void b_scatter_kernel(int16_t *ring, long long cap, const int16_t *src, long long n, int c,
                                  long long start) {
+  int16_t *row = ring + (size_t)c * cap;
   for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x)
-    ring[((start + k) & capm) * C + c] = src[k];
+    row[(start + k) & (cap - 1)] = src[k];
 }
 
 // lockstep batch of one message per channel: src time-major [n][ld], channel
-// j < nch at its own pushed count (the device copy, stream-ordered)
-__global__ void b_batch_scatter_kernel(int16_t *ring, int C, long long capm, const int16_t *src, long long n,
-                                       long long ld, int nch, const long long *avail) {
-  const long long total = n * nch;
-  for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < total;
-       k += (long long)gridDim.x * blockDim.x) {
-    const long long t = k / nch;
-    const int j = (int)(k - t * nch);
-    ring[((avail[j] + t) & capm) * C + j] = src[t * ld + j];
+// j < nch at its own pushed count (the device copy, stream-ordered).  The
+// ring is channel-major (the Hilbert stage reads a channel's block as one
+// run of lines), so each 64 x 64 tile goes through the LDS: read as rows of
+// 64 channels (one line each), written as rows of 64 samples of one channel.
+constexpr int BTILE = 64;
+__global__ __launch_bounds__(256) void b_batch_scatter_kernel(int16_t *ring, long long cap, const int16_t *src,
+                                                              long long n, long long ld, int nch,
+                                                              const long long *avail) {
+  __shared__ int16_t tile[BTILE][BTILE + 2];  // row stride 33 dwords: the column reads hit 64 banks
+  const long long t0 = (long long)blockIdx.x * BTILE;
+  const int j0 = blockIdx.y * BTILE;
+  const int lane = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+  for (int r = r0; r < BTILE; r += 4) {
+    const long long t = t0 + r;
+    if (t < n && j0 + lane < nch) tile[r][lane] = src[t * ld + j0 + lane];
+  }
+  __syncthreads();
+  for (int r = r0; r < BTILE; r += 4) {
+    const int j = j0 + r;
+    const long long t = t0 + lane;
+    if (j < nch && t < n) ring[(size_t)j * cap + ((avail[j] + t) & (cap - 1))] = tile[lane][r];
   }
 }
 
@@ -703,8 +716,8 @@ int burst_push(BurstGroup *g, int c, const int16_t *pcm, size_t n, bool dev, boo
   }
   const long long start = g->avail[c];
   const int grid = (int)std::min<long long>(((long long)n + 255) / 256, 4096);
-  hipLaunchKernelGGL(b_scatter_kernel, dim3(grid), dim3(256), 0, g->st, g->S.pcm, C, B_PCM_CAP - 1, src,
-                     (long long)n, c, start);
+  hipLaunchKernelGGL(b_scatter_kernel, dim3(grid), dim3(256), 0, g->st, g->S.pcm, B_PCM_CAP, src, (long long)n, c,
+                     start);
   BCHK(hipGetLastError());
   // message start (lastmse capture) and the new pushed count
   if (msg_start) {
@@ -751,10 +764,9 @@ int burst_push_batch(BurstGroup *g, const int16_t *src, size_t n, size_t ld, int
     BCHK(hipMemcpyAsync(g->d_scratch, src, need * sizeof(int16_t), hipMemcpyHostToDevice, g->st));
     d = g->d_scratch;
   }
-  const long long total = (long long)n * nch;
-  const int grid = (int)std::min<long long>((total + 255) / 256, 65536);
-  hipLaunchKernelGGL(b_batch_scatter_kernel, dim3(grid), dim3(256), 0, g->st, g->S.pcm, C, B_PCM_CAP - 1, d,
-                     (long long)n, (long long)ld, nch, (const long long *)(g->S.ls + (size_t)BL_AVAIL * C));
+  const dim3 tiles((unsigned)(((long long)n + BTILE - 1) / BTILE), (unsigned)((nch + BTILE - 1) / BTILE));
+  hipLaunchKernelGGL(b_batch_scatter_kernel, tiles, dim3(256), 0, g->st, g->S.pcm, B_PCM_CAP, d, (long long)n,
+                     (long long)ld, nch, (const long long *)(g->S.ls + (size_t)BL_AVAIL * C));
   hipLaunchKernelGGL(b_batch_counts_kernel, dim3((nch + 255) / 256), dim3(256), 0, g->st, g->S.ls, g->S.chunks, C,
                      nch, (long long)n);
   BCHK(hipGetLastError());
