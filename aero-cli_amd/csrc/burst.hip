@@ -123,7 +123,7 @@ __global__ __launch_bounds__(512) void hilbert_kernel(BurstState S, BurstTables 
         double2 y = x[i];
         if (p < HB_REM) y = make_double2(y.x + r[i].x, y.y + r[i].y);
         const long long s = (j + 1) * HB_SNZ + p;
-        S.ana[(size_t)(s & (ANA_LEN - 1)) * C + c] = y;
+        S.ana[ana_idx(s, c, C)] = y;
       } else {
         rem[p - HB_SNZ] = x[i];
       }
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
   long long n = n0;
   // the analytic sample and the AGC slot it replaces are loaded one sample
   // ahead: the sample's whole chain starts from them
-  double2 a_n = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
+  double2 a_n = S.ana[ana_idx(n, c, C)];
   double agc_n = S.agc[(size_t)agc_p * C + c];
   // so are the ring slots the sample reads (none is a slot the sample before
   // writes: every ring is longer than 3); bt_ma_diff's "newer" slot is the
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
     const double pd1_old = pd1_n, pd2_old = pd2_n;
     const DlyPre mdp = {dMD.w[dl_md], dMD.omw[dl_md], md_older, md_newer, nxt(dl_md, dMD.size), false};
     // the next sample's slots
-    a_n = S.ana[(size_t)((n + 1) & (ANA_LEN - 1)) * C + c];  // past the Hilbert stage's output: unused
+    a_n = S.ana[ana_idx(n + 1, c, C)];  // past the Hilbert stage's output: unused
     cvd_n = S.d1[(size_t)nxt(d1r, B_D1) * C + c];
     ma_n = S.ma1[(size_t)nxt(ma1_p, B_MA) * C + c];
     mv_n = S.mav1[(size_t)nxt(mav1_p, B_MA) * C + c];

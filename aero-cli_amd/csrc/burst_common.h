@@ -152,7 +152,7 @@ struct BurstState {
   int *is;
   long long *ls;
   double *fir;      // [2 * 55][C] transposed RRC partial sums (MSK: [2 * 80][C] matched filter)
-  double2 *ana;     // [ANA_LEN][C] analytic signal
+  double2 *ana;     // [ANA_LEN / 4][C][4] analytic signal (ana_idx)
   int16_t *pcm;     // [C][pcm_cap], channel-major (burst_engine.hip b_batch_scatter_kernel)
   long long pcm_cap;
   double2 *hb_rem;  // [C][HB_REM]
@@ -192,6 +192,21 @@ struct BurstTables {
   const int *dio[BDL_COUNT];
   int dsize[BDL_COUNT];
 };
+
+// The analytic-signal ring: a channel's samples in runs of 2^ANA_LB (the
+// runs of all channels side by side, then the next run), so the Hilbert
+// stage's stores of consecutive samples fill whole runs; the front ends'
+// lanes (one channel each) read 16 B at a 2^ANA_LB x 16 B stride.  Runs of
+// 1 / 2 / 4 / 8 measured hilbert 17.2 / 16.3 / 15.5 / 15.0 ms per C4 step,
+// front_burst 26.1 / 26.2 / 26.3 / 26.9.
+#ifndef AERO_ANA_LB
+#define AERO_ANA_LB 2
+#endif
+constexpr int ANA_LB = AERO_ANA_LB;
+__device__ __forceinline__ size_t ana_idx(long long s, int c, int C) {
+  const size_t q = (size_t)(s & (ANA_LEN - 1));
+  return ((((q >> ANA_LB) * (size_t)C) + (size_t)c) << ANA_LB) | (q & ((1u << ANA_LB) - 1));
+}
 
 // Workgroup -> channel map for kernels with one workgroup per channel that
 // read or write time-major [sample][C] arrays (a 128-B line holds 64 int16

@@ -124,7 +124,7 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
   long long n = n0;
   // the analytic sample and the AGC slot it replaces are loaded one sample
   // ahead: the sample's whole chain starts from them
-  double2 a_n = S.ana[(size_t)(n & (ANA_LEN - 1)) * C + c];
+  double2 a_n = S.ana[ana_idx(n, c, C)];
   double agc_n = S.agc[(size_t)agc_p * C + c];
   while (n < end) {
     if (chk_n - chk_done >= TRI_SLOTS) break;  // every slot holds a check not yet applied
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
     const int p2r = pd3_p >= M_PD2 - 1 ? pd3_p - (M_PD2 - 1) : pd3_p + M_PD3 - (M_PD2 - 1);
     const double2 a = a_n;
     const double agc_old = agc_n;
-    a_n = S.ana[(size_t)((n + 1) & (ANA_LEN - 1)) * C + c];  // past the Hilbert stage's output: unused
+    a_n = S.ana[ana_idx(n + 1, c, C)];  // past the Hilbert stage's output: unused
     const double2 cvd = S.d1[(size_t)d1r * C + c];  // d1.update_dont_touch(cval)
     const double2 bt_old = bt_older, bt_new = btd[(size_t)btn * C];
     const double2 ma_old = S.ma1[(size_t)ma1_p * C + c];
