@@ -30,6 +30,7 @@ F_TIMING = 0x4
 F_TRACE_SOFT = 0x8
 F_TRACE_HOPS = 0x10
 F_TRACE_FRAMES = 0x20
+F_DCD_TICK = 0x40  # AeroL's 1 s DCD timer on the sample clock (continuous OQPSK)
 F_TRACE_ALL = F_TRACE_PT | F_TRACE_BLOCKS | F_TRACE_SOFT | F_TRACE_HOPS | F_TRACE_FRAMES
 
 MATH_FN = {'hypot': 0, 'atan2': 1, 'tanh': 2, 'sin': 3, 'cos': 4, 'log10': 5, 'sqrt': 6, 'fmod360': 7,

@@ -20,6 +20,23 @@
  *                table), aero_log10 the e_log10.c wrapper around it
  * tests/test_math_host.py checks every one bitwise against the host glibc;
  * tests/test_gpu_math.py checks the device build against the host build.
+ *
+ * License: these functions restate the GNU C Library's (glibc 2.35) math
+ * routines -- e_atan2.c, s_sin.c / s_sincos.c, e_log.c / e_log10.c,
+ * e_hypot.c, s_tanh.c / s_expm1.c (the last from Sun's fdlibm) -- and are a
+ * derivative work of them.  The GNU C Library is free software; you can
+ * redistribute it and/or modify it under the terms of the GNU Lesser General
+ * Public License as published by the Free Software Foundation; either version
+ * 2.1 of the License, or (at your option) any later version.  It is
+ * distributed WITHOUT ANY WARRANTY; without even the implied warranty of
+ * MERCHANTABILITY or FITNESS FOR A PARTICULAR PURPOSE.  See the GNU Lesser
+ * General Public License for more details.  Portions: Copyright (C)
+ * 1991-2022 Free Software Foundation, Inc.; IBM Accurate Mathematical
+ * Library, Copyright (C) 2001-2022 Free Software Foundation, Inc.; ARM
+ * optimized-routines log, Copyright (c) 2018 Arm Ltd.; fdlibm, Copyright
+ * (C) 1993 by Sun Microsystems, Inc. (permission to use, copy, modify and
+ * distribute this software is freely granted, provided that this notice is
+ * preserved).
  */
 #pragma once
 #include <stdint.h>

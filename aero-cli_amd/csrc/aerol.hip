@@ -16,10 +16,19 @@
  *                   ballot word per codeword in registers.  Then DelayLine dl2, AeroLScrambler, LSB-first byte
  *                   packing and the per-SU CRC-16 (decode/aerol.cpp:1501-1556).
  *
- * Framing never depends on the CRC results: datacd becomes true at the first
- * UW sync and only the (disabled, wall-clock) DCD timer could clear it, so
- * the Viterbi/CRC work can run after the framing pass without changing the
- * framing decisions.
+ * The framing depends on the CRC results only through AeroL's data carrier
+ * detect, and only when its 1 s DCD timer runs (AERO_F_DCD_TICK): datacd
+ * gates the UW search (aerol.cpp:1096, 1108), the timer clears it once the
+ * CRC failures have drained datacdcountdown (:1043-1058, :1545-1556).
+ * Without the timer datacd becomes true at the first UW sync and stays true,
+ * so the Viterbi/CRC work runs after the framing pass without changing any
+ * framing decision.  With it, frame_kernel marks a completed frame's CRCs as
+ * pending (its Viterbi runs after this framing pass) and stops a channel at
+ * the first soft bit where they could matter: a DCD tick, or a bit whose UW
+ * gate reads a datacd they could raise.  The next framing pass (after that
+ * Viterbi, which leaves the frame's CRC-ok mask in IS_CRC_OKM) applies them
+ * in the reference's order and goes on.  A UW sync in between overwrites
+ * what they would have set (datacd = true, countdown = 12, :2010-2011).
  */
 #include <hip/hip_runtime.h>
 
@@ -30,6 +39,32 @@ namespace aero {
 
 constexpr uint32_t UW = 0xE15AE893u;  // 3780831379 (aerol.cpp:933-936)
 
+// one SU CRC result on the DCD countdown (aerol.cpp:1545-1556); *edges
+// counts datacd changes (SignalHunter::handleDcd)
+__device__ __forceinline__ void dcd_su(bool ok, int &cd, int &datacd, int &edges) {
+  if (ok) {
+    if (cd < 12) cd += 2;
+  } else {
+    if (cd > 0) cd -= 3;
+  }
+  if (!datacd && cd > 2) {
+    datacd = 1;
+    edges++;
+  }
+}
+// AeroL::updateDCD (aerol.cpp:1043-1058): a countdown of 2 goes to -1 and is
+// clamped only at the next tick
+__device__ __forceinline__ void dcd_tick(int &cd, int &datacd, int &edges) {
+  if (cd > 0)
+    cd -= 3;
+  else if (cd < 0)
+    cd = 0;
+  if (datacd && !cd) {
+    datacd = 0;
+    edges++;
+  }
+}
+
 __global__ __launch_bounds__(256) void frame_kernel(DevState S, int nch) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= nch) return;
@@ -39,7 +74,16 @@ __global__ __launch_bounds__(256) void frame_kernel(DevState S, int nch) {
   const long long P = ls[LS_SOFT_P * C + c];
   long long q = ls[LS_SOFT_C * C + c];
   const long long E = P & ~31LL;  // delivered in groups of 32 (oqpskdemodulator.cpp:534-540)
-  if (q >= E) return;
+  const bool ticking = S.dcd_tick != 0;
+  int tick_rec = 0, tick_done = 0, pend = 0;
+  if (ticking) {
+    tick_rec = is[IS_TICK_REC * C + c];
+    tick_done = is[IS_TICK_DONE * C + c];
+    pend = is[IS_CRC_PEND * C + c];
+    if (tick_rec - tick_done > DCD_TICK_RING && S.err)  // cannot happen: the framing lags at most one pass
+      __hip_atomic_store(S.err, DERR_TICKS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (q >= E && tick_rec == tick_done && !pend) return;
   int realimag = is[IS_RI * C + c], cntr = is[IS_CNTR * C + c], gsl = is[IS_GSL * C + c];
   uint32_t uwi = (uint32_t)is[IS_UWI * C + c], uwr = (uint32_t)is[IS_UWR * C + c];
   int inv_i = is[IS_UWI_INV * C + c], inv_r = is[IS_UWR_INV * C + c];
@@ -48,10 +92,33 @@ __global__ __launch_bounds__(256) void frame_kernel(DevState S, int nch) {
   int scr_pos = is[IS_SCR_POS * C + c], blkbuf = is[IS_BLKBUF * C + c];
   int has_ov = is[IS_HAS_OVERLAP * C + c];
   int isu_reset = is[IS_DATACDCD * C + c];  // pending isudata.reset() for the next job
+  int cd = is[IS_DCD_COUNT * C + c], edges = is[IS_DCD_EDGES * C + c];
   const uint8_t *soft = S.soft + (size_t)c * SOFT_RING;
   const int NumberOfBits = 4992, BitsInHeader = 194, Total = 5250;
+  if (pend) {  // the last frame's SU CRCs, decoded since the previous pass
+    const unsigned okm = (unsigned)is[IS_CRC_OKM * C + c];
+    const int nsu = is[IS_CRC_NSU * C + c];
+    for (int k = 0; k < nsu; ++k) dcd_su((okm >> k) & 1, cd, datacd, edges);
+    pend = 0;
+  }
 
-  for (; q < E; ++q) {
+  for (;; ++q) {
+    // DCD ticks due before soft bit q
+    bool stop = false;
+    while (tick_done < tick_rec) {
+      if (ls[(LS_TICK_SOFT0 + (tick_done & (DCD_TICK_RING - 1))) * C + c] > q) break;
+      if (pend) {  // the countdown needs the CRCs of the frame that just ended
+        stop = true;
+        break;
+      }
+      dcd_tick(cd, datacd, edges);
+      tick_done++;
+    }
+    if (stop || q >= E) break;
+    // the gate below reads datacd, which pending CRCs could raise (a flywheel
+    // frame after a tick cleared it); and a second frame end needs them too
+    if (pend && ((!datacd && cntr >= 1 && cntr <= NumberOfBits - 68) || cntr + 1 - BitsInHeader == NumberOfBits - 1))
+      break;
     const int sv = soft[q & (SOFT_RING - 1)];
     int bit = sv >= 128 ? 1 : 0;
     int soft_bit = sv;
@@ -114,13 +181,18 @@ __global__ __launch_bounds__(256) void frame_kernel(DevState S, int nch) {
         scr_pos += has_ov ? 2496 : 2483;
         has_ov = 1;
         blkbuf ^= 1;
+        // the SU CRCs of a completed frame update the DCD countdown
+        // (aerol.cpp:1545-1556) once its Viterbi has run
+        if (ticking && (cntr - BitsInHeader) == (NumberOfBits - 1)) pend = 1;
       }
     }
     if (gotsync) {
       if (cntr + 1 != Total) isu_reset = 1;
       cntr = -1;
-      if (!datacd) is[IS_DCD_EDGES * C + c]++;  // SignalHunter::handleDcd: dcdChange(false, true)
+      if (!datacd) edges++;  // SignalHunter::handleDcd: dcdChange(false, true)
       datacd = 1;
+      cd = 12;
+      pend = 0;  // what the pending CRCs would set, this overwrites
       scr_pos = 0;
     }
     if (cntr + 1 == Total) {
@@ -144,6 +216,12 @@ __global__ __launch_bounds__(256) void frame_kernel(DevState S, int nch) {
   is[IS_BLKBUF * C + c] = blkbuf;
   is[IS_HAS_OVERLAP * C + c] = has_ov;
   is[IS_DATACDCD * C + c] = isu_reset;
+  is[IS_DCD_COUNT * C + c] = cd;
+  is[IS_DCD_EDGES * C + c] = edges;
+  if (ticking) {
+    is[IS_CRC_PEND * C + c] = pend;
+    is[IS_TICK_DONE * C + c] = tick_done;
+  }
 }
 
 // AeroL::Decode for continuous 600/1200 bps (decode/aerol.cpp:1060-2038 with
@@ -401,6 +479,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void vi
       ok = calc == rec;
     }
     const unsigned long long okm = __ballot(ok);
+    if (BLK == BLOCK && frame_done && lane == 0 && S.dcd_tick) {  // for frame_kernel's DCD countdown
+      S.is[IS_CRC_OKM * C + c] = (int)(okm & 0x3FFFFFFULL);
+      S.is[IS_CRC_NSU * C + c] = nsu;
+    }
     uint8_t *out = S.jobout + (size_t)job * JOB_OUT;
     for (int b = lane; b < 312; b += 64) out[b] = info[b];
     if (lane == 0) {

@@ -23,6 +23,8 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <climits>
+
 #include "aero_math.h"
 #include "engine_common.h"
 
@@ -141,7 +143,7 @@ __device__ __forceinline__ int qround(double d) {  // qRound (Qt 5.9 qglobal.h:5
 // i.e. once per ~9 samples)
 enum { PD_CTX1, PD_CTX2, PD_CTY1, PD_CTY2, PD_MARG_SUM, PD_PM_SUM, PD_MS_SUM, PD_MSE, PD_PTD_RE, PD_PTD_IM,
        PD_M2_FREQ, PD_N };
-enum { PI_MARG_P, PI_DT_P, PI_PM_P, PI_MS_P, PI_N };
+enum { PI_MARG_P, PI_DT_P, PI_PM_P, PI_MS_P, PI_N, PI_TICK = PI_N, PI_ALL };
 enum { PL_SOFTP, PL_PTN, PL_N };
 
 constexpr int DEMOD_BLOCK = 256;  // channels per workgroup
@@ -170,6 +172,25 @@ __device__ __forceinline__ void raise_device_error(const DevState &S, int code) 
   if (S.err) __hip_atomic_store(S.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// AeroL's 1 s DCD QTimer on the sample clock (AERO_F_DCD_TICK): tick k fires
+// after the first (k + 1) * Fs samples.  The framing must apply it after the
+// soft bits delivered up to then and before the next ones, so the demod
+// records, at its first carrier event of a sample >= the tick's (events come
+// every ~9 samples; soft bits only at events), how many soft bits AeroL had
+// received: groups of 32 (oqpskdemodulator.cpp:534-540).  The next tick's
+// sample relative to the launch's first sample, or INT_MAX:
+__device__ __forceinline__ int dcd_tick_rel(const DevState &S, int c, long long n0) {
+  if (!S.dcd_tick) return INT_MAX;
+  const long long d = (long long)(S.is[IS_TICK_REC * S.C + c] + 1) * 48000 - n0;
+  return d < (long long)INT_MAX ? (int)d : INT_MAX;
+}
+__device__ __forceinline__ void dcd_tick_record(const DevState &S, int c, long long softp) {
+  const int C = S.C;
+  const int r = S.is[IS_TICK_REC * C + c];
+  S.ls[(LS_TICK_SOFT0 + (r & (DCD_TICK_RING - 1))) * C + c] = softp & ~31LL;
+  S.is[IS_TICK_REC * C + c] = r + 1;
+}
+
 // LDS ordering between the two waves of a pair: every LDS access issued
 // before this has completed (the workgroup-scope release of the AMDGPU memory
 // model, without the wait for outstanding global stores a release fence
@@ -191,7 +212,7 @@ struct DemodShared {
   uint32_t ring[RING_GROUP][DEMOD_BLOCK];
   double pd[PD_N][DEMOD_BLOCK];
   long long pl[PL_N][DEMOD_BLOCK];
-  int pi[PI_N][DEMOD_BLOCK];
+  int pi[PI_ALL][DEMOD_BLOCK];  // + PI_TICK: the next DCD tick's sample, relative to n0
   // chain -> FIR: the mixed sample of chain iteration it (slot it & 1) and
   // the lanes that produced one; FIR -> chain: R_53 after iteration it
   double2 x[2][DEMOD_BLOCK];
@@ -410,6 +431,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
     for (int k = 0; k < PI_N; ++k) sh.pi[k][pair] = S.is[pi_src[k] * C + c];
     sh.pl[PL_SOFTP][pair] = S.ls[LS_SOFT_P * C + c];
     sh.pl[PL_PTN][pair] = TRACE ? S.ls[LS_PT_N * C + c] : 0;
+    sh.pi[PI_TICK][pair] = dcd_tick_rel(S, c, n0);
     q54 = S.fir[(size_t)(NTAPS - 1) * C + c];
     q54i = S.fir[(size_t)(2 * NTAPS - 1) * C + c];
     // R_53 before the first sample: the slot chain iteration 0 reads
@@ -700,6 +722,10 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
         // ms_sum sums (|t| - 1)^2 terms: 0 or a multiple of 2^-158, so the short division is exact
         mse = div_c(ms_sum, ((double)MSE_LEN));
       }
+      if (i >= sh.pi[PI_TICK][pair]) {  // the first event at or after the DCD tick's sample
+        dcd_tick_record(S, cl, sh.pl[PL_SOFTP][pair]);
+        sh.pi[PI_TICK][pair] = INT_MAX;
+      }
       if (mse < 0.65) {  // soft bits, imag first (:516-530)
         int ibit = qround(0.75 * qi * 127.0 + 128.0);
         if (ibit > 255) ibit = 255;
@@ -904,6 +930,7 @@ __global__ __launch_bounds__(DMW_WG) void demod_oqpskw_kernel(DevState S, DevTab
   int pm_p = S.is[IS_PM_P * C + c], ms_p = S.is[IS_MS_P * C + c];
   long long softp = S.ls[LS_SOFT_P * C + c];
   long long ptn = TRACE ? S.ls[LS_PT_N * C + c] : 0;
+  int tick_rel = dcd_tick_rel(S, c, n0);
   double qre[DMW_B], qim[DMW_B], tp[DMW_B];
 #pragma unroll
   for (int jj = 0; jj < DMW_B; ++jj) {
@@ -1097,6 +1124,10 @@ __global__ __launch_bounds__(DMW_WG) void demod_oqpskw_kernel(DevState S, DevTab
         ms_p++;
         ms_p %= MSE_LEN;
         mse = div_c(ms_sum, ((double)MSE_LEN));
+      }
+      if (i >= tick_rel) {  // the first event at or after the DCD tick's sample
+        dcd_tick_record(S, c, softp);
+        tick_rel = INT_MAX;
       }
       if (mse < 0.65) {  // soft bits, imag first (:516-530)
         int ibit = qround(0.75 * qi * 127.0 + 128.0);

@@ -311,6 +311,7 @@ size_t layout(DevState &S, DevTables &T, int mode, const ModeGeom &g, int C, int
   char *p = base;
   S.C = C;
   S.mode = mode;
+  S.dcd_tick = (mode == MODE_OQPSK && (flags & AERO_F_DCD_TICK)) ? 1 : 0;
   S.g = g;
   S.ds = carve<double>(p, (size_t)DS_COUNT * C);
   S.is = carve<int>(p, (size_t)IS_COUNT * C);
@@ -814,6 +815,8 @@ int run_begin(Group *e) {
   return poll_slots(e, false);
 }
 
+int frame_round(Group *e, int flush, bool trace);
+
 // one pass (coarse, the previous pass's Viterbi, demod, framing); *more is
 // false when the group had nothing left to do
 int run_pass(Group *e, int flush, bool *more) {
@@ -861,7 +864,20 @@ int run_pass(Group *e, int flush, bool *more) {
       launch_demod_msk(e->st, e->mode, e->S, e->T, e->nch, flush, e->nch <= e->wide_max);
     ev_end(e, b);
     if (int rc = note_consumed(e)) return rc;
-    // framing + Viterbi into the next job slot (at most one job per channel per pass)
+    if (int rc = frame_round(e, flush, trace)) return rc;
+    // with the DCD timer a channel's framing may stop at a tick that needs the
+    // CRCs of the frame this round completed (aerol.hip frame_kernel); a flush
+    // has no next pass to resume it, so it frames once more after that Viterbi
+    if (flush && e->S.dcd_tick)
+      if (int rc = frame_round(e, flush, trace)) return rc;
+  }
+  return AERO_OK;
+}
+
+// framing + Viterbi into the next job slot (at most one job per channel per pass)
+int frame_round(Group *e, int flush, bool trace) {
+  hipEvent_t a, b;
+  {
     const int si = e->next_slot;
     e->next_slot = (si + 1) % Group::NSLOT;
     auto &sl = e->slot[si];

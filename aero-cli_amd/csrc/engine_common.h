@@ -32,6 +32,7 @@ constexpr int BLOCK = 4992;           // 78 x 64 interleaver block (aerol.cpp:10
 constexpr int DL2_LEN = 4987;         // DelayLine setLength(4992-6) (aerol.cpp:1015)
 constexpr int VIT_MAX = 5078;         // 62 overlap + 4992 + 24 pad
 constexpr int JOB_OUT = 328;          // 312 infofield + len + mask + formatid + channel
+constexpr int DCD_TICK_RING = 4;      // LS_TICK_SOFT0.. entries (ticks recorded, not yet applied)
 
 // channel kinds, one engine group per kind: 10500-bps OQPSK, and continuous
 // MSK per (demodulator sample rate, AeroL bit rate).  aero-decode configures
@@ -184,6 +185,11 @@ enum IS : int {
   // MSK: msema's slot offset (its pointer keeps running over a rate change
   // while marg and dt restart with the event counter)
   IS_MS_OFF,
+  // AeroL's 1 s DCD timer on the sample clock (AERO_F_DCD_TICK, continuous
+  // OQPSK; decode/aerol.cpp:900-902, 1043-1058): datacdcountdown; a frame
+  // whose SU CRCs the framing has not seen yet (the Viterbi writes its CRC-ok
+  // mask and SU count); ticks the demod recorded and the framing applied
+  IS_DCD_COUNT, IS_CRC_PEND, IS_CRC_OKM, IS_CRC_NSU, IS_TICK_REC, IS_TICK_DONE,
   IS_COUNT
 };
 
@@ -197,6 +203,9 @@ enum LS : int {
   LS_SOFT_C,      // soft bits consumed by AeroL
   LS_PT_N,        // pt trace records
   LS_EVENTS,      // MSK symbol events (ring pointer of marg / dt / msema)
+  // DCD tick k (k = 0, 1, ...: after (k + 1) * 48000 samples) happens before
+  // delivered soft bit LS_TICK_SOFT0 + (k & 3) (a multiple of 32)
+  LS_TICK_SOFT0, LS_TICK_SOFT_END = LS_TICK_SOFT0 + 3,
   LS_COUNT
 };
 
@@ -212,6 +221,7 @@ struct DevTables {
 struct DevState {
   int C;                   // channel stride
   int mode;                // Mode
+  int dcd_tick;            // AERO_F_DCD_TICK on a continuous OQPSK group
   ModeGeom g;              // ring and block sizes of this group
   MskGen mg;               // generic-rate MSK groups: the rate's constants
   double *ds;              // [DS_COUNT][C]
@@ -248,5 +258,6 @@ struct DevState {
 
 // device error codes (DevState::err)
 constexpr int DERR_HANDOFF = 1;  // a demod wave pair's LDS hand-off timed out
+constexpr int DERR_TICKS = 2;    // DCD ticks recorded faster than the framing applied them
 
 }  // namespace aero

@@ -347,7 +347,13 @@ int main(int argc, char **argv) {
   // every aero_run advances all of them in the same batched launches
   aero_engine *eng = nullptr;
   const char *dev = getenv("AERO_DEVICE");
-  aero_engine_cfg ecfg{dev ? atoi(dev) : 0, (int)topics.size(), 0};
+  // the reference runs Qt's event loop (decode/main.cpp:106), so AeroL's 1 s
+  // DCD timer fires (decode/aerol.cpp:900-902): the engine runs it on the
+  // sample clock.  AERO_DCD_TICK=0 turns it off (the timer-less behaviour of
+  // a reference without an event loop; test support)
+  const char *tick = getenv("AERO_DCD_TICK");
+  const int eflags = (tick && atoi(tick) == 0) ? 0 : AERO_F_DCD_TICK;
+  aero_engine_cfg ecfg{dev ? atoi(dev) : 0, (int)topics.size(), eflags};
   if (int rc = aero_engine_create(&ecfg, &eng)) {
     AH_CRIT("Failed to create the MI355X demodulation engine: %s", aero_strerror(rc));
     return 1;

@@ -27,7 +27,12 @@ import numpy as np
 # queues (4 by default, and the GPU boxes set 4), so the C5 receiver's kinds
 # shared a queue and ran one after the other.  At least 8,
 # set before anything initialises HIP.
-if int(os.environ.get('GPU_MAX_HW_QUEUES', '4')) < 8:
+# The effective value is recorded in every bench line's config
+# (config.gpu_max_hw_queues); --hw-queues 4 measures at the box default.
+HWQ_DEFAULT = int(os.environ.get('GPU_MAX_HW_QUEUES', '4'))
+if '--hw-queues' in sys.argv[1:-1]:
+    os.environ['GPU_MAX_HW_QUEUES'] = sys.argv[sys.argv.index('--hw-queues') + 1]
+elif HWQ_DEFAULT < 8:
     os.environ['GPU_MAX_HW_QUEUES'] = '8'
 
 
@@ -408,7 +413,7 @@ def run_c5(a, rank, world, local):
             'process_group': 'nccl' if use_dist else None, 'steps': a.steps, 'warmup': a.warmup,
             'preroll_reads': 16, 'ms_per_step': round(elapsed / a.steps * 1e3, 3), 'higher_is_better': True,
             'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32 channeliser / f64 demod', 'data': 'synthetic',
-            'config': {'workload': 'C5: 1.536 Msps receiver, 3 main VFOs, 64 [vfos] (6 x 10500, 29 x 600/1200 '
+            'config': {'gpu_max_hw_queues': int(os.environ['GPU_MAX_HW_QUEUES']), 'workload': 'C5: 1.536 Msps receiver, 3 main VFOs, 64 [vfos] (6 x 10500, 29 x 600/1200 '
                                    'alternating), one 0.25 s read per step, reads broadcast to %d rank(s)' % world,
                        'vfos': len(cfg['vfos']), 'vfos_per_rank': per_read and sum(mine),
                        'parallelism': 'vfo-sharded x%d + read broadcast' % world},
@@ -499,7 +504,7 @@ def run_c1(a):
            'value': round(len(pcm) / elapsed / 1e6, 4), 'unit': 'Msamples/s', 'n_gpus': 1, 'steps': 1, 'warmup': 0,
            'ms_per_step': round(elapsed * 1e3, 1), 'higher_is_better': True, 'scaling': 'none', 'vs_baseline': None,
            'dtype': 'f64', 'data': 'synthetic',
-           'config': {'workload': 'C1: one VFO, %.0f s of synthetic 48 kHz int16 10500-bps P-channel in 12000-sample '
+           'config': {'gpu_max_hw_queues': int(os.environ['GPU_MAX_HW_QUEUES']), 'workload': 'C1: one VFO, %.0f s of synthetic 48 kHz int16 10500-bps P-channel in 12000-sample '
                                   'ZeroMQ messages, published without pacing' % C1_SECONDS,
                       'binary': 'aero-cli_amd/bin/aero-decode --format jsondump', 'items': len(got)},
            'realtime_factor': round(C1_SECONDS / elapsed, 2),
@@ -628,7 +633,7 @@ def run_c5bin(a):
            'value': round(ch_samples / elapsed / 1e6, 4), 'unit': 'Msamples/s', 'n_gpus': 1, 'steps': 1,
            'warmup': 0, 'ms_per_step': round(elapsed * 1e3, 1), 'higher_is_better': True, 'scaling': 'none',
            'vs_baseline': None, 'dtype': 'f32 channeliser / f64 demod', 'data': 'synthetic',
-           'config': {'workload': 'C5 through the binaries: %.0f s of 1.536 Msps CF32 (3 main VFOs, 64 [vfos]) read '
+           'config': {'gpu_max_hw_queues': int(os.environ['GPU_MAX_HW_QUEUES']), 'workload': 'C5 through the binaries: %.0f s of 1.536 Msps CF32 (3 main VFOs, 64 [vfos]) read '
                                   'without pacing by bin/aero-publish; one bin/aero-decode with 64 -t topics'
                                   % C5BIN_SECONDS, 'vfos': nv, 'items': n_all, 'items_before_sigterm': n_run},
            'wideband_msps': round(nb * ref.block_len / elapsed / 1e6, 3),
@@ -847,6 +852,20 @@ def main():
             tf = fl * C / (kc['ms_per_step'] / 1e3) / 1e12
             kc['fp64'] = {'flop_per_channel_hop': fl, 'achieved_tflops': round(tf, 2), 'peak_tflops': FP64_PEAK_TFLOPS,
                           'frac': round(tf / FP64_PEAK_TFLOPS, 4)}
+        # the dominant kernel's algorithmic FP64 flops per step: the coarse
+        # estimator's three radix-2 transforms (5 N log2 N each per
+        # channel-hop); another kernel carries the path's SURVEY.md §8(d)
+        # flops per input sample
+        if dom == 'coarse' and 'nfft_log2' in M:
+            nf = 1 << M['nfft_log2']
+            dom_fl = 3 * 5 * nf * M['nfft_log2'] * C * (kt[dom][1] / steps)
+            basis = '3 x 5 N log2 N per channel-hop (N = %d), %d channel-hops per step' % (
+                nf, round(C * kt[dom][1] / steps))
+        else:
+            dom_fl = M['flops'] * C * HOP
+            basis = '%g flop per input sample (SURVEY.md §8(d)) x %d samples per step' % (M['flops'], C * HOP)
+        dom_tf = dom_fl / (dom_ms / 1e3) / 1e12
+        dom_fp64 = {'achieved': round(dom_tf, 3), 'frac': round(dom_tf / FP64_PEAK_TFLOPS, 5), 'basis': basis}
         out = {
             'metric': M['metric'],
             'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world,
@@ -854,7 +873,7 @@ def main():
             'warmup': a.warmup, 'preroll_hops': preroll, 'ms_per_step': round(elapsed / a.steps * 1e3, 3),
             'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
-            'config': {'workload': ('%s x %d: independent single-VFO %d-bps burst %s R/T channels per GPU, '
+            'config': {'gpu_max_hw_queues': int(os.environ['GPU_MAX_HW_QUEUES']), 'workload': ('%s x %d: independent single-VFO %d-bps burst %s R/T channels per GPU, '
                                     '%d Hz int16, one %d-sample message per channel per step' % (
                                         M['config'], C, M['bitrate'], 'OQPSK' if M['bitrate'] == 10500 else 'MSK',
                                         FS, HOP)) if burst else (
@@ -864,9 +883,20 @@ def main():
                                        FS, HOP)),
                        'channels_per_gpu': C, 'total_channels': C * world, 'hop_samples': HOP,
                        'parallelism': 'channel-sharded x%d' % world},
-            'roofline': dict({'bound': 'hbm', 'kernel': M['kernels'][dom], 'achieved': round(achieved, 2),
-                              'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
-                              'traffic': traffic, 'traffic_source': traffic_src},
+            # the dominant kernel is bound by FP64 VALU dependency latency, not
+            # HBM: its FP64 fraction is the
+            # primary figure, the HBM fraction BASELINE.json quotes is
+            # roofline.hbm beside it
+            'roofline': dict({'bound': 'fp64', 'kernel': M['kernels'][dom], 'achieved': dom_fp64['achieved'],
+                              'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': dom_fp64['frac'],
+                              'flop_basis': dom_fp64['basis'],
+                              'binding': 'FP64 dependency latency of one resident channel per CU (barrier-coupled '
+                                         'transforms, exact libm); neither HBM nor the FP64 pipe is saturated',
+                              'traffic': traffic, 'traffic_source': traffic_src,
+                              'hbm': {'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                                      'frac': round(achieved / HBM_PEAK_GBS, 5),
+                                      'basis': 'SURVEY.md §8(d) bytes per input sample x samples per step over '
+                                               "the dominant kernel's device time per step"}},
                              **unit, **{'kernel_traffic': kernel_traffic,
                               'bytes_per_step': int(step_bytes), 'kernel_ms_per_step': round(dom_ms, 3),
                               'launches_per_step': round(kt[dom][1] / steps, 2),

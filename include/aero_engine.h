@@ -38,6 +38,14 @@ extern "C" {
 #define AERO_F_TRACE_SOFT 0x8  /* keep delivered soft bits for aero_pop_softbits      */
 #define AERO_F_TRACE_HOPS 0x10 /* keep per-hop coarse-estimator records              */
 #define AERO_F_TRACE_FRAMES 0x20 /* keep per-frame infofield records (aero_pop_frames) */
+#define AERO_F_DCD_TICK 0x40   /* continuous OQPSK: run AeroL's 1 s data-carrier-detect
+                                  timer (decode/aerol.cpp:900-902, 1043-1058) on the
+                                  sample clock, one tick per 48000 input samples, as
+                                  the shipped binary's event loop fires it once per
+                                  second of real-time audio (decode/main.cpp:106).
+                                  Without it the timer never fires: after a lost
+                                  message a channel that has synced once searches
+                                  for the UW only at the expected frame boundary */
 
 typedef struct aero_engine aero_engine;
 

@@ -40,9 +40,13 @@
  *     feeds an unconnected signal (decode/oqpskdemodulator.cpp:614).
  *   - GUI-only statics/timers (maxval, slowdown, QElapsedTimer) are dropped.
  *   - Function statics become per-channel fields with identical init.
- *   - AeroL's 1 s wall-clock DCD QTimer never fires (no event loop), as in
- *     the survey's oracle treatment; uninitialised realimag/muw/lastframeinfo
- *     are zero.
+ *   - AeroL's 1 s wall-clock DCD QTimer (decode/aerol.cpp:900-902) has no
+ *     event loop to fire it.  By default it never fires (the survey's oracle
+ *     treatment); with ORACLE_DCD_TICK it fires on a sample clock, after every
+ *     Fs input samples of a continuous OQPSK channel (AeroL::updateDCD,
+ *     :1043-1058), the way the shipped binary's event loop (decode/main.cpp:106)
+ *     fires it once per second of real-time audio.  Uninitialised
+ *     realimag/muw/lastframeinfo are zero.
  */
 #include "aero_oracle.h"
 
@@ -1343,6 +1347,15 @@ struct AeroL {
     if (v != datacd) dcd_edges++;
     datacd = v;
   }
+  // AeroL::updateDCD, the 1 s QTimer's slot (decode/aerol.cpp:1043-1058):
+  // a countdown of 2 goes to -1 and is clamped only at the next tick
+  void updateDCD() {
+    if (datacdcountdown > 0)
+      datacdcountdown -= 3;
+    else if (datacdcountdown < 0)
+      datacdcountdown = 0;
+    if (datacd && !datacdcountdown) set_dcd(false);
+  }
   std::vector<int> block;
   std::vector<int> perm;  // interleaverowdepermute
   // JConvolutionalCodec state
@@ -1772,6 +1785,7 @@ struct Oqpsk {
   std::vector<uint8_t> soft_out;
   std::vector<double> hops, pts;
   bool trace_pt = false;
+  bool dcd_tick = false;  // ORACLE_DCD_TICK
 
   Oqpsk() {
     trig();
@@ -1959,6 +1973,8 @@ struct Oqpsk {
       mixer_center.WTnextFrame();
       st_osc.WTnextFrame();
       st_osc_ref.WTnextFrame();
+      // the DCD QTimer on the sample clock: after every Fs samples
+      if (dcd_tick && (nsamples + 1) % (long long)Fs == 0) aerol.updateDCD();
     }
   }
 };
@@ -3009,6 +3025,7 @@ oracle_chan *oracle_create(int bitrate, int flags) {
   } else if (bitrate == 10500) {
     c->oq.reset(new Oqpsk());
     c->oq->trace_pt = tp;
+    c->oq->dcd_tick = (flags & ORACLE_DCD_TICK) != 0;
   } else {
     c->msk.reset(new Msk(bitrate));
     c->msk->trace_pt = tp;

@@ -27,6 +27,8 @@ typedef struct oracle_chan oracle_chan;
 /* flags */
 #define ORACLE_TRACE_PT 1 /* record every rotated pt_qpsk (re,im) */
 #define ORACLE_BURST 2    /* burst mode (aero-decode --burst): 10500 OQPSK, 600/1200 MSK */
+#define ORACLE_DCD_TICK 4 /* continuous OQPSK: AeroL's 1 s DCD timer (aerol.cpp:900-902,
+                             1043-1058) fires after every Fs input samples */
 
 oracle_chan *oracle_create(int bitrate, int flags);
 void oracle_destroy(oracle_chan *c);

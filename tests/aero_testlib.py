@@ -179,10 +179,10 @@ class Oracle:
             cls._libs['L'] = L
         return cls._libs['L']
 
-    def __init__(self, trace_pt=False, bitrate=10500, burst=False):
+    def __init__(self, trace_pt=False, bitrate=10500, burst=False, dcd_tick=False):
         self.L = self.lib()
         self.bitrate = bitrate
-        self.h = self.L.oracle_create(bitrate, (1 if trace_pt else 0) | (2 if burst else 0))
+        self.h = self.L.oracle_create(bitrate, (1 if trace_pt else 0) | (2 if burst else 0) | (4 if dcd_tick else 0))
         assert self.h, 'oracle_create(%d) failed' % bitrate
 
     def __del__(self):

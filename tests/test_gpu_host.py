@@ -132,7 +132,7 @@ def test_zmq_to_acars_json_end_to_end(engine_lib, cpu_libs, tmp_path):
     import build
     build.build_host()
     pcm = tl.synth(seconds=20.0, seed=0xAE70, carrier=12041.0, ebn0=12.0)
-    ref = tl.Oracle()
+    ref = tl.Oracle(dcd_tick=True)  # aero-decode runs the DCD timer (AERO_F_DCD_TICK)
     ref.push_chunked(pcm, 12000)
     want = ref.item_lines('A')
     assert len(want) >= 5
@@ -223,7 +223,7 @@ def test_publish_to_decode_pipeline(engine_lib, cpu_libs, tmp_path):
     wants = []
     for v in picks:
         import aero_engine as ae
-        o = tl.Oracle(bitrate=ae.vfo_bitrate(cfg['vfos'][v]['data_rate']))
+        o = tl.Oracle(bitrate=ae.vfo_bitrate(cfg["vfos"][v]["data_rate"]), dcd_tick=True)
         o.push_chunked(ref.usb(v), ref.info(v)['samples_per_block'])
         wants.append(o.item_lines('A'))
     assert len(wants[0]) >= 5
@@ -277,7 +277,7 @@ def test_multi_topic_decoder(engine_lib, cpu_libs, tmp_path):
     nv = len(cfg['vfos'])
     wants = []
     for v in range(nv):
-        o = tl.Oracle(bitrate=ae.vfo_bitrate(cfg['vfos'][v]['data_rate']))
+        o = tl.Oracle(bitrate=ae.vfo_bitrate(cfg["vfos"][v]["data_rate"]), dcd_tick=True)
         o.push_chunked(ref.usb(v), ref.info(v)['samples_per_block'])
         wants.append(o.item_lines('A'))
     assert sum(len(w) for w in wants) >= 40
