@@ -117,6 +117,11 @@ def parse():
                          'the GPU box CPU share)')
     ap.add_argument('--cpu-runs', type=int, default=3, help='CPU-baseline repetitions (the median is reported)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-dcd-tick', action='store_true',
+                    help="continuous OQPSK without AeroL's 1 s DCD timer (AERO_F_DCD_TICK, on by default as in "
+                         'bin/aero-decode, whose reference runs the Qt event loop)')
+    ap.add_argument('--hw-queues', type=int, default=None,
+                    help='GPU_MAX_HW_QUEUES for this run (default: at least 8; applied before HIP initialises)')
     ap.add_argument('--h2d-steps', type=int, default=None,
                     help='continuous modes: steps of the second, H2D-inclusive timed region (int16 blocks pushed '
                          'from pinned host memory inside it; default: as many as --steps, so both regions carry '
@@ -352,7 +357,8 @@ def run_c5(a, rank, world, local):
     if rank == 0:
         wb.copy_(torch.from_numpy(x[:nread * B].view(np.float32).reshape(nread, B * 2)))
     rd = torch.empty((B * 2,), dtype=torch.float32, device='cuda')
-    eng = ae.Engine(max_channels=max(1, sum(mine)), device=local, flags=ae.F_TIMING)
+    eng = ae.Engine(max_channels=max(1, sum(mine)), device=local,
+                    flags=ae.F_TIMING | (0 if a.no_dcd_tick else ae.F_DCD_TICK))
     chans = [eng.open_channel(ae.vfo_bitrate(v['data_rate'])) if m else -1 for v, m in zip(cfg['vfos'], mine)]
     per_read = sum(ch.vfo_info(v)['samples_per_block'] for v in range(len(cfg['vfos'])) if mine[v])
 
@@ -707,7 +713,7 @@ def main():
         views = [pool[:, int(o) + s * HOP:int(o) + (s + 1) * HOP] for o in offsets]
         return torch.stack(views).permute(2, 0, 1).reshape(HOP, C).contiguous()
 
-    eng = ae.Engine(max_channels=C, device=local, flags=ae.F_TIMING)
+    eng = ae.Engine(max_channels=C, device=local, flags=ae.F_TIMING | (0 if a.no_dcd_tick else ae.F_DCD_TICK))
     for _ in range(C):
         eng.open_channel(M['bitrate'], FS, burst=burst)
     stat_names = ('rt_tests', 'rt_packets') if burst else ('viterbi_jobs', 'frames', 'su_crc_ok')
@@ -882,6 +888,7 @@ def main():
                                        M['config'], C, M['bitrate'], 'OQPSK' if M['bitrate'] == 10500 else 'MSK',
                                        FS, HOP)),
                        'channels_per_gpu': C, 'total_channels': C * world, 'hop_samples': HOP,
+                       'dcd_tick': (not a.no_dcd_tick) and not burst and M['bitrate'] == 10500,
                        'parallelism': 'channel-sharded x%d' % world},
             # the dominant kernel is bound by FP64 VALU dependency latency, not
             # HBM: its FP64 fraction is the
