@@ -122,6 +122,13 @@ struct WaveTable {
     WTstep = (freq) * ((double)WTSIZE) / samplerate;
   }
   double GetFreqHz() const { return freq; }
+  double GetPhaseDeg() const { return (360.0 * WTptr / ((double)WTSIZE)); }  // DSP.cpp:200
+  cpx WTCISValue_conj() const {  // DSP.cpp:90-97
+    int tint = (int)WTptr;
+    if (tint >= WTSIZE) tint = 0;
+    if (tint < 0) tint = WTSIZE - 1;
+    return std::conj(trig().CISWT[tint]);
+  }
   void IncreseFreqHz(double freq_hz) {
     freq_hz += freq;
     SetFreq(freq_hz);
@@ -455,7 +462,19 @@ struct Coarse {
     startbin = (int)std::max(round(lockingbw / hzperbin), 1.0);
     stopbin = (int)nfft - startbin;
     expectedpeakbin = (int)round(fb / (2.0 * hzperbin));
+    // raised-cosine window over +-startbin (coarsefreqestimate.cpp:60-74)
+    window.assign((int)nfft, 0.0);
+    window[0] = 1;
+    for (int i = 1; i <= startbin; i++) {
+      double val = cos(M_PI_2 * ((double)i) / ((double)startbin));
+      val *= val;
+      if (((int)nfft - i) < 0) break;
+      if (i >= (int)nfft) break;
+      window[(int)nfft - i] = val;
+      window[i] = val;
+    }
   }
+  std::vector<double> window;
   void bigchange() {
     emptyingcountdown = 4;
     for (int i = 0; i < (int)nfft; i++) y[i] = 20;
@@ -464,7 +483,10 @@ struct Coarse {
     int N = (int)nfft;
     out = data;
     jfft.fft(out.data(), false);
-    for (int i = startbin; i <= stopbin; i++) out[i] = 0;
+    if (fb != 8400)  // boxcar (coarsefreqestimate.cpp:97-100)
+      for (int i = startbin; i <= stopbin; i++) out[i] = 0;
+    else  // C channel: the raised-cosine window (:101-104)
+      for (int i = 0; i < N; i++) out[i] *= window[i];
     in = out;
     jfft.fft(in.data(), true);
     for (int i = 0; i < N; i++) in[i] *= (double)N;
@@ -495,6 +517,48 @@ struct Coarse {
     if (emptyingcountdown <= 0) return freq_offset_est;
     emptyingcountdown--;
     return 0;
+  }
+};
+
+/* -------------------------------------------------------------- JFastFir */
+// JFastFir::SetKernel / update(cpx) (decode/jfft.cpp:324-367, 445-495):
+// overlap-add fast convolution, one FFT per signal_non_zero_size samples, the
+// output one block behind the input
+struct FastFir {
+  JFFT fft;
+  std::vector<cpx> kernel, sigspace, remainder;
+  int nfft = 0, sigspace_ptr = 0, signal_non_zero_size = 0, remainder_size = 0;
+  void SetKernel(const std::vector<cpx> &k, int approx_fft_size) {
+    const int kernel_non_zero_size = (int)k.size();
+    nfft = 1;
+    if (approx_fft_size <= 0) approx_fft_size = 4 * kernel_non_zero_size;
+    while (nfft < approx_fft_size) nfft <<= 1;
+    kernel = k;
+    kernel.resize(nfft, cpx(0, 0));
+    sigspace.assign(nfft, cpx(0, 0));
+    sigspace_ptr = 0;
+    signal_non_zero_size = nfft + 1 - kernel_non_zero_size;
+    remainder_size = nfft - signal_non_zero_size;
+    remainder.assign(remainder_size, cpx(0, 0));
+    fft.init(nfft);
+    fft.fft(kernel.data(), false);
+  }
+  cpx update(cpx in_val) {
+    if (sigspace_ptr >= signal_non_zero_size) {
+      fft.fft(sigspace.data(), false);
+      for (int k = 0; k < nfft; ++k) sigspace[k] *= kernel[k];
+      fft.fft(sigspace.data(), true);
+      for (int k = 0; k < remainder_size; ++k) {
+        sigspace[k] += remainder[k];
+        remainder[k] = sigspace[signal_non_zero_size + k];
+        sigspace[signal_non_zero_size + k] = 0;
+      }
+      sigspace_ptr = 0;
+    }
+    cpx out_val = sigspace[sigspace_ptr];
+    sigspace[sigspace_ptr] = in_val;
+    sigspace_ptr++;
+    return out_val;
   }
 };
 
@@ -585,6 +649,55 @@ struct UWDetector {
     xorsum += val ^ preamble[n - 1];
     buffer[n - 1] = val;
     if (xorsum >= (n - tollerence)) {
+      inverted = true;
+      return true;
+    }
+    if (xorsum <= tollerence) {
+      inverted = false;
+      return true;
+    }
+    return false;
+  }
+};
+
+// OQPSKPreambleDetectorAndAmbiguityCorrection (decode/aerol.cpp:782-877): two
+// preambles; the second's buffer only moves when the first did not match
+struct UWDetector2 {
+  std::vector<int> preamble1, buffer1, preamble2, buffer2;
+  int tollerence = 0;
+  bool inverted = false;
+  void setPreamble(uint64_t p1, uint64_t p2, int len) {
+    preamble1.clear();
+    preamble2.clear();
+    for (int i = len - 1; i >= 0; i--) {
+      preamble1.push_back((p1 >> i) & 1 ? 1 : 0);
+      preamble2.push_back((p2 >> i) & 1 ? 1 : 0);
+    }
+    buffer1.assign(preamble1.size(), 0);
+    buffer2.assign(preamble2.size(), 0);
+  }
+  static int shift(std::vector<int> &buf, const std::vector<int> &pre, int val) {
+    int xorsum = 0, n = (int)buf.size();
+    for (int i = 0; i < n - 1; i++) {
+      buf[i] = buf[i + 1];
+      xorsum += buf[i] ^ pre[i];
+    }
+    xorsum += val ^ pre[n - 1];
+    buf[n - 1] = val;
+    return xorsum;
+  }
+  int Update(int val) {
+    int xorsum = shift(buffer1, preamble1, val);
+    if (xorsum >= ((int)buffer1.size() - tollerence)) {
+      inverted = true;
+      return true;
+    }
+    if (xorsum <= tollerence) {
+      inverted = false;
+      return true;
+    }
+    xorsum = shift(buffer2, preamble2, val);
+    if (xorsum >= ((int)buffer2.size() - tollerence)) {
       inverted = true;
       return true;
     }
@@ -1385,6 +1498,16 @@ struct AeroL {
     if (bitrate == 10500) {
       leaverN = 78;
       dl2.assign(4986 + 1, 0);
+    } else if (bitrate == 8400) {  // C channel (aerol.cpp:994-1004, 922-929)
+      leaverN = 4;
+      dl2.assign(2708 + 1, 0);
+      NumberOfBits = 4096;
+      BitsInHeader = 0;
+      TotalNumberOfBits = 4096;
+      c_real.setPreamble(216866263330005ULL, 3012071630031408ULL, 52);
+      c_imag.setPreamble(216866263330005ULL, 3012071630031408ULL, 52);
+      c_real.tollerence = 6;  // setSettings, not burst (aerol.cpp:972-973)
+      c_imag.tollerence = 6;
     } else {  // 600 / 1200 (aerol.cpp:975-993)
       leaverN = bitrate == 600 ? 6 : 9;
       dl2.assign(570 + 1, 0);
@@ -1406,6 +1529,162 @@ struct AeroL {
     TotalNumberOfBits = useingOQPSK ? 10500 : (leaverN == 6 ? 600 : 1200) * 3;
   }
   UWDetector msk_uw;  // mskBurstDetector (aerol.cpp:939-940)
+  // C channel: preambledetectorreal / -imag, the 4 x 64 block index (AeroL
+  // ctor sets index = 0, aerol.cpp:931), the deinterleaved frame; outputs:
+  // 12-byte Call_progress SUs, per frame uint32 AES + 300 voice bytes
+  UWDetector2 c_real, c_imag;
+  int c_index = 0;
+  std::vector<uint8_t> c_deleaved;
+  std::vector<uint8_t> *c_units_out = nullptr, *voice_out = nullptr;
+
+  // AeroL::DecodeC (decode/aerol.cpp:2145-2415)
+  void decodeC(const short *bits, int n) {
+    uint32_t hex = 0;  // "000000": the AES of this call's last Call_progress
+    for (int i = 0; i < n; i++) {
+      int bit = ((uint8_t)bits[i]) >= 128 ? 1 : 0;
+      int soft_bit = (uint16_t)bits[i];
+      int gotsync = 0;
+      realimag++;
+      realimag %= 2;
+      UWDetector2 &det = realimag ? c_real : c_imag;
+      if (cntr > NumberOfBits - 112 || cntr <= 0) {
+        gotsync = det.Update(bit);
+        if (!gotsync_last) {
+          gotsync_last = gotsync;
+          gotsync = 0;
+        } else
+          gotsync_last = 0;
+      } else {
+        gotsync = 0;
+        gotsync_last = 0;
+      }
+      if (det.inverted) {
+        bit = 1 - bit;
+        if (soft_bit > 128)
+          soft_bit = 255 - soft_bit;
+        else if (soft_bit < 128)
+          soft_bit = 255 - soft_bit;
+      }
+      if (gotsync) {
+        cntr = -1;
+        c_index = -1;
+        c_deleaved.clear();
+        scr_pos = 0;  // depuncturedBlock.clear(); scrambler.reset()
+        continue;
+      }
+      if (cntr < 1000000000) cntr++;
+      if (cntr <= NumberOfBits - 1) {
+        c_index++;
+        block[c_index] = soft_bit;
+      }
+      if (c_index == 255) {  // deinterleave_ba(block, 4) (aerol.cpp:594-613)
+        for (int j = 0; j < 4; j++)
+          for (int ii = 0; ii < 64; ii++) c_deleaved.push_back((uint8_t)block[perm[ii] * 4 + j]);
+        c_index = -1;
+      }
+      if (cntr == NumberOfBits - 1) frame_c(hex);
+    }
+  }
+  void frame_c(uint32_t &hex) {
+    // PuncturedCode::depunture_soft_block(.., 4, true) (aerol.cpp:2417-2432):
+    // all but the last source value, an erasure after every third
+    std::vector<uint8_t> dep;
+    int ptr = 0;
+    for (int i = 0; i < (int)c_deleaved.size() - 1; i++) {
+      ptr++;
+      dep.push_back(c_deleaved[i]);
+      if (ptr >= 3) dep.push_back(128);
+      ptr %= 3;
+    }
+    std::vector<int> deconvol = decode_continuous(dep);
+    deconvol.resize(2714);
+    if (blocks_out) {
+      uint32_t L = (uint32_t)deconvol.size();
+      uint8_t *lp = (uint8_t *)&L;
+      blocks_out->insert(blocks_out->end(), lp, lp + 4);
+      for (int b : deconvol) blocks_out->push_back((uint8_t)b);
+    }
+    for (size_t q = 0; q < deconvol.size(); q++) {  // DelayLine::update
+      dl2[dl2_ptr] = deconvol[q];
+      dl2_ptr++;
+      dl2_ptr %= (int)dl2.size();
+      deconvol[q] = dl2[dl2_ptr];
+    }
+    for (size_t q = 0; q < deconvol.size(); q++) deconvol[q] = deconvol[q] ^ pre_state[scr_pos++];
+    // 24 sub-data fields of 12 bits at 109 y + 97 (aerol.cpp:2262-2282) -> 3 SUs
+    std::string info;
+    int charptr = 0;
+    uint8_t ch = 0;
+    uint32_t okmask = 0;
+    std::string all;
+    for (int y = 0; y < 24; y++) {
+      const int offset = y * (1 + 96 + 12);
+      for (int h = offset + 97; h < offset + 109; h++) {
+        ch |= deconvol[h] * 128;
+        charptr++;
+        charptr %= 8;
+        if (charptr == 0) {
+          info += (char)ch;
+          ch = 0;
+        } else
+          ch >>= 1;
+      }
+      if (info.size() == 12) {
+        const char *su = info.data();
+        const uint16_t crc_calc = crc16_bytes(su, 10);
+        const uint16_t crc_rec = (uint16_t)((((uint8_t)su[11]) << 8) | ((uint8_t)su[10]));
+        const bool ok = crc_calc == crc_rec;
+        if (ok) {
+          if (datacdcountdown < 12) datacdcountdown += 2;
+        } else {
+          if (datacdcountdown > 0) datacdcountdown -= 5;
+        }
+        if (!datacd && datacdcountdown > 2) set_dcd(true);
+        if (ok) {
+          okmask |= 1u << (all.size() / 12);
+          if ((uint8_t)su[0] == 0x30) {  // Call_progress: Call_progress_Signal, AES -> hex
+            if (c_units_out) c_units_out->insert(c_units_out->end(), su, su + 12);
+            hex = ((uint32_t)(uint8_t)su[1] << 16) | ((uint32_t)(uint8_t)su[2] << 8) | (uint8_t)su[3];
+          }
+        }
+        all += info;
+        info.clear();
+      }
+    }
+    // voice: 96 of every 109 bits from bit 1 (aerol.cpp:2362-2392)
+    std::vector<uint8_t> data;
+    int bitsin = 0;
+    for (int h = 1; h < 2714; h++) {
+      ch |= deconvol[h] * 128;
+      charptr++;
+      charptr %= 8;
+      if (charptr == 0) {
+        data.push_back(ch);
+        ch = 0;
+      } else
+        ch >>= 1;
+      bitsin++;
+      if (bitsin == 96) {
+        bitsin = 0;
+        h += 13;
+      }
+    }
+    if (voice_out) {
+      const uint8_t *hp = (const uint8_t *)&hex;
+      voice_out->insert(voice_out->end(), hp, hp + 4);
+      data.resize(300, 0);
+      voice_out->insert(voice_out->end(), data.begin(), data.end());
+    }
+    if (frames_out) {
+      uint8_t rec[320] = {0};
+      memcpy(rec, all.data(), all.size());
+      uint32_t L = (uint32_t)all.size();
+      memcpy(rec + 312, &L, 4);
+      memcpy(rec + 316, &okmask, 4);
+      frames_out->insert(frames_out->end(), rec, rec + 320);
+    }
+    c_index = -1;
+  }
 
   // R / T packet results (decode/aerol.cpp:1240-1460; only what emits items)
   void rt_result(int result) {
@@ -1786,9 +2065,14 @@ struct Oqpsk {
   std::vector<double> hops, pts;
   bool trace_pt = false;
   bool dcd_tick = false;  // ORACLE_DCD_TICK
+  // C channel (fb = 8400, decode/oqpskdemodulator.cpp:174-240, 292-324): the
+  // JFastFir prefilter between a down- and an up-mix by mixer_fir_pre
+  WaveTable mixer_fir_pre;
+  FastFir fir_pre;
 
-  Oqpsk() {
+  explicit Oqpsk(double _fb = 10500) : aerol((int)_fb) {
     trig();
+    fb = _fb;
     // ctor
     mixer_center.SetFreq(8000.0, 48000);
     mixer2.SetFreq(8000.0, 48000);
@@ -1812,7 +2096,7 @@ struct Oqpsk {
     mixer_center.SetFreq(freq_center, (int)Fs);
     mixer2.SetFreq(freq_center, (int)Fs);
     agc.init(4, Fs);
-    std::vector<double> rrc = rrc_design(1.0, 55, Fs, fb / 2);
+    std::vector<double> rrc = rrc_design(fb == 8400 ? 0.6 : 1.0, 55, Fs, fb / 2);
     fir_re.init(rrc);
     fir_im.init(rrc);
     double T = Fs / (fb / 2);
@@ -1820,16 +2104,33 @@ struct Oqpsk {
     delayt41.setdelay(T / 4.0);
     delayt42.setdelay(T / 4.0);
     delayt8.setdelay(T / 8.0);
-    st_iir_resonator.b[0] = 0.00032714218939589035;
-    st_iir_resonator.b[1] = 0;
-    st_iir_resonator.b[2] = 0.00032714218939589035;
-    st_iir_resonator.a[0] = 1;
-    st_iir_resonator.a[1] = -0.39005299948210803;
-    st_iir_resonator.a[2] = 0.99934571562120822;
-    ee = 0.4;
+    if (fb == 8400) {  // the second ("10Hz bw") design wins (:196-214)
+      st_iir_resonator.b[0] = 0.0012845857864470789;
+      st_iir_resonator.b[1] = 0;
+      st_iir_resonator.b[2] = -0.0012845857864470789;
+      st_iir_resonator.a[0] = 1;
+      st_iir_resonator.a[1] = -0.90681461999279889;
+      st_iir_resonator.a[2] = 0.99743082842710584;
+      ee = 0.65;
+    } else {
+      st_iir_resonator.b[0] = 0.00032714218939589035;
+      st_iir_resonator.b[1] = 0;
+      st_iir_resonator.b[2] = 0.00032714218939589035;
+      st_iir_resonator.a[0] = 1;
+      st_iir_resonator.a[1] = -0.39005299948210803;
+      st_iir_resonator.a[2] = 0.99934571562120822;
+      ee = 0.4;
+    }
     st_iir_resonator.init();
     st_osc.SetFreq(fb, (int)Fs);
     st_osc_ref.SetFreq(fb, (int)Fs);
+    // the ctor's mixer_fir_pre (freq_center 8000 then, :114), setSettings'
+    // prefilter kernel: RRC(0.6, 2048 -> 2049 taps) in 4096-point blocks (:228-236)
+    mixer_fir_pre.SetFreq(8000.0, (int)Fs);
+    if (fb == 8400) {
+      std::vector<double> k = rrc_design(0.6, 2048, Fs, fb / 2);
+      fir_pre.SetKernel(std::vector<cpx>(k.begin(), k.end()), 4096);
+    }
   }
 
   void CenterFreqChangedSlot(double freq_center) {  // :256-280
@@ -1847,6 +2148,9 @@ struct Oqpsk {
   }
 
   void FreqOffsetEstimateSlot(double est) {  // :562-620
+    // the prefilter mixer follows the estimate until dcd (never set) (:565-569);
+    // only the C channel uses it, and its end-of-message SetFreq overrides it
+    if ((mse > signalthreshold) || (!dcd)) mixer_fir_pre.SetFreq(mixer_center.GetFreqHz() + est, (int)Fs);
     if ((mse < signalthreshold) && (!dcd)) {
       if (countdown2 > 0)
         countdown2--;
@@ -1878,6 +2182,24 @@ struct Oqpsk {
 
   void writeData(const short *ptr, int n) {
     std::vector<cpx> bbtmp(bbnfft);
+    std::vector<cpx> pre;
+    if (fb == 8400) {  // prefilter (:292-324): down, JFastFir, up from the saved phase
+      pre.resize(n);
+      const short *p2 = ptr;
+      const double savedphase = mixer_fir_pre.GetPhaseDeg();
+      for (int i = 0; i < n; i++, p2++) {
+        const double dval = ((double)(*p2)) / 32768.0;
+        pre[i] = mixer_fir_pre.WTCISValue() * dval;
+        mixer_fir_pre.WTnextFrame();
+      }
+      for (int i = 0; i < n; i++) pre[i] = fir_pre.update(pre[i]);
+      mixer_fir_pre.SetPhaseDeg(savedphase);
+      for (int i = 0; i < n; i++) {
+        pre[i] *= mixer_fir_pre.WTCISValue_conj();
+        mixer_fir_pre.WTnextFrame();
+      }
+    }
+    double mixer2_freq_sum = 0;
     for (int i = 0; i < n; i++, ptr++, nsamples++) {
       double dval = ((double)(*ptr)) / 32768.0;
       bbcycbuff[bbcycbuff_ptr] = mixer_center.WTCISValue() * dval;
@@ -1899,8 +2221,13 @@ struct Oqpsk {
         hops.push_back(mse > signalthreshold ? 0.0 : 1.0);
       }
       cpx cval, sig2;
-      cval = mixer2.WTCISValue() * dval;
-      sig2 = cpx(fir_re.FIRUpdateAndProcess(cval.real()), fir_im.FIRUpdateAndProcess(cval.imag()));
+      if (fb == 8400) {  // already RRC-filtered: mix only (:376-387)
+        sig2 = mixer2.WTCISValue() * pre[i];
+        mixer2_freq_sum += mixer2.GetFreqHz();
+      } else {
+        cval = mixer2.WTCISValue() * dval;
+        sig2 = cpx(fir_re.FIRUpdateAndProcess(cval.real()), fir_im.FIRUpdateAndProcess(cval.imag()));
+      }
       double dabval = std::sqrt(sig2.real() * sig2.real() + sig2.imag() * sig2.imag());
       sig2 *= agc.Update(dabval);
       double abval = std::abs(sig2);
@@ -1938,11 +2265,16 @@ struct Oqpsk {
           double ct_ec = ct_xt_d - ct_xt;
           if (ct_ec > M_PI) ct_ec = M_PI;
           if (ct_ec < -M_PI) ct_ec = -M_PI;
-          ct_ec = ct_iir_loopfilter.update(ct_ec);
-          if (ct_ec > M_PI_2) ct_ec = M_PI_2;
-          if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
-          mixer2.IncresePhaseDeg(1.0 * ct_ec);
-          mixer2.IncreseFreqHz(0.01 * ct_ec);
+          if (fb > 8400) {
+            ct_ec = ct_iir_loopfilter.update(ct_ec);
+            if (ct_ec > M_PI_2) ct_ec = M_PI_2;
+            if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
+            mixer2.IncresePhaseDeg(1.0 * ct_ec);
+            mixer2.IncreseFreqHz(0.01 * ct_ec);
+          } else {  // 8400: faster phase agility (:463-472)
+            mixer2.IncresePhaseDeg(1.0 * ct_ec);
+            mixer2.IncreseFreqHz(0.5 * 0.01 * ct_iir_loopfilter.update(ct_ec));
+          }
           marg.UpdateSigned(ct_ec);
           dt.update(pt_qpsk);
           pt_qpsk *= cpx(olm::cos(marg.Val), olm::sin(marg.Val));
@@ -1962,7 +2294,11 @@ struct Oqpsk {
             RxDataBits.push_back((short)(uint8_t)ibit);
             if (RxDataBits.size() >= 32) {
               for (short s : RxDataBits) soft_out.push_back((uint8_t)s);
-              aerol.decode(RxDataBits.data(), (int)RxDataBits.size());
+              // AeroL::processDemodulatedSoftBits (aerol.cpp:2040-2051)
+              if (fb == 8400)
+                aerol.decodeC(RxDataBits.data(), (int)RxDataBits.size());
+              else
+                aerol.decode(RxDataBits.data(), (int)RxDataBits.size());
               RxDataBits.clear();
             }
           }
@@ -1976,6 +2312,8 @@ struct Oqpsk {
       // the DCD QTimer on the sample clock: after every Fs samples
       if (dcd_tick && (nsamples + 1) % (long long)Fs == 0) aerol.updateDCD();
     }
+    // the prefilter mixer follows this message's mean carrier (:555-557)
+    if (n > 0) mixer_fir_pre.SetFreq(mixer2_freq_sum / ((double)n));
   }
 };
 
@@ -2363,43 +2701,8 @@ static std::vector<cpx> hilbert_taps(int N) {
   return k;
 }
 
-struct HilbertFir {
-  JFFT fft;
-  std::vector<cpx> kernel, sigspace, remainder;
-  int nfft = 0, sigspace_ptr = 0, signal_non_zero_size = 0, remainder_size = 0;
-  HilbertFir() {
-    const int N = 2048;
-    std::vector<cpx> k = hilbert_taps(N);
-    const int kernel_non_zero_size = N;
-    nfft = 1;
-    while (nfft < 4 * kernel_non_zero_size) nfft <<= 1;
-    kernel = k;
-    kernel.resize(nfft, cpx(0, 0));
-    sigspace.assign(nfft, cpx(0, 0));
-    sigspace_ptr = 0;
-    signal_non_zero_size = nfft + 1 - kernel_non_zero_size;
-    remainder_size = nfft - signal_non_zero_size;
-    remainder.assign(remainder_size, cpx(0, 0));
-    fft.init(nfft);
-    fft.fft(kernel.data(), false);
-  }
-  cpx update(cpx in_val) {
-    if (sigspace_ptr >= signal_non_zero_size) {
-      fft.fft(sigspace.data(), false);
-      for (int k = 0; k < nfft; ++k) sigspace[k] *= kernel[k];
-      fft.fft(sigspace.data(), true);
-      for (int k = 0; k < remainder_size; ++k) {
-        sigspace[k] += remainder[k];
-        remainder[k] = sigspace[signal_non_zero_size + k];
-        sigspace[signal_non_zero_size + k] = 0;
-      }
-      sigspace_ptr = 0;
-    }
-    cpx out_val = sigspace[sigspace_ptr];
-    sigspace[sigspace_ptr] = in_val;
-    sigspace_ptr++;
-    return out_val;
-  }
+struct HilbertFir : FastFir {
+  HilbertFir() { SetKernel(hilbert_taps(2048), -1); }
 };
 
 // FFTrWrapper<double>(32768) -> JFFT::fft_real on a 16384-point complex FFT
@@ -2996,7 +3299,7 @@ struct oracle_chan {
   std::unique_ptr<Msk> msk;
   std::unique_ptr<BurstOqpsk> bq;
   std::unique_ptr<BurstMsk> bm;
-  std::vector<uint8_t> blocks, frames, rt_tests, rt_packets;
+  std::vector<uint8_t> blocks, frames, rt_tests, rt_packets, c_units, voice;
   std::string items;
   AeroL &aerol() { return oq ? oq->aerol : (msk ? msk->aerol : (bq ? bq->aerol : bm->aerol)); }
   const std::vector<uint8_t> &soft() const {
@@ -3009,7 +3312,8 @@ struct oracle_chan {
 extern "C" {
 
 oracle_chan *oracle_create(int bitrate, int flags) {
-  if (bitrate != 10500 && bitrate != 600 && bitrate != 1200) return nullptr;
+  if (bitrate != 10500 && bitrate != 600 && bitrate != 1200 && bitrate != 8400) return nullptr;
+  if (bitrate == 8400 && (flags & ORACLE_BURST)) return nullptr;
   oracle_chan *c = new oracle_chan();
   const bool tp = (flags & ORACLE_TRACE_PT) != 0;
   if (flags & ORACLE_BURST) {
@@ -3022,10 +3326,12 @@ oracle_chan *oracle_create(int bitrate, int flags) {
     }
     c->aerol().rt.tests_out = &c->rt_tests;
     c->aerol().rt.packets_out = &c->rt_packets;
-  } else if (bitrate == 10500) {
-    c->oq.reset(new Oqpsk());
+  } else if (bitrate == 10500 || bitrate == 8400) {
+    c->oq.reset(new Oqpsk(bitrate));
     c->oq->trace_pt = tp;
     c->oq->dcd_tick = (flags & ORACLE_DCD_TICK) != 0;
+    c->oq->aerol.c_units_out = &c->c_units;
+    c->oq->aerol.voice_out = &c->voice;
   } else {
     c->msk.reset(new Msk(bitrate));
     c->msk->trace_pt = tp;
@@ -3060,6 +3366,8 @@ size_t oracle_softbits16(const oracle_chan *c, int16_t *dst, size_t cap) {
   return copy_out(c->bq ? c->bq->soft16 : (c->bm ? c->bm->soft16 : none), dst, cap);
 }
 size_t oracle_rt_tests(const oracle_chan *c, uint8_t *dst, size_t cap) { return copy_out(c->rt_tests, dst, cap); }
+size_t oracle_c_units(const oracle_chan *c, uint8_t *dst, size_t cap) { return copy_out(c->c_units, dst, cap); }
+size_t oracle_voice(const oracle_chan *c, uint8_t *dst, size_t cap) { return copy_out(c->voice, dst, cap); }
 size_t oracle_rt_packets(const oracle_chan *c, uint8_t *dst, size_t cap) { return copy_out(c->rt_packets, dst, cap); }
 size_t oracle_softbits(const oracle_chan *c, uint8_t *dst, size_t cap) {
   return copy_out(c->soft(), dst, cap);

@@ -30,6 +30,7 @@ typedef struct oracle_chan oracle_chan;
 #define ORACLE_DCD_TICK 4 /* continuous OQPSK: AeroL's 1 s DCD timer (aerol.cpp:900-902,
                              1043-1058) fires after every Fs input samples */
 
+/* bitrate 10500 / 8400 (continuous OQPSK P / C channel), 600 / 1200 (MSK) */
 oracle_chan *oracle_create(int bitrate, int flags);
 void oracle_destroy(oracle_chan *c);
 
@@ -48,6 +49,13 @@ size_t oracle_softbits16(const oracle_chan *c, int16_t *dst, size_t cap);
 size_t oracle_rt_tests(const oracle_chan *c, uint8_t *dst, size_t cap);
 /* burst: per decoded R/T packet: uint32 kind ('R'/'T'), uint32 length, infofield bytes */
 size_t oracle_rt_packets(const oracle_chan *c, uint8_t *dst, size_t cap);
+
+/* C channel (bitrate 8400, AeroL::DecodeC, decode/aerol.cpp:2145-2415): every
+ * CRC-valid Call_progress SU (Call_progress_Signal, 12 bytes each), and per
+ * decoded frame a uint32 AES (of the frame's last Call_progress, 0 for
+ * "000000") followed by the 300 voice bytes (Voicesignal). */
+size_t oracle_c_units(const oracle_chan *c, uint8_t *dst, size_t cap);
+size_t oracle_voice(const oracle_chan *c, uint8_t *dst, size_t cap);
 
 /* Per coarse-estimate hop, 6 doubles: sample index, freq_offset_est emitted,
  * mixer2 freq, mixer_center freq (after the slot ran), mse, signal flag. */

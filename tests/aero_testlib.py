@@ -82,6 +82,26 @@ def synth_msk(seconds=10.0, bitrate=600, seed=0xAE40, carrier=1800.0, ebn0=12.0,
     return pcm
 
 
+def synth_c(seconds=10.0, seed=0xAEC0, carrier=12000.0, ebn0=12.0, amplitude=0.25, phase0=0.3, lead_in=1000,
+            return_frames=False):
+    """int16 48 kHz PCM of an 8400-bps C channel (tools/aero_synth.cpp
+    aero_synth_c8400) + per frame the 36 transmitted SU bytes and 300 voice bytes."""
+    global _synth
+    if _synth is None:
+        _synth = ctypes.CDLL(SYNTH_SO)
+    _synth.aero_synth_c8400.restype = ctypes.c_size_t
+    n = int(48000 * seconds)
+    pcm = np.zeros(n, dtype=np.int16)
+    maxf = int(seconds * 2) + 8
+    frames = np.zeros(336 * maxf, dtype=np.uint8)
+    cfg = SynthCfg(48000.0, carrier, phase0, amplitude, ebn0, seed, 0.6, lead_in)
+    nf = _synth.aero_synth_c8400(ctypes.byref(cfg), pcm.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n),
+                                 frames.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(maxf))
+    if return_frames:
+        return pcm, frames[:336 * min(nf, maxf)].reshape(-1, 336)
+    return pcm
+
+
 def synth_burst(seconds=10.0, seed=0xAE50, carrier=12000.0, ebn0=14.0, amplitude=0.25, phase0=0.3, lead_in=24000,
                 return_packets=False):
     """int16 48 kHz PCM of 10500-bps burst OQPSK R/T packets (SURVEY.md §8(d)
@@ -170,7 +190,7 @@ class Oracle:
             L.oracle_twiddles.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
             L.oracle_fft.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
             L.oracle_msk_taps.argtypes = [ctypes.c_int, ctypes.c_void_p]
-            for f in ('oracle_softbits16', 'oracle_rt_tests', 'oracle_rt_packets'):
+            for f in ('oracle_softbits16', 'oracle_rt_tests', 'oracle_rt_packets', 'oracle_c_units', 'oracle_voice'):
                 getattr(L, f).restype = ctypes.c_size_t
                 getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
             L.oracle_events.restype = ctypes.c_size_t
@@ -224,6 +244,15 @@ class Oracle:
         """burst: [(kind 'R'/'T', infofield bytes)] of every decoded R/T packet"""
         raw = self._get(self.L.oracle_rt_packets, np.uint8)
         return parse_rt_packets(raw)
+
+    def c_units(self):
+        """C channel: every CRC-valid Call_progress SU (12 bytes each)"""
+        return self._get(self.L.oracle_c_units, np.uint8).reshape(-1, 12)
+
+    def voice(self):
+        """C channel: per frame (AES of its last Call_progress, 300 voice bytes)"""
+        raw = self._get(self.L.oracle_voice, np.uint8).reshape(-1, 304)
+        return [(int(np.frombuffer(r[:4].tobytes(), np.uint32)[0]), bytes(r[4:])) for r in raw]
 
     def hops(self):
         return self._get(self.L.oracle_hops, np.float64, 6)

@@ -42,6 +42,9 @@ size_t aero_synth_p10500(const aero_synth_cfg *cfg, int16_t *pcm, size_t nsample
 /* 600/1200-bps MSK P-channel (cfg->fs = 12000 / 24000); frames: 72 info bytes each */
 size_t aero_synth_msk(const aero_synth_cfg *cfg, int bitrate, int baud, int16_t *pcm, size_t nsamples,
                       uint8_t *frames, size_t frames_cap);
+/* 8400-bps C channel; frames: 36 SU bytes + 300 voice bytes each */
+size_t aero_synth_c8400(const aero_synth_cfg *cfg, int16_t *pcm, size_t nsamples, uint8_t *frames,
+                        size_t frames_cap);
 }
 
 namespace {
@@ -758,4 +761,164 @@ extern "C" size_t aero_synth_burst_msk(const aero_synth_cfg *cfg, int bitrate, i
     pcm[n] = (int16_t)v;
   }
   return used;
+}
+
+/* C channel (8400 bps OQPSK, AeroL::DecodeC, decode/aerol.cpp:2145-2415),
+ * inverting the receive chain:
+ *   three 12-byte SUs (CRC-16/X-25) at bits 109 y + 97 .. + 108 (y < 24) and
+ *   25 x 96 voice bits at 109 y + 1 .. + 96 of a 2714-bit payload, scrambled
+ *   from position 0 (reset at each UW, :2227)
+ *   -> 2730 encoder input bits per frame: the receiver's Decode_Continuous
+ *      window starts 6 bits before the frame's first bit and its 2708-bit
+ *      delay line (:994-999) then hands back payload bits 0..2707 from
+ *      positions 0..2707 of the previous frame and bits 2708..2713 from
+ *      positions 2724..2729 (positions 2708..2723 are dummy)
+ *   -> K=7 r=1/2 {109,79}, continuous; rate 3/4 by deleting every fourth
+ *      symbol (PuncturedCode::depunture_soft_block(.., 4), :2417-2432), 4095
+ *      symbols + 1 filler the receiver drops
+ *   -> 16 interleaver blocks of 4 x 64 (deinterleave_ba(block, 4))
+ *   -> frame: 52-bit preambles (0xC53D1C96ECD5 on Q, 0xAB376938BCA30 on I,
+ *      :920-928), then the 4096 data bits: 4200 bits = 0.5 s
+ *   -> OQPSK, RRC alpha = 0.6 (the receiver's prefilter, oqpskdemodulator.cpp:228-236).
+ * frames: per frame 36 SU bytes + 300 voice bytes. */
+namespace {
+double rrc_a(double x, double a) {
+  if (fabs(x) < 1e-12) return 1.0 - a + 4.0 * a / M_PI;
+  if (fabs(fabs(x) - 1.0 / (4.0 * a)) < 1e-9)
+    return a / sqrt(2.0) * ((1 + 2 / M_PI) * sin(M_PI / (4 * a)) + (1 - 2 / M_PI) * cos(M_PI / (4 * a)));
+  return (sin(M_PI * x * (1 - a)) + 4 * a * x * cos(M_PI * x * (1 + a))) / (M_PI * x * (1 - 16 * a * a * x * x));
+}
+
+struct CTx {
+  Tx tx;  // scrambler, interleaver permutation, encoder register, RNG
+  explicit CTx(const aero_synth_cfg &c) : tx(c) {}
+  std::vector<int> chan;
+  // builds chan[] (4200 bits) for the next frame; SU and voice bytes to *rec336
+  void next_frame(uint8_t *rec336) {
+    uint8_t su[36], voice[300];
+    for (int k = 0; k < 3; k++) {
+      uint8_t ten[10];
+      const double u = tx.rng.uniform();
+      const unsigned aes = tx.aes_pool[tx.rng.below(8)];
+      if (u < 0.4) {  // Call_progress (AEROTypeC, aerol.h:42-48): AES, GES
+        ten[0] = 0x30;
+        ten[1] = (uint8_t)(aes >> 16), ten[2] = (uint8_t)(aes >> 8), ten[3] = (uint8_t)aes;
+        ten[4] = (uint8_t)(0x80 + tx.rng.below(8));
+        for (int i = 5; i < 10; i++) ten[i] = (uint8_t)tx.rng.below(256);
+      } else if (u < 0.55) {  // Telephony_acknowledge
+        ten[0] = 0x60;
+        for (int i = 1; i < 10; i++) ten[i] = (uint8_t)tx.rng.below(256);
+      } else {  // fill-in
+        ten[0] = 0x01;
+        for (int i = 1; i < 10; i++) ten[i] = (uint8_t)tx.rng.below(256);
+      }
+      SU s = make_su(ten);
+      memcpy(su + 12 * k, s.b, 12);
+    }
+    for (int i = 0; i < 300; i++) voice[i] = (uint8_t)tx.rng.below(256);
+    if (rec336) {
+      memcpy(rec336, su, 36);
+      memcpy(rec336 + 36, voice, 300);
+    }
+    int pay[2714];
+    for (int q = 0; q < 2714; q++) pay[q] = tx.rng.below(2);
+    for (int b = 0; b < 288; b++) {  // LSB-first bytes
+      const int y = b / 12, h = y * 109 + 97 + b % 12;
+      pay[h] = (su[b / 8] >> (b % 8)) & 1;
+    }
+    for (int b = 0; b < 2400; b++) {
+      const int y = b / 96, h = y * 109 + 1 + b % 96;
+      pay[h] = (voice[b / 8] >> (b % 8)) & 1;
+    }
+    int ibits[2730];
+    for (int q = 0; q < 2708; q++) ibits[q] = pay[q] ^ tx.scr[q];
+    for (int q = 2708; q < 2724; q++) ibits[q] = tx.rng.below(2);
+    for (int r = 0; r < 6; r++) ibits[2724 + r] = pay[2708 + r] ^ tx.scr[2708 + r];
+    int coded[5460];
+    for (int t = 0; t < 2730; t++) {
+      tx.enc_reg = ((tx.enc_reg << 1) | (unsigned)ibits[t]) & 127;
+      coded[2 * t] = __builtin_popcount(tx.enc_reg & 109) & 1;
+      coded[2 * t + 1] = __builtin_popcount(tx.enc_reg & 79) & 1;
+    }
+    int deint[4096];
+    int d = 0;
+    for (int m = 0; m < 5460; m++)
+      if (m % 4 != 3) deint[d++] = coded[m];
+    deint[4095] = tx.rng.below(2);
+    chan.assign(4200, 0);
+    const uint64_t pq = 216866263330005ULL, pi = 3012071630031408ULL;
+    for (int k = 0; k < 52; k++) {
+      chan[2 * k] = (int)((pq >> (51 - k)) & 1);
+      chan[2 * k + 1] = (int)((pi >> (51 - k)) & 1);
+    }
+    for (int b = 0; b < 16; b++)
+      for (int j = 0; j < 4; j++)
+        for (int i = 0; i < 64; i++) chan[104 + b * 256 + tx.perm[i] * 4 + j] = deint[b * 256 + j * 64 + i];
+  }
+};
+}  // namespace
+
+extern "C" size_t aero_synth_c8400(const aero_synth_cfg *cfg, int16_t *pcm, size_t nsamples, uint8_t *frames,
+                                   size_t frames_cap) {
+  CTx ct(*cfg);
+  const double Fs = cfg->fs, Ts = Fs / 4200.0;  // samples per arm symbol
+  const int SPAN = 10, OS = 256;
+  std::vector<double> tab(2 * SPAN * OS + 2);
+  double energy = 0;
+  for (size_t i = 0; i < tab.size(); i++) tab[i] = rrc_a((double)i / OS - SPAN, 0.6);
+  for (int i = 0; i < 2 * SPAN * OS; i++) energy += tab[i] * tab[i];
+  energy /= OS;
+  auto pulse = [&](double x) {
+    double p = (x + SPAN) * OS;
+    if (p <= 0 || p >= 2 * SPAN * OS) return 0.0;
+    int ip = (int)p;
+    double f = p - ip;
+    return tab[ip] * (1 - f) + tab[ip + 1] * f;
+  };
+  std::vector<double> qs, is;
+  size_t nframes = 0;
+  auto ensure = [&](size_t k) {
+    while (qs.size() <= k) {
+      uint8_t *dst = (frames && nframes < frames_cap) ? frames + 336 * nframes : nullptr;
+      ct.next_frame(dst);
+      nframes++;
+      for (int b = 0; b < 4200; b += 2) {
+        qs.push_back(ct.chan[b] ? 1.0 : -1.0);
+        is.push_back(ct.chan[b + 1] ? 1.0 : -1.0);
+      }
+    }
+  };
+  const double A = cfg->amplitude;
+  const double P = A * A * (2.0 * energy) / 2.0;
+  double sigma = 0;
+  if (cfg->ebn0_db < 99) {
+    const double Eb = P / 8400.0;
+    const double N0 = Eb / pow(10.0, cfg->ebn0_db / 10.0);
+    sigma = sqrt(N0 / 2.0 * Fs);
+  }
+  Rng nrng(cfg->seed ^ 0xC8400C8400C84001ULL);
+  const double w = 2.0 * M_PI * cfg->carrier_hz / Fs;
+  for (size_t n = 0; n < nsamples; n++) {
+    double x = 0;
+    const long long nn = (long long)n - cfg->lead_in;
+    if (nn >= 0) {
+      const double t = (double)nn / Ts;
+      long long k0 = (long long)floor(t) - SPAN, k1 = (long long)floor(t) + SPAN + 1;
+      if (k0 < 0) k0 = 0;
+      ensure((size_t)k1 + 1);
+      double I = 0, Q = 0;
+      for (long long k = k0; k <= k1; k++) {
+        Q += qs[k] * pulse(t - (double)k);
+        I += is[k] * pulse(t - (double)k - 0.5);
+      }
+      const double ph = w * (double)nn + cfg->phase0;
+      x = A * (I * cos(ph) + Q * sin(ph));
+    }
+    if (sigma > 0) x += sigma * nrng.gauss();
+    double v = floor(x * 32768.0 + 0.5);
+    if (v > 32767) v = 32767;
+    if (v < -32768) v = -32768;
+    pcm[n] = (int16_t)v;
+  }
+  return nframes;
 }
