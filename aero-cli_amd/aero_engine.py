@@ -113,6 +113,10 @@ _SIGS = {
                                        ctypes.POINTER(ctypes.c_size_t)]),
     'aero_pop_rt_tests': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                          ctypes.POINTER(ctypes.c_size_t)]),
+    'aero_pop_c_units': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.POINTER(ctypes.c_size_t)]),
+    'aero_pop_voice': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                      ctypes.POINTER(ctypes.c_size_t)]),
     'aero_pop_rt_packets': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                            ctypes.POINTER(ctypes.c_size_t)]),
     'aero_timing': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
@@ -256,7 +260,7 @@ class Engine:
         self.close()
 
     # sample rate aero-decode feeds each bit rate (decode/decode.cpp:142-159)
-    RATE = {10500: 48000, 600: 12000, 1200: 24000}
+    RATE = {10500: 48000, 600: 12000, 1200: 24000, 8400: 48000}
 
     def open_channel(self, bitrate=10500, fs=None, disable_reassembly=False, burst=False):
         fs = fs or self.RATE.get(bitrate, 48000)
@@ -339,6 +343,15 @@ class Engine:
             out.append((chr(kind), bytes(raw[i + 8:i + 8 + int(ln)])))
             i += 8 + int(ln)
         return out
+
+    def c_units(self, ch):
+        """C channel: every CRC-valid Call_progress SU, [n, 12] bytes"""
+        return self._pop(self.lib.aero_pop_c_units, ch, np.uint8, 12)
+
+    def voice(self, ch):
+        """C channel: per frame (AES of its last Call_progress, 300 voice bytes)"""
+        raw = self._pop(self.lib.aero_pop_voice, ch, np.uint8, 304)
+        return [(int(np.frombuffer(r[:4].tobytes(), np.uint32)[0]), bytes(r[4:])) for r in raw]
 
     def hops(self, ch):
         return self._pop(self.lib.aero_pop_hops, ch, np.float64, 6)

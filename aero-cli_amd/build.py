@@ -30,7 +30,7 @@ HIP_FLAGS = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH] + FP
 CXX_FLAGS = ['-O2', '-std=c++17', '-fPIC', '-Wall'] + FP
 
 HIP_SRCS = ['demod_oqpsk.hip', 'demod_msk.hip', 'coarse.hip', 'aerol.hip', 'engine.hip', 'chan.hip', 'burst.hip', 'burst_msk.hip',
-            'burst_engine.hip']
+            'burst_engine.hip', 'cchan.hip']
 CXX_SRCS = ['tables_host.cpp', 'acars_host.cpp']
 # Per-file codegen: the burst demodulators' loops hold their state in
 # registers; LLVM's machine LICM hoists every FP64 constant of the inlined

@@ -543,8 +543,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void vi
   }  // pair loop
 }
 
+void launch_frame_c(hipStream_t st, const DevState &S, int nch);                             // cchan.hip
+void launch_viterbi_c(hipStream_t st, const DevState &S, const DevTables &T, int max_jobs);  // cchan.hip
+
 void launch_frame(hipStream_t st, int mode, const DevState &S, int nch) {
   const dim3 g((nch + 255) / 256), b(256);
+  if (mode == MODE_C8400) return launch_frame_c(st, S, nch);
   // MSK framing depends on the AeroL bit rate only
   if (mode == MODE_OQPSK)
     hipLaunchKernelGGL(frame_kernel, g, b, 0, st, S, nch);
@@ -558,6 +562,7 @@ void launch_frame(hipStream_t st, int mode, const DevState &S, int nch) {
 // on the device); the grid is capped, blocks stride over the jobs
 void launch_viterbi(hipStream_t st, int mode, const DevState &S, const DevTables &T, int max_jobs, int trace) {
   if (max_jobs <= 0) return;
+  if (mode == MODE_C8400) return launch_viterbi_c(st, S, T, max_jobs);
   max_jobs = (max_jobs + 1) / 2;  // one block per pair of jobs
   max_jobs = max_jobs < 16384 ? max_jobs : 16384;
   if (mode == MODE_OQPSK)

@@ -1,0 +1,750 @@
+/*
+ * cchan.hip — the C channel: 8400-bps OQPSK (OqpskDemodulator at fb = 8400)
+ * and AeroL::DecodeC on gfx950.
+ *
+ *  prefilter_c_kernel : the per-message prefilter of OqpskDemodulator::writeData
+ *                       (decode/oqpskdemodulator.cpp:292-324): down-mix by
+ *                       mixer_fir_pre, JFastFir (RRC 0.6, 2049 taps, 4096-point
+ *                       overlap-add blocks of 2048, decode/jfft.cpp:324-367,
+ *                       445-495), up-mix by the conjugate from the phase saved
+ *                       at the message start.  One workgroup per channel with a
+ *                       message due; the two phase-pointer recurrences run on
+ *                       one lane each, the FFTs (JFFT's radix-2 DIT, bit for bit)
+ *                       over the LDS.
+ *  demod_c_kernel     : the per-sample loop at fb = 8400 (:331-553): no RRC FIR
+ *                       (the prefilter is the matched filter), its own timer
+ *                       delays / resonator / ee, the carrier loop with faster
+ *                       phase agility (:463-472), mixer2's frequency summed over
+ *                       the message and mixer_fir_pre retuned to the mean at
+ *                       its end (:555-557).  One lane per channel.
+ *  frame_c_kernel     : AeroL::DecodeC's framing (decode/aerol.cpp:2145-2240):
+ *                       the two dual-preamble detectors (52 bits, tolerance 6,
+ *                       :782-877) on alternating soft bits, 16 blocks of 4 x 64
+ *                       deinterleaved (deinterleave_ba(block, 4), :594-613) and
+ *                       depunctured (PuncturedCode, :2417-2432) as they fill.
+ *  viterbi_c_kernel   : Decode_Continuous of a 5460-symbol frame
+ *                       (jconvolutionalcodec.cpp:146-198; the soft Viterbi of
+ *                       viterbi_dev.h), the 2714-bit payload through dl2 and
+ *                       the scrambler, the three 12-byte SUs and their CRCs and
+ *                       the 300 voice bytes (:2249-2392) into the job record.
+ *
+ * Bit-exactness rules as in demod_oqpsk.hip: -ffp-contract=off, the
+ * reference's operation order, GCC complex products, aero_math.h for libm;
+ * plain IEEE divisions here (this path is not the headline's).
+ */
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+#include "aero_math.h"
+#include "engine_common.h"
+#include "viterbi_dev.h"
+
+namespace aero {
+
+struct CPreJob {  // one message of one channel: samples [s, e)
+  int c, pad;
+  long long s, e;
+};
+
+namespace {
+
+__constant__ DelayDesc cc_dly[4];  // delays(1), delayt41(T/4), delayt42(T/4), delayt8(T/8), T = 48000 / 4200
+
+__device__ __forceinline__ int c_cis_index(double WTptr) {  // WaveTable::WTCISValue (DSP.cpp:81-88)
+  int tint = (int)WTptr;
+  if (tint >= WTSIZE) tint = 0;
+  if (tint < 0) tint = WTSIZE - 1;
+  return tint;
+}
+__device__ __forceinline__ void c_nco_next(double &ptr, double &step) {  // WTnextFrame (DSP.cpp:71-79)
+  if (step < 0) step = 0;
+  ptr += step;
+  while (((int)ptr) >= WTSIZE) ptr -= WTSIZE;
+}
+__device__ __forceinline__ void c_set_freq(double &freq, double &step, double f) {  // SetFreq(double) (DSP.cpp:163-168)
+  freq = f;
+  if (freq < 0) freq = 0;
+  step = (freq) * ((double)WTSIZE) / 48000.0;
+}
+// Delay<double>::update (DSP.h:365-384) as a shift register (h[0] newest)
+// whose weights depend on the write pointer p (T/8 at 8400 bps does)
+template <int N, int AGE_OLD, int AGE_NEW>
+__device__ __forceinline__ double c_delay(double (&h)[N], int &p, const DelayDesc &d, double sig) {
+#pragma unroll
+  for (int i = N - 1; i > 0; --i) h[i] = h[i - 1];
+  h[0] = sig;
+  const double w = d.w[p], omw = d.omw[p];
+  p = p + 1 == d.size ? 0 : p + 1;
+  return (w * h[AGE_NEW] + omw * h[AGE_OLD]);
+}
+__device__ __forceinline__ double c_iir3(double &x1, double &x2, double &y1, double &y2, const double (&b)[3],
+                                         const double (&a)[3], double sig) {  // IIR::update (DSP.cpp:635-685)
+  double y = 0;
+  y += x2 * b[2];
+  y += x1 * b[1];
+  y += sig * b[0];
+  y -= y2 * a[2];
+  y -= y1 * a[1];
+  x2 = x1;
+  x1 = sig;
+  y2 = y1;
+  y1 = y;
+  return y;
+}
+__device__ __forceinline__ int c_qround(double d) {  // qRound (Qt 5.9 qglobal.h:525)
+  return d >= 0.0 ? int(d + 0.5) : int(d - double(int(d - 1)) + 0.5) + int(d - 1);
+}
+
+// JFFT::fft (decode/jfft.cpp:114-212) of 4096 points in the LDS, 256 threads:
+// the bit-reversal swaps, then every radix-2 stage with the reference's
+// operands and twiddle TW[n - 1 + j]; the inverse scales by 1/N
+__device__ void c_jfft(double2 *x, const double2 *TW, bool inverse, int t) {
+  constexpr int N = C_FIR_N, NT = 256;
+  for (int i = t; i < N; i += NT) {
+    const int j = (int)(__builtin_bitreverse32((uint32_t)i) >> (32 - 12));
+    if (j > i) {
+      const double2 a = x[i];
+      x[i] = x[j];
+      x[j] = a;
+    }
+  }
+  __syncthreads();
+  for (int n = 1; n < N; n <<= 1) {
+    for (int b = t; b < N / 2; b += NT) {
+      const int j = b & (n - 1);
+      const int k = 2 * (b - j) + j, l = k + n;
+      const double2 w = TW[n - 1 + j], xl = x[l], xk = x[k];
+      const double yr = w.x * xl.x - w.y * xl.y, yi = w.x * xl.y + w.y * xl.x;
+      x[l] = make_double2(xk.x - yr, xk.y - yi);
+      x[k] = make_double2(xk.x + yr, xk.y + yi);
+    }
+    __syncthreads();
+  }
+  if (inverse) {
+    for (int i = t; i < N; i += NT) {
+      x[i].x *= (1.0 / ((double)N));
+      x[i].y *= (1.0 / ((double)N));
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void prefilter_c_kernel(DevState S, DevTables T, const CPreJob *jobs) {
+  __shared__ double2 buf[C_FIR_N];  // the FFT block; [0, C_FIR_SNZ) is sigspace between FFTs
+  __shared__ uint16_t idn[C_FIR_SNZ], iup[C_FIR_SNZ];
+  __shared__ double fin_ptr;
+  const CPreJob J = jobs[blockIdx.x];
+  const int c = J.c, t = threadIdx.x, C = S.C;
+  const long long capm = S.pcm_cap - 1;
+  double2 *sig = S.csig + (size_t)c * C_FIR_SNZ;
+  double2 *rem = S.crem + (size_t)c * (C_FIR_N - C_FIR_SNZ);
+  for (int r = t; r < C_FIR_SNZ; r += 256) buf[r] = sig[r];
+  double fp_step = S.ds[DS_FP_STEP * C + c];
+  double dn_ptr = 0, up_ptr = 0;
+  if (t == 0) dn_ptr = S.ds[DS_FP_PTR * C + c];
+  if (t == 64) {  // savedphase = GetPhaseDeg() (DSP.cpp:200), SetPhaseDeg(savedphase) (:177-187)
+    const double ptr0 = S.ds[DS_FP_PTR * C + c];
+    double ph = (360.0 * ptr0 / ((double)WTSIZE));
+    ph = fmod(ph, 360.0);
+    while (ph < 0) ph += 360.0;
+    up_ptr = (ph / 360.0) * ((double)WTSIZE);
+  }
+  __syncthreads();
+  for (long long pos = J.s; pos < J.e;) {
+    if (pos > 0 && pos % C_FIR_SNZ == 0) {  // sigspace full: JFastFir's convolution before this sample
+      for (int r = C_FIR_SNZ + t; r < C_FIR_N; r += 256) buf[r] = make_double2(0.0, 0.0);
+      __syncthreads();
+      c_jfft(buf, T.tw4, false, t);
+      for (int k = t; k < C_FIR_N; k += 256) {  // *psigspace *= *pkernel
+        const double2 a = buf[k], kk = T.cker[k];
+        buf[k] = make_double2(a.x * kk.x - a.y * kk.y, a.x * kk.y + a.y * kk.x);
+      }
+      __syncthreads();
+      c_jfft(buf, T.twi4, true, t);
+      for (int k = t; k < C_FIR_N - C_FIR_SNZ; k += 256) {  // overlap
+        const double2 r = rem[k];
+        buf[k] = make_double2(buf[k].x + r.x, buf[k].y + r.y);
+        rem[k] = buf[C_FIR_SNZ + k];
+      }
+      __syncthreads();
+    }
+    const long long cend = J.e < (pos / C_FIR_SNZ + 1) * C_FIR_SNZ ? J.e : (pos / C_FIR_SNZ + 1) * C_FIR_SNZ;
+    const int m = (int)(cend - pos), r0 = (int)(pos % C_FIR_SNZ);
+    // the down- and up-mix phase pointers, each a serial recurrence, on lanes of two waves
+    if (t == 0)
+      for (int k = 0; k < m; ++k) {
+        idn[k] = (uint16_t)c_cis_index(dn_ptr);
+        c_nco_next(dn_ptr, fp_step);
+      }
+    if (t == 64)
+      for (int k = 0; k < m; ++k) {
+        iup[k] = (uint16_t)c_cis_index(up_ptr);
+        c_nco_next(up_ptr, fp_step);
+      }
+    __syncthreads();
+    for (int k = t; k < m; k += 256) {
+      const long long n = pos + k;
+      const double dval = ((double)S.pcm[(size_t)(n & capm) * C + c]) / 32768.0;
+      const double2 cs = T.cis[idn[k]];
+      const double2 o = buf[r0 + k];  // JFastFir::update: pop the processed value, push the new one
+      buf[r0 + k] = make_double2(cs.x * dval, cs.y * dval);
+      const double2 cu = T.cis[iup[k]];
+      const double cr = cu.x, ci = -cu.y;  // *= WTCISValue_conj()
+      S.cpre[(size_t)(n & (C_PRE_RING - 1)) * C + c] = make_double2(o.x * cr - o.y * ci, o.x * ci + o.y * cr);
+    }
+    __syncthreads();
+    pos = cend;
+  }
+  for (int r = t; r < C_FIR_SNZ; r += 256) sig[r] = buf[r];
+  if (t == 64) fin_ptr = up_ptr;
+  __syncthreads();
+  if (t == 0) {
+    S.ds[DS_FP_PTR * C + c] = fin_ptr;  // after the up-mix
+    S.ls[LS_PRE_END * C + c] = J.e;
+    S.ls[LS_MSG_START * C + c] = J.s;
+  }
+}
+
+// OqpskDemodulator::writeData at fb = 8400 (decode/oqpskdemodulator.cpp:331-557)
+template <bool TRACE>
+__global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, int nch) {
+  __shared__ double cij[241][7];
+  __shared__ double sct[440];
+  for (int q = threadIdx.x; q < 241 * 7; q += 64) (&cij[0][0])[q] = (&aero_g_cij[0][0])[q];
+  for (int q = threadIdx.x; q < 440; q += 64) sct[q] = aero_g_sincostab[q];
+  __syncthreads();
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= nch) return;
+  const int C = S.C;
+  const long long n0 = S.ls[LS_NSAMP * C + c];
+  const long long avail = S.ls[LS_AVAIL * C + c];
+  const long long filled0 = S.ls[LS_FILLED * C + c];
+  const long long pre_end = S.ls[LS_PRE_END * C + c];
+  const int hops_done = S.is[IS_HOPS_DONE * C + c];
+  const long long boundary = (long long)HOP * (hops_done + 1) - 1;
+  const long long end = pre_end < boundary ? pre_end : boundary;
+  const int capm = (int)S.pcm_cap - 1;
+  const int ia = (int)(avail - n0);
+  const int ie = (int)(end - n0);
+  int ifl = (int)(filled0 - n0);
+  double mc_ptr = S.ds[DS_MC_PTR * C + c], mc_step = S.ds[DS_MC_STEP * C + c];
+  if (ifl == 0 && ia > 0) {  // coarse-ring entry of sample n0 (:351-356)
+    const int16_t x = S.pcm[(size_t)(n0 & capm) * C + c];
+    S.cring[(size_t)c * NFFT + (n0 & (NFFT - 1))] = (uint32_t)c_cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
+    ifl = 1;
+  }
+  if (ie <= 0) {
+    S.ls[LS_FILLED * C + c] = n0 + ifl;
+    return;
+  }
+  // the symbol-timer resonator at 8400 bps, the second ("10Hz bw") design (:196-214)
+  const double sr_b[3] = {0.0012845857864470789, 0, -0.0012845857864470789};
+  const double sr_a[3] = {1, -0.90681461999279889, 0.99743082842710584};
+  const double ct_b[3] = {0.0010275610653672064, 0.0020551221307344128, 0.0010275610653672064};
+  const double ct_a[3] = {1, -1.9207386815577139, 0.92509247310306331};
+  const double SO_F = 8400.0;
+  double m2_ptr = S.ds[DS_M2_PTR * C + c], m2_step = S.ds[DS_M2_STEP * C + c], m2_freq = S.ds[DS_M2_FREQ * C + c];
+  double so_ptr = S.ds[DS_SO_PTR * C + c], so_last = S.ds[DS_SO_LAST * C + c];
+  double so_step = S.ds[DS_SO_STEP * C + c], so_freq = S.ds[DS_SO_FREQ * C + c];
+  double agc_sum = S.ds[DS_AGC_SUM * C + c], m2_fsum = S.ds[DS_M2_FSUM * C + c];
+  double d1[2], d41[4], d42[4], d8[3];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) d1[q] = S.ds[(DS_D1_0 + q) * C + c];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) d41[q] = S.ds[(DS_D41_0 + q) * C + c];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) d42[q] = S.ds[(DS_D42_0 + q) * C + c];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) d8[q] = S.ds[(DS_D8_0 + q) * C + c];
+  int p1 = S.is[IS_D1_P * C + c], p41 = S.is[IS_D41_P * C + c], p42 = S.is[IS_D42_P * C + c],
+      p8 = S.is[IS_D8_P * C + c];
+  double srx1 = S.ds[DS_SR_X1 * C + c], srx2 = S.ds[DS_SR_X2 * C + c];
+  double sry1 = S.ds[DS_SR_Y1 * C + c], sry2 = S.ds[DS_SR_Y2 * C + c];
+  double s2l_re = S.ds[DS_S2L_RE * C + c], s2l_im = S.ds[DS_S2L_IM * C + c];
+  double ctx1 = S.ds[DS_CT_X1 * C + c], ctx2 = S.ds[DS_CT_X2 * C + c];
+  double cty1 = S.ds[DS_CT_Y1 * C + c], cty2 = S.ds[DS_CT_Y2 * C + c];
+  double marg_sum = S.ds[DS_MARG_SUM * C + c], pm_sum = S.ds[DS_PM_SUM * C + c];
+  double ms_sum = S.ds[DS_MS_SUM * C + c], mse = S.ds[DS_MSE * C + c];
+  double ptd_re = S.ds[DS_PTD_RE * C + c], ptd_im = S.ds[DS_PTD_IM * C + c];
+  int agc_ptr = S.is[IS_AGC_PTR * C + c];
+  int yui = S.is[IS_YUI * C + c], s2l_init = S.is[IS_S2L_INIT * C + c];
+  int marg_p = S.is[IS_MARG_P * C + c], dt_p = S.is[IS_DT_P * C + c];
+  int pm_p = S.is[IS_PM_P * C + c], ms_p = S.is[IS_MS_P * C + c];
+  long long softp = S.ls[LS_SOFT_P * C + c];
+  long long ptn = TRACE ? S.ls[LS_PT_N * C + c] : 0;
+  double *marg = S.marg + (size_t)c * MARG_LEN;
+  double2 *dtb = S.dt + (size_t)c * DT_LEN;
+  double2 *pmsb = reinterpret_cast<double2 *>(S.pm) + (size_t)c * MSE_LEN;
+  uint8_t *soft = S.soft + (size_t)c * SOFT_RING;
+  const double PT = 0.65 * WTSIZE;  // IfHavePassedPoint(ee), ee = 0.65 at 8400 (:213)
+  int i = 0;
+  for (; i < ie; ++i) {
+    const long long n = n0 + i;
+    const double2 pre = S.cpre[(size_t)(n & (C_PRE_RING - 1)) * C + c];
+    const double2 cm = T.cis[c_cis_index(m2_ptr)];
+    // mix only: sig2 = mixer2.WTCISValue() * cval_prefiltered[i] (:376-385)
+    double s2r = cm.x * pre.x - cm.y * pre.y, s2i = cm.x * pre.y + cm.y * pre.x;
+    m2_fsum += m2_freq;
+    const double dab = sqrt(s2r * s2r + s2i * s2i);
+    {  // AGC (DSP.cpp:371-380)
+      const double agc_old = S.agc[(size_t)agc_ptr * C + c];
+      agc_sum = agc_sum - agc_old;
+      agc_sum = agc_sum + fabs(dab);
+      S.agc[(size_t)agc_ptr * C + c] = fabs(dab);
+      agc_ptr++;
+      if (agc_ptr == AGC_LEN) agc_ptr = 0;
+      double g = 1.414213562 / fmax(agc_sum / ((double)AGC_LEN), 0.000001);
+      g = fmax(g, 0.000001);
+      s2r *= g;
+      s2i *= g;
+    }
+    const double ab = aero_hypot_w(s2r, s2i);  // clipping (:408-410)
+    if (ab > 2.84) {
+      const double kk = 2.84 / ab;
+      s2r = kk * s2r;
+      s2i = kk * s2i;
+    }
+    // symbol timer (:413-426)
+    const double st_diff = c_delay<2, 1, 0>(d1, p1, cc_dly[0], ab * ab) - (ab * ab);
+    const double st_d1out = c_delay<4, 3, 2>(d41, p41, cc_dly[1], st_diff);
+    const double st_d2out = c_delay<4, 3, 2>(d42, p42, cc_dly[2], st_d1out);
+    double st_eta = (st_d2out - st_diff) * st_d1out;
+    st_eta = c_iir3(srx1, srx2, sry1, sry2, sr_b, sr_a, st_eta);
+    const double m1r = st_eta, m1i = -c_delay<3, 2, 1>(d8, p8, cc_dly[3], st_eta);
+    const double2 so = T.cis[c_cis_index(so_ptr)];
+    const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
+    const double st_angle_error = aero_atan2_bf(oim, ore, cij);
+    c_set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
+    so_ptr += (-st_angle_error * 0.01 / 360.0) * WTSIZE;
+    while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
+    while (so_ptr < 0) so_ptr += WTSIZE;
+    if (so_freq < (SO_F - 0.1)) c_set_freq(so_freq, so_step, (SO_F - 0.1));
+    if (so_freq > (SO_F + 0.1)) c_set_freq(so_freq, so_step, (SO_F + 0.1));
+    if (!s2l_init) {
+      s2l_re = s2r;
+      s2l_im = s2i;
+      s2l_init = 1;
+    }
+    bool pend = false;
+    double ev_pr = 0.0, ev_pi = 0.0;
+    {  // sample instant (:430) IfHavePassedPoint (DSP.cpp:222-238)
+      double tl = so_last - PT, tw = so_ptr - PT;
+      if (tl < 0.0) tl += WTSIZE;
+      if (tw < 0.0) tw += WTSIZE;
+      if ((tl > 3.0 * WTSIZE / 4.0) && (tw < 1.0 * WTSIZE / 4.0)) {
+        const double pt_last = tw / so_step;
+        const double pt_this = 1.0 - pt_last;
+        const double pr = pt_this * s2r + pt_last * s2l_re;
+        const double pi = pt_this * s2i + pt_last * s2l_im;
+        yui++;
+        yui %= 2;
+        if (!yui) {
+          ptd_re = pr;
+          ptd_im = pi;
+        } else {
+          ev_pr = pr;
+          ev_pi = pi;
+          pend = true;
+        }
+      }
+    }
+    s2l_re = s2r;
+    s2l_im = s2i;
+    if (pend) {  // carrier step (:447-541)
+      const int dt_rp = (dt_p + 1) % DT_LEN;
+      const double marg_old = marg[marg_p];
+      const double2 dv = dtb[dt_rp];
+      const double2 pms_old = pmsb[pm_p];
+      const double pr = ev_pr, pi = ev_pi;
+      double qr = pr, qi = ptd_im;  // pt_qpsk
+      const double ct_xt = aero_tanh(pi) * pr;
+      const double ct_xt_d = aero_tanh(ptd_re) * ptd_im;
+      double ct_ec = ct_xt_d - ct_xt;
+      if (ct_ec > M_PI) ct_ec = M_PI;
+      if (ct_ec < -M_PI) ct_ec = -M_PI;
+      {  // 8400: mixer2.IncresePhaseDeg(1.0 * ct_ec) unfiltered (DSP.cpp:177-187)
+        double phase_deg = 1.0 * ct_ec;
+        phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
+        phase_deg = fmod(phase_deg, 360.0);
+        while (phase_deg < 0) phase_deg += 360.0;
+        m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+      }
+      // mixer2.IncreseFreqHz(0.5 * 0.01 * ct_iir_loopfilter.update(ct_ec)) (:470)
+      c_set_freq(m2_freq, m2_step, 0.5 * 0.01 * c_iir3(ctx1, ctx2, cty1, cty2, ct_b, ct_a, ct_ec) + m2_freq);
+      marg_sum = marg_sum - marg_old;  // marg->UpdateSigned (DSP.cpp:419-427)
+      marg_sum = marg_sum + (ct_ec);
+      marg[marg_p] = ct_ec;
+      marg_p++;
+      marg_p %= MARG_LEN;
+      const double mval = marg_sum / ((double)MARG_LEN);
+      dtb[dt_p] = make_double2(qr, qi);  // dt.update (DSP.h:456-461)
+      dt_p = dt_rp;
+      qr = dv.x;
+      qi = dv.y;
+      double rs, rc;
+      aero_sincos_t(mval, rs, rc, sct);
+      const double rr = qr * rc - qi * rs, ri = qr * rs + qi * rc;
+      qr = rr;
+      qi = ri;
+      if (TRACE) {
+        if (ptn < S.pt_cap) S.pt[(size_t)c * S.pt_cap + ptn] = make_double2(qr, qi);
+        ptn++;
+      }
+      {  // MSEcalc::Update (DSP.cpp:449-461)
+        const double av = aero_hypot_w(qr, qi);
+        pm_sum = pm_sum - pms_old.x;
+        pm_sum = pm_sum + fabs(av);
+        const int slot = pm_p;
+        pm_p++;
+        pm_p %= MSE_LEN;
+        double mu = pm_sum / ((double)MSE_LEN);
+        if (mu < 0.000001) mu = 0.000001;
+        const double tr = (1.4142135623730951 * qr) / mu, ti = (1.4142135623730951 * qi) / mu;
+        const double tda = (fabs(tr) - 1.0), tdb = (fabs(ti) - 1.0);
+        const double v = (tda * tda) + (tdb * tdb);
+        ms_sum = ms_sum - pms_old.y;
+        ms_sum = ms_sum + fabs(v);
+        pmsb[slot] = make_double2(fabs(av), fabs(v));
+        ms_p++;
+        ms_p %= MSE_LEN;
+        mse = ms_sum / ((double)MSE_LEN);
+      }
+      if (mse < 0.65) {  // soft bits, imag first (:516-530)
+        int ibit = c_qround(0.75 * qi * 127.0 + 128.0);
+        if (ibit > 255) ibit = 255;
+        if (ibit < 0) ibit = 0;
+        int rbit = c_qround(0.75 * qr * 127.0 + 128.0);
+        if (rbit > 255) rbit = 255;
+        if (rbit < 0) rbit = 0;
+        soft[softp & (SOFT_RING - 1)] = (uint8_t)ibit;
+        soft[(softp + 1) & (SOFT_RING - 1)] = (uint8_t)rbit;
+        softp += 2;
+      }
+    }
+    c_nco_next(m2_ptr, m2_step);
+    c_nco_next(mc_ptr, mc_step);
+    so_last = so_ptr;
+    c_nco_next(so_ptr, so_step);
+    if (i + 1 < ia) {  // coarse-ring entry of the next sample (:351-356)
+      const long long n1 = n + 1;
+      const int16_t x = S.pcm[(size_t)(n1 & capm) * C + c];
+      S.cring[(size_t)c * NFFT + (n1 & (NFFT - 1))] = (uint32_t)c_cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
+      ifl = i + 2;
+    }
+  }
+  double *ds = S.ds + c;
+  int *is = S.is + c;
+  long long *ls = S.ls + c;
+  if (n0 + i == pre_end) {  // end of the message: mixer_fir_pre.SetFreq(mixer2_freq_sum / i) (:555-557)
+    double f = m2_fsum / ((double)(pre_end - ls[LS_MSG_START * C]));
+    double st = 0;
+    c_set_freq(f, st, f);
+    ds[DS_FP_FREQ * C] = f;
+    ds[DS_FP_STEP * C] = st;
+    m2_fsum = 0;
+  }
+  ls[LS_NSAMP * C] = n0 + i;
+  ls[LS_FILLED * C] = n0 + ifl;
+  ls[LS_SOFT_P * C] = softp;
+  if (TRACE) ls[LS_PT_N * C] = ptn;
+  ds[DS_M2_FSUM * C] = m2_fsum;
+  ds[DS_CT_X1 * C] = ctx1;
+  ds[DS_CT_X2 * C] = ctx2;
+  ds[DS_CT_Y1 * C] = cty1;
+  ds[DS_CT_Y2 * C] = cty2;
+  ds[DS_MARG_SUM * C] = marg_sum;
+  ds[DS_PM_SUM * C] = pm_sum;
+  ds[DS_MS_SUM * C] = ms_sum;
+  ds[DS_MSE * C] = mse;
+  ds[DS_PTD_RE * C] = ptd_re;
+  ds[DS_PTD_IM * C] = ptd_im;
+  ds[DS_M2_FREQ * C] = m2_freq;
+  ds[DS_M2_PTR * C] = m2_ptr;
+  ds[DS_M2_STEP * C] = m2_step;
+  ds[DS_MC_PTR * C] = mc_ptr;
+  ds[DS_MC_STEP * C] = mc_step;
+  ds[DS_SO_PTR * C] = so_ptr;
+  ds[DS_SO_LAST * C] = so_last;
+  ds[DS_SO_STEP * C] = so_step;
+  ds[DS_SO_FREQ * C] = so_freq;
+  ds[DS_AGC_SUM * C] = agc_sum;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) ds[(DS_D1_0 + q) * C] = d1[q];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) ds[(DS_D41_0 + q) * C] = d41[q];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) ds[(DS_D42_0 + q) * C] = d42[q];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) ds[(DS_D8_0 + q) * C] = d8[q];
+  ds[DS_SR_X1 * C] = srx1;
+  ds[DS_SR_X2 * C] = srx2;
+  ds[DS_SR_Y1 * C] = sry1;
+  ds[DS_SR_Y2 * C] = sry2;
+  ds[DS_S2L_RE * C] = s2l_re;
+  ds[DS_S2L_IM * C] = s2l_im;
+  is[IS_AGC_PTR * C] = agc_ptr;
+  is[IS_YUI * C] = yui;
+  is[IS_S2L_INIT * C] = s2l_init;
+  is[IS_MARG_P * C] = marg_p;
+  is[IS_DT_P * C] = dt_p;
+  is[IS_PM_P * C] = pm_p;
+  is[IS_MS_P * C] = ms_p;
+  is[IS_D1_P * C] = p1;
+  is[IS_D41_P * C] = p41;
+  is[IS_D42_P * C] = p42;
+  is[IS_D8_P * C] = p8;
+}
+
+namespace {
+// OQPSKPreambleDetectorAndAmbiguityCorrection::Update (decode/aerol.cpp:842-877)
+// on 52-bit shift registers (newest bit lowest): preamble 1, and only if it
+// does not match, preamble 2's buffer shifts and is checked
+constexpr uint64_t C_PRE1 = 216866263330005ULL, C_PRE2 = 3012071630031408ULL;
+constexpr uint64_t C_M52 = (1ULL << 52) - 1;
+__device__ __forceinline__ int c_detect(uint64_t &r1, uint64_t &r2, int &inv, int bit) {
+  const int tol = 6;  // AeroL::setSettings, continuous (aerol.cpp:972-973)
+  r1 = ((r1 << 1) | (uint64_t)bit) & C_M52;
+  int x = __builtin_popcountll(r1 ^ C_PRE1);
+  if (x >= 52 - tol) {
+    inv = 1;
+    return 1;
+  }
+  if (x <= tol) {
+    inv = 0;
+    return 1;
+  }
+  r2 = ((r2 << 1) | (uint64_t)bit) & C_M52;
+  x = __builtin_popcountll(r2 ^ C_PRE2);
+  if (x >= 52 - tol) {
+    inv = 1;
+    return 1;
+  }
+  if (x <= tol) {
+    inv = 0;
+    return 1;
+  }
+  return 0;
+}
+}  // namespace
+
+// AeroL::DecodeC's framing (decode/aerol.cpp:2145-2240); every completed
+// frame becomes a Viterbi job over its depunctured block
+__global__ __launch_bounds__(256) void frame_c_kernel(DevState S, int nch) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nch) return;
+  const int C = S.C;
+  int *is = S.is;
+  long long *ls = S.ls;
+  const long long P = ls[LS_SOFT_P * C + c];
+  long long q = ls[LS_SOFT_C * C + c];
+  const long long E = P & ~31LL;  // delivered in groups of 32 (oqpskdemodulator.cpp:534-540)
+  if (q >= E) return;
+  int realimag = is[IS_RI * C + c], cntr = is[IS_CNTR * C + c], gsl = is[IS_GSL * C + c];
+  int inv_r = is[IS_UWR_INV * C + c], inv_i = is[IS_UWI_INV * C + c];
+  int index = is[IS_C_INDEX * C + c];
+  int blkbuf = is[IS_BLKBUF * C + c], has_ov = is[IS_HAS_OVERLAP * C + c];
+  uint64_t r1 = (uint64_t)ls[LS_C_R1 * C + c], r2 = (uint64_t)ls[LS_C_R2 * C + c];
+  uint64_t i1 = (uint64_t)ls[LS_C_I1 * C + c], i2 = (uint64_t)ls[LS_C_I2 * C + c];
+  const uint8_t *soft = S.soft + (size_t)c * SOFT_RING;
+  for (; q < E; ++q) {
+    const int sv = soft[q & (SOFT_RING - 1)];
+    int bit = sv >= 128 ? 1 : 0;
+    int soft_bit = sv;
+    int gotsync = 0;
+    realimag++;
+    realimag %= 2;
+    if (cntr > C_FRAME - 112 || cntr <= 0) {
+      gotsync = realimag ? c_detect(r1, r2, inv_r, bit) : c_detect(i1, i2, inv_i, bit);
+      if (!gsl) {
+        gsl = gotsync;
+        gotsync = 0;
+      } else
+        gsl = 0;
+    } else {
+      gotsync = 0;
+      gsl = 0;
+    }
+    if (realimag ? inv_r : inv_i) {
+      bit = 1 - bit;
+      if (soft_bit != 128) soft_bit = 255 - soft_bit;
+    }
+    if (gotsync) {  // a new frame; deleaved / depunctured blocks cleared, scrambler reset
+      cntr = -1;
+      index = -1;
+      continue;
+    }
+    if (cntr < 1000000000) cntr++;
+    if (cntr <= C_FRAME - 1) {
+      index++;
+      // block kb of the frame, entry index = perm[i] * 4 + j -> deinterleaved
+      // d = kb 256 + j 64 + i (perm[i] = 27 i mod 64, so i = 19 row mod 64),
+      // depunctured d + d / 3; the frame's last value (d = 4095) is dropped
+      const int kb = cntr >> 8;
+      const int d = kb * 256 + (index & 3) * 64 + ((19 * (index >> 2)) & 63);
+      if (d < C_FRAME - 1) S.block[((size_t)c * 2 + blkbuf) * C_BLOCK + d + d / 3] = (uint8_t)soft_bit;
+    }
+    if (index == 255) index = -1;
+    if (cntr == C_FRAME - 1) {
+      const int j = atomicAdd(S.njobs, 1);
+      reinterpret_cast<int4 *>(S.jobs)[j] = make_int4(c, blkbuf | ((has_ov ? 0 : 1) << 1), 0, 0);
+      has_ov = 1;
+      blkbuf ^= 1;
+      index = -1;
+    }
+  }
+  ls[LS_SOFT_C * C + c] = q;
+  is[IS_RI * C + c] = realimag;
+  is[IS_CNTR * C + c] = cntr;
+  is[IS_GSL * C + c] = gsl;
+  is[IS_UWR_INV * C + c] = inv_r;
+  is[IS_UWI_INV * C + c] = inv_i;
+  is[IS_C_INDEX * C + c] = index;
+  is[IS_BLKBUF * C + c] = blkbuf;
+  is[IS_HAS_OVERLAP * C + c] = has_ov;
+  ls[LS_C_R1 * C + c] = (long long)r1;
+  ls[LS_C_R2 * C + c] = (long long)r2;
+  ls[LS_C_I1 * C + c] = (long long)i1;
+  ls[LS_C_I2 * C + c] = (long long)i2;
+}
+
+namespace {
+// soft value p of a C job's decoder input: the previous frame's last 62
+// depunctured values, the 5460 depunctured ones (erasures at 4k + 3), 24 erasures
+struct CSoft {
+  const uint8_t *blk;
+  int ov, ovr;
+  __device__ __forceinline__ int get(int p, bool may_ov) const {
+    const int qq = p - ov;
+    int v = 128;
+    if (qq >= 0 && qq < C_BLOCK && (qq & 3) != 3) v = blk[qq];
+    if (may_ov) {
+      const int o = __builtin_amdgcn_ds_bpermute((p & 63) << 2, ovr);
+      if (qq < 0) v = o;
+    }
+    return v;
+  }
+};
+}  // namespace
+
+__global__ __launch_bounds__(64) void viterbi_c_kernel(DevState S, DevTables T) {
+  constexpr int NW = (62 + C_BLOCK + 24) / 2 / 64 + 1;
+  __shared__ uint64_t obits[NW];
+  __shared__ uint8_t pay[C_PAYLOAD];
+  __shared__ uint8_t rec[336];
+  const int njobs = *S.njobs;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && S.njobs_host) *S.njobs_host = njobs;
+  const int lane = threadIdx.x, C = S.C;
+  for (int job = blockIdx.x; job < njobs; job += gridDim.x) {
+    __syncthreads();
+    const int4 jd = reinterpret_cast<const int4 *>(S.jobs)[job];
+    const int c = jd.x, buf = jd.y & 1, first = (jd.y >> 1) & 1;
+    CSoft src;
+    src.blk = S.block + ((size_t)c * 2 + buf) * C_BLOCK;
+    src.ov = first ? 0 : 62;
+    src.ovr = (!first && lane < 62) ? S.overlap[(size_t)c * 64 + lane] : 0;
+    if (lane < 62) S.overlap[(size_t)c * 64 + lane] = (uint8_t)src.get(src.ov + C_BLOCK - 62 + lane, false);
+    const int nsoft = src.ov + C_BLOCK + 24;
+    uint64_t obw, unused;
+    viterbi_decode_regs2(src, src, nsoft, obw, unused, lane);
+    if (lane < NW) obits[lane] = obw;
+    __syncthreads();
+    // Decode_Continuous keeps bits [25, 25 + 2730), deconvol.resize(2714)
+    // (jconvolutionalcodec.cpp:186-191, aerol.cpp:2249); DelayLine dl2
+    // (aerol.h:464-471) out[q] = buffer[(p + q + 1) % L] before the q-th write,
+    // i.e. an old value for q + 1 < L and in[q + 1 - L] after the wrap; then
+    // AeroLScrambler from position 0 (reset at the frame's UW)
+    uint8_t *dlg = S.dl2 + (size_t)c * C_DL2_LEN;
+    const int p0 = S.is[IS_DL2_PTR * C + c];
+    auto obit = [&](int k) { return (int)((obits[k >> 6] >> (k & 63)) & 1ULL); };
+    for (int k = lane; k < C_PAYLOAD; k += 64) {
+      int v;
+      if (k + 1 < C_DL2_LEN) {
+        int r = p0 + k + 1;
+        r = r >= C_DL2_LEN ? r - C_DL2_LEN : r;
+        v = dlg[r];
+      } else {
+        v = obit(25 + k + 1 - C_DL2_LEN);
+      }
+      pay[k] = (uint8_t)((v ^ T.scr[k]) & 1);
+    }
+    __syncthreads();  // every old delay-line value read
+    for (int k = lane; k < C_PAYLOAD; k += 64) {
+      if (k + C_DL2_LEN < C_PAYLOAD) continue;  // overwritten by a later input of this block
+      int w = p0 + k;
+      w %= C_DL2_LEN;
+      dlg[w] = (uint8_t)obit(25 + k);
+    }
+    if (lane == 0) S.is[IS_DL2_PTR * C + c] = (p0 + C_PAYLOAD) % C_DL2_LEN;
+    // three SUs from 24 sub-data fields of 12 bits at 109 y + 97, LSB-first
+    // bytes (aerol.cpp:2262-2282); 25 voice frames of 96 bits at 109 y + 1 (:2362-2392)
+    if (lane < 36) {
+      int v = 0;
+      for (int b = 0; b < 8; ++b) {
+        const int kb = 8 * lane + b, y = kb / 12;
+        v |= pay[y * 109 + 97 + kb % 12] << b;
+      }
+      rec[lane] = (uint8_t)v;
+    }
+    for (int byte = lane; byte < 300; byte += 64) {
+      int v = 0;
+      for (int b = 0; b < 8; ++b) {
+        const int kb = 8 * byte + b, y = kb / 96;
+        v |= pay[y * 109 + 1 + kb % 96] << b;
+      }
+      rec[36 + byte] = (uint8_t)v;
+    }
+    __syncthreads();
+    bool ok = false;
+    if (lane < 3) {  // AeroLcrc16::calcusingbytes (aerol.h:332-367), no all-zero exception here
+      const uint8_t *su = rec + 12 * lane;
+      unsigned crc = 0xFFFF;
+      for (int k = 0; k < 10; ++k) {
+        unsigned mb = su[k];
+        for (int b = 0; b < 8; ++b) {
+          const unsigned cb = crc & 1, bt = mb & 1;
+          mb >>= 1;
+          crc >>= 1;
+          if (cb ^ bt) crc ^= 0x8408;
+        }
+      }
+      ok = ((~crc) & 0xFFFF) == (((unsigned)su[11] << 8) | su[10]);
+    }
+    const unsigned long long okm = __ballot(ok);
+    uint8_t *out = S.jobout + (size_t)job * JOB_OUT_C;
+    for (int b = lane; b < 336; b += 64) out[b] = rec[b];
+    if (lane == 0) {
+      int *o = reinterpret_cast<int *>(out + 336);
+      o[0] = 36;
+      o[1] = (int)(okm & 7);
+      o[2] = 0;
+      o[3] = c;
+    }
+  }
+}
+
+void launch_prefilter_c(hipStream_t st, const DevState &S, const DevTables &T, const void *jobs, int njobs) {
+  if (njobs > 0)
+    hipLaunchKernelGGL(prefilter_c_kernel, dim3(njobs), dim3(256), 0, st, S, T, (const CPreJob *)jobs);
+}
+void launch_demod_c(hipStream_t st, const DevState &S, const DevTables &T, int nch, bool trace) {
+  const dim3 g((nch + 63) / 64), b(64);
+  if (trace)
+    hipLaunchKernelGGL(demod_c_kernel<true>, g, b, 0, st, S, T, nch);
+  else
+    hipLaunchKernelGGL(demod_c_kernel<false>, g, b, 0, st, S, T, nch);
+}
+void launch_frame_c(hipStream_t st, const DevState &S, int nch) {
+  hipLaunchKernelGGL(frame_c_kernel, dim3((nch + 255) / 256), dim3(256), 0, st, S, nch);
+}
+void launch_viterbi_c(hipStream_t st, const DevState &S, const DevTables &T, int max_jobs) {
+  if (max_jobs <= 0) return;
+  max_jobs = max_jobs < 16384 ? max_jobs : 16384;
+  hipLaunchKernelGGL(viterbi_c_kernel, dim3(max_jobs), dim3(64), 0, st, S, T);
+}
+void upload_c_constants(const DelayDesc *dly) { hipMemcpyToSymbol(HIP_SYMBOL(cc_dly), dly, sizeof(DelayDesc) * 4); }
+int c_prejob_bytes() { return (int)sizeof(CPreJob); }
+
+}  // namespace aero

@@ -45,6 +45,15 @@ struct CoarseK<MODE_OQPSK> {
   static constexpr int YLO = 2815, YHI = 13568;
   static constexpr double FS = 48000.0;
 };
+// the C channel: setSettings(14, 10500, 8400, 48000): the OQPSK bins, the
+// expected peak at round(8400 / (2 hzperbin)) = 1434; the raised-cosine window
+// in place of the boxcar (coarsefreqestimate.cpp:97-104)
+template <>
+struct CoarseK<MODE_C8400> {
+  static constexpr int LOG2N = 14, HOPN = 4096, START = 3584, STOP = 12800, ILO = 4608, IHI = 11776, EPB = 1434;
+  static constexpr int YLO = 2815, YHI = 13568;
+  static constexpr double FS = 48000.0;
+};
 // MSK at Fs (setSettings(13, 900, 600, Fs)): hzperbin = Fs / 8192; startbin
 // round(900 / hzperbin), stopbin nfft - startbin, the fold search over
 // [round(-900 / hzperbin + 4096), round(900 / hzperbin + 4096)) with
@@ -106,8 +115,8 @@ struct HopCtl {
 // SignalHunter (decode/hunter.cpp:21-42; maxTries 15, params 0/25000/10500,
 // decode/decode.cpp:161,169) and CenterFreqChangedSlot (:256-280).  dcd is
 // never set (DCDstatSlot unconnected, decode/decode.cpp:168-241).
-__device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<int, MODE_OQPSK>, double, double est,
-                                            double mse, unsigned &iter, int &scans, long long nk) {
+__device__ __forceinline__ bool hop_control_oqpsk(HopCtl &h, bool c8400, double est, double mse, unsigned &iter,
+                                                  int &scans, long long nk) {
   const double thr = 0.65, lockingbw = 10500.0, Fs = 48000.0;
   if (mse < thr) {
     if (h.countdown2 > 0)
@@ -144,9 +153,13 @@ __device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<in
       }
       h.stepped = true;
       h.step_fc = fc;
-      // CenterFreqChangedSlot, fb != 8400, afc on
-      if (fc < (0.5 * 10500.0)) fc = 0.5 * 10500.0;
-      if (fc > (Fs / 2.0 - 0.5 * 10500.0)) fc = Fs / 2.0 - 0.5 * 10500.0;
+      // CenterFreqChangedSlot, afc on; fb != 8400 clamps the centre
+      // (oqpskdemodulator.cpp:256-265); fb is 10500 as aero-decode's Decoder
+      // leaves it (decode/decode.cpp:152-159, oqpskdemodulator.h:24-32)
+      if (!c8400) {
+        if (fc < (0.5 * 10500.0)) fc = 0.5 * 10500.0;
+        if (fc > (Fs / 2.0 - 0.5 * 10500.0)) fc = Fs / 2.0 - 0.5 * 10500.0;
+      }
       set_freq1(h.mcf, h.mcs, fc, Fs);
       set_freq1(h.m2f, h.m2s, h.mcf, Fs);
       if ((h.m2f - h.mcf) > (lockingbw / 2.0)) set_freq1(h.m2f, h.m2s, h.mcf + (lockingbw / 2.0), Fs);
@@ -155,6 +168,17 @@ __device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<in
     }
   }
   return gotasignal;
+}
+
+__device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<int, MODE_OQPSK>, double, double est,
+                                            double mse, unsigned &iter, int &scans, long long nk) {
+  return hop_control_oqpsk(h, false, est, mse, iter, scans, nk);
+}
+// the C channel: the same slot (its prefilter mixer's retune there is
+// overridden by the message-end retune before any prefilter runs, :555-569)
+__device__ __forceinline__ bool hop_control(HopCtl &h, std::integral_constant<int, MODE_C8400>, double, double est,
+                                            double mse, unsigned &iter, int &scans, long long nk) {
+  return hop_control_oqpsk(h, true, est, mse, iter, scans, nk);
 }
 
 // MskDemodulator::FreqOffsetEstimateSlot (decode/mskdemodulator.cpp:430-469;
@@ -295,12 +319,18 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   // forward FFT
   chain::fft<L, true, false>(x, t, lds, T.tw, s_tw);
   CSTAMP(3);
-  // boxcar: zero bins startbin..stopbin (coarsefreqestimate.cpp:143-146)
+  // boxcar: zero bins startbin..stopbin (coarsefreqestimate.cpp:97-100);
+  // the C channel multiplies by the raised-cosine window instead (:101-104)
   const int bin_t = chain::out_bin_thread<L>(t);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int p = bin_t | chain::out_bin_reg<L>(i);
-    if (p >= KB.start && p <= KB.stop) x[i] = make_double2(0.0, 0.0);
+    if constexpr (M == MODE_C8400) {
+      const double w = T.cwin[p];
+      x[i] = make_double2(x[i].x * w, x[i].y * w);
+    } else {
+      if (p >= KB.start && p <= KB.stop) x[i] = make_double2(0.0, 0.0);
+    }
   }
   // inverse FFT.  JFFT scales by 1/N and FFTWrapper multiplies by N
   // (jfft.cpp:206-212, fftwrapper.cpp:22-29): x * 2^-L * 2^L == x exactly for every
@@ -494,6 +524,7 @@ void coarse_read_stamps(unsigned long long *out) {
 void launch_coarse(hipStream_t st, int mode, const DevState &S, const DevTables &T, int nch) {
   switch (mode) {
     case MODE_OQPSK: hipLaunchKernelGGL(coarse_kernel<MODE_OQPSK>, dim3(nch), dim3(1024), 0, st, S, T, nch); break;
+    case MODE_C8400: hipLaunchKernelGGL(coarse_kernel<MODE_C8400>, dim3(nch), dim3(1024), 0, st, S, T, nch); break;
     case MODE_MSK600: hipLaunchKernelGGL(coarse_kernel<MODE_MSK600>, dim3(nch), dim3(512), 0, st, S, T, nch); break;
     case MODE_MSK1200: hipLaunchKernelGGL(coarse_kernel<MODE_MSK1200>, dim3(nch), dim3(512), 0, st, S, T, nch); break;
     case MODE_MSK600_24K:

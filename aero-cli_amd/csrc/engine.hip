@@ -53,6 +53,11 @@ void burst_read_stamps(unsigned long long *);
 void launch_coarse(hipStream_t, int, const DevState &, const DevTables &, int);
 void launch_frame(hipStream_t, int, const DevState &, int);
 void launch_viterbi(hipStream_t, int, const DevState &, const DevTables &, int, int);
+// the C channel (cchan.hip)
+void launch_prefilter_c(hipStream_t, const DevState &, const DevTables &, const void *, int);
+void launch_demod_c(hipStream_t, const DevState &, const DevTables &, int, bool);
+void upload_c_constants(const DelayDesc *);
+int c_prejob_bytes();
 }  // namespace aero
 
 using namespace aero;
@@ -193,6 +198,17 @@ struct Group {
   // samples the channel demodulated before it moved into this group (an MSK
   // rate change): hop records count from the channel's first sample
   std::vector<long long> hop_base;
+  // the C channel (MODE_C8400): the pushed messages' ends not yet
+  // prefiltered, the prefiltered end (host mirror of LS_PRE_END), decoded
+  // Call_progress SUs and voice frames, AeroL's DCD countdown (aerol.cpp:2300-2315)
+  int job_out = JOB_OUT;  // bytes per Viterbi job record
+  std::vector<std::deque<long long>> msg_end;
+  std::vector<long long> pre_end;
+  std::vector<std::vector<uint8_t>> cunit_hold, voice_hold;
+  std::vector<int> c_cd, c_dcd, c_edges;
+  void *pin_cjobs[4] = {}, *d_cjobs[4] = {};
+  hipEvent_t cjob_ev[4] = {};
+  int next_cjob = 0;
   // aero_trace_select: host-side trace collection for these local channels
   // only (empty: every channel)
   bool trace_some = false;
@@ -289,7 +305,8 @@ constexpr int MODE_BURST = 1 << 20;
 
 struct aero_engine {
   int device = 0, flags = 0, max_channels = 0;
-  std::vector<std::unique_ptr<Group>> groups = std::vector<std::unique_ptr<Group>>(MODE_COUNT);  // by gid
+  // by gid: the fixed kinds (Mode), GID_C8400, then generic-rate MSK groups
+  std::vector<std::unique_ptr<Group>> groups = std::vector<std::unique_ptr<Group>>(MODE_COUNT + 1);
   BurstGroup *burst[2] = {nullptr, nullptr};  // BURST_OQPSK, BURST_MSK
   std::vector<std::pair<int, int>> chmap;  // engine channel -> (gid or MODE_BURST + kind, local index)
   std::unique_ptr<HostPool> hpool;
@@ -307,7 +324,7 @@ T *carve(char *&p, size_t count) {
 }
 
 size_t layout(DevState &S, DevTables &T, int mode, const ModeGeom &g, int C, int flags, char *base) {
-  const bool msk = mode != MODE_OQPSK;
+  const bool msk = mode != MODE_OQPSK && mode != MODE_C8400;
   char *p = base;
   S.C = C;
   S.mode = mode;
@@ -342,6 +359,14 @@ size_t layout(DevState &S, DevTables &T, int mode, const ModeGeom &g, int C, int
   S.njobs = carve<int>(p, 1);
   S.jobout = carve<uint8_t>(p, (size_t)JOB_OUT * C);
   S.blocks_dbg = carve<uint8_t>(p, (flags & AERO_F_TRACE_BLOCKS) ? (size_t)2500 * C : 1);
+  const bool cch = mode == MODE_C8400;
+  S.cpre = carve<double2>(p, cch ? (size_t)C_PRE_RING * C : 1);
+  S.csig = carve<double2>(p, cch ? (size_t)C_FIR_SNZ * C : 1);
+  S.crem = carve<double2>(p, cch ? (size_t)(C_FIR_N - C_FIR_SNZ) * C : 1);
+  T.cker = carve<double2>(p, cch ? C_FIR_N : 1);
+  T.tw4 = carve<double2>(p, cch ? C_FIR_N : 1);
+  T.twi4 = carve<double2>(p, cch ? C_FIR_N : 1);
+  T.cwin = carve<double>(p, cch ? NFFT : 1);
   T.cis = carve<double2>(p, WTSIZE);
   T.tw = carve<double2>(p, g.nfft);
   T.twi = carve<double2>(p, g.nfft);
@@ -391,6 +416,14 @@ int init_scalars(Group *e, int lo, int hi) {
     ds[DS_SO_FREQ] = 10500;
     ds[DS_SO_STEP] = (10500.0) * ((double)WTSIZE) / ((float)48000);
     ds[DS_MSE] = 100;
+  } else if (e->mode == MODE_C8400) {
+    // st_osc.SetFreq(fb = 8400, Fs) (oqpskdemodulator.cpp:225-227); the ctor's
+    // mixer_fir_pre.SetFreq(freq_center = 8000, Fs) (:114), phase 0
+    ds[DS_SO_FREQ] = 8400;
+    ds[DS_SO_STEP] = (8400.0) * ((double)WTSIZE) / ((float)48000);
+    ds[DS_MSE] = 100;
+    ds[DS_FP_FREQ] = 8000;
+    ds[DS_FP_STEP] = (8000.0) * ((double)WTSIZE) / ((float)48000);
   } else {
     // st_osc.SetFreq(fb / 2, Fs) (mskdemodulator.cpp:117); mse = 10.0 (:146);
     // DiffDecode::lastsoftstate = -1 (DSP.cpp:517-520)
@@ -506,10 +539,11 @@ int process_slot(Group *e, int si) {
   e->max_jobs_seen = std::max(e->max_jobs_seen, njobs);
   HOST_TIMER(e, "host_frames");
   e->hpool->wait();  // previous slot's frames first (per-channel order)
-  e->h_jobs_task.resize((size_t)std::max(njobs, 1) * JOB_OUT);
-  if (njobs > 0) memcpy(e->h_jobs_task.data(), sl.h_out, (size_t)njobs * JOB_OUT);
+  const size_t JO = (size_t)e->job_out;
+  e->h_jobs_task.resize((size_t)std::max(njobs, 1) * JO);
+  if (njobs > 0) memcpy(e->h_jobs_task.data(), sl.h_out, (size_t)njobs * JO);
   sl.pending = false;
-  const bool blocks = (e->flags & AERO_F_TRACE_BLOCKS) != 0;
+  const bool blocks = (e->flags & AERO_F_TRACE_BLOCKS) != 0 && e->mode != MODE_C8400;
   if (blocks) {
     // traces run synchronously (run_group waited for this slot): blocks_dbg is this pass's
     e->h_dbg_task.resize((size_t)2500 * C);
@@ -523,19 +557,59 @@ int process_slot(Group *e, int si) {
   }
   if (njobs <= 0) return AERO_OK;
   e->st_jobs += (uint64_t)njobs;
-  const bool msk = e->mode != MODE_OQPSK;
+  const bool msk = e->mode != MODE_OQPSK && e->mode != MODE_C8400;
+  const bool cch = e->mode == MODE_C8400;
   // channels partitioned over workers (c % T): a channel's frames stay in
   // queue order and no two workers share state
-  auto work = [e, njobs, nch, blocks, msk](int t, int T) {
+  auto work = [e, njobs, nch, blocks, msk, cch, JO](int t, int T) {
     const uint8_t *jobs = e->h_jobs_task.data();
     uint64_t frames = 0, su_ok = 0;  // this worker's counts, added once (no shared atomics per job)
     for (int j = 0; j < njobs; j++) {
-      const uint8_t *o = jobs + (size_t)j * JOB_OUT;
+      const uint8_t *o = jobs + (size_t)j * JO;
       int meta[4];
-      memcpy(meta, o + 312, 16);
+      memcpy(meta, o + (cch ? 336 : 312), 16);
       const int c = meta[3] & 0x3FFFFFFF;
       const int reset = (meta[3] >> 30) & 1;
       if (c < 0 || c >= nch || c % T != t) continue;
+      if (cch) {
+        // AeroL::DecodeC's frame end (decode/aerol.cpp:2284-2405): per SU the DCD
+        // countdown (+2 / -5) and datacd; Call_progress_Signal for a CRC-valid
+        // Call_progress SU (0x30), whose AES tags the frame's Voicesignal
+        const uint32_t mask = (uint32_t)meta[1];
+        uint32_t aes = 0;
+        for (int k = 0; k < 3; k++) {
+          const bool ok = (mask >> k) & 1;
+          int &cd = e->c_cd[c];
+          if (ok) {
+            if (cd < 12) cd += 2;
+          } else {
+            if (cd > 0) cd -= 5;
+          }
+          if (!e->c_dcd[c] && cd > 2) {
+            e->c_dcd[c] = 1;
+            e->c_edges[c]++;
+          }
+          const uint8_t *su = o + 12 * k;
+          if (ok && su[0] == 0x30) {
+            e->cunit_hold[c].insert(e->cunit_hold[c].end(), su, su + 12);
+            aes = ((uint32_t)su[1] << 16) | ((uint32_t)su[2] << 8) | su[3];
+          }
+        }
+        auto &v = e->voice_hold[c];
+        v.insert(v.end(), (const uint8_t *)&aes, (const uint8_t *)&aes + 4);
+        v.insert(v.end(), o + 36, o + 336);
+        frames++;
+        su_ok += (uint64_t)__builtin_popcount(mask);
+        if ((e->flags & AERO_F_TRACE_FRAMES) && e->traced(c)) {
+          uint8_t rec[320] = {0};
+          memcpy(rec, o, 36);
+          const uint32_t L = 36, M = mask;
+          memcpy(rec + 312, &L, 4);
+          memcpy(rec + 316, &M, 4);
+          e->frame_hold[c].insert(e->frame_hold[c].end(), rec, rec + 320);
+        }
+        continue;
+      }
       if (blocks && e->traced(c)) {
         const uint8_t *d = e->h_dbg_task.data() + (size_t)c * 2500;
         int nb;
@@ -825,9 +899,34 @@ int run_pass(Group *e, int flush, bool *more) {
   const int tflags = AERO_F_TRACE_PT | AERO_F_TRACE_BLOCKS | AERO_F_TRACE_SOFT | AERO_F_TRACE_HOPS;
   const bool trace = (e->flags & tflags) != 0;
   const long long HOPN = e->g.hop;
+  const bool cch = e->mode == MODE_C8400;
   {
     // host mirror of the hop and segment rules of coarse.hip / demod_*.hip
     bool any_hop = false, progress = false;
+    // the C channel: the next message of every channel whose demod has
+    // reached the end of the prefiltered one (cchan.hip prefilter_c_kernel)
+    int ncj = 0, kcj = 0;
+    if (cch) {
+      kcj = e->next_cjob;
+      struct HostCPreJob {
+        int c, pad;
+        long long s, e;
+      };
+      static_assert(sizeof(HostCPreJob) == 24, "CPreJob layout");
+      HostCPreJob *jt = reinterpret_cast<HostCPreJob *>(e->pin_cjobs[kcj]);
+      bool waited = false;
+      for (int c = 0; c < e->nch; c++) {
+        if (e->nsamp[c] != e->pre_end[c] || e->msg_end[c].empty()) continue;
+        if (!waited) {  // the table of NPIN passes ago has been read
+          HIPCHK(hipEventSynchronize(e->cjob_ev[kcj]));
+          waited = true;
+        }
+        jt[ncj++] = {c, 0, e->pre_end[c], e->msg_end[c].front()};
+        e->pre_end[c] = e->msg_end[c].front();
+        e->msg_end[c].pop_front();
+      }
+      if (ncj) e->next_cjob = (kcj + 1) % Group::NPIN;
+    }
     for (int c = 0; c < e->nch; c++) {
       const long long boundary = HOPN * (e->hops[c] + 1) - 1;
       if (e->nsamp[c] == boundary && e->avail[c] > boundary) {
@@ -839,13 +938,14 @@ int run_pass(Group *e, int flush, bool *more) {
       const long long boundary = HOPN * (e->hops[c] + 1) - 1;
       long long end = std::min(e->avail[c], boundary);
       if (!flush && e->avail[c] <= boundary) end = e->nsamp[c];
+      if (cch) end = std::min(e->pre_end[c], boundary);  // whole messages, prefiltered
       if (end > e->nsamp[c]) {
         e->processed += (uint64_t)(end - e->nsamp[c]);
         e->nsamp[c] = end;
         progress = true;
       }
     }
-    if (!any_hop && !progress) {
+    if (!any_hop && !progress && !ncj) {
       *more = false;
       return AERO_OK;
     }
@@ -856,9 +956,20 @@ int run_pass(Group *e, int flush, bool *more) {
       ev_end(e, b);
     }
     if (int rc = issue_viterbi(e)) return rc;  // the previous pass's decode, before this demod
+    if (ncj) {
+      HIPCHK(hipMemcpyAsync(e->d_cjobs[kcj], e->pin_cjobs[kcj], (size_t)c_prejob_bytes() * ncj,
+                            hipMemcpyHostToDevice, e->st));
+      HIPCHK(hipEventRecord(e->cjob_ev[kcj], e->st));
+      ev_begin(e, "prefilter", a, b);
+      launch_prefilter_c(e->st, e->S, e->T, e->d_cjobs[kcj], ncj);
+      ev_end(e, b);
+      HIPCHK(hipGetLastError());
+    }
     if (!progress) return AERO_OK;  // no new soft bits: framing has nothing to do
     ev_begin(e, "demod", a, b);
-    if (e->mode == MODE_OQPSK)
+    if (cch)
+      launch_demod_c(e->st, e->S, e->T, e->nch, (e->flags & AERO_F_TRACE_PT) != 0);
+    else if (e->mode == MODE_OQPSK)
       launch_demod(e->st, e->S, e->T, e->nch, flush, (e->flags & AERO_F_TRACE_PT) != 0, e->nch <= e->wide_max);
     else
       launch_demod_msk(e->st, e->mode, e->S, e->T, e->nch, flush, e->nch <= e->wide_max);
@@ -1046,7 +1157,7 @@ int group_create(aero_engine *E, int mode, int gid, int fs, std::unique_ptr<Grou
   e->flags = E->flags;
   e->hpool = E->hpool.get();
   MskGen mg{};
-  if (mode != MODE_OQPSK) {
+  if (mode != MODE_OQPSK && mode != MODE_C8400) {
     // every MSK group carries its rate's constants (the generic-rate and the
     // few-channel kernels read them)
     if (!msk_gen_consts(msk_generic(mode) ? fs : msk_fs(mode), mg)) return AERO_E_RATE;
@@ -1058,6 +1169,10 @@ int group_create(aero_engine *E, int mode, int gid, int fs, std::unique_ptr<Grou
   if (msk_generic(mode)) {
     e->g = msk_geom(msk_bitrate(mode), fs);
     e->tag = "msk" + std::to_string(msk_bitrate(mode)) + "_" + std::to_string(fs) + "_";
+  } else if (mode == MODE_C8400) {
+    e->g = mode_geom(mode);
+    e->tag = "c8400_";
+    e->job_out = JOB_OUT_C;
   } else {
     static const char *const tags[MODE_COUNT] = {"", "msk600_", "msk1200_", "msk600_24k_", "msk600_48k_",
                                                   "msk1200_12k_", "msk1200_48k_"};
@@ -1083,7 +1198,7 @@ int group_create(aero_engine *E, int mode, int gid, int fs, std::unique_ptr<Grou
     // kernel-written zero-copy buffers: mapped (a device address for the
     // Viterbi kernel) and coherent (its system-scope stores reach host memory
     // without a cache flush); read by the host after the slot's event
-    if (hipHostMalloc(&sl.h_out, (size_t)JOB_OUT * e->C, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+    if (hipHostMalloc(&sl.h_out, (size_t)e->job_out * e->C, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
       return AERO_E_NOMEM;
     if (hipHostMalloc(&sl.h_n, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return AERO_E_NOMEM;
     HIPCHK(hipHostGetDevicePointer((void **)&sl.h_out_dev, sl.h_out, 0));
@@ -1140,6 +1255,37 @@ int group_create(aero_engine *E, int mode, int gid, int fs, std::unique_ptr<Grou
     const double ct_b[3] = {0.0010275610653672064, 0.0020551221307344128, 0.0010275610653672064};
     const double ct_a[3] = {1, -1.9207386815577139, 0.92509247310306331};
     upload_demod_constants(taps.data(), dly, sr_b, sr_a, ct_b, ct_a);
+  } else if (mode == MODE_C8400) {
+    // the prefilter kernel: RRC(0.6, 2048 -> 2049 taps, 48000, 4200) into a
+    // 4096-point block, its JFFT (oqpskdemodulator.cpp:228-236, jfft.cpp:324-367)
+    std::vector<double> k(2 * C_FIR_N, 0.0), rrc(2049), t4(2 * C_FIR_N), ti4(2 * C_FIR_N);
+    if (host_rrc(0.6, 2048, 48000, 8400 / 2, rrc.data()) != 2049) return AERO_E_INVALID;
+    for (int j = 0; j < 2049; j++) k[2 * j] = rrc[j];
+    host_twiddles(C_FIR_N, t4.data(), ti4.data());
+    host_jfft(k.data(), C_FIR_N, false, t4.data(), ti4.data());
+    std::vector<double> win(NFFT);
+    host_coarse_window(NFFT, 10500.0, 48000.0, win.data());
+    HIPCHK(hipMemcpy((void *)e->T.cker, k.data(), sizeof(double) * 2 * C_FIR_N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy((void *)e->T.tw4, t4.data(), sizeof(double) * 2 * C_FIR_N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy((void *)e->T.twi4, ti4.data(), sizeof(double) * 2 * C_FIR_N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy((void *)e->T.cwin, win.data(), sizeof(double) * NFFT, hipMemcpyHostToDevice));
+    // symbol timer delays at T = 48000 / 4200 (:186-190): the kernel reads ages
+    // {1,0}, {3,2}, {3,2}, {2,1}; T/8's weights depend on the write pointer
+    const double T84 = 48000.0 / (8400.0 / 2);
+    DelayDesc dly[4];
+    if (!host_delay(1, dly[0]) || !host_delay(T84 / 4.0, dly[1]) || !host_delay(T84 / 4.0, dly[2]) ||
+        !host_delay(T84 / 8.0, dly[3]))
+      return AERO_E_INVALID;
+    static const int ages[4][3] = {{2, 1, 0}, {4, 3, 2}, {4, 3, 2}, {3, 2, 1}};  // {size, age_old, age_new}
+    for (int j = 0; j < 4; j++)
+      if (dly[j].size != ages[j][0] || dly[j].age_old != ages[j][1] || dly[j].age_new != ages[j][2])
+        return AERO_E_INVALID;
+    upload_c_constants(dly);
+    for (int j = 0; j < Group::NPIN; j++) {
+      if (hipHostMalloc(&e->pin_cjobs[j], (size_t)c_prejob_bytes() * e->C) != hipSuccess) return AERO_E_NOMEM;
+      if (hipMalloc(&e->d_cjobs[j], (size_t)c_prejob_bytes() * e->C) != hipSuccess) return AERO_E_NOMEM;
+      HIPCHK(hipEventCreateWithFlags(&e->cjob_ev[j], hipEventDisableTiming));
+    }
   } else if (msk_generic(mode)) {
     host_msk_taps(e->g.fs / 600, taps.data());  // delayt8 ages and weights: S.mg
   } else {
@@ -1191,6 +1337,11 @@ void group_destroy(Group *e) {
     if (e->hq_ev[k]) (void)hipEventDestroy(e->hq_ev[k]);
   }
   if (e->d_hq) (void)hipFree(e->d_hq);
+  for (int k = 0; k < Group::NPIN; k++) {
+    if (e->pin_cjobs[k]) (void)hipHostFree(e->pin_cjobs[k]);
+    if (e->d_cjobs[k]) (void)hipFree(e->d_cjobs[k]);
+    if (e->cjob_ev[k]) (void)hipEventDestroy(e->cjob_ev[k]);
+  }
   if (e->pin_stat) (void)hipHostFree(e->pin_stat);
   if (e->pin_pcm) (void)hipHostFree(e->pin_pcm);
   if (e->pin_pcm_ev) (void)hipEventDestroy(e->pin_pcm_ev);
@@ -1432,6 +1583,7 @@ int feed_group(Group *e, const std::vector<std::pair<int, std::pair<const int16_
     j.c = c;
     j.later = 0;
     e->avail[c] += n;
+    if (e->mode == MODE_C8400 && n) e->msg_end[c].push_back(e->avail[c]);  // one message per item
     mx = std::max(mx, n);
   }
   mark_last_jobs(e->pin_gjobs[k], items.size(), e->C);
@@ -1517,6 +1669,13 @@ int group_add_channel(aero_engine *e, int gid, const aero_channel_cfg &cfg, int 
   g->frame_hold.emplace_back();
   g->soft_seen.push_back(0);
   g->hop_base.push_back(0);
+  g->msg_end.emplace_back();
+  g->pre_end.push_back(0);
+  g->cunit_hold.emplace_back();
+  g->voice_hold.emplace_back();
+  g->c_cd.push_back(0);
+  g->c_dcd.push_back(0);
+  g->c_edges.push_back(0);
   if (g->trace_some) g->trace_mask.resize(g->C, 0);
   *local = c;
   return AERO_OK;
@@ -1643,7 +1802,8 @@ int msk_migrate(aero_engine *e, int ch, uint32_t fs) {
 Group *route_rate(aero_engine *e, int ch, uint32_t fs, int &local, int &rc) {
   rc = AERO_OK;
   Group *g = route(e, ch, local);
-  if (!g || g->mode == MODE_OQPSK || fs == (uint32_t)g->g.fs) return g;  // OQPSK only logs it (:626-628)
+  if (!g || g->mode == MODE_OQPSK || g->mode == MODE_C8400 || fs == (uint32_t)g->g.fs)
+    return g;  // OQPSK only logs it (:626-628)
   if ((rc = msk_migrate(e, ch, fs))) return nullptr;
   return route(e, ch, local);
 }
@@ -1728,15 +1888,21 @@ int aero_channel_open(aero_engine *e, const aero_channel_cfg *cfg, int *ch_out) 
     return AERO_OK;
   }
   // decode/decode.h:42 validBitRates: 10500 (48 kHz), 600 and 1200 at any
-  // rate MSK is served at (12 / 24 kHz as decode/decode.cpp:145)
-  if (!(cfg->bitrate == 10500 && cfg->fs == 48000) && !(cfg->bitrate == 600 || cfg->bitrate == 1200))
-    return AERO_E_INVALID;
-  if (cfg->bitrate != 10500 && (cfg->fs < (uint32_t)MSK_FS_MIN || cfg->fs > (uint32_t)MSK_FS_MAX)) return AERO_E_RATE;
+  // rate MSK is served at (12 / 24 kHz as decode/decode.cpp:145); and the C
+  // channel, 8400 at 48 kHz (OqpskDemodulator at fb = 8400 + AeroL::DecodeC)
+  const bool oq = (cfg->bitrate == 10500 || cfg->bitrate == 8400) && cfg->fs == 48000;
+  if (!oq && !(cfg->bitrate == 600 || cfg->bitrate == 1200)) return AERO_E_INVALID;
+  if (!oq && (cfg->fs < (uint32_t)MSK_FS_MIN || cfg->fs > (uint32_t)MSK_FS_MAX)) return AERO_E_RATE;
   HIPCHK(hipSetDevice(e->device));
   host_wait(e);  // the host task indexes the per-channel tables
   int gid = MODE_OQPSK;
-  if (cfg->bitrate != 10500)
+  if (cfg->bitrate == 8400) {
+    gid = GID_C8400;
+    if (!e->groups[gid])
+      if (int rc = group_create(e, MODE_C8400, gid, 48000, e->groups[gid])) return rc;
+  } else if (cfg->bitrate != 10500) {
     if (int rc = msk_gid(e, (int)cfg->bitrate, (int)cfg->fs, gid)) return rc;
+  }
   int c;
   if (int rc = group_add_channel(e, gid, *cfg, (int)e->chmap.size(), &c)) return rc;
   *ch_out = (int)e->chmap.size();
@@ -1769,7 +1935,9 @@ int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t
   Group *g = route_rate(e, ch, fs, c, rc);
   if (rc) return rc;
   if (!g) return AERO_E_INVALID;
-  if (!n) return AERO_OK;
+  if (!n) return AERO_OK;  // dataReceived with an empty message returns at once (:286-287)
+  // a C-channel message is one prefilter block (oqpskdemodulator.cpp:292-324): whole, at most half the ring
+  if (g->mode == MODE_C8400 && n > (size_t)PCM_CAP / 2) return AERO_E_INVALID;
   HIPCHK(hipSetDevice(e->device));
   // split so one piece never exceeds the ring
   size_t off = 0;
@@ -1779,6 +1947,7 @@ int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t
     if (rc) return rc;
     off += piece;
   }
+  if (g->mode == MODE_C8400) g->msg_end[c].push_back(g->avail[c]);
   return AERO_OK;
 }
 
@@ -1792,6 +1961,7 @@ int aero_push_pcm_dev(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint
   if (rc) return rc;
   if (!g) return AERO_E_INVALID;
   if (!n) return AERO_OK;
+  if (g->mode == MODE_C8400 && n > (size_t)PCM_CAP / 2) return AERO_E_INVALID;
   HIPCHK(hipSetDevice(e->device));
   size_t off = 0;
   while (off < n) {
@@ -1800,6 +1970,7 @@ int aero_push_pcm_dev(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint
     if (rc) return rc;
     off += piece;
   }
+  if (g->mode == MODE_C8400) g->msg_end[c].push_back(g->avail[c]);
   return AERO_OK;
 }
 
@@ -1815,6 +1986,7 @@ int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld,
     return burst_push_batch(e->burst[mode - MODE_BURST], pcm, n, ld, nch, dev != 0);
   }
   Group *g = e->groups[mode].get();
+  if (g->mode == MODE_C8400 && n > (size_t)PCM_CAP / 2) return AERO_E_INVALID;
   HIPCHK(hipSetDevice(e->device));
   size_t off = 0;
   while (off < n) {
@@ -1823,6 +1995,8 @@ int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld,
     if (rc) return rc;
     off += piece;
   }
+  if (g->mode == MODE_C8400 && n)  // one message per channel
+    for (int j = 0; j < nch; j++) g->msg_end[j].push_back(g->avail[j]);
   return AERO_OK;
 }
 
@@ -1950,6 +2124,32 @@ int aero_pop_frames(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n)
   if (!g) return AERO_E_INVALID;
   host_wait(e);
   return pop_vec(g->frame_hold[c], dst, cap, n);
+}
+
+int aero_pop_c_units(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
+  int c;
+  Group *g = route(e, ch, c);
+  if (!g || g->mode != MODE_C8400) return AERO_E_INVALID;
+  host_wait(e);
+  auto &v = g->cunit_hold[c];
+  const size_t k = std::min(cap, v.size() / 12);
+  if (dst && k) memcpy(dst, v.data(), 12 * k);
+  v.erase(v.begin(), v.begin() + 12 * k);
+  if (n) *n = k;
+  return AERO_OK;
+}
+
+int aero_pop_voice(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
+  int c;
+  Group *g = route(e, ch, c);
+  if (!g || g->mode != MODE_C8400) return AERO_E_INVALID;
+  host_wait(e);
+  auto &v = g->voice_hold[c];
+  const size_t k = std::min(cap, v.size() / 304);
+  if (dst && k) memcpy(dst, v.data(), 304 * k);
+  v.erase(v.begin(), v.begin() + 304 * k);
+  if (n) *n = k;
+  return AERO_OK;
 }
 
 int aero_pop_rt_tests(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n) {
@@ -2081,6 +2281,10 @@ int aero_channel_get_events(aero_engine *e, int ch, aero_channel_events *out) {
   out->dcd_edges = pi[0];
   out->hunter_steps = pi[1];
   for (int k = 0; k < 8; k++) out->hunter_fc[k] = pd[k];
+  if (g->mode == MODE_C8400) {  // DecodeC's datacd follows the SU CRCs only (host, process_slot)
+    host_wait(e);
+    out->dcd_edges = g->c_edges[c];
+  }
   return AERO_OK;
 }
 

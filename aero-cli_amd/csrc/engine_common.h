@@ -59,6 +59,23 @@ enum Mode : int {
 // such groups are above MODE_COUNT; Group::mode holds one of these)
 constexpr int MODE_MSKG600 = 8, MODE_MSKG1200 = 9;
 constexpr bool msk_generic(int m) { return m == MODE_MSKG600 || m == MODE_MSKG1200; }
+// The C channel (8400 bps OQPSK, AeroL::DecodeC): its own
+// kernel family and a fixed engine group slot after the fixed-rate MSK ones
+// (generic-rate MSK groups are appended after it).  OqpskDemodulator at
+// fb = 8400 (decode/oqpskdemodulator.cpp:136-254, 284-560) prefilters every
+// message with a JFastFir between a down- and an up-mix by mixer_fir_pre and
+// retunes that mixer to the message's mean carrier, so unlike the P channel
+// its output depends on the message boundaries: the group keeps them.
+constexpr int MODE_C8400 = 10;
+constexpr int GID_C8400 = MODE_COUNT;
+constexpr int C_FRAME = 4096;         // AERO_SPEC_NumberOfBits (aerol.cpp:994-1004)
+constexpr int C_BLOCK = 5460;         // depunctured frame: 4095 soft bits + 1365 erasures (aerol.cpp:2417-2432)
+constexpr int C_DL2_LEN = 2709;       // dl2.setLength(2714 - 6) + 1
+constexpr int C_PAYLOAD = 2714;       // deconvol.resize(2714) (aerol.cpp:2249)
+constexpr int C_FIR_N = 4096;         // fir_pre.SetKernel(RRC 0.6 x 2049 taps, 4096) (oqpskdemodulator.cpp:228-236)
+constexpr int C_FIR_SNZ = 2048;       // signal_non_zero_size = 4096 + 1 - 2049 (jfft.cpp:347-352)
+constexpr int C_PRE_RING = 65536;     // prefiltered samples per channel (a message fits: PCM ring 65536)
+constexpr int JOB_OUT_C = 352;        // 36 SU bytes + 300 voice bytes + len, mask, AES, channel
 // MSK sample rates served.  Below 12000 the coarse estimator's fold search
 // would read y bins outside the range every MSK group keeps (MSK_YLO..MSK_YHI,
 // which a channel carries over a rate change); aero-publish's VFO rate is
@@ -127,6 +144,7 @@ inline ModeGeom msk_geom(int bitrate, int fs) {
 }
 inline ModeGeom mode_geom(int m) {
   if (m == MODE_OQPSK) return {48000, 16384, 4096, 192000, 55, 800, 401, 400, 0, 0, 4992, 78, 4987, 2815, 13568, 32};
+  if (m == MODE_C8400) return {48000, 16384, 4096, 192000, 55, 800, 401, 400, 0, 0, C_BLOCK, 4, C_DL2_LEN, 2815, 13568, 32};
   return msk_geom(msk_bitrate(m), msk_fs(m));
 }
 
@@ -162,6 +180,9 @@ enum DS : int {
   // SignalHunter::newFreqCenter values (decode/hunter.cpp:34-40) of the last
   // eight steps: step k (1-based) at DS_HUNT_FC0 + ((k - 1) & 7)
   DS_HUNT_FC0, DS_HUNT_FC_END = DS_HUNT_FC0 + 7,
+  // C channel: mixer_fir_pre (phase pointer, step, Hz) and the message's
+  // running sum of mixer2's frequency (oqpskdemodulator.cpp:385, 557)
+  DS_FP_PTR, DS_FP_STEP, DS_FP_FREQ, DS_M2_FSUM,
   DS_COUNT
 };
 
@@ -190,6 +211,8 @@ enum IS : int {
   // whose SU CRCs the framing has not seen yet (the Viterbi writes its CRC-ok
   // mask and SU count); ticks the demod recorded and the framing applied
   IS_DCD_COUNT, IS_CRC_PEND, IS_CRC_OKM, IS_CRC_NSU, IS_TICK_REC, IS_TICK_DONE,
+  // C channel framing: the 4 x 64 block index (AeroL ctor: index = 0, aerol.cpp:931)
+  IS_C_INDEX,
   IS_COUNT
 };
 
@@ -206,6 +229,10 @@ enum LS : int {
   // DCD tick k (k = 0, 1, ...: after (k + 1) * 48000 samples) happens before
   // delivered soft bit LS_TICK_SOFT0 + (k & 3) (a multiple of 32)
   LS_TICK_SOFT0, LS_TICK_SOFT_END = LS_TICK_SOFT0 + 3,
+  // C channel: samples prefiltered (the demod stops there: a message end),
+  // the current message's first sample; the 52-bit shift registers of the
+  // two dual-preamble detectors (real: r1, r2; imag: i1, i2, aerol.cpp:782-877)
+  LS_PRE_END, LS_MSG_START, LS_C_R1, LS_C_R2, LS_C_I1, LS_C_I2,
   LS_COUNT
 };
 
@@ -216,6 +243,11 @@ struct DevTables {
   const double2 *twi;      // [NFFT] inverse twiddles
   const uint8_t *scr;      // [5000] scrambler bits      decode/aerol.h:408-427
   const double *taps;      // [ntaps] RRC (OQPSK) / half-sine matched filter (MSK)
+  // C channel: JFastFir kernel spectrum and the 4096-point twiddles
+  // (decode/jfft.cpp:324-367), the coarse estimator's raised-cosine window
+  // (decode/coarsefreqestimate.cpp:60-74)
+  const double2 *cker, *tw4, *twi4;
+  const double *cwin;
 };
 
 struct DevState {
@@ -253,6 +285,9 @@ struct DevState {
   uint8_t *jobout;         // [C][JOB_OUT] (the Viterbi writes it in pinned host memory)
   int *njobs_host;         // [1] pinned host copy of the job count, written by the Viterbi kernel
   uint8_t *blocks_dbg;     // [C][2500] decoded bits (trace)
+  double2 *cpre;           // C channel: [C_PRE_RING][C] prefiltered samples (time-major)
+  double2 *csig;           // C channel: [C][C_FIR_SNZ] JFastFir sigspace (the input block)
+  double2 *crem;           // C channel: [C][C_FIR_N - C_FIR_SNZ] JFastFir remainder
   int *err;                // [1] mapped pinned device-error word (DERR_*), sticky; read by the host
 };
 

@@ -6,6 +6,7 @@
  */
 #include "tables_host.h"
 
+#include <algorithm>
 #include <cmath>
 #include <complex>
 #include <cstring>
@@ -109,6 +110,50 @@ bool host_delay_uniform(double fractdelay, int &size, int &age_old, int &age_new
     }
   }
   return true;
+}
+
+// JFFT::fft (decode/jfft.cpp:114-212) on interleaved (re, im) doubles with
+// the tables of host_twiddles; the inverse scales by 1/N as JFFT does
+void host_jfft(double *xd, int nfft, bool inverse, const double *tw, const double *twi) {
+  typedef std::complex<double> cpx;
+  cpx *x = reinterpret_cast<cpx *>(xd);
+  const cpx *TW = reinterpret_cast<const cpx *>(inverse ? twi : tw);
+  int pw = 0;
+  while ((1 << pw) < nfft) pw++;
+  for (uint32_t i = 0; i < (uint32_t)nfft; ++i) {
+    uint32_t y = i;
+    y = (((y & 0xaaaaaaaa) >> 1) | ((y & 0x55555555) << 1));
+    y = (((y & 0xcccccccc) >> 2) | ((y & 0x33333333) << 2));
+    y = (((y & 0xf0f0f0f0) >> 4) | ((y & 0x0f0f0f0f) << 4));
+    y = (((y & 0xff00ff00) >> 8) | ((y & 0x00ff00ff) << 8));
+    y = ((y >> 16) | (y << 16)) >> (32 - pw);
+    if (y > i) std::swap(x[i], x[y]);
+  }
+  for (int n = 1; n < nfft; n <<= 1)
+    for (int g = 0; g < nfft; g += 2 * n)
+      for (int j = 0; j < n; j++) {
+        const cpx y = TW[n - 1 + j] * x[g + n + j];
+        x[g + n + j] = x[g + j] - y;
+        x[g + j] += y;
+      }
+  if (inverse)
+    for (int i = 0; i < nfft; ++i) x[i] *= (1.0 / ((double)nfft));
+}
+
+// CoarseFreqEstimate::setSettings' raised-cosine window (decode/coarsefreqestimate.cpp:56-74)
+void host_coarse_window(int nfft, double lockingbw, double fs, double *window) {
+  const double hzperbin = fs / ((double)nfft);
+  const int startbin = (int)std::max(round(lockingbw / hzperbin), 1.0);
+  for (int i = 0; i < nfft; i++) window[i] = 0;
+  window[0] = 1;
+  for (int i = 1; i <= startbin; i++) {
+    double val = cos(M_PI_2 * ((double)i) / ((double)startbin));
+    val *= val;
+    if ((nfft - i) < 0) break;
+    if (i >= nfft) break;
+    window[nfft - i] = val;
+    window[i] = val;
+  }
 }
 
 void host_msk_taps(int sps, double *taps) {

@@ -16,6 +16,8 @@ bool host_delay(double fractdelay, DelayDesc &d);
 // Delay<double> of any length whose weights do not depend on the write pointer
 bool host_delay_uniform(double fractdelay, int &size, int &age_old, int &age_new, double &w, double &omw);
 // MskDemodulator matched filter, 2*sps taps (decode/mskdemodulator.cpp:126-133)
+void host_jfft(double *x, int nfft, bool inverse, const double *tw, const double *twi);  // JFFT::fft, interleaved
+void host_coarse_window(int nfft, double lockingbw, double fs, double *window);       // CoarseFreqEstimate window
 void host_msk_taps(int sps, double *taps);
 void host_scrambler(uint8_t *pre);                              // [5000]
 

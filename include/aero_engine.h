@@ -56,7 +56,10 @@ typedef struct {
 } aero_engine_cfg;
 
 typedef struct {
-  int bitrate;            /* 10500 (OQPSK), 600 or 1200 (MSK); decode/decode.h:42 */
+  int bitrate;            /* 10500 (OQPSK), 600 or 1200 (MSK); decode/decode.h:42;
+                             8400: the C channel (OqpskDemodulator at fb = 8400 +
+                             AeroL::DecodeC, decode/aerol.cpp:2145-2415), outside
+                             aero-decode's validBitRates; continuous only, fs 48000 */
   int burst;              /* 1: aero-decode --burst: 10500 bps OQPSK, or
                              600 / 1200 bps MSK (one fb = 1200 demodulator at
                              48 kHz, decode/decode.cpp:123-132)               */
@@ -163,6 +166,18 @@ int aero_pop_frames(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n)
  * (uint32 'R'/'T', uint32 length, the infofield bytes), in order
  * (decode/aerol.h:755-836). */
 int aero_pop_rt_tests(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
+
+/* C channel (bitrate 8400).  A C-channel message is one prefilter block
+ * (decode/oqpskdemodulator.cpp:292-324, output depends on message boundaries):
+ * at most 32768 samples per aero_push_pcm (AERO_E_INVALID above).
+ * c_units: the 12-byte SUs AeroL::DecodeC emits on Call_progress_Signal
+ * (CRC-valid, message 0x30, decode/aerol.cpp:2329-2346), cap / *n in SUs.
+ * voice: per decoded frame (Voicesignal, :2394-2402) a 304-byte record: uint32
+ * LE AES of the frame's last Call_progress SU (0 = "000000"), then the 300
+ * voice bytes (25 frames of 12); cap / *n in records.  Frames (36 SU bytes,
+ * CRC mask of the 3 SUs) through aero_pop_frames with AERO_F_TRACE_FRAMES. */
+int aero_pop_c_units(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
+int aero_pop_voice(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
 int aero_pop_rt_packets(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t *n);
 
 /* Timing (AERO_F_TIMING): kernel names {"demod","coarse","frame","viterbi"}
