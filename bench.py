@@ -79,6 +79,15 @@ MODES = {
                          kernels={'hilbert': 'hilbert_kernel', 'front': 'front_bmsk_kernel', 'demod': 'demod_bmsk_kernel',
                                   'trident': 'trident_bmsk_kernel', 'frame': 'frame_bmsk_kernel',
                                   'viterbi': 'rt_viterbi_kernel'}),
+    # the C channel: OQPSK 8400 with its per-message JFastFir prefilter, AeroL::DecodeC;
+    # 2 B int16 in + 16 B AGC ring r/w + soft bits out as C2 (the prefiltered-sample ring, 32 B per
+    # sample written and read, is this engine's and reported beside it); a step is one 12000-sample
+    # message per channel (the prefilter follows message boundaries, oqpskdemodulator.cpp:292-324)
+    'c8400': dict(bitrate=8400, hop=12000, fs=48000, bytes=18.22, timing='c8400_demod', preroll=8,
+                  metric='Msamples/s demod+Viterbi, 8400bps C channel (f4); SUs and voice bit-exact vs ref',
+                  cpu_seconds=240.0, config='f4 (C channel 8400)', flops=1300.0, nfft_log2=14, kind='C-channel',
+                  kernels={'prefilter': 'prefilter_c_kernel', 'demod': 'demod_c_kernel', 'coarse': 'coarse_kernel',
+                           'frame': 'frame_c_kernel', 'viterbi': 'viterbi_c_kernel'}),
     # 2 B int16 in + 0.025 B soft bits out (fb stays 600 at 24 kHz, decode/decode.cpp:142-150)
     'msk1200': dict(bitrate=1200, hop=2048, fs=24000, bytes=2.025,
                     timing='msk1200_demod', metric='Msamples/s demod+Viterbi, 1200bps MSK; ACARS frames bit-exact vs ref',
@@ -145,6 +154,9 @@ def synth_one(M, seconds, seed, k=0, lead_in=0):
         # C4: R/T bursts every 1-3 s on a carrier near 12 kHz (the burst demod has no hunter)
         return tl.synth_burst(seconds=seconds, seed=seed, carrier=12000.0 + 0.5 * (k % 64), ebn0=14.0,
                               phase0=0.1 * k, lead_in=lead_in or 24000)
+    if M['bitrate'] == 8400:
+        return tl.synth_c(seconds=seconds, seed=seed, carrier=12000.0 + 0.5 * (k % 64), ebn0=12.0, phase0=0.1 * k,
+                          lead_in=lead_in)
     if M['bitrate'] == 10500:
         # seed 0xAE20+k, carrier 12000 + 37.5 + 0.5 k Hz, Eb/N0 12 dB
         return tl.synth(seconds=seconds, seed=seed, carrier=12037.5 + 0.5 * (k % 64), ebn0=12.0, phase0=0.1 * k,
@@ -224,9 +236,9 @@ def cpu_baseline(mode, M, seconds, procs, runs=3):
         nvis = os.cpu_count() or 1
     med = sorted(rates)[len(rates) // 2]
     out = {'value': round(med, 4), 'unit': 'Msamples/s', 'cores': procs, 'kind': 'port',
-           'sample': '%d processes x %.0f s of synthetic %d-bps P-channel (%d Hz int16) through '
-                     'oracle/liboracle.so (demod + coarse + hunter + AeroL + Viterbi + ACARS), '
-                     '%d-sample messages; median of %d runs (%.1f s CPU each)' % (
+           'sample': ('%d processes x %.0f s of synthetic %d-bps ' + M.get('kind', 'P-channel') + ' (%d Hz int16) '
+                      'through oracle/liboracle.so (demod + coarse + hunter + AeroL + Viterbi + ACARS), '
+                      '%d-sample messages; median of %d runs (%.1f s CPU each)') % (
                          procs, seconds, M['bitrate'], M['fs'], M['fs'] // 4, len(rates), sorted(cpus)[len(cpus) // 2]),
            'runs_msps': [round(v, 4) for v in rates],
            'one_core_msps': round(sorted(ones)[len(ones) // 2], 4), 'cpu_model': cpu_model(),
@@ -245,7 +257,7 @@ def _cpu_one(arg):
     M, seconds, seed = arg
     import aero_testlib as tl
     pcm = synth_one(M, seconds, seed, lead_in=1000)
-    o = tl.Oracle(bitrate=M['bitrate'], burst=bool(M.get('burst')))
+    o = tl.Oracle(bitrate=M['bitrate'], burst=bool(M.get('burst')), dcd_tick=bool(M.get('dcd_tick')))
     t = time.perf_counter()
     o.push_chunked(pcm, M['fs'] // 4)
     return len(pcm), time.perf_counter() - t
@@ -698,7 +710,9 @@ def main():
     # CPU baseline first, in worker processes forked before this process touches the GPU
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(a.mode, M, a.cpu_seconds or M['cpu_seconds'], a.cpu_procs or host_cores(), a.cpu_runs)
+        # the oracle runs what the GPU runs: the DCD timer on the P channel unless --no-dcd-tick
+        Mc = dict(M, dcd_tick=M['bitrate'] == 10500 and not M.get('burst') and not a.no_dcd_tick)
+        cpu = cpu_baseline(a.mode, Mc, a.cpu_seconds or M['cpu_seconds'], a.cpu_procs or host_cores(), a.cpu_runs)
 
     import torch
     import torch.distributed as dist
@@ -756,6 +770,8 @@ def main():
         kt = {k: eng.timing('burst_' + k) for k in ('hilbert', 'front', 'demod', 'trident', 'frame', 'viterbi')}
     else:
         kt = {k: eng.timing(tag + k) for k in ('demod', 'coarse', 'frame', 'viterbi')}
+        if 'prefilter' in M['kernels']:
+            kt['prefilter'] = eng.timing(tag + 'prefilter')
     ht = {k: eng.timing(k) for k in ('host_push', 'host_run', 'host_wait_njobs', 'host_wait_jobs', 'host_frames')}
     del timed_inputs
     h2d = None
@@ -883,10 +899,12 @@ def main():
                                     '%d Hz int16, one %d-sample message per channel per step' % (
                                         M['config'], C, M['bitrate'], 'OQPSK' if M['bitrate'] == 10500 else 'MSK',
                                         FS, HOP)) if burst else (
-                                   '%s x %d: independent single-VFO %d-bps continuous %s P-channels '
-                                   'per GPU, %d Hz int16, one %d-sample hop per step' % (
-                                       M['config'], C, M['bitrate'], 'OQPSK' if M['bitrate'] == 10500 else 'MSK',
-                                       FS, HOP)),
+                                   '%s x %d: independent single-VFO %d-bps continuous %s %ss '
+                                   'per GPU, %d Hz int16, one %d-sample %s per step' % (
+                                       M['config'], C, M['bitrate'],
+                                       'OQPSK' if M['bitrate'] in (10500, 8400) else 'MSK',
+                                       M.get('kind', 'P-channel'), FS, HOP,
+                                       'message' if M['bitrate'] == 8400 else 'hop')),
                        'channels_per_gpu': C, 'total_channels': C * world, 'hop_samples': HOP,
                        'dcd_tick': (not a.no_dcd_tick) and not burst and M['bitrate'] == 10500,
                        'parallelism': 'channel-sharded x%d' % world},
@@ -933,7 +951,8 @@ def main():
     eng.close()
     if use_dist:
         dist.destroy_process_group()
-    if rank == 0 and (stats[stat_names[0]] <= 0 or stats['acars_items'] <= 0):
+    decoded = stats['su_crc_ok'] if M['bitrate'] == 8400 else stats['acars_items']  # C: SUs, no ACARS
+    if rank == 0 and (stats[stat_names[0]] <= 0 or decoded <= 0):
         # the metric names demod + Viterbi: a timed region without decoded frames measured something else
         print('bench: timed region decoded no Viterbi jobs / ACARS items (%s)' % stats, file=sys.stderr)
         sys.exit(3)
