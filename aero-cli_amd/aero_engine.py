@@ -403,7 +403,8 @@ class Engine:
         self.lib.aero_timing_reset(self.h)
 
     def stat(self, name):
-        """aero_stat counter: 'viterbi_jobs', 'frames' or 'su_crc_ok'."""
+        """aero_stat counter: 'viterbi_jobs', 'frames', 'su_crc_ok' (and burst 'rt_*'), or the
+        continuous groups' 'device_bytes' / 'groups'."""
         v = ctypes.c_uint64()
         _check(self.lib.aero_stat(self.h, name.encode(), ctypes.byref(v)), 'aero_stat')
         return int(v.value)

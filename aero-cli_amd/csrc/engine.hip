@@ -64,6 +64,7 @@ using namespace aero;
 
 namespace {
 
+constexpr int GENERIC_GROUP_CAP = 256;  // channels per generic-rate MSK group
 constexpr long long PCM_CAP = 65536;  // per-channel PCM ring: a second of 48 kHz audio per run without an early pass
 constexpr int PT_CAP = 4096;
 constexpr int HOP_CAP = 64;
@@ -311,6 +312,7 @@ struct aero_engine {
   std::vector<std::pair<int, int>> chmap;  // engine channel -> (gid or MODE_BURST + kind, local index)
   std::unique_ptr<HostPool> hpool;
   std::map<std::string, TimingSlot> timing;  // engine-level host sections
+  uint64_t retired_jobs = 0, retired_frames = 0, retired_su_ok = 0;  // counters of released groups
 };
 
 namespace {
@@ -1179,7 +1181,12 @@ int group_create(aero_engine *E, int mode, int gid, int fs, std::unique_ptr<Grou
     e->g = mode_geom(mode);
     e->tag = tags[mode];
   }
+  // a generic-rate MSK group serves the channels that happen to arrive at
+  // its rate: a small pool (another group of the rate opens when it is
+  // full), not max_channels (one 96 kHz channel of a 65536-channel engine
+  // would otherwise ask for ~50 GB of AGC ring)
   e->C = (E->max_channels + 63) & ~63;
+  if (msk_generic(mode)) e->C = std::min(e->C, GENERIC_GROUP_CAP);
   DevState S{};
   DevTables T{};
   const size_t bytes = layout(S, T, mode, e->g, e->C, e->flags, nullptr) + 4096;
@@ -1616,15 +1623,25 @@ int msk_gid(aero_engine *e, int bitrate, int fs, int &gid) {
     return AERO_OK;
   }
   const int gm = bitrate == 600 ? MODE_MSKG600 : MODE_MSKG1200;
-  for (size_t k = MODE_COUNT; k < e->groups.size(); k++)
-    if (e->groups[k] && e->groups[k]->mode == gm && e->groups[k]->g.fs == fs) {
+  int free_gid = -1;
+  for (size_t k = MODE_COUNT + 1; k < e->groups.size(); k++) {
+    Group *h = e->groups[k].get();
+    if (!h) {
+      if (free_gid < 0) free_gid = (int)k;  // a retired group's slot
+      continue;
+    }
+    if (h->mode == gm && h->g.fs == fs && (h->nch < h->C || !h->free_slots.empty())) {
       gid = (int)k;
       return AERO_OK;
     }
+  }
   std::unique_ptr<Group> g;
-  if (int rc = group_create(e, gm, (int)e->groups.size(), fs, g)) return rc;
-  gid = (int)e->groups.size();
-  e->groups.push_back(std::move(g));
+  gid = free_gid >= 0 ? free_gid : (int)e->groups.size();
+  if (int rc = group_create(e, gm, gid, fs, g)) return rc;
+  if (free_gid >= 0)
+    e->groups[gid] = std::move(g);
+  else
+    e->groups.push_back(std::move(g));
   return AERO_OK;
 }
 
@@ -1794,6 +1811,14 @@ int msk_migrate(aero_engine *e, int ch, uint32_t fs) {
   // samples left: the group ran and drained it above)
   g->gch[c] = -1;
   g->free_slots.push_back(c);
+  // a generic-rate group nobody is left in is released (its device pool,
+  // stream and pinned buffers); its counters stay in the engine's totals
+  if (msk_generic(g->mode) && (int)g->free_slots.size() == g->nch) {
+    e->retired_jobs += g->st_jobs.load();
+    e->retired_frames += g->st_frames.load();
+    e->retired_su_ok += g->st_su_ok.load();
+    e->groups[from].reset();
+  }
   return AERO_OK;
 }
 
@@ -2201,8 +2226,14 @@ int aero_stat(aero_engine *e, const char *name, uint64_t *value) {
   uint64_t v = 0;
   const std::string n(name);
   if (n != "rt_tests" && n != "rt_packets" && n != "rt_pass_max" && n != "viterbi_jobs" && n != "frames" &&
-      n != "su_crc_ok")
+      n != "su_crc_ok" && n != "device_bytes" && n != "groups")
     return AERO_E_INVALID;
+  if (n == "device_bytes" || n == "groups") {  // continuous groups' device pools, and how many exist
+    for (auto &g : e->groups)
+      if (g) v += n == "groups" ? 1 : (uint64_t)g->pool_bytes;
+    *value = v;
+    return AERO_OK;
+  }
   if (n == "rt_pass_max") {
     *value = std::max(burst_stat(e->burst[0], 2), burst_stat(e->burst[1], 2));
     return AERO_OK;
@@ -2211,6 +2242,7 @@ int aero_stat(aero_engine *e, const char *name, uint64_t *value) {
     *value = burst_stat(e->burst[0], n == "rt_packets") + burst_stat(e->burst[1], n == "rt_packets");
     return AERO_OK;
   }
+  v = n == "viterbi_jobs" ? e->retired_jobs : (n == "frames" ? e->retired_frames : e->retired_su_ok);
   for (auto &g : e->groups) {
     if (!g) continue;
     if (n == "viterbi_jobs")

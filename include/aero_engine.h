@@ -115,7 +115,10 @@ int aero_push_pcm(aero_engine *e, int ch, const int16_t *pcm, size_t n, uint32_t
  * must be of one kind (continuous bit rate, burst OQPSK or burst MSK).  For
  * burst channels the batch is one message per channel (at most 16384
  * samples; burst OQPSK output depends on message boundaries,
- * decode/burstoqpskdemodulator.cpp:264). */
+ * decode/burstoqpskdemodulator.cpp:264).  The channels must have been opened
+ * in order into one group (engine channel j is the group's slot j): once an
+ * MSK rate change has moved a channel into a slot another channel left, that
+ * group no longer qualifies (AERO_E_INVALID; push per channel instead). */
 int aero_push_pcm_batch(aero_engine *e, const int16_t *pcm, size_t n, size_t ld, int nch, int dev);
 
 /* aero_push_pcm with pcm a HIP device pointer (e.g. channeliser audio already
@@ -188,7 +191,10 @@ int aero_pop_rt_packets(aero_engine *e, int ch, uint8_t *dst, size_t cap, size_t
 int aero_timing(aero_engine *e, const char *name, double *ms, long *launches);
 void aero_timing_reset(aero_engine *e);
 
-/* Counters since creation.  Continuous channels: "viterbi_jobs" (blocks
+/* Counters since creation.  "device_bytes" / "groups": the device pools of
+ * the continuous channel groups that exist now and their number (a
+ * generic-rate MSK group holds at most 256 channels and is released when its
+ * last channel moves to another rate).  Continuous channels: "viterbi_jobs" (blocks
  * the GPU Viterbi decoded and handed back), "frames" (frames delivered to
  * the SU/ACARS host), "su_crc_ok" (SUs whose CRC-16 checked); burst
  * channels: "rt_tests" (RTChannelDeleaveFECScram decodes run),

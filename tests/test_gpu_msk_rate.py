@@ -171,3 +171,38 @@ def test_msk_rate_change_in_a_full_group(engine_lib):
         assert h.shape == rh.shape and np.array_equal(h.view(np.int64), rh.view(np.int64)), ch
         assert eng.items(ch) == o.item_lines('A'), 'channel %d items differ' % ch
     eng.close()
+
+
+def test_generic_groups_small_and_released(engine_lib):
+    """A 65536-channel engine whose one MSK channel moves through generic
+    rates: each generic-rate group holds at most 256 channels (a 96 kHz group
+    sized for 65536 would ask for ~50 GB of AGC ring), a group is released
+    when its last channel leaves, a rate's group is re-created when the
+    channel comes back, and the channel still equals the oracle."""
+    import aero_engine as ae
+    segs = [(15000, 4.0, 0xE400, 1800.0, 14.0), (96000, 2.0, 0xE401, 1800.0, 14.0),
+            (18750, 4.0, 0xE402, 1800.0, 14.0), (40000, 3.0, 0xE403, 1800.0, 14.0),
+            (15000, 10.0, 0xE404, 1800.0, 14.0)]
+    msgs = _messages(600, segs, 0.25)
+    eng = ae.Engine(max_channels=65536, flags=ae.F_TRACE_SOFT | ae.F_TRACE_HOPS | ae.F_TRACE_FRAMES)
+    ch = eng.open_channel(600, 15000)
+    last_fs, peak = None, 0
+    for pcm, fs in msgs:
+        eng.push(ch, pcm, fs=fs)
+        eng.run()
+        if fs != last_fs:
+            # one group alive (the channel's), sized for 256 channels
+            assert eng.stat('groups') == 1, 'a left generic group was kept'
+            peak = max(peak, eng.stat('device_bytes'))
+            last_fs = fs
+    eng.flush()
+    assert peak < (2 << 30), 'generic group pools too large: %d bytes' % peak
+    o = tl.Oracle(bitrate=600)
+    for pcm, fs in msgs:
+        o.push(pcm, fs=fs)
+    sb, rsb = eng.softbits(ch), o.softbits()
+    assert len(rsb) > 1000 and np.array_equal(sb, rsb)
+    h, rh = eng.hops(ch), o.hops()
+    assert h.shape == rh.shape and np.array_equal(h.view(np.int64), rh.view(np.int64))
+    assert np.array_equal(eng.frames(ch), o.frames())
+    eng.close()
