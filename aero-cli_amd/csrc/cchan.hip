@@ -2,15 +2,15 @@
  * cchan.hip — the C channel: 8400-bps OQPSK (OqpskDemodulator at fb = 8400)
  * and AeroL::DecodeC on gfx950.
  *
- *  prefilter_c_kernel : the per-message prefilter of OqpskDemodulator::writeData
- *                       (decode/oqpskdemodulator.cpp:292-324): down-mix by
+ *  prefilter_dn_kernel  the per-message prefilter of OqpskDemodulator::writeData
+ *  prefilter_blk_kernel (decode/oqpskdemodulator.cpp:292-324): down-mix by
  *                       mixer_fir_pre, JFastFir (RRC 0.6, 2049 taps, 4096-point
  *                       overlap-add blocks of 2048, decode/jfft.cpp:324-367,
  *                       445-495), up-mix by the conjugate from the phase saved
- *                       at the message start.  One workgroup per channel with a
- *                       message due; the two phase-pointer recurrences run on
- *                       one lane each, the FFTs (JFFT's radix-2 DIT, bit for bit)
- *                       over the LDS.
+ *                       at the message start.  The down-mix's phase pointer on
+ *                       one lane per channel, the block transforms by one
+ *                       workgroup per channel in registers (fft_dit.h), the
+ *                       up-mix in the demod as it reads each sample.
  *  demod_c_kernel     : the per-sample loop at fb = 8400 (:331-553): no RRC FIR
  *                       (the prefilter is the matched filter), its own timer
  *                       delays / resonator / ee, the carrier loop with faster
@@ -38,6 +38,7 @@
 
 #include "aero_math.h"
 #include "engine_common.h"
+#include "fft_dit.h"
 #include "viterbi_dev.h"
 
 namespace aero {
@@ -96,115 +97,123 @@ __device__ __forceinline__ int c_qround(double d) {  // qRound (Qt 5.9 qglobal.h
   return d >= 0.0 ? int(d + 0.5) : int(d - double(int(d - 1)) + 0.5) + int(d - 1);
 }
 
-// JFFT::fft (decode/jfft.cpp:114-212) of 4096 points in the LDS, 256 threads:
-// the bit-reversal swaps, then every radix-2 stage with the reference's
-// operands and twiddle TW[n - 1 + j]; the inverse scales by 1/N
-__device__ void c_jfft(double2 *x, const double2 *TW, bool inverse, int t) {
-  constexpr int N = C_FIR_N, NT = 256;
-  for (int i = t; i < N; i += NT) {
-    const int j = (int)(__builtin_bitreverse32((uint32_t)i) >> (32 - 12));
-    if (j > i) {
-      const double2 a = x[i];
-      x[i] = x[j];
-      x[j] = a;
-    }
-  }
-  __syncthreads();
-  for (int n = 1; n < N; n <<= 1) {
-    for (int b = t; b < N / 2; b += NT) {
-      const int j = b & (n - 1);
-      const int k = 2 * (b - j) + j, l = k + n;
-      const double2 w = TW[n - 1 + j], xl = x[l], xk = x[k];
-      const double yr = w.x * xl.x - w.y * xl.y, yi = w.x * xl.y + w.y * xl.x;
-      x[l] = make_double2(xk.x - yr, xk.y - yi);
-      x[k] = make_double2(xk.x + yr, xk.y + yi);
-    }
-    __syncthreads();
-  }
-  if (inverse) {
-    for (int i = t; i < N; i += NT) {
-      x[i].x *= (1.0 / ((double)N));
-      x[i].y *= (1.0 / ((double)N));
-    }
-    __syncthreads();
-  }
-}
-
 }  // namespace
 
-__global__ __launch_bounds__(256) void prefilter_c_kernel(DevState S, DevTables T, const CPreJob *jobs) {
-  __shared__ double2 buf[C_FIR_N];  // the FFT block; [0, C_FIR_SNZ) is sigspace between FFTs
-  __shared__ uint16_t idn[C_FIR_SNZ], iup[C_FIR_SNZ];
-  __shared__ double fin_ptr;
-  const CPreJob J = jobs[blockIdx.x];
-  const int c = J.c, t = threadIdx.x, C = S.C;
+// The per-message prefilter (decode/oqpskdemodulator.cpp:292-324) in three
+// parts, each in the layout its work wants:
+//  1. prefilter_dn_kernel, one lane per channel: the down-mix's phase pointer
+//     (a serial recurrence) over the message, with the PCM rows read
+//     coalesced; each sample's table index and pcm word go to the channel's
+//     run of `cin`.  It also restores the saved phase for the up-mix
+//     (GetPhaseDeg / SetPhaseDeg, DSP.cpp:177-200) into DS_FP_PTR.
+//  2. prefilter_blk_kernel, one 256-thread workgroup per channel: JFastFir
+//     (jfft.cpp:445-495) block by block, each 4096-point transform pair in
+//     registers (fft_dit.h); the outputs into the channel's run of `cout`.
+//  3. the up-mix by WTCISValue_conj from the restored phase, in
+//     demod_c_kernel as it reads each sample (the pointer advances with the
+//     step the message started with; the demod retunes it only at the end).
+__global__ __launch_bounds__(64) void prefilter_dn_kernel(DevState S, const CPreJob *jobs, int njobs) {
+  const int q = blockIdx.x * 64 + threadIdx.x;
+  if (q >= njobs) return;
+  const CPreJob J = jobs[q];
+  const int c = J.c, C = S.C;
   const long long capm = S.pcm_cap - 1;
-  double2 *sig = S.csig + (size_t)c * C_FIR_SNZ;
-  double2 *rem = S.crem + (size_t)c * (C_FIR_N - C_FIR_SNZ);
-  for (int r = t; r < C_FIR_SNZ; r += 256) buf[r] = sig[r];
   double fp_step = S.ds[DS_FP_STEP * C + c];
-  double dn_ptr = 0, up_ptr = 0;
-  if (t == 0) dn_ptr = S.ds[DS_FP_PTR * C + c];
-  if (t == 64) {  // savedphase = GetPhaseDeg() (DSP.cpp:200), SetPhaseDeg(savedphase) (:177-187)
-    const double ptr0 = S.ds[DS_FP_PTR * C + c];
-    double ph = (360.0 * ptr0 / ((double)WTSIZE));
+  double dn_ptr = S.ds[DS_FP_PTR * C + c];
+  {  // savedphase = GetPhaseDeg() (DSP.cpp:200), SetPhaseDeg(savedphase) (:177-187)
+    double ph = (360.0 * dn_ptr / ((double)WTSIZE));
     ph = fmod(ph, 360.0);
     while (ph < 0) ph += 360.0;
-    up_ptr = (ph / 360.0) * ((double)WTSIZE);
+    S.ds[DS_FP_PTR * C + c] = (ph / 360.0) * ((double)WTSIZE);
+  }
+  uint32_t *cin = S.cin + (size_t)c * C_IN_RING;
+  long long n = J.s;
+  // eight PCM rows in flight ahead of the chain
+  for (; n + 8 <= J.e; n += 8) {
+    int16_t x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = S.pcm[(size_t)((n + k) & capm) * C + c];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      cin[(n + k) & (C_IN_RING - 1)] = (uint32_t)c_cis_index(dn_ptr) | ((uint32_t)(uint16_t)x[k] << 16);
+      c_nco_next(dn_ptr, fp_step);
+    }
+  }
+  for (; n < J.e; ++n) {
+    const int16_t x = S.pcm[(size_t)(n & capm) * C + c];
+    cin[n & (C_IN_RING - 1)] = (uint32_t)c_cis_index(dn_ptr) | ((uint32_t)(uint16_t)x << 16);
+    c_nco_next(dn_ptr, fp_step);
+  }
+  S.ls[LS_PRE_END * C + c] = J.e;
+  S.ls[LS_MSG_START * C + c] = J.s;
+}
+
+// JFastFir::update over one message [s, e): sample n's output is the value
+// the block transform at 2048 * floor(n / 2048) left in sigspace (zero
+// before the first); that transform runs before sample n = 2048 B > 0 is
+// pushed, on the down-mixed inputs of samples [n - 2048, n) and zeros:
+// y = IFFT(FFT(block) * K) / 4096; outputs y[k] + remainder[k] (k < 2048);
+// the remainder becomes y[2048 + k].  Outputs of samples past the message
+// wait in `csig` for the next one.
+__global__ __launch_bounds__(256, 2) void prefilter_blk_kernel(DevState S, DevTables T, const CPreJob *jobs) {
+  constexpr int L = 12, PADDED = C_FIR_N + C_FIR_N / 16;
+  static_assert(C_FIR_N == 1 << L && C_FIR_SNZ == C_FIR_N / 2, "4096-point blocks of 2048 inputs");
+  __shared__ double lds[PADDED];
+  __shared__ double2 s_tw[TwLds<L>::LEN];
+  const CPreJob J = jobs[blockIdx.x];
+  const int c = J.c, t = threadIdx.x;
+  load_tw_lds<L>(s_tw, T.tw4, t, 256);
+  const uint32_t *cin = S.cin + (size_t)c * C_IN_RING;
+  double2 *out = S.cout + (size_t)c * C_OUT_RING;
+  double2 *pend = S.csig + (size_t)c * C_FIR_SNZ;
+  double2 *rem = S.crem + (size_t)c * (C_FIR_N - C_FIR_SNZ);
+  const long long s = J.s, e = J.e;
+  if (s % C_FIR_SNZ != 0 || s == 0) {  // the samples before the message's first transform
+    const long long be = (s / C_FIR_SNZ + 1) * C_FIR_SNZ < e ? (s / C_FIR_SNZ + 1) * C_FIR_SNZ : e;
+    for (long long n = s + t; n < be; n += 256) out[n & (C_OUT_RING - 1)] = pend[n & (C_FIR_SNZ - 1)];
   }
   __syncthreads();
-  for (long long pos = J.s; pos < J.e;) {
-    if (pos > 0 && pos % C_FIR_SNZ == 0) {  // sigspace full: JFastFir's convolution before this sample
-      for (int r = C_FIR_SNZ + t; r < C_FIR_N; r += 256) buf[r] = make_double2(0.0, 0.0);
-      __syncthreads();
-      c_jfft(buf, T.tw4, false, t);
-      for (int k = t; k < C_FIR_N; k += 256) {  // *psigspace *= *pkernel
-        const double2 a = buf[k], kk = T.cker[k];
-        buf[k] = make_double2(a.x * kk.x - a.y * kk.y, a.x * kk.y + a.y * kk.x);
+  for (long long p = (s + C_FIR_SNZ - 1) / C_FIR_SNZ * C_FIR_SNZ; p < e; p += C_FIR_SNZ) {
+    if (p == 0) continue;
+    double2 x[16];
+    // (t laundered per loop: the compiler would otherwise keep every loop's
+    // per-value addresses live across the transforms, which spills)
+    const int t0 = fresh(t);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {  // inputs [p - 2048, p) (mixer_fir_pre.WTCISValue() * dval), then zeros
+      const int q = bitrev<L>(epos<L, 0>(t0, i));
+      if (q < C_FIR_SNZ) {
+        const uint32_t w = cin[(p - C_FIR_SNZ + q) & (C_IN_RING - 1)];
+        const double dval = ((double)(int16_t)(w >> 16)) / 32768.0;
+        const double2 cs = T.cis[w & 0xFFFF];
+        x[i] = make_double2(cs.x * dval, cs.y * dval);
+      } else {
+        x[i] = make_double2(0.0, 0.0);
       }
-      __syncthreads();
-      c_jfft(buf, T.twi4, true, t);
-      for (int k = t; k < C_FIR_N - C_FIR_SNZ; k += 256) {  // overlap
-        const double2 r = rem[k];
-        buf[k] = make_double2(buf[k].x + r.x, buf[k].y + r.y);
-        rem[k] = buf[C_FIR_SNZ + k];
-      }
-      __syncthreads();
     }
-    const long long cend = J.e < (pos / C_FIR_SNZ + 1) * C_FIR_SNZ ? J.e : (pos / C_FIR_SNZ + 1) * C_FIR_SNZ;
-    const int m = (int)(cend - pos), r0 = (int)(pos % C_FIR_SNZ);
-    // the down- and up-mix phase pointers, each a serial recurrence, on lanes of two waves
-    if (t == 0)
-      for (int k = 0; k < m; ++k) {
-        idn[k] = (uint16_t)c_cis_index(dn_ptr);
-        c_nco_next(dn_ptr, fp_step);
-      }
-    if (t == 64)
-      for (int k = 0; k < m; ++k) {
-        iup[k] = (uint16_t)c_cis_index(up_ptr);
-        c_nco_next(up_ptr, fp_step);
-      }
-    __syncthreads();
-    for (int k = t; k < m; k += 256) {
-      const long long n = pos + k;
-      const double dval = ((double)S.pcm[(size_t)(n & capm) * C + c]) / 32768.0;
-      const double2 cs = T.cis[idn[k]];
-      const double2 o = buf[r0 + k];  // JFastFir::update: pop the processed value, push the new one
-      buf[r0 + k] = make_double2(cs.x * dval, cs.y * dval);
-      const double2 cu = T.cis[iup[k]];
-      const double cr = cu.x, ci = -cu.y;  // *= WTCISValue_conj()
-      S.cpre[(size_t)(n & (C_PRE_RING - 1)) * C + c] = make_double2(o.x * cr - o.y * ci, o.x * ci + o.y * cr);
+    fft_dit<L, false>(x, t, lds, T.tw4, s_tw);
+    const int t1 = fresh(t);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {  // *psigspace *= *pkernel
+      const double2 k = T.cker[epos<L, 2>(t1, i)];
+      x[i] = make_double2(x[i].x * k.x - x[i].y * k.y, x[i].x * k.y + x[i].y * k.x);
+    }
+    exchange<L, 2, 0, true>(x, t, lds);
+    fft_dit<L, true>(x, t, lds, T.twi4, s_tw);
+    // positions t + 256 i: registers 0-7 hold the outputs, 8-15 the next
+    // remainder, so a thread reads and replaces only its own remainder slots
+    const bool last = p + C_FIR_SNZ >= e;
+    const int t2 = fresh(t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = epos<L, 2>(t2, i);
+      const double2 r = rem[k];
+      const double2 y = make_double2(x[i].x * (1.0 / ((double)C_FIR_N)) + r.x, x[i].y * (1.0 / ((double)C_FIR_N)) + r.y);
+      if (p + k < e) out[(p + k) & (C_OUT_RING - 1)] = y;
+      if (last) pend[k] = y;
+      rem[k] = make_double2(x[i + 8].x * (1.0 / ((double)C_FIR_N)), x[i + 8].y * (1.0 / ((double)C_FIR_N)));
     }
     __syncthreads();
-    pos = cend;
-  }
-  for (int r = t; r < C_FIR_SNZ; r += 256) sig[r] = buf[r];
-  if (t == 64) fin_ptr = up_ptr;
-  __syncthreads();
-  if (t == 0) {
-    S.ds[DS_FP_PTR * C + c] = fin_ptr;  // after the up-mix
-    S.ls[LS_PRE_END * C + c] = J.e;
-    S.ls[LS_MSG_START * C + c] = J.s;
   }
 }
 
@@ -279,11 +288,20 @@ __global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, in
   double2 *dtb = S.dt + (size_t)c * DT_LEN;
   double2 *pmsb = reinterpret_cast<double2 *>(S.pm) + (size_t)c * MSE_LEN;
   uint8_t *soft = S.soft + (size_t)c * SOFT_RING;
+  const double2 *cout = S.cout + (size_t)c * C_OUT_RING;
+  double up_ptr = S.ds[DS_FP_PTR * C + c], fp_step = S.ds[DS_FP_STEP * C + c];
   const double PT = 0.65 * WTSIZE;  // IfHavePassedPoint(ee), ee = 0.65 at 8400 (:213)
   int i = 0;
   for (; i < ie; ++i) {
     const long long n = n0 + i;
-    const double2 pre = S.cpre[(size_t)(n & (C_PRE_RING - 1)) * C + c];
+    double2 pre;
+    {  // the prefilter's up-mix: *= mixer_fir_pre.WTCISValue_conj(), WTnextFrame() (:316-322)
+      const double2 o = cout[n & (C_OUT_RING - 1)];
+      const double2 cu = T.cis[c_cis_index(up_ptr)];
+      c_nco_next(up_ptr, fp_step);
+      const double cr = cu.x, ci = -cu.y;
+      pre = make_double2(o.x * cr - o.y * ci, o.x * ci + o.y * cr);
+    }
     const double2 cm = T.cis[c_cis_index(m2_ptr)];
     // mix only: sig2 = mixer2.WTCISValue() * cval_prefiltered[i] (:376-385)
     double s2r = cm.x * pre.x - cm.y * pre.y, s2i = cm.x * pre.y + cm.y * pre.x;
@@ -438,6 +456,7 @@ __global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, in
   double *ds = S.ds + c;
   int *is = S.is + c;
   long long *ls = S.ls + c;
+  ds[DS_FP_PTR * C] = up_ptr;
   if (n0 + i == pre_end) {  // end of the message: mixer_fir_pre.SetFreq(mixer2_freq_sum / i) (:555-557)
     double f = m2_fsum / ((double)(pre_end - ls[LS_MSG_START * C]));
     double st = 0;
@@ -726,8 +745,9 @@ __global__ __launch_bounds__(64) void viterbi_c_kernel(DevState S, DevTables T) 
 }
 
 void launch_prefilter_c(hipStream_t st, const DevState &S, const DevTables &T, const void *jobs, int njobs) {
-  if (njobs > 0)
-    hipLaunchKernelGGL(prefilter_c_kernel, dim3(njobs), dim3(256), 0, st, S, T, (const CPreJob *)jobs);
+  if (njobs <= 0) return;
+  hipLaunchKernelGGL(prefilter_dn_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, S, (const CPreJob *)jobs, njobs);
+  hipLaunchKernelGGL(prefilter_blk_kernel, dim3(njobs), dim3(256), 0, st, S, T, (const CPreJob *)jobs);
 }
 void launch_demod_c(hipStream_t st, const DevState &S, const DevTables &T, int nch, bool trace) {
   const dim3 g((nch + 63) / 64), b(64);

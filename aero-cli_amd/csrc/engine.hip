@@ -362,7 +362,8 @@ size_t layout(DevState &S, DevTables &T, int mode, const ModeGeom &g, int C, int
   S.jobout = carve<uint8_t>(p, (size_t)JOB_OUT * C);
   S.blocks_dbg = carve<uint8_t>(p, (flags & AERO_F_TRACE_BLOCKS) ? (size_t)2500 * C : 1);
   const bool cch = mode == MODE_C8400;
-  S.cpre = carve<double2>(p, cch ? (size_t)C_PRE_RING * C : 1);
+  S.cin = carve<uint32_t>(p, cch ? (size_t)C_IN_RING * C : 1);
+  S.cout = carve<double2>(p, cch ? (size_t)C_OUT_RING * C : 1);
   S.csig = carve<double2>(p, cch ? (size_t)C_FIR_SNZ * C : 1);
   S.crem = carve<double2>(p, cch ? (size_t)(C_FIR_N - C_FIR_SNZ) * C : 1);
   T.cker = carve<double2>(p, cch ? C_FIR_N : 1);
@@ -502,6 +503,10 @@ int reset_slot(Group *e, int c) {
   HIPCHK(row(S.overlap, 64));
   HIPCHK(row(S.dl2, (size_t)g.dl2_len));
   if (e->flags & AERO_F_TRACE_BLOCKS) HIPCHK(row(S.blocks_dbg, 2500));
+  if (e->mode == MODE_C8400) {  // JFastFir's state: no outputs yet, no remainder
+    HIPCHK(row(S.csig, (size_t)16 * C_FIR_SNZ));
+    HIPCHK(row(S.crem, (size_t)16 * (C_FIR_N - C_FIR_SNZ)));
+  }
   HIPCHK(hipStreamSynchronize(st));
   return init_scalars(e, c, c + 1);
 }

@@ -74,7 +74,8 @@ constexpr int C_DL2_LEN = 2709;       // dl2.setLength(2714 - 6) + 1
 constexpr int C_PAYLOAD = 2714;       // deconvol.resize(2714) (aerol.cpp:2249)
 constexpr int C_FIR_N = 4096;         // fir_pre.SetKernel(RRC 0.6 x 2049 taps, 4096) (oqpskdemodulator.cpp:228-236)
 constexpr int C_FIR_SNZ = 2048;       // signal_non_zero_size = 4096 + 1 - 2049 (jfft.cpp:347-352)
-constexpr int C_PRE_RING = 65536;     // prefiltered samples per channel (a message fits: PCM ring 65536)
+constexpr int C_OUT_RING = 32768;     // prefiltered (before the up-mix) samples per channel: one message, <= half the PCM ring
+constexpr int C_IN_RING = 65536;      // down-mix words per channel: a message plus the block it starts in
 constexpr int JOB_OUT_C = 352;        // 36 SU bytes + 300 voice bytes + len, mask, AES, channel
 // MSK sample rates served.  Below 12000 the coarse estimator's fold search
 // would read y bins outside the range every MSK group keeps (MSK_YLO..MSK_YHI,
@@ -285,8 +286,9 @@ struct DevState {
   uint8_t *jobout;         // [C][JOB_OUT] (the Viterbi writes it in pinned host memory)
   int *njobs_host;         // [1] pinned host copy of the job count, written by the Viterbi kernel
   uint8_t *blocks_dbg;     // [C][2500] decoded bits (trace)
-  double2 *cpre;           // C channel: [C_PRE_RING][C] prefiltered samples (time-major)
-  double2 *csig;           // C channel: [C][C_FIR_SNZ] JFastFir sigspace (the input block)
+  uint32_t *cin;           // C channel: [C][C_IN_RING] the down-mix's table index | pcm << 16 per sample
+  double2 *cout;           // C channel: [C][C_OUT_RING] JFastFir outputs (the up-mix is the demod's)
+  double2 *csig;           // C channel: [C][C_FIR_SNZ] outputs of the last block transform (samples past its message)
   double2 *crem;           // C channel: [C][C_FIR_N - C_FIR_SNZ] JFastFir remainder
   int *err;                // [1] mapped pinned device-error word (DERR_*), sticky; read by the host
 };

@@ -1,12 +1,13 @@
 /*
  * fft_dit.h — JFFT's radix-2 decimation-in-time FFT (decode/jfft.cpp:114-212)
- * for one 8192- or 16384-point transform per workgroup of N/16 threads on
- * gfx950: 16 complex FP64 values per thread in registers, four register
- * phases of up to four stages with padded LDS transposes between them.  Every
+ * for one 4096-, 8192- or 16384-point transform per workgroup of N/16 threads
+ * on gfx950: 16 complex FP64 values per thread in registers, three (4096) or
+ * four register phases of up to four stages with padded LDS transposes
+ * between them.  Every
  * butterfly uses the reference's operands and twiddle (TW[n - 1 + k]), so the
  * result is bit-identical to JFFT however the butterflies are scheduled.
- * Used by coarse.hip (coarse frequency estimate) and burst.hip (Hilbert
- * fast-FIR blocks, trident check).
+ * Used by burst.hip (Hilbert fast-FIR blocks, trident check) and cchan.hip
+ * (the C channel's 4096-point prefilter blocks).
  */
 #pragma once
 #include <hip/hip_runtime.h>
@@ -189,7 +190,8 @@ __device__ __forceinline__ void stage0(double2 (&x)[16], int t0, const double2 *
 }
 
 // full JFFT::fft on values already loaded in bit-reversed order in layout 0;
-// leaves the natural-order result in layout 3.  TW: this direction's table;
+// leaves the natural-order result in layout 3 (4096 points: layout 2, which
+// is epos<12, 3> as well).  TW: this direction's table;
 // stw: LDS copy of the forward table's first TwLds<L>::LEN entries.
 // SKIP1: skip the exact-(1, +-0) twiddle multiplies of phase 0 (stage0);
 // only for callers whose outputs are magnitudes / squares (coarse.hip), as
@@ -197,7 +199,7 @@ __device__ __forceinline__ void stage0(double2 (&x)[16], int t0, const double2 *
 template <int L, bool INV, bool SKIP1 = false>
 __device__ __forceinline__ void fft_dit(double2 (&x)[16], int t, double *lds, const double2 *__restrict__ TW,
                                         const double2 *stw) {
-  static_assert(L == 13 || L == 14, "register phases cover 13 or 14 stages");
+  static_assert(L == 12 || L == 13 || L == 14, "register phases cover 12, 13 or 14 stages");
   if (SKIP1) {
     stage0<L, INV, 0>(x, t, TW, stw);
     stage0<L, INV, 1>(x, t, TW, stw);
@@ -231,6 +233,15 @@ __device__ __forceinline__ void fft_dit(double2 (&x)[16], int t, double *lds, co
     tw_load<L, 3, INV>(wb, t, 1, 8192, TW, stw);
     bfly(x, 0, wa);
     bfly(x, 1, wb);
+  } else if (L == 12) {
+    tw_load<L, 2, INV>(wa, t, 1, 512, TW, stw);
+    exchange<L, 1, 2, false>(x, t, lds);
+    stage<L, 2, INV>(x, t, 0, 256, TW, stw);
+    tw_load<L, 2, INV>(wb, t, 2, 1024, TW, stw);
+    bfly(x, 1, wa);
+    tw_load<L, 2, INV>(wa, t, 3, 2048, TW, stw);
+    bfly(x, 2, wb);
+    bfly(x, 3, wa);
   } else {
     tw_load<L, 2, INV>(wa, t, 1, 512, TW, stw);
     exchange<L, 1, 2, false>(x, t, lds);
