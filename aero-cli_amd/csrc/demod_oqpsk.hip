@@ -229,6 +229,10 @@ struct DemodShared {
   // LDS gather instead of an L2 round trip on the per-sample chain
   double cij[241][7];
   double sct[440];
+  // the soft-ring group (16 bytes) each channel is filling: written to the
+  // ring as one 16-byte store when its last pair arrives, and at the end of
+  // the launch (the group's earlier bytes are loaded at the start)
+  uint32_t softw[4][DEMOD_BLOCK];
 };
 
 // dst += a (dst = a + b) for the lanes in m only, the rest keep dst: one
@@ -431,6 +435,14 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
     for (int k = 0; k < PI_N; ++k) sh.pi[k][pair] = S.is[pi_src[k] * C + c];
     sh.pl[PL_SOFTP][pair] = S.ls[LS_SOFT_P * C + c];
     sh.pl[PL_PTN][pair] = TRACE ? S.ls[LS_PT_N * C + c] : 0;
+    {
+      const uint4 g = *reinterpret_cast<const uint4 *>(S.soft + (size_t)c * SOFT_RING +
+                                                       (sh.pl[PL_SOFTP][pair] & (SOFT_RING - 16)));
+      sh.softw[0][pair] = g.x;
+      sh.softw[1][pair] = g.y;
+      sh.softw[2][pair] = g.z;
+      sh.softw[3][pair] = g.w;
+    }
     sh.pi[PI_TICK][pair] = dcd_tick_rel(S, c, n0);
     q54 = S.fir[(size_t)(NTAPS - 1) * C + c];
     q54i = S.fir[(size_t)(2 * NTAPS - 1) * C + c];
@@ -734,11 +746,14 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
         if (rbit > 255) rbit = 255;
         if (rbit < 0) rbit = 0;
         const long long softp = sh.pl[PL_SOFTP][pair];
-        if (!(AERO_X_DROP & 2)) {
-          uint8_t *soft = S.soft + (size_t)cl * SOFT_RING;
-          soft[softp & (SOFT_RING - 1)] = (uint8_t)ibit;
-          soft[(softp + 1) & (SOFT_RING - 1)] = (uint8_t)rbit;
-        }
+        // the pair into the channel's 16-byte group (softp is even), the
+        // group to the ring once complete: one store per 8 pairs instead of
+        // two 1-byte stores into the channel-major ring per pair
+        reinterpret_cast<uint16_t *>(&sh.softw[(softp >> 2) & 3][pair])[(softp >> 1) & 1] =
+            (uint16_t)(ibit | (rbit << 8));
+        if ((softp & 15) == 14 && !(AERO_X_DROP & 2))
+          *reinterpret_cast<uint4 *>(S.soft + (size_t)cl * SOFT_RING + (softp & (SOFT_RING - 16))) =
+              make_uint4(sh.softw[0][pair], sh.softw[1][pair], sh.softw[2][pair], sh.softw[3][pair]);
         sh.pl[PL_SOFTP][pair] = softp + 2;
       }
       sh.pd[PD_CTX1][pair] = ctx1;
@@ -792,6 +807,9 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
   ls[LS_FILLED * C] = n0 + ifl;
   ls[LS_SOFT_P * C] = sh.pl[PL_SOFTP][pair];
   if (TRACE) ls[LS_PT_N * C] = sh.pl[PL_PTN][pair];
+  if ((sh.pl[PL_SOFTP][pair] & 15) && !(AERO_X_DROP & 2))  // the group being filled (bytes past softp are not read)
+    *reinterpret_cast<uint4 *>(S.soft + (size_t)cl * SOFT_RING + (sh.pl[PL_SOFTP][pair] & (SOFT_RING - 16))) =
+        make_uint4(sh.softw[0][pair], sh.softw[1][pair], sh.softw[2][pair], sh.softw[3][pair]);
   {
     static constexpr int pd_dst[PD_N] = {DS_CT_X1, DS_CT_X2, DS_CT_Y1, DS_CT_Y2, DS_MARG_SUM, DS_PM_SUM,
                                          DS_MS_SUM, DS_MSE, DS_PTD_RE, DS_PTD_IM, DS_M2_FREQ};

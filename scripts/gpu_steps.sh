@@ -10,6 +10,8 @@
 #   ab=VARIANT:M       bench.py --mode M on libaero_engine_VARIANT.so, no CPU baseline
 #   env=VAR=VALUE      export VAR=VALUE for the steps after it
 #   pmcdrop            demod HBM traffic per buffer (scripts/pmc_demod_buffers.sh)
+#   pmc                FETCH_SIZE / WRITE_SIZE of the headline's demod and coarse
+#                      kernels (two passes) -> pmc_oqpsk10500.json
 #   trace=M            rocprofv3 kernel trace of bench.py --mode M (kernel_trace_M.csv)
 #   stamps[=VARIANT]   per-section cycle totals (libaero_engine_stamps.so or _VARIANT.so)
 # Usage: bash scripts/gpu_steps.sh TAG STEP...
@@ -48,6 +50,15 @@ for st in "$@"; do
       cd /tmp; TMPDIR=/tmp step 400 trace_$m.log rocprofv3 --kernel-trace --output-format csv -d /tmp/tr_${TAG}_$m -o tr -- python3 $R/bench.py --mode ${st#trace=} --no-cpu-baseline; cd $R
       find /tmp/tr_${TAG}_$m -name '*kernel_trace.csv' -exec cp {} $OUT/kernel_trace_$m.csv \; ;;
     pmcdrop) step 900 pmcdrop.log bash scripts/pmc_demod_buffers.sh $TAG ;;
+    pmc) cd /tmp
+      for c in FETCH_SIZE WRITE_SIZE; do
+        TMPDIR=/tmp step 400 pmc_$c.log rocprofv3 --pmc $c --kernel-include-regex 'demod_oqpsk|coarse_kernel' --output-format csv \
+          -d /tmp/pmc_${TAG}_$c -o pmc -- python3 $R/bench.py --steps 4 --warmup 1 --no-cpu-baseline --h2d-steps 0
+        find /tmp/pmc_${TAG}_$c -name '*counter_collection.csv' -exec cp {} $OUT/pmc_$c.csv \;
+      done
+      cd $R
+      python3 tools/pmc_json.py $OUT/pmc_FETCH_SIZE.csv $OUT/pmc_WRITE_SIZE.csv $OUT/pmc_oqpsk10500.json oqpsk10500 65536 \
+        "rocprofv3 --pmc, one pass per counter, bench.py --steps 4 --warmup 1" > /dev/null ;;
     env=*) export "${st#env=}"; echo "[step] export ${st#env=}" ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
