@@ -47,7 +47,8 @@ CXX_SRCS = ['tables_host.cpp', 'acars_host.cpp']
 FILE_FLAGS = {'burst.hip': ['-mllvm', '-disable-machine-licm'],
               'burst_msk.hip': ['-mllvm', '-disable-machine-licm'],
               'demod_oqpsk.hip': ['-mllvm', '--amdgpu-sched-strategy=max-memory-clause', '-mllvm',
-                                  '-disable-machine-licm']}
+                                  '-disable-machine-licm'],
+              'cchan.hip': ['-mllvm', '-disable-machine-licm']}
 
 
 def _run(cmd):

@@ -30,7 +30,7 @@
  *
  * Bit-exactness rules as in demod_oqpsk.hip: -ffp-contract=off, the
  * reference's operation order, GCC complex products, aero_math.h for libm;
- * plain IEEE divisions here (this path is not the headline's).
+ * the short exact divisions of aero_math.h where demod_oqpsk.hip uses them.
  */
 #include <hip/hip_runtime.h>
 
@@ -66,7 +66,7 @@ __device__ __forceinline__ void c_nco_next(double &ptr, double &step) {  // WTne
 __device__ __forceinline__ void c_set_freq(double &freq, double &step, double f) {  // SetFreq(double) (DSP.cpp:163-168)
   freq = f;
   if (freq < 0) freq = 0;
-  step = (freq) * ((double)WTSIZE) / 48000.0;
+  step = div_c((freq) * ((double)WTSIZE), 48000.0);
 }
 // Delay<double>::update (DSP.h:365-384) as a shift register (h[0] newest)
 // whose weights depend on the write pointer p (T/8 at 8400 bps does)
@@ -222,8 +222,10 @@ template <bool TRACE>
 __global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, int nch) {
   __shared__ double cij[241][7];
   __shared__ double sct[440];
+  __shared__ DelayDesc sdly[4];  // the timer delays' pointer-indexed weights: an LDS read, not an L2 round trip
   for (int q = threadIdx.x; q < 241 * 7; q += 64) (&cij[0][0])[q] = (&aero_g_cij[0][0])[q];
   for (int q = threadIdx.x; q < 440; q += 64) sct[q] = aero_g_sincostab[q];
+  if (threadIdx.x < 4) sdly[threadIdx.x] = cc_dly[threadIdx.x];
   __syncthreads();
   const int c = blockIdx.x * 64 + threadIdx.x;
   if (c >= nch) return;
@@ -291,86 +293,119 @@ __global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, in
   const double2 *cout = S.cout + (size_t)c * C_OUT_RING;
   double up_ptr = S.ds[DS_FP_PTR * C + c], fp_step = S.ds[DS_FP_STEP * C + c];
   const double PT = 0.65 * WTSIZE;  // IfHavePassedPoint(ee), ee = 0.65 at 8400 (:213)
+  // Event-aligned (as demod_oqpsk.hip): each lane runs its samples up to
+  // its next carrier event, then the carrier step runs once for every lane
+  // at one; a sample's mixer2 advance waits for its carrier step.  The
+  // carrier step reads none of what the sample's other NCOs and the
+  // coarse-ring entry change, so running those first keeps the order of
+  // every value.
+  // the table entries, prefiltered value and AGC slot a sample uses are
+  // loaded a sample ahead (each would otherwise be an L2 round trip on the
+  // sample's chain)
+  double2 cm_next = T.cis[c_cis_index(m2_ptr)], so_next = T.cis[c_cis_index(so_ptr)];
+  double2 cu_next = T.cis[c_cis_index(up_ptr)], o_next = cout[n0 & (C_OUT_RING - 1)];
+  double agc_next = S.agc[(size_t)agc_ptr * C + c];
   int i = 0;
-  for (; i < ie; ++i) {
-    const long long n = n0 + i;
-    double2 pre;
-    {  // the prefilter's up-mix: *= mixer_fir_pre.WTCISValue_conj(), WTnextFrame() (:316-322)
-      const double2 o = cout[n & (C_OUT_RING - 1)];
-      const double2 cu = T.cis[c_cis_index(up_ptr)];
-      c_nco_next(up_ptr, fp_step);
-      const double cr = cu.x, ci = -cu.y;
-      pre = make_double2(o.x * cr - o.y * ci, o.x * ci + o.y * cr);
-    }
-    const double2 cm = T.cis[c_cis_index(m2_ptr)];
-    // mix only: sig2 = mixer2.WTCISValue() * cval_prefiltered[i] (:376-385)
-    double s2r = cm.x * pre.x - cm.y * pre.y, s2i = cm.x * pre.y + cm.y * pre.x;
-    m2_fsum += m2_freq;
-    const double dab = sqrt(s2r * s2r + s2i * s2i);
-    {  // AGC (DSP.cpp:371-380)
-      const double agc_old = S.agc[(size_t)agc_ptr * C + c];
-      agc_sum = agc_sum - agc_old;
-      agc_sum = agc_sum + fabs(dab);
-      S.agc[(size_t)agc_ptr * C + c] = fabs(dab);
-      agc_ptr++;
-      if (agc_ptr == AGC_LEN) agc_ptr = 0;
-      double g = 1.414213562 / fmax(agc_sum / ((double)AGC_LEN), 0.000001);
-      g = fmax(g, 0.000001);
-      s2r *= g;
-      s2i *= g;
-    }
-    const double ab = aero_hypot_w(s2r, s2i);  // clipping (:408-410)
-    if (ab > 2.84) {
-      const double kk = 2.84 / ab;
-      s2r = kk * s2r;
-      s2i = kk * s2i;
-    }
-    // symbol timer (:413-426)
-    const double st_diff = c_delay<2, 1, 0>(d1, p1, cc_dly[0], ab * ab) - (ab * ab);
-    const double st_d1out = c_delay<4, 3, 2>(d41, p41, cc_dly[1], st_diff);
-    const double st_d2out = c_delay<4, 3, 2>(d42, p42, cc_dly[2], st_d1out);
-    double st_eta = (st_d2out - st_diff) * st_d1out;
-    st_eta = c_iir3(srx1, srx2, sry1, sry2, sr_b, sr_a, st_eta);
-    const double m1r = st_eta, m1i = -c_delay<3, 2, 1>(d8, p8, cc_dly[3], st_eta);
-    const double2 so = T.cis[c_cis_index(so_ptr)];
-    const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
-    const double st_angle_error = aero_atan2_bf(oim, ore, cij);
-    c_set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
-    so_ptr += (-st_angle_error * 0.01 / 360.0) * WTSIZE;
-    while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
-    while (so_ptr < 0) so_ptr += WTSIZE;
-    if (so_freq < (SO_F - 0.1)) c_set_freq(so_freq, so_step, (SO_F - 0.1));
-    if (so_freq > (SO_F + 0.1)) c_set_freq(so_freq, so_step, (SO_F + 0.1));
-    if (!s2l_init) {
-      s2l_re = s2r;
-      s2l_im = s2i;
-      s2l_init = 1;
-    }
+  while (i < ie) {
     bool pend = false;
     double ev_pr = 0.0, ev_pi = 0.0;
-    {  // sample instant (:430) IfHavePassedPoint (DSP.cpp:222-238)
-      double tl = so_last - PT, tw = so_ptr - PT;
-      if (tl < 0.0) tl += WTSIZE;
-      if (tw < 0.0) tw += WTSIZE;
-      if ((tl > 3.0 * WTSIZE / 4.0) && (tw < 1.0 * WTSIZE / 4.0)) {
-        const double pt_last = tw / so_step;
-        const double pt_this = 1.0 - pt_last;
-        const double pr = pt_this * s2r + pt_last * s2l_re;
-        const double pi = pt_this * s2i + pt_last * s2l_im;
-        yui++;
-        yui %= 2;
-        if (!yui) {
-          ptd_re = pr;
-          ptd_im = pi;
-        } else {
-          ev_pr = pr;
-          ev_pi = pi;
-          pend = true;
+    do {
+      const long long n = n0 + i;
+      double2 pre;
+      {  // the prefilter's up-mix: *= mixer_fir_pre.WTCISValue_conj(), WTnextFrame() (:316-322)
+        const double2 o = o_next, cu = cu_next;
+        c_nco_next(up_ptr, fp_step);
+        o_next = cout[(n + 1) & (C_OUT_RING - 1)];
+        cu_next = T.cis[c_cis_index(up_ptr)];
+        const double cr = cu.x, ci = -cu.y;
+        pre = make_double2(o.x * cr - o.y * ci, o.x * ci + o.y * cr);
+      }
+      const double2 cm = cm_next;
+      // mix only: sig2 = mixer2.WTCISValue() * cval_prefiltered[i] (:376-385)
+      double s2r = cm.x * pre.x - cm.y * pre.y, s2i = cm.x * pre.y + cm.y * pre.x;
+      m2_fsum += m2_freq;
+      const double dab = sqrt(s2r * s2r + s2i * s2i);
+      {  // AGC (DSP.cpp:371-380)
+        const double agc_old = agc_next;
+        agc_sum = agc_sum - agc_old;
+        agc_sum = agc_sum + fabs(dab);
+        S.agc[(size_t)agc_ptr * C + c] = fabs(dab);
+        agc_ptr++;
+        if (agc_ptr == AGC_LEN) agc_ptr = 0;
+        agc_next = S.agc[(size_t)agc_ptr * C + c];
+        // the short exact divisions of aero_math.h at the call sites whose
+        // operand ranges demod_oqpsk.hip argues (the same expressions)
+        double g = div_n(1.414213562, fmax(div_c(agc_sum, ((double)AGC_LEN)), 0.000001));
+        g = fmax(g, 0.000001);
+        s2r *= g;
+        s2i *= g;
+      }
+      const double ab = aero_hypot_w(s2r, s2i);  // clipping (:408-410)
+      if (ab > 2.84) {
+        const double kk = div_n(2.84, ab);
+        s2r = kk * s2r;
+        s2i = kk * s2i;
+      }
+      // symbol timer (:413-426)
+      const double st_diff = c_delay<2, 1, 0>(d1, p1, sdly[0], ab * ab) - (ab * ab);
+      const double st_d1out = c_delay<4, 3, 2>(d41, p41, sdly[1], st_diff);
+      const double st_d2out = c_delay<4, 3, 2>(d42, p42, sdly[2], st_d1out);
+      double st_eta = (st_d2out - st_diff) * st_d1out;
+      st_eta = c_iir3(srx1, srx2, sry1, sry2, sr_b, sr_a, st_eta);
+      const double m1r = st_eta, m1i = -c_delay<3, 2, 1>(d8, p8, sdly[3], st_eta);
+      const double2 so = so_next;
+      const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
+      const double st_angle_error = aero_atan2_bf(oim, ore, cij);
+      c_set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
+      so_ptr += div_c(-st_angle_error * 0.01, 360.0) * WTSIZE;
+      while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
+      while (so_ptr < 0) so_ptr += WTSIZE;
+      if (so_freq < (SO_F - 0.1)) c_set_freq(so_freq, so_step, (SO_F - 0.1));
+      if (so_freq > (SO_F + 0.1)) c_set_freq(so_freq, so_step, (SO_F + 0.1));
+      if (!s2l_init) {
+        s2l_re = s2r;
+        s2l_im = s2i;
+        s2l_init = 1;
+      }
+      {  // sample instant (:430) IfHavePassedPoint (DSP.cpp:222-238)
+        double tl = so_last - PT, tw = so_ptr - PT;
+        if (tl < 0.0) tl += WTSIZE;
+        if (tw < 0.0) tw += WTSIZE;
+        if ((tl > 3.0 * WTSIZE / 4.0) && (tw < 1.0 * WTSIZE / 4.0)) {
+          const double pt_last = div_n(tw, so_step);  // tw: 0 or >= 2^-40, so_step ~3500
+          const double pt_this = 1.0 - pt_last;
+          const double pr = pt_this * s2r + pt_last * s2l_re;
+          const double pi = pt_this * s2i + pt_last * s2l_im;
+          yui++;
+          yui %= 2;
+          if (!yui) {
+            ptd_re = pr;
+            ptd_im = pi;
+          } else {
+            ev_pr = pr;
+            ev_pi = pi;
+            pend = true;
+          }
         }
       }
-    }
-    s2l_re = s2r;
-    s2l_im = s2i;
+      s2l_re = s2r;
+      s2l_im = s2i;
+      c_nco_next(mc_ptr, mc_step);
+      so_last = so_ptr;
+      c_nco_next(so_ptr, so_step);
+      so_next = T.cis[c_cis_index(so_ptr)];
+      if (i + 1 < ia) {  // coarse-ring entry of the next sample (:351-356)
+        const long long n1 = n + 1;
+        const int16_t x = S.pcm[(size_t)(n1 & capm) * C + c];
+        S.cring[(size_t)c * NFFT + (n1 & (NFFT - 1))] = (uint32_t)c_cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
+        ifl = i + 2;
+      }
+      if (!pend) {
+        c_nco_next(m2_ptr, m2_step);
+        cm_next = T.cis[c_cis_index(m2_ptr)];
+        ++i;
+      }
+    } while (!pend && i < ie);
     if (pend) {  // carrier step (:447-541)
       const int dt_rp = (dt_p + 1) % DT_LEN;
       const double marg_old = marg[marg_p];
@@ -418,9 +453,10 @@ __global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, in
         const int slot = pm_p;
         pm_p++;
         pm_p %= MSE_LEN;
-        double mu = pm_sum / ((double)MSE_LEN);
+        double mu = div_c(pm_sum, ((double)MSE_LEN));
         if (mu < 0.000001) mu = 0.000001;
-        const double tr = (1.4142135623730951 * qr) / mu, ti = (1.4142135623730951 * qi) / mu;
+        const double rmu = rcp_div(mu);  // mu >= 1e-6
+        const double tr = div_r(1.4142135623730951 * qr, mu, rmu), ti = div_r(1.4142135623730951 * qi, mu, rmu);
         const double tda = (fabs(tr) - 1.0), tdb = (fabs(ti) - 1.0);
         const double v = (tda * tda) + (tdb * tdb);
         ms_sum = ms_sum - pms_old.y;
@@ -428,7 +464,7 @@ __global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, in
         pmsb[slot] = make_double2(fabs(av), fabs(v));
         ms_p++;
         ms_p %= MSE_LEN;
-        mse = ms_sum / ((double)MSE_LEN);
+        mse = div_c(ms_sum, ((double)MSE_LEN));  // exact: ms_sum is 0 or a multiple of 2^-158
       }
       if (mse < 0.65) {  // soft bits, imag first (:516-530)
         int ibit = c_qround(0.75 * qi * 127.0 + 128.0);
@@ -441,16 +477,9 @@ __global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, in
         soft[(softp + 1) & (SOFT_RING - 1)] = (uint8_t)rbit;
         softp += 2;
       }
-    }
-    c_nco_next(m2_ptr, m2_step);
-    c_nco_next(mc_ptr, mc_step);
-    so_last = so_ptr;
-    c_nco_next(so_ptr, so_step);
-    if (i + 1 < ia) {  // coarse-ring entry of the next sample (:351-356)
-      const long long n1 = n + 1;
-      const int16_t x = S.pcm[(size_t)(n1 & capm) * C + c];
-      S.cring[(size_t)c * NFFT + (n1 & (NFFT - 1))] = (uint32_t)c_cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
-      ifl = i + 2;
+      c_nco_next(m2_ptr, m2_step);
+      cm_next = T.cis[c_cis_index(m2_ptr)];
+      ++i;
     }
   }
   double *ds = S.ds + c;

@@ -326,7 +326,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   for (int i = 0; i < 16; ++i) {
     const int p = bin_t | chain::out_bin_reg<L>(i);
     if constexpr (M == MODE_C8400) {
-      const double w = T.cwin[p];
+      const double w = T.cwin[i * FT + t];  // = window[p], stored in this layout's order (engine.hip)
       x[i] = make_double2(x[i].x * w, x[i].y * w);
     } else {
       if (p >= KB.start && p <= KB.stop) x[i] = make_double2(0.0, 0.0);

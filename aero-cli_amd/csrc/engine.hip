@@ -36,6 +36,7 @@
 #include "burst_engine.h"
 #include "aero_math.h"
 #include "engine_common.h"
+#include "fft_layout.h"
 #include "host_pool.h"
 #include "engine_internal.h"
 #include "tables_host.h"
@@ -1280,7 +1281,18 @@ int group_create(aero_engine *E, int mode, int gid, int fs, std::unique_ptr<Grou
     HIPCHK(hipMemcpy((void *)e->T.cker, k.data(), sizeof(double) * 2 * C_FIR_N, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy((void *)e->T.tw4, t4.data(), sizeof(double) * 2 * C_FIR_N, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy((void *)e->T.twi4, ti4.data(), sizeof(double) * 2 * C_FIR_N, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy((void *)e->T.cwin, win.data(), sizeof(double) * NFFT, hipMemcpyHostToDevice));
+    // in the order the coarse kernel's threads hold the bins after the
+    // forward transform (fft_layout.h, G layout): entry i * 1024 + t is bin
+    // out_bin_thread(t) | out_bin_reg(i), so a wave's load of register i's
+    // weights is one contiguous 512-byte run
+    std::vector<double> wperm(NFFT);
+    {
+      constexpr int L = 14, FT = NFFT / 16;
+      const uint64_t G = fftl::lay_g<L>();
+      for (int t = 0; t < FT; t++)
+        for (int i = 0; i < 16; i++) wperm[(size_t)i * FT + t] = win[fftl::athr<L, fftl::K_G, false>(t) | fftl::areg(G, L, i)];
+    }
+    HIPCHK(hipMemcpy((void *)e->T.cwin, wperm.data(), sizeof(double) * NFFT, hipMemcpyHostToDevice));
     // symbol timer delays at T = 48000 / 4200 (:186-190): the kernel reads ages
     // {1,0}, {3,2}, {3,2}, {2,1}; T/8's weights depend on the write pointer
     const double T84 = 48000.0 / (8400.0 / 2);

@@ -87,3 +87,35 @@ def test_c_channel_deferred_viterbi(engine_lib, c_refs):
         assert np.array_equal(eng.c_units(ch), rcu), 'case %d Call_progress SUs differ' % k
         assert eng.voice(ch) == rv, 'case %d voice frames differ' % k
     eng.close()
+
+
+def test_c_channel_ragged_messages(engine_lib, cpu_libs):
+    """Message sizes around the prefilter's 2048-sample blocks (shorter than a
+    block, ending on and just past a block boundary, the 32768 maximum, one
+    sample): everything equal to the oracle fed the same messages."""
+    import aero_engine as ae
+    pcm = tl.synth_c(seconds=14.0, seed=0xC1A5, carrier=11000.0, ebn0=12.0)
+    sizes = [1, 2047, 2048, 2049, 32768, 100, 4096, 12000, 6143, 1, 30000, 2048, 9000]
+    msgs, p, k = [], 0, 0
+    while p < len(pcm):
+        n = sizes[k % len(sizes)]
+        msgs.append(pcm[p:p + n])
+        p += n
+        k += 1
+    o = tl.Oracle(bitrate=8400, trace_pt=True)
+    for m in msgs:
+        o.push(m)
+    eng = ae.Engine(max_channels=1, flags=ae.F_TRACE_PT | ae.F_TRACE_SOFT | ae.F_TRACE_HOPS | ae.F_TRACE_FRAMES)
+    ch = eng.open_channel(8400, 48000)
+    for m in msgs:
+        eng.push(ch, m)
+        eng.run()
+    eng.flush()
+    sb = eng.softbits(ch)
+    assert len(sb) > 10000 and np.array_equal(sb, o.softbits())
+    assert np.array_equal(eng.pt(ch).view(np.int64), o.pt().view(np.int64))
+    assert np.array_equal(eng.hops(ch).view(np.int64), o.hops().view(np.int64))
+    assert np.array_equal(eng.frames(ch), o.frames()) and len(o.frames()) > 0
+    assert np.array_equal(eng.c_units(ch), o.c_units())
+    assert eng.voice(ch) == o.voice()
+    eng.close()
