@@ -317,7 +317,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   __syncthreads();  // the ring image is read: the LDS is the transforms' from here on
   CSTAMP(2);
   // forward FFT
-  chain::fft<L, true, false>(x, t, lds, T.tw, s_tw);
+  chain::fft<L, true, false>(x, t, lds, T.tw, s_tw, T.twg);
   CSTAMP(3);
   // boxcar: zero bins startbin..stopbin (coarsefreqestimate.cpp:97-100);
   // the C channel multiplies by the raised-cosine window instead (:101-104)
@@ -337,7 +337,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
   // x with |x| >= 2^-1008, and a nonzero value of this path is far above that
   // (magnitudes >= ~2^-200: sums and products of pcm/32768, CIS and twiddle
   // values), so both multiplies are the identity here and are skipped.
-  chain::fft<L, false, true>(x, t, lds, T.twi, s_tw);
+  chain::fft<L, false, true>(x, t, lds, T.twi, s_tw, T.twgi);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     // square
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(1 << (CoarseK<M>::LOG2N - 4), CoarseK<M>::LOG2N == 
     x[i] = make_double2(r, im);
   }
   CSTAMP(4);
-  chain::fft<L, false, false>(x, t, lds, T.tw, s_tw);
+  chain::fft<L, false, false>(x, t, lds, T.tw, s_tw, T.twg);
   CSTAMP(5);
   // fftshift + smoothing y = 0.9 y + 10 log10(max(|X|,1)) over the bins the
   // fold reads: |X| per bin to LDS first (keeps the log10 out of the

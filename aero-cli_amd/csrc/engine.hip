@@ -374,6 +374,8 @@ size_t layout(DevState &S, DevTables &T, int mode, const ModeGeom &g, int C, int
   T.cis = carve<double2>(p, WTSIZE);
   T.tw = carve<double2>(p, g.nfft);
   T.twi = carve<double2>(p, g.nfft);
+  T.twg = carve<double2>(p, g.nfft);
+  T.twgi = carve<double2>(p, g.nfft);
   T.scr = carve<uint8_t>(p, 5000);
   T.taps = carve<double>(p, MAX_TAPS);
   return (size_t)(p - base);
@@ -1242,6 +1244,18 @@ int group_create(aero_engine *E, int mode, int gid, int fs, std::unique_ptr<Grou
   HIPCHK(hipMemcpy((void *)e->T.cis, cis.data(), sizeof(double) * 2 * WTSIZE, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy((void *)e->T.tw, tw.data(), sizeof(double) * 2 * nfft, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy((void *)e->T.twi, twi.data(), sizeof(double) * 2 * nfft, hipMemcpyHostToDevice));
+  {
+    std::vector<double> pg(2 * nfft, 0.0), pgi(2 * nfft, 0.0);
+    if (nfft == 16384) {
+      fftl::twg_build<14>(tw.data(), pg.data());
+      fftl::twg_build<14>(twi.data(), pgi.data());
+    } else {
+      fftl::twg_build<13>(tw.data(), pg.data());
+      fftl::twg_build<13>(twi.data(), pgi.data());
+    }
+    HIPCHK(hipMemcpy((void *)e->T.twg, pg.data(), sizeof(double) * 2 * nfft, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy((void *)e->T.twgi, pgi.data(), sizeof(double) * 2 * nfft, hipMemcpyHostToDevice));
+  }
   HIPCHK(hipMemcpy((void *)e->T.scr, scr.data(), 5000, hipMemcpyHostToDevice));
   if (mode == MODE_OQPSK) {
     if (host_rrc(1.0, 55, 48000, 10500 / 2, taps.data()) != NTAPS) return AERO_E_INVALID;

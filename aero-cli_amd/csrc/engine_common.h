@@ -242,6 +242,8 @@ struct DevTables {
   const double2 *cis;      // [WTSIZE] (CosWT, SinWT)   decode/DSP.cpp:10-33
   const double2 *tw;       // [NFFT] forward twiddles   decode/jfft.cpp:41-53
   const double2 *twi;      // [NFFT] inverse twiddles
+  const double2 *twg;      // the coarse transforms' stages past the LDS copy, permuted to the threads' order (fft_layout.h)
+  const double2 *twgi;     // the same of the inverse table
   const uint8_t *scr;      // [5000] scrambler bits      decode/aerol.h:408-427
   const double *taps;      // [ntaps] RRC (OQPSK) / half-sine matched filter (MSK)
   // C channel: JFastFir kernel spectrum and the 4096-point twiddles

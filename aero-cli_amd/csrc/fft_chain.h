@@ -35,22 +35,35 @@ using namespace fftl;
 // in order); identical indices fold into one load.  Stages n <= TwLds<L>::N
 // read the LDS copy of the forward table (an inverse negates the imaginary
 // part: JFFT's inverse table is the forward one conjugated bit for bit,
-// tests/test_abi.py::test_twiddle_inverse_is_conjugate).
+// tests/test_abi.py::test_twiddle_inverse_is_conjugate); the later stages,
+// all in the G layout, this direction's permuted copy TWG (fft_layout.h
+// twg_build: one contiguous run per wave and row).
 template <int L, uint64_t LAY, int S, bool INV>
 __device__ __forceinline__ void tw_fetch(double2 (&w)[8], int athr_v, const double2 *__restrict__ TW,
-                                         const double2 *stw) {
-  constexpr int rb = sb(LAY, S), n = 1 << S;
+                                         const double2 *stw, const double2 *__restrict__ TWG, int t) {
+  constexpr int rb = sb(LAY, S), n = 1 << S, FT = 1 << (L - 4);
   constexpr bool lds_tw = n <= TwLds<L>::N;
-  // the laundered index keeps the compiler from computing every stage's
-  // address up front and holding them all (that spills)
-  const double2 *base = (lds_tw ? stw : TW) + (n - 1) + (fresh(athr_v) & (n - 1));
-  int j = 0;
+  if constexpr (!lds_tw && LAY == lay_g<L>()) {
+    // the laundered index keeps the compiler from computing every stage's
+    // address up front and holding them all (that spills)
+    const double2 *base = TWG + twg_base<L>(S) * FT + fresh(t);
+    int j = 0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    if (i & (1 << rb)) continue;
-    w[j] = base[areg(LAY, L, i) & (n - 1)];
-    if (lds_tw && INV) w[j].y = -w[j].y;
-    ++j;
+    for (int i = 0; i < 16; ++i) {
+      if (i & (1 << rb)) continue;
+      w[j] = base[twg_row<L>(S, i) * FT];
+      ++j;
+    }
+  } else {
+    const double2 *base = (lds_tw ? stw : TW) + (n - 1) + (fresh(athr_v) & (n - 1));
+    int j = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (i & (1 << rb)) continue;
+      w[j] = base[areg(LAY, L, i) & (n - 1)];
+      if (lds_tw && INV) w[j].y = -w[j].y;
+      ++j;
+    }
   }
 }
 
@@ -85,7 +98,7 @@ template <int L, uint64_t LAY, int S, bool INV>
 __device__ __forceinline__ void stage(double2 (&x)[16], int athr_v, const double2 *__restrict__ TW,
                                       const double2 *stw) {
   double2 w[8];
-  tw_fetch<L, LAY, S, INV>(w, athr_v, TW, stw);
+  tw_fetch<L, LAY, S, INV>(w, athr_v, TW, stw, nullptr, 0);
   bfly<L, LAY, S>(x, w);
 }
 
@@ -197,11 +210,12 @@ __device__ __forceinline__ void gx(double2 (&x)[16], double *lds, int t) {
 
 // one transform from its START layout to the G layout (the next one's START).
 // TW: this direction's global table; stw: LDS copy of the forward table's
-// first TwLds<L>::LEN entries.  The global twiddles of the stages after G
-// are fetched before the exchange / one stage ahead.
+// first TwLds<L>::LEN entries; TWG: this direction's permuted copy for the
+// stages after G.  Those twiddles are fetched before the exchange / one
+// stage ahead.
 template <int L, bool FIRST, bool INV>
 __device__ __forceinline__ void fft(double2 (&x)[16], int t, double *lds, const double2 *__restrict__ TW,
-                                    const double2 *stw) {
+                                    const double2 *stw, const double2 *__restrict__ TWG) {
   constexpr uint64_t S0 = lay_start<L>(FIRST), W = lay_wl<L>(FIRST), P = lay_perm<L>(FIRST), G = lay_g<L>();
   const int a0 = athr<L, K_START, FIRST>(t);
   stage<L, S0, 0, INV>(x, a0, TW, stw);
@@ -220,15 +234,15 @@ __device__ __forceinline__ void fft(double2 (&x)[16], int t, double *lds, const 
   stage<L, P, 9, INV>(x, a2, TW, stw);
   const int a3 = athr<L, K_G, false>(t);
   double2 wa[8], wb[8];
-  tw_fetch<L, G, 10, INV>(wa, a3, TW, stw);
-  tw_fetch<L, G, 11, INV>(wb, a3, TW, stw);
+  tw_fetch<L, G, 10, INV>(wa, a3, TW, stw, TWG, t);
+  tw_fetch<L, G, 11, INV>(wb, a3, TW, stw, TWG, t);
   gx<L, FIRST>(x, lds, t);
   bfly<L, G, 10>(x, wa);
   // each later fetch is tied to the butterflies before it, so the scheduler
   // cannot issue all four stages' global twiddles at once (that spills)
-  tw_fetch<L, G, 12, INV>(wa, after(a3, x), TW, stw);
+  tw_fetch<L, G, 12, INV>(wa, after(a3, x), TW, stw, TWG, after(t, x));
   bfly<L, G, 11>(x, wb);
-  if (L == 14) tw_fetch<L, G, (L == 14 ? 13 : 12), INV>(wb, after(a3, x), TW, stw);
+  if (L == 14) tw_fetch<L, G, (L == 14 ? 13 : 12), INV>(wb, after(a3, x), TW, stw, TWG, after(t, x));
   bfly<L, G, 12>(x, wa);
   if (L == 14) bfly<L, G, (L == 14 ? 13 : 12)>(x, wb);
   pin(x);

@@ -162,6 +162,44 @@ AERO_HD constexpr int wl_r(int lane, int i) { return (lane >> 4) * 272 + i * 17 
 template <int S>
 AERO_HD constexpr int ypadn(int q) { return q + (q >> S); }
 
+// The L2-served stages of the G layout (S >= 10, past the LDS twiddle copy)
+// read their twiddles from a copy permuted into the threads' order
+// (DevTables::twg / twgi): row r of stage S holds, for every thread t in
+// turn, the twiddle TW[n - 1 + ((athr_G(t) | r << (L - 4)) & (n - 1))] of
+// the thread's butterflies whose register part of the array index below bit
+// S is r << (L - 4).  A wave's load of one row is then one contiguous run
+// instead of 64 lines (the G layout's lanes hold bit-reversed index bits).
+template <int L>
+AERO_HD constexpr int twg_rows(int S) {
+  return 1 << (S - (L - 4));
+}
+template <int L>
+AERO_HD constexpr int twg_base(int S) {
+  int b = 0;
+  for (int s = 10; s < S; s++) b += twg_rows<L>(s);
+  return b;
+}
+template <int L>
+AERO_HD constexpr int twg_row(int S, int i) {
+  return (areg(lay_g<L>(), L, i) & ((1 << S) - 1)) >> (L - 4);
+}
+// the permuted table of one direction from JFFT's (tw: [2^L] complex as re, im pairs)
+template <int L>
+inline void twg_build(const double *tw, double *twg) {
+  constexpr int FT = 1 << (L - 4);
+  for (int S = 10; S < L; S++) {
+    const int n = 1 << S;
+    for (int r = 0; r < twg_rows<L>(S); r++)
+      for (int t = 0; t < FT; t++) {
+        const int k = n - 1 + ((athr<L, K_G, false>(t) | (r << (L - 4))) & (n - 1));
+        const size_t o = (size_t)(twg_base<L>(S) + r) * FT + t;
+        twg[2 * o] = tw[2 * k];
+        twg[2 * o + 1] = tw[2 * k + 1];
+      }
+  }
+}
+static_assert(twg_base<14>(14) == 15 && twg_base<13>(13) == 14, "permuted twiddle rows");
+
 // static checks of the closed forms for the two transform sizes in use
 template <int L, int KIND, bool FIRST>
 constexpr bool athr_ok() {
