@@ -93,7 +93,12 @@ __global__ __launch_bounds__(256) void frame_kernel(DevState S, int nch) {
   int has_ov = is[IS_HAS_OVERLAP * C + c];
   int isu_reset = is[IS_DATACDCD * C + c];  // pending isudata.reset() for the next job
   int cd = is[IS_DCD_COUNT * C + c], edges = is[IS_DCD_EDGES * C + c];
-  const uint8_t *soft = S.soft + (size_t)c * SOFT_RING;
+  // the soft ring read 16 bytes at a time, the next group in flight (one
+  // 1-byte load per bit, each waited for, was most of this kernel's time)
+  const uint4 *soft16 = reinterpret_cast<const uint4 *>(S.soft + (size_t)c * SOFT_RING);
+  constexpr int G16 = SOFT_RING / 16;
+  long long grp = q >> 4;
+  uint4 cur = soft16[grp & (G16 - 1)], nxt = soft16[(grp + 1) & (G16 - 1)];
   const int NumberOfBits = 4992, BitsInHeader = 194, Total = 5250;
   if (pend) {  // the last frame's SU CRCs, decoded since the previous pass
     const unsigned okm = (unsigned)is[IS_CRC_OKM * C + c];
@@ -119,7 +124,14 @@ __global__ __launch_bounds__(256) void frame_kernel(DevState S, int nch) {
     // frame after a tick cleared it); and a second frame end needs them too
     if (pend && ((!datacd && cntr >= 1 && cntr <= NumberOfBits - 68) || cntr + 1 - BitsInHeader == NumberOfBits - 1))
       break;
-    const int sv = soft[q & (SOFT_RING - 1)];
+    if ((q >> 4) != grp) {  // q advances by one: the next group
+      cur = nxt;
+      grp++;
+      nxt = soft16[(grp + 1) & (G16 - 1)];
+    }
+    const int wi = (int)(q >> 2) & 3;
+    const uint32_t wd = wi == 0 ? cur.x : wi == 1 ? cur.y : wi == 2 ? cur.z : cur.w;
+    const int sv = (int)((wd >> (8 * (q & 3))) & 0xFF);
     int bit = sv >= 128 ? 1 : 0;
     int soft_bit = sv;
     int gotsync;

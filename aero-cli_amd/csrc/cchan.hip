@@ -596,9 +596,20 @@ __global__ __launch_bounds__(256) void frame_c_kernel(DevState S, int nch) {
   int blkbuf = is[IS_BLKBUF * C + c], has_ov = is[IS_HAS_OVERLAP * C + c];
   uint64_t r1 = (uint64_t)ls[LS_C_R1 * C + c], r2 = (uint64_t)ls[LS_C_R2 * C + c];
   uint64_t i1 = (uint64_t)ls[LS_C_I1 * C + c], i2 = (uint64_t)ls[LS_C_I2 * C + c];
-  const uint8_t *soft = S.soft + (size_t)c * SOFT_RING;
+  // the soft ring 16 bytes at a time, the next group in flight (as frame_kernel)
+  const uint4 *soft16 = reinterpret_cast<const uint4 *>(S.soft + (size_t)c * SOFT_RING);
+  constexpr int G16 = SOFT_RING / 16;
+  long long grp = q >> 4;
+  uint4 cur = soft16[grp & (G16 - 1)], nxt = soft16[(grp + 1) & (G16 - 1)];
   for (; q < E; ++q) {
-    const int sv = soft[q & (SOFT_RING - 1)];
+    if ((q >> 4) != grp) {
+      cur = nxt;
+      grp++;
+      nxt = soft16[(grp + 1) & (G16 - 1)];
+    }
+    const int wi = (int)(q >> 2) & 3;
+    const uint32_t wd = wi == 0 ? cur.x : wi == 1 ? cur.y : wi == 2 ? cur.z : cur.w;
+    const int sv = (int)((wd >> (8 * (q & 3))) & 0xFF);
     int bit = sv >= 128 ? 1 : 0;
     int soft_bit = sv;
     int gotsync = 0;
