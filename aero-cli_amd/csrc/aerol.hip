@@ -32,6 +32,8 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <climits>
+
 #include "engine_common.h"
 #include "viterbi_dev.h"
 
@@ -107,17 +109,22 @@ __global__ __launch_bounds__(256) void frame_kernel(DevState S, int nch) {
     pend = 0;
   }
 
+  // the soft position of the next recorded tick, loaded once per tick (not per bit)
+  auto tick_pos = [&](int k) {
+    return k < tick_rec ? ls[(LS_TICK_SOFT0 + (k & (DCD_TICK_RING - 1))) * C + c] : LLONG_MAX;
+  };
+  long long tick_q = tick_pos(tick_done);
   for (;; ++q) {
     // DCD ticks due before soft bit q
     bool stop = false;
-    while (tick_done < tick_rec) {
-      if (ls[(LS_TICK_SOFT0 + (tick_done & (DCD_TICK_RING - 1))) * C + c] > q) break;
+    while (tick_q <= q) {
       if (pend) {  // the countdown needs the CRCs of the frame that just ended
         stop = true;
         break;
       }
       dcd_tick(cd, datacd, edges);
       tick_done++;
+      tick_q = tick_pos(tick_done);
     }
     if (stop || q >= E) break;
     // the gate below reads datacd, which pending CRCs could raise (a flywheel
