@@ -143,7 +143,7 @@ __device__ __forceinline__ int qround(double d) {  // qRound (Qt 5.9 qglobal.h:5
 // i.e. once per ~9 samples)
 enum { PD_CTX1, PD_CTX2, PD_CTY1, PD_CTY2, PD_MARG_SUM, PD_PM_SUM, PD_MS_SUM, PD_MSE, PD_PTD_RE, PD_PTD_IM,
        PD_M2_FREQ, PD_N };
-enum { PI_MARG_P, PI_DT_P, PI_PM_P, PI_MS_P, PI_N, PI_TICK = PI_N, PI_ALL };
+enum { PI_MARG_P, PI_DT_P, PI_PM_P, PI_MS_P, PI_N, PI_TICK = PI_N, PI_DTW0, PI_PMW0, PI_ALL };
 enum { PL_SOFTP, PL_PTN, PL_N };
 
 constexpr int DEMOD_BLOCK = 256;  // channels per workgroup
@@ -207,6 +207,11 @@ __device__ __forceinline__ void lds_store(int *p, int v) {
 }
 
 constexpr int FIR_LDS_IM = 11, FIR_LDS_RE = 5;
+// the dt and MSEcalc rings through LDS windows of DT_WIN / PM_WIN events
+// (the dt window holds one slot more: an event writes slot p and reads p + 1):
+// one read and one write of the window's slots per DT_WIN / PM_WIN events
+// instead of a line fetched and written back per event
+constexpr int DT_WIN = 4, PM_WIN = 4;
 
 struct DemodShared {
   uint32_t ring[RING_GROUP][DEMOD_BLOCK];
@@ -233,6 +238,8 @@ struct DemodShared {
   // ring as one 16-byte store when its last pair arrives, and at the end of
   // the launch (the group's earlier bytes are loaded at the start)
   uint32_t softw[4][DEMOD_BLOCK];
+  double2 dtw[DT_WIN + 1][DEMOD_BLOCK];  // dt slots PI_DTW0 .. + DT_WIN
+  double2 pmw[PM_WIN][DEMOD_BLOCK];      // MSEcalc slots PI_PMW0 .. + PM_WIN - 1
 };
 
 // dst += a (dst = a + b) for the lanes in m only, the rest keep dst: one
@@ -444,6 +451,19 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       sh.softw[3][pair] = g.w;
     }
     sh.pi[PI_TICK][pair] = dcd_tick_rel(S, c, n0);
+    {  // the ring windows from the current slots
+      const int dp = sh.pi[PI_DT_P][pair], pp = sh.pi[PI_PM_P][pair];
+      const double2 *dtb = S.dt + (size_t)c * DT_LEN;
+      const double2 *pmsb = reinterpret_cast<const double2 *>(S.pm) + (size_t)c * MSE_LEN;
+#pragma unroll
+      for (int k = 0; k <= DT_WIN; ++k)
+        sh.dtw[k][pair] = (AERO_X_DROP & 4) ? make_double2(0.0, 0.0) : dtb[(dp + k) % DT_LEN];
+#pragma unroll
+      for (int k = 0; k < PM_WIN; ++k)
+        sh.pmw[k][pair] = (AERO_X_DROP & 4) ? make_double2(0.0, 0.0) : pmsb[(pp + k) % MSE_LEN];
+      sh.pi[PI_DTW0][pair] = dp;
+      sh.pi[PI_PMW0][pair] = pp;
+    }
     q54 = S.fir[(size_t)(NTAPS - 1) * C + c];
     q54i = S.fir[(size_t)(2 * NTAPS - 1) * C + c];
     // R_53 before the first sample: the slot chain iteration 0 reads
@@ -661,9 +681,13 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       // the four moving-average rings of this symbol, loaded together
       // before any ring store so their latencies overlap
       const int dt_rp = (dt_p + 1) % DT_LEN;
+      const int dtw0 = sh.pi[PI_DTW0][pair], pmw0 = sh.pi[PI_PMW0][pair];
+      int dk = dt_p - dtw0, pk = pm_p - pmw0;  // the slots' places in the windows
+      if (dk < 0) dk += DT_LEN;
+      if (pk < 0) pk += MSE_LEN;
       const double marg_old = (AERO_X_DROP & 4) ? 0.0 : marg[marg_p];
-      const double2 dv = (AERO_X_DROP & 4) ? make_double2(0.0, 0.0) : dtb[dt_rp];
-      const double2 pms_old = (AERO_X_DROP & 4) ? make_double2(0.0, 0.0) : pmsb[pm_p];
+      const double2 dv = sh.dtw[dk + 1][pair];
+      const double2 pms_old = sh.pmw[pk][pair];
       const double pm_old = pms_old.x, ms_old = pms_old.y;
       double ctx1 = sh.pd[PD_CTX1][pair], ctx2 = sh.pd[PD_CTX2][pair];
       double cty1 = sh.pd[PD_CTY1][pair], cty2 = sh.pd[PD_CTY2][pair];
@@ -697,7 +721,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       marg_p %= MARG_LEN;
       const double mval = DM_DIVC(marg_sum, ((double)MARG_LEN));
       // dt.update (DSP.h:456-461): slot p written, slot p+1 read
-      if (!(AERO_X_DROP & 4)) dtb[dt_p] = make_double2(qr, qi);
+      sh.dtw[dk][pair] = make_double2(qr, qi);
       dt_p = dt_rp;
       qr = dv.x;
       qi = dv.y;
@@ -728,7 +752,8 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
         const double v = (tda * tda) + (tdb * tdb);
         ms_sum = ms_sum - ms_old;
         ms_sum = ms_sum + fabs(v);
-        if (!(AERO_X_DROP & 4)) pmsb[pms_slot] = make_double2(fabs(av), fabs(v));
+        (void)pms_slot;
+        sh.pmw[pk][pair] = make_double2(fabs(av), fabs(v));
         ms_p++;
         ms_p %= MSE_LEN;
         // ms_sum sums (|t| - 1)^2 terms: 0 or a multiple of 2^-158, so the short division is exact
@@ -769,6 +794,24 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       sh.pi[PI_DT_P][pair] = dt_p;
       sh.pi[PI_PM_P][pair] = pm_p;
       sh.pi[PI_MS_P][pair] = ms_p;
+      if (dk == DT_WIN - 1) {  // the dt window written back, the next one read
+        if (!(AERO_X_DROP & 4)) {
+#pragma unroll
+          for (int k = 0; k < DT_WIN; ++k) dtb[(dtw0 + k) % DT_LEN] = sh.dtw[k][pair];
+#pragma unroll
+          for (int k = 0; k <= DT_WIN; ++k) sh.dtw[k][pair] = dtb[(dtw0 + DT_WIN + k) % DT_LEN];
+        }
+        sh.pi[PI_DTW0][pair] = (dtw0 + DT_WIN) % DT_LEN;
+      }
+      if (pk == PM_WIN - 1) {  // the same for MSEcalc
+        if (!(AERO_X_DROP & 4)) {
+#pragma unroll
+          for (int k = 0; k < PM_WIN; ++k) pmsb[(pmw0 + k) % MSE_LEN] = sh.pmw[k][pair];
+#pragma unroll
+          for (int k = 0; k < PM_WIN; ++k) sh.pmw[k][pair] = pmsb[(pmw0 + PM_WIN + k) % MSE_LEN];
+        }
+        sh.pi[PI_PMW0][pair] = (pmw0 + PM_WIN) % MSE_LEN;
+      }
       nco_next(m2_ptr, m2_step);
       cm_next = T.cis[cis_index(m2_ptr)];  // the event moved mixer2
       ++i;
@@ -807,6 +850,15 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
   ls[LS_FILLED * C] = n0 + ifl;
   ls[LS_SOFT_P * C] = sh.pl[PL_SOFTP][pair];
   if (TRACE) ls[LS_PT_N * C] = sh.pl[PL_PTN][pair];
+  if (!(AERO_X_DROP & 4)) {  // the ring windows back (their unwritten slots hold what was read)
+    double2 *dtb = S.dt + (size_t)cl * DT_LEN;
+    double2 *pmsb = reinterpret_cast<double2 *>(S.pm) + (size_t)cl * MSE_LEN;
+    const int dtw0 = sh.pi[PI_DTW0][pair], pmw0 = sh.pi[PI_PMW0][pair];
+#pragma unroll
+    for (int k = 0; k < DT_WIN; ++k) dtb[(dtw0 + k) % DT_LEN] = sh.dtw[k][pair];
+#pragma unroll
+    for (int k = 0; k < PM_WIN; ++k) pmsb[(pmw0 + k) % MSE_LEN] = sh.pmw[k][pair];
+  }
   if ((sh.pl[PL_SOFTP][pair] & 15) && !(AERO_X_DROP & 2))  // the group being filled (bytes past softp are not read)
     *reinterpret_cast<uint4 *>(S.soft + (size_t)cl * SOFT_RING + (sh.pl[PL_SOFTP][pair] & (SOFT_RING - 16))) =
         make_uint4(sh.softw[0][pair], sh.softw[1][pair], sh.softw[2][pair], sh.softw[3][pair]);
