@@ -143,7 +143,7 @@ __device__ __forceinline__ int qround(double d) {  // qRound (Qt 5.9 qglobal.h:5
 // i.e. once per ~9 samples)
 enum { PD_CTX1, PD_CTX2, PD_CTY1, PD_CTY2, PD_MARG_SUM, PD_PM_SUM, PD_MS_SUM, PD_MSE, PD_PTD_RE, PD_PTD_IM,
        PD_M2_FREQ, PD_N };
-enum { PI_MARG_P, PI_DT_P, PI_PM_P, PI_MS_P, PI_N, PI_TICK = PI_N, PI_DTW0, PI_PMW0, PI_ALL };
+enum { PI_MARG_P, PI_DT_P, PI_PM_P, PI_MS_P, PI_N, PI_TICK = PI_N, PI_DTW0, PI_PMW0, PI_MGW0, PI_ALL };
 enum { PL_SOFTP, PL_PTN, PL_N };
 
 constexpr int DEMOD_BLOCK = 256;  // channels per workgroup
@@ -207,11 +207,12 @@ __device__ __forceinline__ void lds_store(int *p, int v) {
 }
 
 constexpr int FIR_LDS_IM = 11, FIR_LDS_RE = 5;
-// the dt and MSEcalc rings through LDS windows of DT_WIN / PM_WIN events
-// (the dt window holds one slot more: an event writes slot p and reads p + 1):
-// one read and one write of the window's slots per DT_WIN / PM_WIN events
-// instead of a line fetched and written back per event
-constexpr int DT_WIN = 4, PM_WIN = 4;
+// the carrier-event rings (dt, MSEcalc, marg) through LDS windows of
+// DT_WIN / PM_WIN / MG_WIN events (the dt window holds one slot more: an
+// event writes slot p and reads p + 1): one read and one write of the
+// window's slots per window instead of a line fetched and written back per
+// event
+constexpr int DT_WIN = 4, PM_WIN = 4, MG_WIN = 4;
 
 struct DemodShared {
   uint32_t ring[RING_GROUP][DEMOD_BLOCK];
@@ -240,6 +241,7 @@ struct DemodShared {
   uint32_t softw[4][DEMOD_BLOCK];
   double2 dtw[DT_WIN + 1][DEMOD_BLOCK];  // dt slots PI_DTW0 .. + DT_WIN
   double2 pmw[PM_WIN][DEMOD_BLOCK];      // MSEcalc slots PI_PMW0 .. + PM_WIN - 1
+  double mgw[MG_WIN][DEMOD_BLOCK];       // marg slots PI_MGW0 .. + MG_WIN - 1
 };
 
 // dst += a (dst = a + b) for the lanes in m only, the rest keep dst: one
@@ -463,6 +465,11 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
         sh.pmw[k][pair] = (AERO_X_DROP & 4) ? make_double2(0.0, 0.0) : pmsb[(pp + k) % MSE_LEN];
       sh.pi[PI_DTW0][pair] = dp;
       sh.pi[PI_PMW0][pair] = pp;
+      const int mp = sh.pi[PI_MARG_P][pair];
+      const double *mgb = S.marg + (size_t)c * MARG_LEN;
+#pragma unroll
+      for (int k = 0; k < MG_WIN; ++k) sh.mgw[k][pair] = (AERO_X_DROP & 4) ? 0.0 : mgb[(mp + k) % MARG_LEN];
+      sh.pi[PI_MGW0][pair] = mp;
     }
     q54 = S.fir[(size_t)(NTAPS - 1) * C + c];
     q54i = S.fir[(size_t)(2 * NTAPS - 1) * C + c];
@@ -685,7 +692,10 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       int dk = dt_p - dtw0, pk = pm_p - pmw0;  // the slots' places in the windows
       if (dk < 0) dk += DT_LEN;
       if (pk < 0) pk += MSE_LEN;
-      const double marg_old = (AERO_X_DROP & 4) ? 0.0 : marg[marg_p];
+      const int mgw0 = sh.pi[PI_MGW0][pair];
+      int mk = marg_p - mgw0;
+      if (mk < 0) mk += MARG_LEN;
+      const double marg_old = sh.mgw[mk][pair];
       const double2 dv = sh.dtw[dk + 1][pair];
       const double2 pms_old = sh.pmw[pk][pair];
       const double pm_old = pms_old.x, ms_old = pms_old.y;
@@ -716,7 +726,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       // marg->UpdateSigned (DSP.cpp:419-427)
       marg_sum = marg_sum - marg_old;
       marg_sum = marg_sum + (ct_ec);
-      if (!(AERO_X_DROP & 4)) marg[marg_p] = ct_ec;
+      sh.mgw[mk][pair] = ct_ec;
       marg_p++;
       marg_p %= MARG_LEN;
       const double mval = DM_DIVC(marg_sum, ((double)MARG_LEN));
@@ -803,6 +813,15 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
         }
         sh.pi[PI_DTW0][pair] = (dtw0 + DT_WIN) % DT_LEN;
       }
+      if (mk == MG_WIN - 1) {  // the same for marg
+        if (!(AERO_X_DROP & 4)) {
+#pragma unroll
+          for (int k = 0; k < MG_WIN; ++k) marg[(mgw0 + k) % MARG_LEN] = sh.mgw[k][pair];
+#pragma unroll
+          for (int k = 0; k < MG_WIN; ++k) sh.mgw[k][pair] = marg[(mgw0 + MG_WIN + k) % MARG_LEN];
+        }
+        sh.pi[PI_MGW0][pair] = (mgw0 + MG_WIN) % MARG_LEN;
+      }
       if (pk == PM_WIN - 1) {  // the same for MSEcalc
         if (!(AERO_X_DROP & 4)) {
 #pragma unroll
@@ -858,6 +877,10 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
     for (int k = 0; k < DT_WIN; ++k) dtb[(dtw0 + k) % DT_LEN] = sh.dtw[k][pair];
 #pragma unroll
     for (int k = 0; k < PM_WIN; ++k) pmsb[(pmw0 + k) % MSE_LEN] = sh.pmw[k][pair];
+    double *mgb = S.marg + (size_t)cl * MARG_LEN;
+    const int mgw0 = sh.pi[PI_MGW0][pair];
+#pragma unroll
+    for (int k = 0; k < MG_WIN; ++k) mgb[(mgw0 + k) % MARG_LEN] = sh.mgw[k][pair];
   }
   if ((sh.pl[PL_SOFTP][pair] & 15) && !(AERO_X_DROP & 2))  // the group being filled (bytes past softp are not read)
     *reinterpret_cast<uint4 *>(S.soft + (size_t)cl * SOFT_RING + (sh.pl[PL_SOFTP][pair] & (SOFT_RING - 16))) =
