@@ -305,6 +305,10 @@ __global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, in
   double2 cm_next = T.cis[c_cis_index(m2_ptr)], so_next = T.cis[c_cis_index(so_ptr)];
   double2 cu_next = T.cis[c_cis_index(up_ptr)], o_next = cout[n0 & (C_OUT_RING - 1)];
   double agc_next = S.agc[(size_t)agc_ptr * C + c];
+  // the PCM word of the coarse-ring entry a sample writes (the next
+  // sample's) is loaded two samples ahead: one ahead it would be waited for
+  // at once by the entry's store
+  int16_t pcm_n1 = S.pcm[(size_t)((n0 + 1) & capm) * C + c], pcm_n2 = S.pcm[(size_t)((n0 + 2) & capm) * C + c];
   int i = 0;
   while (i < ie) {
     bool pend = false;
@@ -396,10 +400,11 @@ __global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, in
       so_next = T.cis[c_cis_index(so_ptr)];
       if (i + 1 < ia) {  // coarse-ring entry of the next sample (:351-356)
         const long long n1 = n + 1;
-        const int16_t x = S.pcm[(size_t)(n1 & capm) * C + c];
-        S.cring[(size_t)c * NFFT + (n1 & (NFFT - 1))] = (uint32_t)c_cis_index(mc_ptr) | ((uint32_t)(uint16_t)x << 16);
+        S.cring[(size_t)c * NFFT + (n1 & (NFFT - 1))] = (uint32_t)c_cis_index(mc_ptr) | ((uint32_t)(uint16_t)pcm_n1 << 16);
         ifl = i + 2;
       }
+      pcm_n1 = pcm_n2;
+      pcm_n2 = S.pcm[(size_t)((n + 3) & capm) * C + c];  // past the pushed samples: unused
       if (!pend) {
         c_nco_next(m2_ptr, m2_step);
         cm_next = T.cis[c_cis_index(m2_ptr)];
