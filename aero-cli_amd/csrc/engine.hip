@@ -914,7 +914,7 @@ int run_pass(Group *e, int flush, bool *more) {
     // host mirror of the hop and segment rules of coarse.hip / demod_*.hip
     bool any_hop = false, progress = false;
     // the C channel: the next message of every channel whose demod has
-    // reached the end of the prefiltered one (cchan.hip prefilter_c_kernel)
+    // reached the end of the prefiltered one (cchan.hip prefilter_dn_kernel, prefilter_blk_kernel)
     int ncj = 0, kcj = 0;
     if (cch) {
       kcj = e->next_cjob;

@@ -80,13 +80,13 @@ MODES = {
                                   'trident': 'trident_bmsk_kernel', 'frame': 'frame_bmsk_kernel',
                                   'viterbi': 'rt_viterbi_kernel'}),
     # the C channel: OQPSK 8400 with its per-message JFastFir prefilter, AeroL::DecodeC;
-    # 2 B int16 in + 16 B AGC ring r/w + soft bits out as C2 (the prefiltered-sample ring, 32 B per
-    # sample written and read, is this engine's and reported beside it); a step is one 12000-sample
+    # 2 B int16 in + 16 B AGC ring r/w + soft bits out as C2 (the prefilter's down-mix words and
+    # outputs, 4 + 16 B per sample written and read, are this engine's); a step is one 12000-sample
     # message per channel (the prefilter follows message boundaries, oqpskdemodulator.cpp:292-324)
     'c8400': dict(bitrate=8400, hop=12000, fs=48000, bytes=18.22, timing='c8400_demod', preroll=8,
                   metric='Msamples/s demod+Viterbi, 8400bps C channel (f4); SUs and voice bit-exact vs ref',
                   cpu_seconds=240.0, config='f4 (C channel 8400)', flops=1300.0, nfft_log2=14, kind='C-channel',
-                  kernels={'prefilter': 'prefilter_c_kernel', 'demod': 'demod_c_kernel', 'coarse': 'coarse_kernel',
+                  kernels={'prefilter': 'prefilter_dn_kernel + prefilter_blk_kernel', 'demod': 'demod_c_kernel', 'coarse': 'coarse_kernel',
                            'frame': 'frame_c_kernel', 'viterbi': 'viterbi_c_kernel'}),
     # 2 B int16 in + 0.025 B soft bits out (fb stays 600 at 24 kHz, decode/decode.cpp:142-150)
     'msk1200': dict(bitrate=1200, hop=2048, fs=24000, bytes=2.025,
