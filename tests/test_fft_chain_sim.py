@@ -5,7 +5,9 @@ tools/fft_chain_sim.cpp): the three transforms of CoarseFreqEstimate
 134-160) through the register stages, the wave-local LDS transpose, the
 v_permlane16/32_swap steps and the G exchange equal the oracle's JFFT chain
 (decode/jfft.cpp:114-212) value for value, up to the sign of exact zeros
-(the kernel skips the exact (1, +-0) twiddle products)."""
+(the kernel skips the exact (1, +-0) twiddle products), with
+the G-layout stages past the LDS twiddles reading the permuted copy the
+kernel reads (fft_layout.h twg_build)."""
 import ctypes
 import os
 

@@ -30,6 +30,15 @@ struct Sim {
   std::vector<C> v = std::vector<C>((size_t)T * 16);
   std::vector<double> lds = std::vector<double>((size_t)N + N / 16);
   const C *tw = nullptr, *twi = nullptr;
+  // the permuted copies the kernel reads its G-layout stages past the LDS
+  // twiddles from (fft_layout.h twg_build)
+  std::vector<C> twg = std::vector<C>((size_t)N), twgi = std::vector<C>((size_t)N);
+  void set_tables(const C *f, const C *i) {
+    tw = f;
+    twi = i;
+    twg_build<L>(reinterpret_cast<const double *>(f), reinterpret_cast<double *>(twg.data()));
+    twg_build<L>(reinterpret_cast<const double *>(i), reinterpret_cast<double *>(twgi.data()));
+  }
 
   C &at(int t, int i) { return v[(size_t)t * 16 + i]; }
 
@@ -51,7 +60,9 @@ struct Sim {
           yr = xl.x;
           yi = xl.y;
         } else {
-          const C w = table[n - 1 + ((a & (n - 1)) | kr)];
+          constexpr bool perm = KIND == K_G && n > (L >= 14 ? 512 : 256);  // TwLds<L>::N
+          const C w = perm ? (INV ? twgi : twg)[(size_t)(twg_base<L>(S) + twg_row<L>(S, i)) * T + t]
+                           : table[n - 1 + ((a & (n - 1)) | kr)];
           yr = w.x * xl.x - w.y * xl.y;
           yi = w.x * xl.y + w.y * xl.x;
         }
@@ -157,15 +168,13 @@ extern "C" int fft_chain_sim(int L, const double *tw, const double *twi, const d
                              double *out) {
   if (L == 14) {
     Sim<14> s;
-    s.tw = reinterpret_cast<const C *>(tw);
-    s.twi = reinterpret_cast<const C *>(twi);
+    s.set_tables(reinterpret_cast<const C *>(tw), reinterpret_cast<const C *>(twi));
     s.run(reinterpret_cast<const C *>(in), start, stop, reinterpret_cast<C *>(out));
     return 0;
   }
   if (L == 13) {
     Sim<13> s;
-    s.tw = reinterpret_cast<const C *>(tw);
-    s.twi = reinterpret_cast<const C *>(twi);
+    s.set_tables(reinterpret_cast<const C *>(tw), reinterpret_cast<const C *>(twi));
     s.run(reinterpret_cast<const C *>(in), start, stop, reinterpret_cast<C *>(out));
     return 0;
   }
