@@ -34,7 +34,8 @@ F_DCD_TICK = 0x40  # AeroL's 1 s DCD timer on the sample clock (continuous OQPSK
 F_TRACE_ALL = F_TRACE_PT | F_TRACE_BLOCKS | F_TRACE_SOFT | F_TRACE_HOPS | F_TRACE_FRAMES
 
 MATH_FN = {'hypot': 0, 'atan2': 1, 'tanh': 2, 'sin': 3, 'cos': 4, 'log10': 5, 'sqrt': 6, 'fmod360': 7,
-           'div': 8, 'div_c48000': 9, 'div_c360': 10, 'div_n': 11, 'div_c192000': 13, 'hypot_nr': 14, 'atan2_bf': 15}
+           'div': 8, 'div_c48000': 9, 'div_c360': 10, 'div_n': 11, 'div_c192000': 13, 'hypot_nr': 14, 'atan2_bf': 15,
+           'tanh_bf': 16, 'sin_bf': 17, 'cos_bf': 18}
 
 
 class EngineCfg(ctypes.Structure):

@@ -321,6 +321,81 @@ AERO_HD double aero_tanh(double x) {
   return (jx >= 0) ? z : -z;
 }
 
+/* aero_expm1 on the arguments aero_tanh gives it for 2^-55 <= |x| < 22:
+ * a = 2|x| in [2, 44) or a = -2|x| in (-2, -2^-54], without a branch.  There
+ * glibc returns none of its early values, and k is 0 (|a| <= 0x3fd62e42's
+ * binade bound), -1 (forced, |a| below 0x3ff0a2b2), or (int)(a/ln2 -+ 1/2)
+ * in {-3, -2, -1} and [3, 63]; its k = 1 case needs a positive a < 1.04 and
+ * does not occur.  One reduction serves every k: t = k gives x - t ln2_hi =
+ * x -+ ln2_hi and t ln2_lo = +-ln2_lo bit for bit for the forced k = +-1, and
+ * x - 0 = x, c = (x - x) - 0 = +0 for k = 0, which is what glibc's
+ * unreduced path holds.  The tail's five forms are evaluated side by side and
+ * selected.  (r1 - t) / (6 - x t) is a division by div_n: the numerator is
+ * about -2 and the divisor about 6 for every reduced x (|x| <= 0.35), inside
+ * its contract. */
+AERO_HD double g_expm1_tanh_bf(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+               invln2 = 1.44269504088896338700e+00, Q1 = -3.33333333333331316428e-02,
+               Q2 = 1.58730158725481460165e-03, Q3 = -7.93650757867487942473e-05,
+               Q4 = 4.00821782732936239552e-06, Q5 = -2.01099218183624371326e-07;
+  const uint32_t hx0 = hiw(x), xsb = hx0 & 0x80000000u, hx = hx0 & 0x7fffffffu;
+  int32_t k = (int32_t)(invln2 * x + ((xsb == 0) ? 0.5 : -0.5));
+  k = hx < 0x3FF0A2B2u ? ((xsb == 0) ? 1 : -1) : k;
+  k = hx > 0x3fd62e42u ? k : 0;
+  const double tk = k;
+  const double hi = x - tk * ln2_hi, lo = tk * ln2_lo;
+  x = hi - lo;
+  const double c = (hi - x) - lo;
+  const double hfx = 0.5 * x;
+  const double hxs = x * hfx;
+  const double R1 = 1.0 + hxs * Q1;
+  const double h2 = hxs * hxs;
+  const double R2 = Q2 + hxs * Q3;
+  const double h4 = h2 * h2;
+  const double R3 = Q4 + hxs * Q5;
+  const double r1 = R1 + h2 * R2 + h4 * R3;
+  const double t = 3.0 - r1 * hfx;
+  const double e = hxs * div_n(r1 - t, 6.0 - x * t);
+  const double r_k0 = x - (x * e - hxs);
+  double e2 = (x * (e - c) - c);
+  e2 -= hxs;
+  const double r_m1 = 0.5 * (x - e2) - 0.5;
+  const uint32_t kup = (uint32_t)k << 20;
+  double yb = 1.0 - (e2 - x);
+  yb = sethi(yb, hiw(yb) + kup);
+  const double r_far = yb - 1.0;  // k <= -2 or k > 56 (k == 1024 does not occur)
+  const int32_t ks = k < 0 ? 0 : (k > 19 ? 19 : k);  // the shift's count where it is selected
+  double y1 = mkd(0x3ff00000u - (0x200000u >> ks), 0) - (e2 - x);
+  y1 = sethi(y1, hiw(y1) + kup);  // 3 <= k < 20
+  double y2 = x - (e2 + mkd((uint32_t)((0x3ff - k) << 20), 0));
+  y2 += 1.0;
+  y2 = sethi(y2, hiw(y2) + kup);  // 20 <= k <= 56
+  return k == 0 ? r_k0 : (k == -1 ? r_m1 : ((k <= -2 || k > 56) ? r_far : (k < 20 ? y1 : y2)));
+}
+
+/* aero_tanh without branches when every active lane of the wave has
+ * 2^-55 <= |x| < 22 (the demods' soft values, |x| < 4); the general code
+ * otherwise.  Its two forms share one expm1 and one division:
+ * 1 - 2 / (t + 2) with t = expm1(2|x|) for |x| >= 1, -t / (t + 2) with
+ * t = expm1(-2|x|) below; both quotients are in div_r's contract (t + 2 in
+ * (1.13, 2) or >= 8.3, the numerator 2 or |t| >= 2^-54). */
+AERO_HD double aero_tanh_bf(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int32_t jx = (int32_t)hiw(x), ix = jx & 0x7fffffff;
+  const bool ok = ix < 0x40360000 && ix >= 0x3c800000;
+  if (!__builtin_expect(__all(ok), 1)) return aero_tanh(x);
+  const bool big = ix >= 0x3ff00000;
+  const double ax = __builtin_fabs(x);
+  const double t = g_expm1_tanh_bf(big ? 2.0 * ax : -2.0 * ax);
+  const double d = t + 2.0;
+  const double q = div_r(big ? 2.0 : -t, d, rcp_div(d));
+  const double z = big ? 1.0 - q : q;
+  return (jx >= 0) ? z : -z;
+#else
+  return aero_tanh(x);
+#endif
+}
+
 /* ------------------------------------------------------------ sincos
  * glibc 2.35 sincos (sysdeps/ieee754/dbl-64/s_sincos.c + the do_sin /
  * do_cos / reduce_sincos helpers of s_sin.c), SSE2 build: libm.so.6's
@@ -430,6 +505,48 @@ AERO_HD void aero_sincos_t(double x, double &so, double &co, const double *sct) 
 }
 
 AERO_HD void aero_sincos(double x, double &so, double &co) { aero_sincos_t(x, so, co, aero_g_sincostab); }
+
+/* aero_sincos_t without branches when every active lane of the wave has
+ * |x| < 0.855469 (hi word below 0x3feb6000: the loop corrections and
+ * rotator frequencies of the demods); the general code otherwise.  There
+ * sincos is (x, 1) below 2^-27 and (do_sin(x, 0), do_cos(x, 0)) above, and
+ * do_sin is the Taylor form below 0.126 and the table form above: all four
+ * are evaluated and selected, the two table forms on the one row of
+ * u = BIG + |x|. */
+AERO_HD void aero_sincos_bf(double x, double &so, double &co, const double *sct) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t k = hiw(x) & 0x7fffffffu;
+  if (!__builtin_expect(__all(k < 0x3feb6000u), 1)) {
+    aero_sincos_t(x, so, co, sct);
+    return;
+  }
+  const double ax = __builtin_fabs(x);
+  const double s_tay = g_taylor_sin(x * x, x, 0.0);
+  const double dxs = x <= 0 ? -0.0 : 0.0;  // do_sin's dx = -dx for x <= 0
+  const double u = AERO_G_BIG + ax;
+  const double xs = ax - (u - AERO_G_BIG);
+  const double xxs = xs * xs;
+  const double ss = xs + (dxs + (xs * xxs) * (xxs * AERO_G_SN5 - AERO_G_NSN3));
+  const double cs_ = xs * dxs + xxs * ((xxs * AERO_G_CS6 - AERO_G_NCS4) * xxs + AERO_G_CS2);
+  const int row = (int)(low(u) << 2);
+  const double sn = sct[row], ssn = sct[row + 1], cs = sct[row + 2], ccs = sct[row + 3];
+  const double cor_s = (ssn + ss * ccs - sn * cs_) + cs * ss;
+  const double s_tab = __builtin_copysign(sn + cor_s, x);
+  // do_cos(x, 0): dx = -0 for x < 0, added to the reduced argument
+  const double dxc = x < 0 ? -0.0 : 0.0;
+  const double xc = ax - (u - AERO_G_BIG) + dxc;
+  const double xxc = xc * xc;
+  const double sc = xc + (xc * xxc) * (xxc * AERO_G_SN5 - AERO_G_NSN3);
+  const double cc = xxc * ((xxc * AERO_G_CS6 - AERO_G_NCS4) * xxc + AERO_G_CS2);
+  const double cor_c = (ccs - sc * ssn - cs * cc) - sn * sc;
+  const double c_tab = cs + cor_c;
+  const bool tiny = k < 0x3e400000u;
+  so = tiny ? x : (ax < 0.126 ? s_tay : s_tab);
+  co = tiny ? 1.0 : c_tab;
+#else
+  aero_sincos_t(x, so, co, sct);
+#endif
+}
 
 AERO_HD double aero_sin(double x) {
   double s, c;

@@ -608,7 +608,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
           div_c(((double)cntr) - (SPS * (128 + 10)), (double)(((256 - 10) * SPS) - (SPS * (128 + 10))));  // integer numerator
       const double t1r = s2r * str_r - s2i * str_i, t1i = s2r * str_i + s2i * str_r;
       const double spr = t1r * 0.0 - t1i * 1.0, spi = t1r * 1.0 + t1i * 0.0;  // * imag
-      const double er = aero_tanh(spi) * (spr);
+      const double er = aero_tanh_bf(spi) * (spr);
       double ec, es;
       b_cexp_i(er * 0.01, ec, es);
       const double nr = str_r * ec - str_i * es, ni = str_r * es + str_i * ec;
@@ -622,7 +622,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       double st_err = B_ATAN2(er_i, er_r);
       st_err *= 1.5 * (1.0 - progress * progress);
       b_advance(q_ptr, -(1.0 / (2.0 * M_PI)) * st_err * 0.1);
-      b_set_phase_deg(so_ptr, (360.0 * q_ptr / ((double)WTSIZE)) * 4.0 + (360.0 * 0.4));
+      b_set_phase_deg_pos(so_ptr, (360.0 * q_ptr / ((double)WTSIZE)) * 4.0 + (360.0 * 0.4));
       so_n = T.cis[b_cis_index(so_ptr)];
     }
     {  // sig2 *= symboltone_averotator; rotator *= exp(i rotator_freq); sig2 *= rotator
@@ -693,8 +693,9 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         const double pt_last = div_n(tw, so_step);  // tw: 0 or >= 2^-40, so_step ~4375
         const double pt_this = 1.0 - pt_last;
         const double ptr_ = pt_this * s2r + pt_last * s2l_r, pti = pt_this * s2i + pt_last * s2l_i;
+        // the remainder of a value in [72, 792): 0 or a multiple of ulp(72), in div_c's contract
         const double twospeed =
-            -4.0 * ((b_fmod360((360.0 * q_ptr / ((double)WTSIZE)) * 2.0 + (360.0 * 0.4 * 0.5)) / 360.0) -
+            -4.0 * (div_c(b_fmod360((360.0 * q_ptr / ((double)WTSIZE)) * 2.0 + (360.0 * 0.4 * 0.5)), 360.0) -
                     (0.34046 + 0.4111 * 0.4));
         const bool even = !(twospeed < 0);
         yui++;
@@ -710,8 +711,8 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
           ptd_i = pti;
         } else {
           const double qr = ptr_, qi = ptd_i;  // pt_qpsk
-          const double ct_xt = aero_tanh(pti) * ptr_;
-          const double ct_xt_d = aero_tanh(ptd_r) * ptd_i;
+          const double ct_xt = aero_tanh_bf(pti) * ptr_;
+          const double ct_xt_d = aero_tanh_bf(ptd_r) * ptd_i;
           double ct_ec = ct_xt_d - ct_xt;
           if (ct_ec > M_PI) ct_ec = M_PI;
           if (ct_ec < -M_PI) ct_ec = -M_PI;

@@ -37,10 +37,16 @@ __device__ __forceinline__ int b_cis_index(double WTptr) {  // WaveTable::WTCISV
   return tint;
 }
 
+// The wrap loops below run their first iteration as a select and the rest
+// behind a wave-uniform test (the same iterations in the same order: a peeled
+// loop); a step never exceeds a wave, so the rest never runs in practice, and
+// the divergent loop's exec-mask bookkeeping is gone from the per-sample path.
 __device__ __forceinline__ void b_nco_next(double &ptr, double &step) {  // WTnextFrame (DSP.cpp:71-79)
   if (step < 0) step = 0;
   ptr += step;
-  while (((int)ptr) >= WTSIZE) ptr -= WTSIZE;
+  ptr = ((int)ptr) >= WTSIZE ? ptr - WTSIZE : ptr;
+  if (__builtin_expect(__any(((int)ptr) >= WTSIZE), 0))
+    while (((int)ptr) >= WTSIZE) ptr -= WTSIZE;
 }
 
 __device__ __forceinline__ void b_set_freq(double &freq, double &step, double f) {  // SetFreq (DSP.cpp:163-168)
@@ -55,23 +61,37 @@ __device__ __forceinline__ void b_set_freq(double &freq, double &step, double f)
 // ulp(x), and each difference is no larger than x) and so equals fmod's
 // exact remainder; otherwise fmod itself
 __device__ __forceinline__ double b_fmod360(double x) {
-  if (x >= 0.0 && x < 1800.0) {
-    while (x >= 360.0) x -= 360.0;
-    return x;
-  }
-  return fmod(x, 360.0);
+  const bool in = x >= 0.0 && x < 1800.0;
+  double r = x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r = r >= 360.0 ? r - 360.0 : r;  // the loop's (at most 4) iterations
+  if (__builtin_expect(__any(!in), 0)) r = in ? r : fmod(x, 360.0);
+  return r;
 }
 
 __device__ __forceinline__ void b_set_phase_deg(double &ptr, double phase_deg) {  // SetPhaseDeg (DSP.cpp:177-187)
   phase_deg = b_fmod360(phase_deg);
-  while (phase_deg < 0) phase_deg += 360.0;
+  // fmod's remainder is above -360: the loop adds 360 at most once
+  phase_deg = phase_deg < 0 ? phase_deg + 360.0 : phase_deg;
   ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+}
+// SetPhaseDeg for a phase in [0, 1800) made of pointer values (the symbol-tone
+// PLL's 4 x (360 q_ptr / W) + 144): the remainder is 0 or a multiple of
+// ulp(144) >= 2^-45, inside div_c's contract
+__device__ __forceinline__ void b_set_phase_deg_pos(double &ptr, double phase_deg) {
+  phase_deg = b_fmod360(phase_deg);
+  phase_deg = phase_deg < 0 ? phase_deg + 360.0 : phase_deg;
+  ptr = div_c(phase_deg, 360.0) * ((double)WTSIZE);
 }
 
 __device__ __forceinline__ void b_advance(double &ptr, double frac) {  // AdvanceFractionOfWave (DSP.h:59-65)
   ptr += frac * WTSIZE;
-  while (ptr >= WTSIZE) ptr -= WTSIZE;
-  while (ptr < 0) ptr += WTSIZE;
+  ptr = ptr >= WTSIZE ? ptr - WTSIZE : ptr;
+  if (__builtin_expect(__any(ptr >= WTSIZE), 0))
+    while (ptr >= WTSIZE) ptr -= WTSIZE;
+  ptr = ptr < 0 ? ptr + WTSIZE : ptr;
+  if (__builtin_expect(__any(ptr < 0), 0))
+    while (ptr < 0) ptr += WTSIZE;
 }
 
 __device__ __forceinline__ int b_qround(double d) {  // qRound (Qt 5.9 qglobal.h:525)
@@ -79,14 +99,11 @@ __device__ __forceinline__ int b_qround(double d) {  // qRound (Qt 5.9 qglobal.h
 }
 
 // std::exp(complex(0 * y, y)) as glibc's cexp returns it: (cos y, sin y), or
-// (1, y) when |y| <= DBL_MIN
+// (1, y) when |y| <= DBL_MIN, which is also sincos's value there (below 2^-27
+// it returns (y, 1)): sincos alone, branch-free for the small arguments of the
+// loop corrections (aero_sincos_bf)
 __device__ __forceinline__ void b_cexp_i(double y, double &c, double &s) {
-  if (fabs(y) > 2.2250738585072014e-308) {
-    aero_sincos(y, s, c);
-  } else {
-    s = y;
-    c = 1.0;
-  }
+  aero_sincos_bf(y, s, c, aero_g_sincostab);
 }
 
 // PeakDetector's d3.findmaxpos (DSP.h:491-566): the position of the first

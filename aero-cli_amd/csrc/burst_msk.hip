@@ -444,7 +444,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
       if (tone) {  // symbol-tone x4 PLL (:555-578)
         const double t1r = s2r * str_r - s2i * str_i, t1i = s2r * str_i + s2i * str_r;
         const double spr = t1r * 0.0 - t1i * 1.0, spi = t1r * 1.0 + t1i * 0.0;  // * imag
-        const double er = aero_tanh(spi) * (spr);
+        const double er = aero_tanh_bf(spi) * (spr);
         double ec, es;
         b_cexp_i(er * 0.5, ec, es);
         const double nr = str_r * ec - str_i * es, ni = str_r * es + str_i * ec;
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         double st_err = B_ATAN2(er_i, er_r);
         st_err *= 0.5 * (1.0 - progress * progress);
         b_advance(sh_ptr, -(1.0 / (2.0 * M_PI)) * st_err * 0.05);
-        b_set_phase_deg(so_ptr, (360.0 * sh_ptr / ((double)WTSIZE)) + (360.0 * (1.0 - M_EE)));
+        b_set_phase_deg_pos(so_ptr, (360.0 * sh_ptr / ((double)WTSIZE)) + (360.0 * (1.0 - M_EE)));  // in [351, 711)
         so_n = T.cis[b_cis_index(so_ptr)];
       }
       {  // sig2 *= symboltone_averotator; rotator *= exp(i rotator_freq); sig2 *= rotator
@@ -529,8 +529,8 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         if (tl < 0.0) tl += WTSIZE;
         if (tw < 0.0) tw += WTSIZE;
         if ((tl > 3.0 * WTSIZE / 4.0) && (tw < 1.0 * WTSIZE / 4.0)) {
-          const double ct_xt = aero_tanh(s2i) * s2r;
-          const double ct_xt_d = aero_tanh(pdr) * pdi;
+          const double ct_xt = aero_tanh_bf(s2i) * s2r;
+          const double ct_xt_d = aero_tanh_bf(pdr) * pdi;
           double ct_ec = ct_xt_d - ct_xt;
           if (ct_ec > M_PI) ct_ec = M_PI;
           if (ct_ec < -M_PI) ct_ec = -M_PI;

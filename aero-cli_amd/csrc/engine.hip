@@ -130,6 +130,9 @@ __global__ void math_kernel(int fn, const double *x, const double *y, double *ou
     case 13: r = div_c(a, 192000.0); break;
     case 14: r = aero_hypot_nr(a, b); break;
     case 15: r = aero_atan2_bf(a, b, aero_g_cij); break;
+    case 16: r = aero_tanh_bf(a); break;
+    case 17: { double sn, cs; aero_sincos_bf(a, sn, cs, aero_g_sincostab); r = sn; break; }
+    case 18: { double sn, cs; aero_sincos_bf(a, sn, cs, aero_g_sincostab); r = cs; break; }
     default: break;
   }
   out[i] = r;

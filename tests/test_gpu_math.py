@@ -137,3 +137,64 @@ def test_atan2_branch_free_main_path_is_glibc(engine_lib):
             same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
             assert same.all(), (yy[~same][:3], xx[~same][:3])
     eng.close()
+
+
+@pytest.mark.gpu
+def test_tanh_and_sincos_branch_free_paths_are_glibc(engine_lib):
+    """aero_tanh_bf (2^-55 <= |x| < 22 in every lane of the wave: one expm1
+    with its five tail forms selected, div_n / div_r divisions) and
+    aero_sincos_bf (|x| < 0.855: the Taylor and table forms of do_sin and
+    do_cos selected) equal glibc's tanh and sincos bit for bit; whole waves
+    in range (the branch-free path runs), the form boundaries (|x| = 1,
+    expm1's k = 0 / -1 / general cuts at 2|x| = 0.3466 and 1.0397, the k < 20
+    and k > 56 forms, 0.126, 2^-27, table rows), and waves that mix special
+    or out-of-range lanes in (the general code runs)."""
+    import aero_engine as ae
+    import mathhost
+    eng = ae.Engine(max_channels=1)
+    rng = np.random.default_rng(31)
+    n = 1 << 19
+    sg = rng.choice([-1.0, 1.0], n)
+
+    def near(v, rel=1e-12):
+        return np.repeat(v, n // len(v) + 1)[:n] * (1 + rng.standard_normal(n) * rel) * sg
+
+    ln2 = np.log(2.0)
+    th_cases = [rng.uniform(-4, 4, n),                                            # soft values
+                sg * np.exp2(rng.uniform(-55, np.log2(21.9), n)),                  # the whole range
+                near(np.array([1.0, 0.3466 / 2, 1.0397 / 2, 0.1733, 0.51985])),
+                near(np.array([(k + 0.5) * ln2 / 2 for k in list(range(-4, 0)) + list(range(2, 64))]), 1e-15),
+                near(np.array([19.5 * ln2 / 2, 20.5 * ln2 / 2, 56.5 * ln2 / 2, 21.99, 2.0 ** -55]), 1e-15)]
+    mixed = th_cases[1].copy()
+    mixed[::61] = 0.0
+    mixed[1::67] = -0.0
+    mixed[2::71] = np.inf
+    mixed[3::73] = np.nan
+    mixed[4::79] = 30.0
+    mixed[5::83] = 1e-20
+    th_cases.append(mixed)
+    for x in th_cases:
+        got = eng.device_math('tanh_bf', x)
+        ref = mathhost.glibc('tanh', x)
+        same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
+        assert same.all(), (x[~same][:4], got[~same][:4], ref[~same][:4])
+    sc_cases = [rng.uniform(-0.855, 0.855, n),
+                sg * np.exp2(rng.uniform(-40, np.log2(0.8554), n)),
+                near(np.array([0.126, 2.0 ** -27, 0.855])),
+                near(np.arange(1, 110) / 128.0, 1e-13),
+                sg * rng.uniform(0, 1e-300, n)]
+    mixed = sc_cases[1].copy()
+    mixed[::61] = 0.0
+    mixed[1::67] = -0.0
+    mixed[2::71] = np.inf
+    mixed[3::73] = np.nan
+    mixed[4::79] = 2.0
+    mixed[5::83] = 1e6  # reduced by reduce_sincos (|x| >= 105414350 needs __branred: NaN, aero_math.h)
+    sc_cases.append(mixed)
+    for x in sc_cases:
+        for fn in ('sin', 'cos'):
+            got = eng.device_math(fn + '_bf', x)
+            ref = mathhost.glibc(fn, x)
+            same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
+            assert same.all(), (fn, x[~same][:4], got[~same][:4], ref[~same][:4])
+    eng.close()
