@@ -418,8 +418,8 @@ __global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, in
       const double2 pms_old = pmsb[pm_p];
       const double pr = ev_pr, pi = ev_pi;
       double qr = pr, qi = ptd_im;  // pt_qpsk
-      const double ct_xt = aero_tanh(pi) * pr;
-      const double ct_xt_d = aero_tanh(ptd_re) * ptd_im;
+      const double ct_xt = aero_tanh_bf(pi) * pr;
+      const double ct_xt_d = aero_tanh_bf(ptd_re) * ptd_im;
       double ct_ec = ct_xt_d - ct_xt;
       if (ct_ec > M_PI) ct_ec = M_PI;
       if (ct_ec < -M_PI) ct_ec = -M_PI;
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, in
       qr = dv.x;
       qi = dv.y;
       double rs, rc;
-      aero_sincos_t(mval, rs, rc, sct);
+      aero_sincos_bf(mval, rs, rc, sct);
       const double rr = qr * rc - qi * rs, ri = qr * rs + qi * rc;
       qr = rr;
       qi = ri;

@@ -281,7 +281,7 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       const double2 so = T.cis[cis_index(so_ptr)];
       const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
       const double ang = LTAB ? aero_atan2_bf(oim, ore, s_cij) : aero_atan2_bf(oim, ore, aero_g_cij);
-      const double weighting = fabs(aero_tanh(ang));
+      const double weighting = fabs(aero_tanh_bf(ang));
       {  // st_osc.AdvanceFractionOfWave (DSP.h:59-65), dcd false
         so_ptr += (-(1.0 - weighting) * ang * (0.05 / 360.0)) * WTSIZE;
         while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
@@ -319,8 +319,8 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
     } while (!pend && i < ie);
     if (pend) {
       // carrier tracking (mskdemodulator.cpp:333-357)
-      const double ct_xt = aero_tanh(e_s2i) * e_s2r;
-      const double ct_xt_d = aero_tanh(e_pdr) * e_pdi;
+      const double ct_xt = aero_tanh_bf(e_s2i) * e_s2r;
+      const double ct_xt_d = aero_tanh_bf(e_pdr) * e_pdi;
       double ct_ec = ct_xt_d - ct_xt;
       if (ct_ec > M_PI) ct_ec = M_PI;
       if (ct_ec < -M_PI) ct_ec = -M_PI;
@@ -366,9 +366,9 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       {  // pt_msk *= cpx(cos(marg->Val), sin(marg->Val))
         double rs, rc;
         if (LTAB)
-          aero_sincos_t(mval, rs, rc, s_sct);
+          aero_sincos_bf(mval, rs, rc, s_sct);
         else
-          aero_sincos(mval, rs, rc);
+          aero_sincos_bf(mval, rs, rc, aero_g_sincostab);
         const double rr = pr * rc - pi * rs, ri = pr * rs + pi * rc;
         pr = rr;
         pi = ri;
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(MSKG_WG) void demod_mskg_kernel(DevState S, DevTabl
     const double2 so = T.cis[cis_index(so_ptr)];
     const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
     const double ang = aero_atan2_bf(oim, ore, aero_g_cij);
-    const double weighting = fabs(aero_tanh(ang));
+    const double weighting = fabs(aero_tanh_bf(ang));
     {  // st_osc.AdvanceFractionOfWave (DSP.h:59-65), dcd false
       so_ptr += (-(1.0 - weighting) * ang * (0.05 / 360.0)) * WTSIZE;
       while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
@@ -589,8 +589,8 @@ __global__ __launch_bounds__(MSKG_WG) void demod_mskg_kernel(DevState S, DevTabl
     }
     if (pend) {
       // carrier tracking (mskdemodulator.cpp:333-357)
-      const double ct_xt = aero_tanh(s2i) * s2r;
-      const double ct_xt_d = aero_tanh(pdr) * pdi;
+      const double ct_xt = aero_tanh_bf(s2i) * s2r;
+      const double ct_xt_d = aero_tanh_bf(pdr) * pdi;
       double ct_ec = ct_xt_d - ct_xt;
       if (ct_ec > M_PI) ct_ec = M_PI;
       if (ct_ec < -M_PI) ct_ec = -M_PI;
@@ -633,7 +633,7 @@ __global__ __launch_bounds__(MSKG_WG) void demod_mskg_kernel(DevState S, DevTabl
       }
       {  // pt_msk *= cpx(cos(marg->Val), sin(marg->Val))
         double rs, rc;
-        aero_sincos(mval, rs, rc);
+        aero_sincos_bf(mval, rs, rc, aero_g_sincostab);
         const double rr = pr * rc - pi * rs, ri = pr * rs + pi * rc;
         pr = rr;
         pi = ri;
@@ -869,7 +869,7 @@ __global__ __launch_bounds__(MSKW_WG) void demod_mskw_kernel(DevState S, DevTabl
     const double2 so = T.cis[cis_index(so_ptr)];
     const double ore = so.x * m1r - so.y * m1i, oim = so.x * m1i + so.y * m1r;
     const double ang = aero_atan2_bf(oim, ore, s_cij);
-    const double weighting = fabs(aero_tanh(ang));
+    const double weighting = fabs(aero_tanh_bf(ang));
     {  // st_osc.AdvanceFractionOfWave (DSP.h:59-65), dcd false
       so_ptr += (-(1.0 - weighting) * ang * (0.05 / 360.0)) * WTSIZE;
       while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
@@ -897,8 +897,8 @@ __global__ __launch_bounds__(MSKW_WG) void demod_mskw_kernel(DevState S, DevTabl
     }
     if (pend) {
       // carrier tracking (mskdemodulator.cpp:333-357)
-      const double ct_xt = aero_tanh(s2i) * s2r;
-      const double ct_xt_d = aero_tanh(pdr) * pdi;
+      const double ct_xt = aero_tanh_bf(s2i) * s2r;
+      const double ct_xt_d = aero_tanh_bf(pdr) * pdi;
       double ct_ec = ct_xt_d - ct_xt;
       if (ct_ec > M_PI) ct_ec = M_PI;
       if (ct_ec < -M_PI) ct_ec = -M_PI;
@@ -941,7 +941,7 @@ __global__ __launch_bounds__(MSKW_WG) void demod_mskw_kernel(DevState S, DevTabl
       }
       {  // pt_msk *= cpx(cos(marg->Val), sin(marg->Val))
         double rs, rc;
-        aero_sincos_t(mval, rs, rc, s_sct);
+        aero_sincos_bf(mval, rs, rc, s_sct);
         const double rr = pr * rc - pi * rs, ri = pr * rs + pi * rc;
         pr = rr;
         pi = ri;

@@ -40,8 +40,8 @@ namespace aero {
 #else
 #define DM_HYPOT aero_hypot_w
 #define DM_ATAN2(y, x) aero_atan2_bf(y, x, sh.cij)
-#define DM_TANH aero_tanh
-#define DM_SINCOS(x, s, c) aero_sincos_t(x, s, c, sh.sct)
+#define DM_TANH aero_tanh_bf
+#define DM_SINCOS(x, s, c) aero_sincos_bf(x, s, c, sh.sct)
 #endif
 // AERO_X_DROP (diagnostic builds only, never bit-exact): leave out one
 // buffer's HBM accesses to attribute the demod's PMC traffic buffer by buffer
@@ -1163,8 +1163,8 @@ __global__ __launch_bounds__(DMW_WG) void demod_oqpskw_kernel(DevState S, DevTab
       const double pm_old = pms_old.x, ms_old = pms_old.y;
       const double pr = ev_pr, pi = ev_pi;
       double qr = pr, qi = ptd_im;  // pt_qpsk
-      const double ct_xt = aero_tanh(pi) * pr;
-      const double ct_xt_d = aero_tanh(ptd_re) * ptd_im;
+      const double ct_xt = aero_tanh_bf(pi) * pr;
+      const double ct_xt_d = aero_tanh_bf(ptd_re) * ptd_im;
       double ct_ec = ct_xt_d - ct_xt;
       if (ct_ec > M_PI) ct_ec = M_PI;
       if (ct_ec < -M_PI) ct_ec = -M_PI;
@@ -1190,7 +1190,7 @@ __global__ __launch_bounds__(DMW_WG) void demod_oqpskw_kernel(DevState S, DevTab
       qr = dv.x;
       qi = dv.y;
       double rs, rc;
-      aero_sincos_t(mval, rs, rc, sh.sct);
+      aero_sincos_bf(mval, rs, rc, sh.sct);
       const double rr = qr * rc - qi * rs, ri = qr * rs + qi * rc;
       qr = rr;
       qi = ri;
