@@ -294,12 +294,15 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
       ma1i = ma1i + pi;
       S.ma1[(size_t)ma1_p * C + c] = make_double2(pr, pi);
       ma1_p = ma1_p + 1 == B_MA ? 0 : ma1_p + 1;
-      fastarm = B_HYPOT(ma1r / ((double)B_MA), ma1i / ((double)B_MA));
+      // div_c (aero_math.h): the running sums are zero or far above 2^-969
+      // (int16 PCM through the Hilbert transform, the AGC gain and two
+      // products stay on a grid of about 2^-400), so the contract holds
+      fastarm = B_HYPOT(div_c(ma1r, (double)B_MA), div_c(ma1i, (double)B_MA));
       mav1_sum = mav1_sum - mv_old;
       mav1_sum = mav1_sum + (fastarm);
       S.mav1[(size_t)mav1_p * C + c] = fastarm;
       mav1_p = mav1_p + 1 == B_MA ? 0 : mav1_p + 1;
-      fastarm = mav1_sum / ((double)B_MA);
+      fastarm = div_c(mav1_sum, (double)B_MA);
       fastarm -= dly_commit(mdr, C, dl_md, mdp, fastarm);
       md_older = md_newer;
       md_newer = md_next;

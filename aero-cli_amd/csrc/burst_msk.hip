@@ -180,12 +180,15 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
       ma1i = ma1i + pi;
       S.ma1[(size_t)ma1_p * C + c] = make_double2(pr, pi);
       ma1_p = ma1_p + 1 == M_MA ? 0 : ma1_p + 1;
-      fastarm = B_HYPOT(ma1r / ((double)M_MA), ma1i / ((double)M_MA));
+      // div_c (aero_math.h): the running sums are zero or far above 2^-969
+      // (int16 PCM through the Hilbert transform, the AGC gain and two
+      // products stay on a grid of about 2^-400), so the contract holds
+      fastarm = B_HYPOT(div_c(ma1r, (double)M_MA), div_c(ma1i, (double)M_MA));
       mav1_sum = mav1_sum - mv_old;
       mav1_sum = mav1_sum + (fastarm);
       S.mav1[(size_t)mav1_p * C + c] = fastarm;
       mav1_p = mav1_p + 1 == M_MA ? 0 : mav1_p + 1;
-      fastarm = mav1_sum / ((double)M_MA);
+      fastarm = div_c(mav1_sum, (double)M_MA);
       madiff[(size_t)madiff_p * C] = fastarm;  // bt_ma_diff.update(fastarm), whole-sample delay
       madiff_p = mdo;
       md_older = md_new;
