@@ -150,7 +150,11 @@ __global__ __launch_bounds__(512) void hilbert_kernel(BurstState S, BurstTables 
 constexpr int BD_BLOCK = 64;
 constexpr int BD_LDS_TAPS = 36, BD_REG_TAPS = NTAPS - BD_LDS_TAPS;
 constexpr int BD_DBLK = 40 - BD_LDS_TAPS;  // samples per slide of the line
+#ifndef AERO_X_BD_DCH
 constexpr int BD_DCH = 8;                  // line entries read per chunk
+#else
+constexpr int BD_DCH = AERO_X_BD_DCH;      // timing builds: other chunk sizes
+#endif
 
 // AERO_X_BSTAMPS (diagnostic build only): s_memtime cycle totals per section
 // of the demod loop, each wave's maximum over its lanes (the wave's time in
