@@ -35,7 +35,8 @@ F_TRACE_ALL = F_TRACE_PT | F_TRACE_BLOCKS | F_TRACE_SOFT | F_TRACE_HOPS | F_TRAC
 
 MATH_FN = {'hypot': 0, 'atan2': 1, 'tanh': 2, 'sin': 3, 'cos': 4, 'log10': 5, 'sqrt': 6, 'fmod360': 7,
            'div': 8, 'div_c48000': 9, 'div_c360': 10, 'div_n': 11, 'div_c192000': 13, 'hypot_nr': 14, 'atan2_bf': 15,
-           'tanh_bf': 16, 'sin_bf': 17, 'cos_bf': 18}
+           'tanh_bf': 16, 'sin_bf': 17, 'cos_bf': 18,
+           'div_cw_wt': 19, 'set_phase_ptr': 20}
 
 
 class EngineCfg(ctypes.Structure):

@@ -101,6 +101,17 @@ AERO_HD double div_c(double a, double c) {
 #endif
 }
 
+/* div_c behind a wave-uniform test of its contract (every lane's numerator
+ * zero or at least 2^-900 in magnitude), the IEEE division otherwise: for
+ * numerators whose range is not argued, e.g. 360 x a phase pointer */
+AERO_HD double div_cw(double a, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double m = __builtin_fabs(a);
+  if (__builtin_expect(__all(m == 0.0 || m >= 0x1p-900), 1)) return div_c(a, c);
+#endif
+  return a / c;
+}
+
 AERO_HD double rcp_div(double b) {
 #if defined(__HIP_DEVICE_COMPILE__)
   double r = __builtin_amdgcn_rcp(b);

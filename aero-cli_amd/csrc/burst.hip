@@ -629,7 +629,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
       double st_err = B_ATAN2(er_i, er_r);
       st_err *= 1.5 * (1.0 - progress * progress);
       b_advance(q_ptr, -(1.0 / (2.0 * M_PI)) * st_err * 0.1);
-      b_set_phase_deg_pos(so_ptr, (360.0 * q_ptr / ((double)WTSIZE)) * 4.0 + (360.0 * 0.4));
+      b_set_phase_deg_pos(so_ptr, div_cw(360.0 * q_ptr, (double)WTSIZE) * 4.0 + (360.0 * 0.4));
       so_n = T.cis[b_cis_index(so_ptr)];
     }
     {  // sig2 *= symboltone_averotator; rotator *= exp(i rotator_freq); sig2 *= rotator
@@ -702,7 +702,7 @@ __global__ __launch_bounds__(BD_BLOCK) void demod_burst_kernel(BurstState S, Bur
         const double ptr_ = pt_this * s2r + pt_last * s2l_r, pti = pt_this * s2i + pt_last * s2l_i;
         // the remainder of a value in [72, 792): 0 or a multiple of ulp(72), in div_c's contract
         const double twospeed =
-            -4.0 * (div_c(b_fmod360((360.0 * q_ptr / ((double)WTSIZE)) * 2.0 + (360.0 * 0.4 * 0.5)), 360.0) -
+            -4.0 * (div_c(b_fmod360(div_cw(360.0 * q_ptr, (double)WTSIZE) * 2.0 + (360.0 * 0.4 * 0.5)), 360.0) -
                     (0.34046 + 0.4111 * 0.4));
         const bool even = !(twospeed < 0);
         yui++;

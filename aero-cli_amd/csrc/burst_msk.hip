@@ -466,7 +466,7 @@ __global__ __launch_bounds__(BM_BLOCK) void demod_bmsk_kernel(BurstState S, Burs
         double st_err = B_ATAN2(er_i, er_r);
         st_err *= 0.5 * (1.0 - progress * progress);
         b_advance(sh_ptr, -(1.0 / (2.0 * M_PI)) * st_err * 0.05);
-        b_set_phase_deg_pos(so_ptr, (360.0 * sh_ptr / ((double)WTSIZE)) + (360.0 * (1.0 - M_EE)));  // in [351, 711)
+        b_set_phase_deg_pos(so_ptr, div_cw(360.0 * sh_ptr, (double)WTSIZE) + (360.0 * (1.0 - M_EE)));  // in [351, 711)
         so_n = T.cis[b_cis_index(so_ptr)];
       }
       {  // sig2 *= symboltone_averotator; rotator *= exp(i rotator_freq); sig2 *= rotator

@@ -61,7 +61,7 @@ __device__ __forceinline__ int c_cis_index(double WTptr) {  // WaveTable::WTCISV
 __device__ __forceinline__ void c_nco_next(double &ptr, double &step) {  // WTnextFrame (DSP.cpp:71-79)
   if (step < 0) step = 0;
   ptr += step;
-  while (((int)ptr) >= WTSIZE) ptr -= WTSIZE;
+  wt_wrap_int(ptr);
 }
 __device__ __forceinline__ void c_set_freq(double &freq, double &step, double f) {  // SetFreq(double) (DSP.cpp:163-168)
   freq = f;
@@ -121,10 +121,7 @@ __global__ __launch_bounds__(64) void prefilter_dn_kernel(DevState S, const CPre
   double fp_step = S.ds[DS_FP_STEP * C + c];
   double dn_ptr = S.ds[DS_FP_PTR * C + c];
   {  // savedphase = GetPhaseDeg() (DSP.cpp:200), SetPhaseDeg(savedphase) (:177-187)
-    double ph = (360.0 * dn_ptr / ((double)WTSIZE));
-    ph = fmod(ph, 360.0);
-    while (ph < 0) ph += 360.0;
-    S.ds[DS_FP_PTR * C + c] = (ph / 360.0) * ((double)WTSIZE);
+    S.ds[DS_FP_PTR * C + c] = set_phase_ptr(div_cw(360.0 * dn_ptr, (double)WTSIZE));
   }
   uint32_t *cin = S.cin + (size_t)c * C_IN_RING;
   long long n = J.s;
@@ -362,8 +359,7 @@ __global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, in
       const double st_angle_error = aero_atan2_bf(oim, ore, cij);
       c_set_freq(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
       so_ptr += div_c(-st_angle_error * 0.01, 360.0) * WTSIZE;
-      while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
-      while (so_ptr < 0) so_ptr += WTSIZE;
+      wt_wrap(so_ptr);
       if (so_freq < (SO_F - 0.1)) c_set_freq(so_freq, so_step, (SO_F - 0.1));
       if (so_freq > (SO_F + 0.1)) c_set_freq(so_freq, so_step, (SO_F + 0.1));
       if (!s2l_init) {
@@ -425,10 +421,8 @@ __global__ __launch_bounds__(64) void demod_c_kernel(DevState S, DevTables T, in
       if (ct_ec < -M_PI) ct_ec = -M_PI;
       {  // 8400: mixer2.IncresePhaseDeg(1.0 * ct_ec) unfiltered (DSP.cpp:177-187)
         double phase_deg = 1.0 * ct_ec;
-        phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
-        phase_deg = fmod(phase_deg, 360.0);
-        while (phase_deg < 0) phase_deg += 360.0;
-        m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+        phase_deg += div_cw(360.0 * m2_ptr, (double)WTSIZE);
+        m2_ptr = set_phase_ptr(phase_deg);
       }
       // mixer2.IncreseFreqHz(0.5 * 0.01 * ct_iir_loopfilter.update(ct_ec)) (:470)
       c_set_freq(m2_freq, m2_step, 0.5 * 0.01 * c_iir3(ctx1, ctx2, cty1, cty2, ct_b, ct_a, ct_ec) + m2_freq);

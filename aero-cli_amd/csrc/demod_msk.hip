@@ -44,7 +44,7 @@ __device__ __forceinline__ int cis_index(double WTptr) {  // WaveTable::WTCISVal
 __device__ __forceinline__ void nco_next(double &ptr, double &step) {  // WTnextFrame (DSP.cpp:71-79)
   if (step < 0) step = 0;
   ptr += step;
-  while (((int)ptr) >= WTSIZE) ptr -= WTSIZE;
+  wt_wrap_int(ptr);
 }
 
 __device__ __forceinline__ int qround(double d) {  // qRound (Qt 5.9 qglobal.h:525)
@@ -284,8 +284,7 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       const double weighting = fabs(aero_tanh_bf(ang));
       {  // st_osc.AdvanceFractionOfWave (DSP.h:59-65), dcd false
         so_ptr += (-(1.0 - weighting) * ang * (0.05 / 360.0)) * WTSIZE;
-        while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
-        while (so_ptr < 0) so_ptr += WTSIZE;
+        wt_wrap(so_ptr);
       }
       {  // IfHavePassedPoint (DSP.cpp:222-238)
         double tl = so_last - PT, tw = so_ptr - PT;
@@ -329,10 +328,8 @@ __global__ __launch_bounds__(MskK<M>::WG) void demod_msk_kernel(DevState S, DevT
       const double carrier_aggression = 12.0 * 1.0;  // correctionfactor 1.0 (fb < 1200)
       {  // mixer2.IncresePhaseDeg (DSP.cpp:177-187)
         double phase_deg = carrier_aggression * 1.0 * ct_ec;
-        phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
-        phase_deg = fmod(phase_deg, 360.0);
-        while (phase_deg < 0) phase_deg += 360.0;
-        m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+        phase_deg += div_cw(360.0 * m2_ptr, (double)WTSIZE);
+        m2_ptr = set_phase_ptr(phase_deg);
       }
       {  // mixer2.IncreseFreqHz -> SetFreq(double) (DSP.cpp:163-175)
         double f = carrier_aggression * 0.01 * ct_ec;
@@ -564,8 +561,7 @@ __global__ __launch_bounds__(MSKG_WG) void demod_mskg_kernel(DevState S, DevTabl
     const double weighting = fabs(aero_tanh_bf(ang));
     {  // st_osc.AdvanceFractionOfWave (DSP.h:59-65), dcd false
       so_ptr += (-(1.0 - weighting) * ang * (0.05 / 360.0)) * WTSIZE;
-      while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
-      while (so_ptr < 0) so_ptr += WTSIZE;
+      wt_wrap(so_ptr);
     }
     bool pend = false;
     {  // IfHavePassedPoint (DSP.cpp:222-238)
@@ -599,10 +595,8 @@ __global__ __launch_bounds__(MSKG_WG) void demod_mskg_kernel(DevState S, DevTabl
       const double carrier_aggression = 12.0 * 1.0;  // correctionfactor 1.0 (fb < 1200)
       {  // mixer2.IncresePhaseDeg (DSP.cpp:177-187)
         double phase_deg = carrier_aggression * 1.0 * ct_ec;
-        phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
-        phase_deg = fmod(phase_deg, 360.0);
-        while (phase_deg < 0) phase_deg += 360.0;
-        m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+        phase_deg += div_cw(360.0 * m2_ptr, (double)WTSIZE);
+        m2_ptr = set_phase_ptr(phase_deg);
       }
       {  // mixer2.IncreseFreqHz -> SetFreq(double) (DSP.cpp:163-175)
         double f = carrier_aggression * 0.01 * ct_ec;
@@ -872,8 +866,7 @@ __global__ __launch_bounds__(MSKW_WG) void demod_mskw_kernel(DevState S, DevTabl
     const double weighting = fabs(aero_tanh_bf(ang));
     {  // st_osc.AdvanceFractionOfWave (DSP.h:59-65), dcd false
       so_ptr += (-(1.0 - weighting) * ang * (0.05 / 360.0)) * WTSIZE;
-      while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
-      while (so_ptr < 0) so_ptr += WTSIZE;
+      wt_wrap(so_ptr);
     }
     bool pend;
     {  // IfHavePassedPoint (DSP.cpp:222-238)
@@ -907,10 +900,8 @@ __global__ __launch_bounds__(MSKW_WG) void demod_mskw_kernel(DevState S, DevTabl
       const double carrier_aggression = 12.0 * 1.0;  // correctionfactor 1.0 (fb < 1200)
       {  // mixer2.IncresePhaseDeg (DSP.cpp:177-187)
         double phase_deg = carrier_aggression * 1.0 * ct_ec;
-        phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
-        phase_deg = fmod(phase_deg, 360.0);
-        while (phase_deg < 0) phase_deg += 360.0;
-        m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+        phase_deg += div_cw(360.0 * m2_ptr, (double)WTSIZE);
+        m2_ptr = set_phase_ptr(phase_deg);
       }
       {  // mixer2.IncreseFreqHz -> SetFreq(double) (DSP.cpp:163-175)
         double f = carrier_aggression * 0.01 * ct_ec;

@@ -87,7 +87,7 @@ __device__ __forceinline__ int cis_index(double WTptr) {  // WaveTable::WTCISVal
 __device__ __forceinline__ void nco_next(double &ptr, double &step) {  // WTnextFrame (DSP.cpp:71-79)
   if (step < 0) step = 0;
   ptr += step;
-  while (((int)ptr) >= WTSIZE) ptr -= WTSIZE;
+  wt_wrap_int(ptr);
 }
 
 __device__ __forceinline__ void set_freq(double &freq, double &step, double f) {  // SetFreq (DSP.cpp:163-168)
@@ -608,8 +608,7 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       // (a quotient below 2^-969 could differ from IEEE in its last
       // subnormal bit, and vanishes in so_ptr + x W either way)
       so_ptr += div_c(-st_angle_error * 0.01, 360.0) * WTSIZE;
-      while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
-      while (so_ptr < 0) so_ptr += WTSIZE;
+      wt_wrap(so_ptr);
       if (so_freq < (10500.0 - 0.1)) set_freq_st(so_freq, so_step, (10500.0 - 0.1));
       if (so_freq > (10500.0 + 0.1)) set_freq_st(so_freq, so_step, (10500.0 + 0.1));
       if (!s2l_init) {
@@ -717,10 +716,8 @@ __device__ __forceinline__ void demod_chain_wave(const DevState &S, const DevTab
       if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
       {  // mixer2.IncresePhaseDeg / SetPhaseDeg (DSP.cpp:177-187)
         double phase_deg = 1.0 * ct_ec;
-        phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
-        phase_deg = fmod(phase_deg, 360.0);
-        while (phase_deg < 0) phase_deg += 360.0;
-        m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+        phase_deg += div_cw(360.0 * m2_ptr, (double)WTSIZE);
+        m2_ptr = set_phase_ptr(phase_deg);
       }
       set_freq(m2_freq, m2_step, 0.01 * ct_ec + m2_freq);  // IncreseFreqHz
       // marg->UpdateSigned (DSP.cpp:419-427)
@@ -1110,8 +1107,7 @@ __global__ __launch_bounds__(DMW_WG) void demod_oqpskw_kernel(DevState S, DevTab
     const double st_angle_error = aero_atan2_bf(oim, ore, sh.cij);
     set_freq_st(so_freq, so_step, -st_angle_error * 0.00000001 + so_freq);
     so_ptr += div_c(-st_angle_error * 0.01, 360.0) * WTSIZE;
-    while (so_ptr >= WTSIZE) so_ptr -= WTSIZE;
-    while (so_ptr < 0) so_ptr += WTSIZE;
+    wt_wrap(so_ptr);
     if (so_freq < (10500.0 - 0.1)) set_freq_st(so_freq, so_step, (10500.0 - 0.1));
     if (so_freq > (10500.0 + 0.1)) set_freq_st(so_freq, so_step, (10500.0 + 0.1));
     if (!s2l_init) {
@@ -1173,10 +1169,8 @@ __global__ __launch_bounds__(DMW_WG) void demod_oqpskw_kernel(DevState S, DevTab
       if (ct_ec < -M_PI_2) ct_ec = -M_PI_2;
       {  // mixer2.IncresePhaseDeg / SetPhaseDeg (DSP.cpp:177-187)
         double phase_deg = 1.0 * ct_ec;
-        phase_deg += (360.0 * m2_ptr / ((double)WTSIZE));
-        phase_deg = fmod(phase_deg, 360.0);
-        while (phase_deg < 0) phase_deg += 360.0;
-        m2_ptr = (phase_deg / 360.0) * ((double)WTSIZE);
+        phase_deg += div_cw(360.0 * m2_ptr, (double)WTSIZE);
+        m2_ptr = set_phase_ptr(phase_deg);
       }
       set_freq(m2_freq, m2_step, 0.01 * ct_ec + m2_freq);  // IncreseFreqHz
       marg_sum = marg_sum - marg_old;  // marg->UpdateSigned (DSP.cpp:419-427)

@@ -133,6 +133,8 @@ __global__ void math_kernel(int fn, const double *x, const double *y, double *ou
     case 16: r = aero_tanh_bf(a); break;
     case 17: { double sn, cs; aero_sincos_bf(a, sn, cs, aero_g_sincostab); r = sn; break; }
     case 18: { double sn, cs; aero_sincos_bf(a, sn, cs, aero_g_sincostab); r = cs; break; }
+    case 19: r = div_cw(a, (double)WTSIZE); break;
+    case 20: r = set_phase_ptr(a); break;
     default: break;
   }
   out[i] = r;

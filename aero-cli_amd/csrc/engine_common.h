@@ -13,6 +13,7 @@
 #pragma once
 #include <stdint.h>
 
+#include "aero_math.h"    // div_cw (set_phase_ptr)
 #include "tables_host.h"  // DelayDesc
 
 namespace aero {
@@ -294,6 +295,38 @@ struct DevState {
   double2 *crem;           // C channel: [C][C_FIR_N - C_FIR_SNZ] JFastFir remainder
   int *err;                // [1] mapped pinned device-error word (DERR_*), sticky; read by the host
 };
+
+#if defined(__HIPCC__)
+// WaveTable's pointer wraps (DSP.h:59-65's loops) with their first iteration
+// as a select and the rest behind a wave-uniform test: the same iterations in
+// the same order (a peeled loop), without a divergent loop's exec-mask
+// bookkeeping on the per-sample path
+__device__ __forceinline__ void wt_wrap(double &ptr) {
+  ptr = ptr >= WTSIZE ? ptr - WTSIZE : ptr;
+  if (__builtin_expect(__any(ptr >= WTSIZE), 0))
+    while (ptr >= WTSIZE) ptr -= WTSIZE;
+  ptr = ptr < 0 ? ptr + WTSIZE : ptr;
+  if (__builtin_expect(__any(ptr < 0), 0))
+    while (ptr < 0) ptr += WTSIZE;
+}
+// WTnextFrame's wrap (DSP.cpp:71-79), peeled the same way
+__device__ __forceinline__ void wt_wrap_int(double &ptr) {
+  ptr = ((int)ptr) >= WTSIZE ? ptr - WTSIZE : ptr;
+  if (__builtin_expect(__any(((int)ptr) >= WTSIZE), 0))
+    while (((int)ptr) >= WTSIZE) ptr -= WTSIZE;
+}
+// SetPhaseDeg (DSP.cpp:177-187): fmod(x, 360), the loop that adds 360 while
+// negative, and the pointer (phase / 360) W.  For -360 < x < 720 fmod is x or
+// the exact x - 360 (Sterbenz), and its remainder is above -360, so the loop
+// adds at most once; other waves take fmod.  The quotient by div_cw.
+__device__ __forceinline__ double set_phase_ptr(double x) {
+  const bool in = x > -360.0 && x < 720.0;
+  double r = x >= 360.0 ? x - 360.0 : x;
+  if (__builtin_expect(__any(!in), 0)) r = in ? r : fmod(x, 360.0);
+  r = r < 0 ? r + 360.0 : r;
+  return div_cw(r, 360.0) * ((double)WTSIZE);
+}
+#endif
 
 // device error codes (DevState::err)
 constexpr int DERR_HANDOFF = 1;  // a demod wave pair's LDS hand-off timed out

@@ -198,3 +198,41 @@ def test_tanh_and_sincos_branch_free_paths_are_glibc(engine_lib):
             same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
             assert same.all(), (fn, x[~same][:4], got[~same][:4], ref[~same][:4])
     eng.close()
+
+
+@pytest.mark.gpu
+def test_phase_pointer_helpers_are_exact(engine_lib):
+    """div_cw (div_c behind a wave-uniform test of its contract, the IEEE
+    division otherwise) and set_phase_ptr (SetPhaseDeg's fmod(x, 360), its
+    add-while-negative loop and (phase / 360) W, DSP.cpp:177-187, with fmod
+    by one conditional subtraction on -360 < x < 720) equal the host's IEEE
+    arithmetic bit for bit: the carrier steps' phases, the edges of the fast
+    range, signed zeros, and waves with tiny, huge or NaN lanes."""
+    import aero_engine as ae
+    eng = ae.Engine(max_channels=1)
+    rng = np.random.default_rng(37)
+    n = 1 << 19
+    W = 19999.0
+    ptr = rng.uniform(0, W, n)
+    tiny = ptr.copy()
+    tiny[::67] = rng.uniform(0, 1, n)[::67] * 2.0 ** -1000
+    tiny[1::71] = 0.0
+    for a in (360.0 * ptr, tiny, -360.0 * ptr):
+        got = eng.device_math('div_cw_wt', a)
+        assert np.array_equal(got.view(np.uint64), (a / W).view(np.uint64))
+    x = rng.uniform(-1.6, 361.6, n)
+    edge = np.repeat(np.array([-360.0, -359.99999999999994, -0.0, 0.0, 359.99999999999994, 360.0,
+                               719.9999999999999, 720.0, 1e-310, -1e-310]), n // 10 + 1)[:n]
+    wide = rng.uniform(-1e4, 1e4, n)
+    mixed = x.copy()
+    mixed[::97] = np.nan
+    mixed[1::89] = 1e6
+    mixed[2::83] = -5e3
+    for x in (x, edge, wide, mixed):
+        r = np.fmod(x, 360.0)
+        r = np.where(r < 0, r + 360.0, r)
+        ref = (r / 360.0) * W
+        got = eng.device_math('set_phase_ptr', x)
+        same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
+        assert same.all(), (x[~same][:4], got[~same][:4], ref[~same][:4])
+    eng.close()
