@@ -237,7 +237,7 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
   // next sample's "older"
   auto nxt = [](int p, int len) { return p + 1 == len ? 0 : p + 1; };
   auto pd2_slot = [](int p3) { return p3 >= B_PD2 - 1 ? p3 - (B_PD2 - 1) : p3 + B_PD3 - (B_PD2 - 1); };
-  double2 cvd_n = S.d1[(size_t)nxt(d1_p, B_D1) * C + c];
+  double cvd_n = S.d1[(size_t)nxt(d1_p, B_D1) * C + c];
   double2 ma_n = S.ma1[(size_t)ma1_p * C + c];
   double mv_n = S.mav1[(size_t)mav1_p * C + c];
   double md_older = mdr[(size_t)nxt(dl_md, dMD.size) * C];
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
     const int p1r = nxt(pd3_p, B_PD3);
     const double2 a = a_n;
     const double agc_old = agc_n;
-    const double2 cvd = cvd_n;  // d1.update_dont_touch(cval)
+    const double cvd = cvd_n;  // real(d1.update_dont_touch(cval)): the only part read
     const double2 ma_old = ma_n;
     const double mv_old = mv_n;
     const double pd1_old = pd1_n, pd2_old = pd2_n;
@@ -284,10 +284,10 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
       cr *= g;
       ci *= g;
     }
-    S.d1[(size_t)d1_p * C + c] = make_double2(cr, ci);
+    S.d1[(size_t)d1_p * C + c] = cr;
     d1_p = d1r;
     // d2.update_dont_touch(real(cval_d)): the demodulator reads it back B_D2 - 1 samples later
-    S.vring[(size_t)(n & (BV_LEN - 1)) * C + c] = cvd.x;
+    S.vring[(size_t)(n & (BV_LEN - 1)) * C + c] = cvd;
     double fastarm;
     {  // burst-timing statistic (:326-339)
       const double2 bd = dly_reg2(hBT, wBT, oBT, make_double2(cr, ci));
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(64) void front_burst_kernel(BurstState S, BurstTabl
       if (hit) tri_ptr = 0;
     }
     if (tri_ptr < B_TRI) {
-      tri[tri_ptr] = cvd.x;
+      tri[tri_ptr] = cvd;
       tri_ptr++;
     } else if (tri_ptr == B_TRI) {
       // the reference checks the buffer at this sample (:343-440); the

@@ -157,7 +157,7 @@ struct BurstState {
   long long pcm_cap;
   double2 *hb_rem;  // [C][HB_REM]
   double *agc, *agc2;           // [len][C]
-  double2 *d1;                  // [B_D1][C]
+  double *d1;                   // [B_D1][C] d1's real part (its only output read: val_to_demod, the trident buffer)
   double *vring;                // [BV_LEN or MV_LEN][C] val_to_demod of sample n at n & (len - 1)
   double2 *ma1;                 // [B_MA][C]
   double *mav1;                 // [B_MA][C]

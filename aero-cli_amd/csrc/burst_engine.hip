@@ -201,7 +201,7 @@ size_t burst_layout(int kind, BurstState &S, BurstTables &T, int C, char *base, 
   S.hb_rem = carve<double2>(p, (size_t)HB_REM * C);
   S.agc = carve<double>(p, (size_t)B_AGC * C);
   S.agc2 = carve<double>(p, (size_t)(msk ? M_AGC2 : B_AGC2) * C);
-  S.d1 = carve<double2>(p, (size_t)(msk ? M_D1 : B_D1) * C);
+  S.d1 = carve<double>(p, (size_t)(msk ? M_D1 : B_D1) * C);
   S.vring = carve<double>(p, (size_t)(msk ? MV_LEN : BV_LEN) * C);
   S.ma1 = carve<double2>(p, (size_t)(msk ? M_MA : B_MA) * C);
   S.mav1 = carve<double>(p, (size_t)(msk ? M_MA : B_MA) * C);

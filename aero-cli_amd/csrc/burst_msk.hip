@@ -142,7 +142,7 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
     const double2 a = a_n;
     const double agc_old = agc_n;
     a_n = S.ana[ana_idx(n + 1, c, C)];  // past the Hilbert stage's output: unused
-    const double2 cvd = S.d1[(size_t)d1r * C + c];  // d1.update_dont_touch(cval)
+    const double cvd = S.d1[(size_t)d1r * C + c];  // real(d1.update_dont_touch(cval)): the only part read
     const double2 bt_old = bt_older, bt_new = btd[(size_t)btn * C];
     const double2 ma_old = S.ma1[(size_t)ma1_p * C + c];
     const double mv_old = S.mav1[(size_t)mav1_p * C + c];
@@ -162,10 +162,10 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
       cr *= g;
       ci *= g;
     }
-    S.d1[(size_t)d1_p * C + c] = make_double2(cr, ci);
+    S.d1[(size_t)d1_p * C + c] = cr;
     d1_p = d1r;
     // d2.update_dont_touch(real(cval_d)): the demodulator reads it back M_D2 - 1 samples later
-    S.vring[(size_t)(n & (MV_LEN - 1)) * C + c] = cvd.x;
+    S.vring[(size_t)(n & (MV_LEN - 1)) * C + c] = cvd;
     double fastarm;
     {  // burst-timing statistic (:376-385); bt_d1 = Delay(SPS): weights 0 / 1 (dly_int2)
       btd[(size_t)btd_p * C] = make_double2(cr, ci);
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(64) void front_bmsk_kernel(BurstState S, BurstTable
       if (hit) tri_ptr = 0;
     }
     if (tri_ptr < M_TRI) {
-      tri[tri_ptr] = cvd.x;
+      tri[tri_ptr] = cvd;
       tri_ptr++;
     } else if (tri_ptr == M_TRI) {
       // the reference computes the trident spectra at this sample

@@ -1082,8 +1082,10 @@ int run_impl(aero_engine *e, int flush) {
       if (int rc = burst_run(b, flush)) return rc;
   std::vector<Group *> act(e->groups.size());
   int na = 0;
+  // a group whose channels have all moved to another rate's group (every
+  // slot free, each drained when its channel left) is not launched
   for (auto &g : e->groups)
-    if (g && g->nch) {
+    if (g && g->nch && (int)g->free_slots.size() < g->nch) {
       if (int rc = run_begin(g.get())) return rc;
       act[na++] = g.get();
     }
