@@ -332,6 +332,15 @@ AERO_HD double aero_tanh(double x) {
   return (jx >= 0) ? z : -z;
 }
 
+/* The branch-free forms' fallbacks (a wave with an out-of-range lane): inline
+ * by default; AERO_X_COLD (timing builds) calls them out of line instead */
+#if defined(__HIP_DEVICE_COMPILE__) && defined(AERO_X_COLD)
+#define AERO_COLD __device__ __noinline__
+#else
+#define AERO_COLD AERO_HD
+#endif
+AERO_COLD double aero_tanh_cold(double x) { return aero_tanh(x); }
+
 /* aero_expm1 on the arguments aero_tanh gives it for 2^-55 <= |x| < 22:
  * a = 2|x| in [2, 44) or a = -2|x| in (-2, -2^-54], without a branch.  There
  * glibc returns none of its early values, and k is 0 (|a| <= 0x3fd62e42's
@@ -394,7 +403,7 @@ AERO_HD double aero_tanh_bf(double x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const int32_t jx = (int32_t)hiw(x), ix = jx & 0x7fffffff;
   const bool ok = ix < 0x40360000 && ix >= 0x3c800000;
-  if (!__builtin_expect(__all(ok), 1)) return aero_tanh(x);
+  if (!__builtin_expect(__all(ok), 1)) return aero_tanh_cold(x);
   const bool big = ix >= 0x3ff00000;
   const double ax = __builtin_fabs(x);
   const double t = g_expm1_tanh_bf(big ? 2.0 * ax : -2.0 * ax);
@@ -514,6 +523,7 @@ AERO_HD void aero_sincos_t(double x, double &so, double &co, const double *sct) 
   }
   so = co = x / x;
 }
+AERO_COLD void aero_sincos_cold(double x, double &so, double &co, const double *sct) { aero_sincos_t(x, so, co, sct); }
 
 AERO_HD void aero_sincos(double x, double &so, double &co) { aero_sincos_t(x, so, co, aero_g_sincostab); }
 
@@ -528,7 +538,7 @@ AERO_HD void aero_sincos_bf(double x, double &so, double &co, const double *sct)
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t k = hiw(x) & 0x7fffffffu;
   if (!__builtin_expect(__all(k < 0x3feb6000u), 1)) {
-    aero_sincos_t(x, so, co, sct);
+    aero_sincos_cold(x, so, co, sct);
     return;
   }
   const double ax = __builtin_fabs(x);
@@ -715,6 +725,7 @@ AERO_HD double aero_atan2_t(double y, double x, const double (*cij)[7]) {
   }
   return __builtin_copysign(__builtin_fabs(z), y);
 }
+AERO_COLD double aero_atan2_cold(double y, double x, const double (*cij)[7]) { return aero_atan2_t(y, x, cij); }
 
 AERO_HD double aero_atan2(double y, double x) { return aero_atan2_t(y, x, aero_g_cij); }
 
@@ -739,7 +750,7 @@ AERO_HD double aero_atan2_bf(double y, double x, const double (*cij)[7]) {
   const int32_t de = (int32_t)((hiw(y) & 0x7ff00000u) - (hiw(x) & 0x7ff00000u));
   const bool ok = ax >= 0x1p-500 && ax <= 0x1p500 && ay >= 0x1p-500 && ay <= 0x1p500 && de < 59768832 &&
                   de > -59768832;
-  if (!__builtin_expect(__all(ok), 1)) return aero_atan2_t(y, x, cij);
+  if (!__builtin_expect(__all(ok), 1)) return aero_atan2_cold(y, x, cij);
   const bool gt = ax > ay;  // u = ay / ax, else u = ax / ay
   const double a = gt ? ay : ax, b = gt ? ax : ay;
   const double r = rcp_div(b);
