@@ -421,8 +421,8 @@ AERO_HD double aero_tanh_bf(double x) {
  * do_cos / reduce_sincos helpers of s_sin.c), SSE2 build: libm.so.6's
  * `sincos` is not an ifunc in 2.35, so every host runs this code.  Read
  * from its disassembly; the operation order below is the instructions'.
- * |x| >= 105414350 would need __branred (not restated: the demods' arguments
- * are loop corrections and averaged phase errors, |x| < 2*pi); NaN there. */
+ * |x| >= 105414350 goes through __branred (g_branred), as glibc's does; the
+ * demods' arguments never get there (loop corrections, |x| < 2 pi). */
 
 /* TAYLOR_SIN(xx, a, da) */
 AERO_HD double g_taylor_sin(double xx, double a, double da) {
@@ -478,6 +478,76 @@ AERO_HD int g_reduce_sincos(double x, double &a, double &da) {
   return n;
 }
 
+/* __branred (branred.c): x = N pi/2 + (a + aa) for |x| >= 105414350, N mod
+ * 4 returned; x scaled by 2^-600 and split into two 26-bit halves, each
+ * multiplied by 2/pi in 24-bit digits (toverp) from the digit its exponent
+ * needs, the integer parts removed (+- big), the halves' fractions summed,
+ * and the fraction times pi/2 in double-double.  Restated from the SSE2
+ * build's disassembly (libm 0x6f180, called by sincos): its packed ops are
+ * these operations two at a time; additions and products are commutative,
+ * and every grouping below is the one its instruction sequence has. */
+AERO_HD int g_branred(double x, double &a, double &aa) {
+  x *= AERO_G_BR_TM600;
+  double t = x * AERO_G_BR_SPLIT;
+  const double xs[2] = {t - (t - x), 0.0};
+  double hb[2], hbb[2], hsum[2];
+  const double x2 = x - xs[0];
+  for (int h = 0; h < 2; h++) {
+    const double xh = h ? x2 : xs[0];
+    int k = (int)((d2u(xh) >> 52) & 2047);
+    k = (k - 450) / 24;
+    if (k < 0) k = 0;
+    double gor = mkd(0x63f00000u - ((uint32_t)(k * 24) << 20), 0);
+    double r[6];
+    for (int i = 0; i < 6; i++) {
+      r[i] = xh * aero_g_toverp[k + i] * gor;
+      gor *= AERO_G_BR_TM24;
+    }
+    double sum = 0, s;
+    for (int i = 0; i < 3; i++) {
+      s = (r[i] + AERO_G_BR_BIG) - AERO_G_BR_BIG;
+      sum += s;
+      r[i] -= s;
+    }
+    t = 0;
+    for (int i = 0; i < 6; i++) t += r[5 - i];
+    double bb = (((((r[0] - t) + r[1]) + r[2]) + r[3]) + r[4]) + r[5];
+    s = (t + AERO_G_BR_BIG) - AERO_G_BR_BIG;
+    sum += s;
+    t -= s;
+    const double b = t + bb;
+    bb = (t - b) + bb;
+    s = (sum + AERO_G_BR_BIG1) - AERO_G_BR_BIG1;
+    sum -= s;
+    hb[h] = b;
+    hbb[h] = bb;
+    hsum[h] = sum;
+  }
+  const double b1 = hb[0], bb1 = hbb[0], b2 = hb[1], bb2 = hbb[1];
+  double sum = hsum[0] + hsum[1];
+  double b = b1 + b2;
+  double bb = (__builtin_fabs(b1) > __builtin_fabs(b2)) ? (b1 - b) + b2 : (b2 - b) + b1;
+  if (b > 0.5) {
+    b -= 1.0;
+    sum += 1.0;
+  } else if (b < -0.5) {
+    b += 1.0;
+    sum -= 1.0;
+  }
+  double s = b + (bb + bb1 + bb2);
+  t = ((b - s) + bb) + (bb1 + bb2);
+  b = s * AERO_G_BR_SPLIT;
+  const double t1 = b - (b - s), t2 = s - t1;
+  b = s * AERO_G_HPI;
+  bb = (((t1 * AERO_G_MP1 - b) + t1 * AERO_G_BR_MP2) + t2 * AERO_G_MP1) +
+       (t2 * AERO_G_BR_MP2 + s * AERO_G_HP1 + t * AERO_G_HPI);
+  s = b + bb;
+  t = (b - s) + bb;
+  a = s;
+  aa = t;
+  return ((int)sum) & 3;
+}
+
 /* sct: __sincostab (aero_g_sincostab, 440 doubles) or a copy of it, e.g. in
  * LDS (aero_sincos_t); the results do not depend on where it lives */
 AERO_HD void aero_sincos_t(double x, double &so, double &co, const double *sct) {
@@ -499,12 +569,8 @@ AERO_HD void aero_sincos_t(double x, double &so, double &co, const double *sct) 
     return;
   }
   if (k < 0x7ff00000u) {
-    if (k >= 0x419921fbu) {  // __branred range, not restated (header)
-      so = co = __builtin_nan("");
-      return;
-    }
     double a, da;
-    const int n = g_reduce_sincos(x, a, da);
+    const int n = k < 0x419921fbu ? g_reduce_sincos(x, a, da) : g_branred(x, a, da);
     if ((unsigned)(n - 1) <= 1u) {
       a = -a;
       da = -da;

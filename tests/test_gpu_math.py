@@ -41,6 +41,11 @@ def test_device_math_matches_host_build(engine_lib):
         dev = eng.device_math(fn, x, y)
         host = mathhost.evaluate(fn, x, y)
         assert np.array_equal(dev.view(np.uint64), host.view(np.uint64)), fn
+    # sincos beyond 105414350 (__branred) on the device
+    huge = np.sign(a) * np.exp2(np.abs(b) % 1 * 996 + 27) * (1 + np.abs(a) % 1)
+    for fn in ('sin', 'cos'):
+        dev = eng.device_math(fn, huge)
+        assert np.array_equal(dev.view(np.uint64), mathhost.glibc(fn, huge).view(np.uint64)), fn + ' huge'
     eng.close()
 
 
