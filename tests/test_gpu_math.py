@@ -194,7 +194,8 @@ def test_tanh_and_sincos_branch_free_paths_are_glibc(engine_lib):
     mixed[2::71] = np.inf
     mixed[3::73] = np.nan
     mixed[4::79] = 2.0
-    mixed[5::83] = 1e6  # reduced by reduce_sincos (|x| >= 105414350 needs __branred: NaN, aero_math.h)
+    mixed[5::83] = 1e6  # the Cody-Waite reduction (below 105414350)
+    mixed[6::89] = 1e10  # __branred (g_branred)
     sc_cases.append(mixed)
     for x in sc_cases:
         for fn in ('sin', 'cos'):
